@@ -1,0 +1,50 @@
+import json
+import os
+import sys
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(REPO / "video-gen-evals_amd"))
+sys.path.insert(0, str(REPO))
+
+GOLDEN = REPO / "tests" / "golden"
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libvge.so on cuda:0)")
+
+
+@pytest.fixture(scope="session")
+def golden_dataset(tmp_path_factory):
+    """The synthetic dataset + checkpoint the golden vectors were generated from."""
+    from tests.golden.dataset_spec import build_golden_dataset
+    root = tmp_path_factory.mktemp("golden_ds")
+    paths, ckpt, digest = build_golden_dataset(str(root))
+    flow = np.load(GOLDEN / "golden_flow.npz")
+    assert bytes(flow["dataset_digest"]).hex() == digest, "synthetic generator drifted from the golden fixtures"
+    return paths, ckpt
+
+
+@pytest.fixture(scope="session")
+def golden_flow():
+    return dict(np.load(GOLDEN / "golden_flow.npz"))
+
+
+@pytest.fixture(scope="session")
+def golden_meta():
+    with open(GOLDEN / "golden_scores.json") as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def golden_ops():
+    return dict(np.load(GOLDEN / "golden_ops.npz"))
+
+
+@pytest.fixture(scope="session")
+def golden_state_dict():
+    from vge import synth
+    return synth.make_state_dict(synth.DIMS_RAW, synth.DIMS_DIFF)

@@ -1,0 +1,50 @@
+"""The deterministic synthetic dataset behind the golden fixtures (shared by make_golden.py and the
+tests, so both sides see byte-identical inputs; `digest` guards against generator drift)."""
+from __future__ import annotations
+
+import hashlib
+import os
+from pathlib import Path
+
+import numpy as np
+
+from vge import synth
+
+GOLDEN_SPEC = {
+    "n_real_per_class": 4,
+    "T_real": (32, 40, 64, 20),
+    "n_gen": 16,
+    "T_gen": (32, 64, 20, 45, 33),
+    "kp_short_every": 3,
+    "feat_windows": [0, 5, 13],
+}
+
+
+def build_golden_dataset(root: str):
+    """Write dataset + checkpoint under `root`; returns (paths, checkpoint_path, sha256 hexdigest)."""
+    paths = synth.write_dataset(root, n_real_per_class=GOLDEN_SPEC["n_real_per_class"],
+                                n_gen=GOLDEN_SPEC["n_gen"], T_real=GOLDEN_SPEC["T_real"],
+                                T_gen=GOLDEN_SPEC["T_gen"], kp_short_every=GOLDEN_SPEC["kp_short_every"])
+    # one generated clip whose filename carries no known action -> class "Testmodel", no AC score
+    clip = synth.make_clip(synth.SEED_GEN, 999, 32)
+    stem = "Testmodel_Xyzzy_00_deadbeef"
+    synth.save_clip_npz(Path(paths["generated_meshes"]) / f"{stem}.npz", clip)
+    kd = Path(paths["generated_kps"]) / stem
+    kd.mkdir(parents=True, exist_ok=True)
+    np.save(kd / "keypoints.npy", clip.keypoints)
+    sd = synth.make_state_dict(synth.DIMS_RAW, synth.DIMS_DIFF)
+    ckpt = os.path.join(root, "model.pt")
+    synth.save_checkpoint(ckpt, sd)
+    h = hashlib.sha256()
+    for sub in ("real", "real_kp", "generated_meshes", "generated_kps"):
+        for p in sorted(Path(paths[sub]).rglob("*")):
+            if p.suffix == ".npz":
+                with np.load(p) as z:
+                    for k in ("pose", "global_orient", "betas", "vit"):
+                        h.update(np.ascontiguousarray(z[k]).tobytes())
+            elif p.suffix == ".npy":
+                h.update(np.load(p).tobytes())
+    for k in sorted(sd):
+        h.update(k.encode())
+        h.update(np.ascontiguousarray(sd[k]).tobytes())
+    return paths, ckpt, h.hexdigest()

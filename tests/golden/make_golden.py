@@ -1,0 +1,185 @@
+"""Generate the golden vectors in tests/golden/ by running the REFERENCE itself (build container only).
+
+    PYTHONDONTWRITEBYTECODE=1 python -B tests/golden/make_golden.py
+
+Imports /root/reference (eval.py, utils.py, model.py) read-only, runs it on the deterministic
+synthetic dataset and weights of vge.synth, and stores inputs/outputs as small fixtures:
+
+  golden_ops.npz      op-level known answers: _log_so3, _rotmat_delta, _vit_delta, _betas_delta,
+                      _procrustes_kp_delta (random / static / all -1 / collinear), _slice_or_pad
+  svd2x2.npz          torch.linalg.svd (MKL sgesdd) on random, keypoint-like and special 2x2 H
+  golden_flow.npz     ModalityStats, feats of 3 windows, seq_embed of every generated window,
+                      frame_embeds of 4 windows, centroids + counts, label order
+  golden_scores.json  video_scores.json of the eval.py flow + Spearman on TAG_final_human_scores names
+
+Nothing from the reference is copied; only arrays and numbers it produced.  This script never runs
+on the GPU box (the reference is not there); tests regenerate the same synthetic inputs from seeds.
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import tempfile
+from pathlib import Path
+
+import numpy as np
+import torch
+
+HERE = Path(__file__).resolve().parent
+REPO = HERE.parent.parent
+sys.path.insert(0, str(REPO / "video-gen-evals_amd"))
+sys.path.insert(0, str(REPO))
+
+from vge import synth  # noqa: E402
+from tests.golden.dataset_spec import GOLDEN_SPEC, build_golden_dataset  # noqa: E402
+
+REF = "/root/reference"
+
+
+def main():
+    sys.path.insert(0, REF)
+    import utils as U  # noqa
+    import eval as E  # noqa
+    torch.manual_seed(0)
+    out = {}
+
+    # ---------------- op-level known answers
+    rng = np.random.default_rng(123)
+    aa = rng.normal(0, 0.7, (40, 24, 3))
+    R = synth._rodrigues(aa).astype(np.float32)
+    aa_small = rng.normal(0, 1e-4, (40, 24, 3))
+    Rs = synth._rodrigues(aa + aa_small * 0).astype(np.float32)
+    Rnear = synth._rodrigues(np.cumsum(rng.normal(0, 1e-3, (40, 24, 3)), 0)).astype(np.float32)
+    out["rot_in"] = R
+    out["rot_delta"] = U._rotmat_delta(torch.from_numpy(R)).numpy()
+    out["rotnear_in"] = Rnear
+    out["rotnear_delta"] = U._rotmat_delta(torch.from_numpy(Rnear)).numpy()
+    out["logso3_in"] = Rs.reshape(-1, 3, 3)
+    out["logso3_out"] = U._log_so3(torch.from_numpy(Rs.reshape(-1, 3, 3))).numpy()
+    vit = rng.normal(0, 1, (32, 1024)).astype(np.float32)
+    out["vit_in"] = vit
+    out["vit_delta"] = U._vit_delta(torch.from_numpy(vit)).numpy()
+    b = rng.normal(0, 1, (32, 10)).astype(np.float32)
+    out["beta_in"] = b
+    out["beta_delta"] = U._betas_delta(torch.from_numpy(b)).numpy()
+    kp = rng.random((32, 120)).astype(np.float32)
+    kp[rng.random(kp.shape) < 0.05] = -1
+    kp_static = np.repeat(kp[:1], 32, 0)
+    kp_neg = -np.ones((32, 120), np.float32)
+    t = np.linspace(0, 1, 60, dtype=np.float32)
+    line = np.stack([t, 0.5 * t + 0.1], -1).reshape(1, 120)
+    kp_col = (line + rng.normal(0, 0.01, (32, 1)).astype(np.float32)).astype(np.float32)
+    kp_mixed = kp.copy()
+    kp_mixed[5] = -1
+    for name, arr in (("kp_rand", kp), ("kp_static", kp_static), ("kp_neg", kp_neg), ("kp_col", kp_col),
+                      ("kp_mixed", kp_mixed)):
+        out[name + "_in"] = arr
+        out[name + "_delta"] = U._procrustes_kp_delta(torch.from_numpy(arr)).numpy()
+    ds_dummy = U.WindowDataset([], clip_len=32)
+    seq = rng.normal(0, 1, (20, 7)).astype(np.float32)
+    for s in (0, 5, 19, 25, -1):
+        out[f"sop_{s}"] = ds_dummy._slice_or_pad(seq, s, 32)
+    out["sop_in"] = seq
+    np.savez_compressed(HERE / "golden_ops.npz", **out)
+
+    # ---------------- 2x2 SVD (LAPACK signs)
+    H = [rng.standard_normal((3000, 2, 2)).astype(np.float32)]
+    kpb = rng.random((1500, 60, 2)).astype(np.float32)
+    kpb[rng.random(kpb.shape) < 0.05] = -1
+    c = kpb - kpb.mean(1, keepdims=True)
+    c = c / np.linalg.norm(c, axis=(1, 2), keepdims=True)
+    H.append(np.einsum("nki,nkj->nij", c[:-1], c[1:]).astype(np.float32))
+    H.append(np.einsum("nki,nkj->nij", c, c).astype(np.float32))
+    H.append(np.array([[[0, 0], [0, 0]], [[1, 0], [0, 1]], [[1, 0], [0, 2]], [[0, 1], [1, 0]], [[1, 1], [1, 1]],
+                       [[1, 2], [2, 4]], [[0, 0], [1, 0]], [[0, 1], [0, 0]], [[1e-3, 1], [0, 1e-3]],
+                       [[-1, 0], [0, -1]], [[2, 0], [0, -3]], [[3, 1e-9], [0, 2]]], np.float32))
+    H = np.concatenate(H)
+    Ut, St, Vt = torch.linalg.svd(torch.from_numpy(H))
+    np.savez_compressed(HERE / "svd2x2.npz", H=H, U=Ut.numpy(), S=St.numpy(), Vh=Vt.numpy())
+
+    # ---------------- full eval.py flow on the synthetic dataset
+    with tempfile.TemporaryDirectory() as tmp:
+        paths, ckpt, digest = build_golden_dataset(tmp)
+        real_ds = U.NpzVideoDataset(paths["real"], filter_classes=E.ACTION_CLASSES)
+        train_ds, _ = U.train_test_split(real_ds, train_ratio=0.8, seed=1337)
+        stats = U.compute_stats_from_npz(train_ds.items, keypoint_dir=paths["real_kp"])
+        dims_raw, dims_diff = E.infer_dims_from_stats(stats)
+        model = E.load_model(ckpt, dims_raw, dims_diff)
+        centroids, label_dict = E.build_real_centroids(model, paths["real"], paths["real_kp"], stats, 32, 8)
+        # counts (build_real_centroids prints them; recompute the same loader to capture them)
+        loader = U.make_test_loader(train_ds, clip_len=32, stride=8, stats=stats, seed=1337, batch_size=64,
+                                    keypoint_dir=paths["real_kp"], num_workers=0)
+        _, counts = U.build_train_centroids_subset(model, loader, label_dict, device="cpu")
+        dataset = E.create_dataset_from_generated_meshes(paths["generated_meshes"])
+        samples = U.sample_all_windows_npz(dataset, clip_len=32, stride=8)
+        wds = U.WindowDataset(samples=samples, clip_len=32, stats=stats, keypoint_dir=paths["generated_kps"])
+        dl = torch.utils.data.DataLoader(wds, batch_size=32, shuffle=False, num_workers=0,
+                                         collate_fn=U.safe_collate)
+        feats_all = torch.stack([wds[i][0] for i in range(len(wds))])
+        features = E.extract_window_features(model, dl)
+        ac = E.compute_action_consistency_scores(features, centroids, label_dict)
+        tc = E.compute_temporal_coherence_scores(features)
+        vids = sorted(set(ac) | set(tc))
+        combined = {}
+        for v in vids:
+            e = {}
+            if v in ac:
+                e["ac"] = ac[v]
+            if v in tc:
+                e["tc"] = tc[v]
+            combined[v] = e
+
+        def sarr(name):
+            x = getattr(stats, name)
+            return None if x is None else x.numpy()
+
+        mods = ["vit", "gori", "pose", "beta", "keypoints"]
+        flow = {
+            "stats_mean": np.concatenate([sarr(f"{m}_raw_mean") for m in mods] + [sarr(f"{m}_diff_mean") for m in mods]),
+            "stats_std": np.concatenate([sarr(f"{m}_raw_std") for m in mods] + [sarr(f"{m}_diff_std") for m in mods]),
+            "centroids": centroids.numpy(), "counts": counts.numpy(),
+            "seq_embeds": features["seq_embeds"].numpy(),
+            "frame_embeds_first4": features["frame_embeds"][:4].numpy(),
+            "feat_windows": np.array(GOLDEN_SPEC["feat_windows"], np.int64),
+            "feats_sel": feats_all[GOLDEN_SPEC["feat_windows"]].numpy(),
+            "feats_absmean": feats_all.abs().mean(dim=(1, 2)).numpy(),
+            "dataset_digest": np.frombuffer(bytes.fromhex(digest), np.uint8),
+        }
+        np.savez_compressed(HERE / "golden_flow.npz", **flow)
+        meta = {
+            "label_dict": label_dict,
+            "window_vids": features["vid_names"],
+            "window_cls": features["cls_names"],
+            "n_train_real": len(train_ds),
+            "train_real": [it.name for it in train_ds.items],
+            "video_scores": combined,
+            "dims_raw": list(dims_raw.items()), "dims_diff": list(dims_diff.items()),
+        }
+
+        # Spearman plumbing on the reference's own fixture names (eval.py:297-347)
+        with open(os.path.join(REF, "TAG_final_human_scores.json")) as f:
+            human = json.load(f)
+        srng = np.random.default_rng(7)
+        names = sorted(human)
+        model_scores = {}
+        for i, n in enumerate(names):
+            if i % 7 == 3:
+                continue       # some videos unscored
+            key = os.path.splitext(n)[0]
+            if i % 5 == 1:
+                key = key.replace("_", "_videos_", 1)   # exercise _norm_name
+            model_scores[key] = float(srng.random())
+        meta["spearman_model_scores"] = model_scores
+        sp = {}
+        for hk in ("ac", "tc"):
+            corr, p, matched = E.compute_spearman_correlation(model_scores, os.path.join(REF, "TAG_final_human_scores.json"), hk)
+            sp[hk] = {"corr": corr, "p": p, "n_matched": len(matched)}
+        meta["spearman"] = sp
+        with open(HERE / "golden_scores.json", "w") as f:
+            json.dump(meta, f, indent=1, sort_keys=True)
+    print("golden written to", HERE)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,211 @@
+"""Deterministic synthetic inputs in the reference's on-disk layout.
+
+There are no datasets, checkpoints or extractors offline, so every test, fixture and benchmark
+runs on data from this generator.  Values are shaped like the real extractor outputs:
+
+* pose / global_orient: valid SO(3) matrices from Rodrigues of a per-joint axis-angle random walk
+  (24 joints, base ~ N(0, 0.5^2), per-frame step ~ N(0, 0.05^2)); joint 0 -> global_orient
+  [T,1,3,3], joints 1..23 -> pose [T,23,3,3]  (layout written by extract_mesh.py:18-43).
+* betas ~ N(0,1) [T,10];  vit ~ N(0,1) [T,1024]  (token_head.py token_out).
+* keypoints ~ U[0,1] [T',120] with ~5% coordinates set to -1 (dwpose_init.py:57-60 marks
+  low-score points -1) and an optional T' < T (process_video.py drops frames).
+
+Seeds: real = 1, generated = 2, weights = 3, kp = 4 (mixed with the video index so every clip is
+independent of how many other clips are generated).
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+from dataclasses import dataclass
+from pathlib import Path
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+
+from .data import ACTION_CLASSES
+
+SEED_REAL, SEED_GEN, SEED_WEIGHTS, SEED_KP = 1, 2, 3, 4
+GEN_MODELS = ["Hunyuan", "Opensora_768", "wan21", "RunwayGen4", "Wan2.2"]
+
+
+def _rodrigues(aa: np.ndarray) -> np.ndarray:
+    """axis-angle [...,3] (float64) -> rotation matrices [...,3,3] (float64)."""
+    theta = np.linalg.norm(aa, axis=-1, keepdims=True)
+    k = aa / np.maximum(theta, 1e-12)
+    kx, ky, kz = k[..., 0], k[..., 1], k[..., 2]
+    z = np.zeros_like(kx)
+    K = np.stack([np.stack([z, -kz, ky], -1), np.stack([kz, z, -kx], -1),
+                  np.stack([-ky, kx, z], -1)], -2)
+    s = np.sin(theta)[..., None]
+    c = np.cos(theta)[..., None]
+    eye = np.broadcast_to(np.eye(3), K.shape)
+    return eye + s * K + (1.0 - c) * (K @ K)
+
+
+@dataclass
+class SynthClip:
+    pose: np.ndarray           # [T,23,3,3] f32
+    global_orient: np.ndarray  # [T,1,3,3] f32
+    betas: np.ndarray          # [T,10] f32
+    vit: np.ndarray            # [T,1024] f32
+    keypoints: np.ndarray      # [T',120] f32
+
+
+def make_clip(seed: int, index: int, T: int, kp_len: Optional[int] = None, vit_dim: int = 1024,
+              kp_seed: int = SEED_KP) -> SynthClip:
+    rng = np.random.default_rng([seed, index])
+    base = rng.normal(0.0, 0.5, size=(1, 24, 3))
+    steps = rng.normal(0.0, 0.05, size=(T, 24, 3))
+    aa = base + np.cumsum(steps, axis=0)
+    R = _rodrigues(aa).astype(np.float32)                       # [T,24,3,3]
+    betas = rng.normal(0.0, 1.0, size=(T, 10)).astype(np.float32)
+    vit = rng.normal(0.0, 1.0, size=(T, vit_dim)).astype(np.float32)
+    krng = np.random.default_rng([kp_seed, seed, index])
+    Tk = T if kp_len is None else kp_len
+    kp = krng.random((Tk, 120), dtype=np.float64).astype(np.float32)
+    kp[krng.random((Tk, 120)) < 0.05] = -1.0
+    return SynthClip(pose=np.ascontiguousarray(R[:, 1:]), global_orient=np.ascontiguousarray(R[:, :1]),
+                     betas=betas, vit=vit, keypoints=kp)
+
+
+def save_clip_npz(path: Path, clip: SynthClip, meta: Optional[dict] = None) -> None:
+    """Same keys and dtypes as extract_mesh.py:35-43 (np.savez_compressed)."""
+    path.parent.mkdir(parents=True, exist_ok=True)
+    T = clip.pose.shape[0]
+    np.savez_compressed(path, pose=clip.pose, betas=clip.betas, global_orient=clip.global_orient,
+                        vit=clip.vit, frame_idx=np.arange(T, dtype=np.int32),
+                        meta=json.dumps(meta or {}, ensure_ascii=False))
+
+
+def _hash8(s: str) -> str:
+    return hashlib.sha1(s.encode()).hexdigest()[:8]
+
+
+def generated_name(i: int, classes: Sequence[str] = ACTION_CLASSES) -> str:
+    model = GEN_MODELS[i % len(GEN_MODELS)]
+    action = classes[(i // len(GEN_MODELS)) % len(classes)]
+    nn = i // (len(GEN_MODELS) * len(classes))
+    return f"{model}_{action}_{nn:02d}_{_hash8(f'{model}{action}{i}')}"
+
+
+def write_dataset(root: str, n_real_per_class: int = 5, n_gen: int = 4, T_real: Sequence[int] = (32,),
+                  T_gen: Sequence[int] = (32,), kp_short_every: int = 0, classes: Sequence[str] = ACTION_CLASSES,
+                  vit_dim: int = 1024) -> Dict[str, str]:
+    """Write a synthetic dataset in the reference layout.
+
+    real:      <root>/real/<Class>/v_<Class>_gNN.npz     + <root>/real_kp/<Class>/<stem>/keypoints.npy
+    generated: <root>/generated_meshes/<name>.npz        + <root>/generated_kps/<stem>/keypoints.npy
+    Lengths cycle through T_real / T_gen; every `kp_short_every`-th clip gets a keypoint file
+    5 frames shorter than its mesh sequence (process_video.py drops frames)."""
+    root_p = Path(root)
+    paths = {k: str(root_p / k) for k in ("real", "real_kp", "generated_meshes", "generated_kps")}
+    idx = 0
+    for ci, cls in enumerate(classes):
+        for j in range(n_real_per_class):
+            T = T_real[idx % len(T_real)]
+            kp_len = max(1, T - 5) if kp_short_every and idx % kp_short_every == kp_short_every - 1 else None
+            clip = make_clip(SEED_REAL, idx, T, kp_len, vit_dim)
+            stem = f"v_{cls}_g{j:02d}"
+            save_clip_npz(root_p / "real" / cls / f"{stem}.npz", clip, {"video": stem})
+            kp_dir = root_p / "real_kp" / cls / stem
+            kp_dir.mkdir(parents=True, exist_ok=True)
+            np.save(kp_dir / "keypoints.npy", clip.keypoints)
+            idx += 1
+    for i in range(n_gen):
+        T = T_gen[i % len(T_gen)]
+        kp_len = max(1, T - 5) if kp_short_every and i % kp_short_every == kp_short_every - 1 else None
+        clip = make_clip(SEED_GEN, i, T, kp_len, vit_dim)
+        stem = generated_name(i, classes)
+        save_clip_npz(root_p / "generated_meshes" / f"{stem}.npz", clip, {"video": stem})
+        kp_dir = root_p / "generated_kps" / stem
+        kp_dir.mkdir(parents=True, exist_ok=True)
+        np.save(kp_dir / "keypoints.npy", clip.keypoints)
+    return paths
+
+
+# ----------------------------------------------------------------------------- weights
+
+def _sinusoidal_pe(d_model: int, max_len: int = 5000) -> np.ndarray:
+    """Same formula and float32 evaluation order as model.py:9-16 (computed with torch)."""
+    import math
+    import torch
+    pe = torch.zeros(max_len, d_model)
+    pos = torch.arange(0, max_len, dtype=torch.float32).unsqueeze(1)
+    div = torch.exp(torch.arange(0, d_model, 2, dtype=torch.float32) * (-math.log(10000.0) / d_model))
+    pe[:, 0::2] = torch.sin(pos * div)
+    pe[:, 1::2] = torch.cos(pos * div)
+    return pe.unsqueeze(0).numpy()
+
+
+def make_state_dict(dims_raw: Dict[str, int], dims_diff: Dict[str, int], d_model: int = 256,
+                    time_layers: int = 4, ff_mult: int = 4, seed: int = SEED_WEIGHTS,
+                    max_len: int = 5000) -> Dict[str, np.ndarray]:
+    """Deterministic random weights with exactly the reference state_dict key set
+    (model.py:102-148; 241 tensors for the 5-modality model).
+
+    Matrices are U(-1/sqrt(fan_in), 1/sqrt(fan_in)) like torch's default init; norm affines are
+    1 + N(0, 0.1) / N(0, 0.1) so the affine paths are exercised; fusion temperature/bias
+    ~ N(0, 0.5)."""
+    rng = np.random.default_rng(seed)
+    sd: Dict[str, np.ndarray] = {}
+
+    def U(shape, fan_in):
+        b = 1.0 / np.sqrt(fan_in)
+        return rng.uniform(-b, b, size=shape).astype(np.float32)
+
+    def affine(prefix, n):
+        sd[prefix + ".weight"] = (1.0 + rng.normal(0, 0.1, n)).astype(np.float32)
+        sd[prefix + ".bias"] = rng.normal(0, 0.1, n).astype(np.float32)
+
+    mods = list(dims_raw.keys())
+    D = d_model
+    for kind, dims in (("state_enc", dims_raw), ("motion_enc", dims_diff)):
+        for m in mods:
+            if kind == "motion_enc" and dims[m] <= 0:
+                continue
+            p = f"{kind}.{m}"
+            sd[p + ".stem.weight"] = U((D, dims[m], 1), dims[m])
+            for i in range(4):
+                sd[f"{p}.blocks.{i}.conv1.weight"] = U((D, D, 5), D * 5)
+                sd[f"{p}.blocks.{i}.conv2.weight"] = U((D, D, 5), D * 5)
+                affine(f"{p}.blocks.{i}.norm", D)
+            sd[p + ".proj.weight"] = U((D, D), D)
+    M = len(mods)
+    sd["fusion.latent"] = rng.normal(0, 1, (1, 1, D)).astype(np.float32)
+    sd["fusion.logit_temp"] = rng.normal(0, 0.5, M).astype(np.float32)
+    sd["fusion.logit_bias"] = rng.normal(0, 0.5, M).astype(np.float32)
+    affine("fusion.q_ln", D)
+    affine("fusion.kv_ln", D)
+    for w in ("Wq", "Wk", "Wv", "Wo"):
+        sd[f"fusion.{w}.weight"] = U((D, D), D)
+    sd["cls"] = rng.normal(0, 1, (1, 1, D)).astype(np.float32)
+    sd["pos_enc.pe"] = _sinusoidal_pe(D, max_len)
+    F = ff_mult * D
+    for l in range(time_layers):
+        p = f"temporal.layers.{l}"
+        sd[p + ".self_attn.in_proj_weight"] = U((3 * D, D), D)
+        sd[p + ".self_attn.in_proj_bias"] = rng.normal(0, 0.02, 3 * D).astype(np.float32)
+        sd[p + ".self_attn.out_proj.weight"] = U((D, D), D)
+        sd[p + ".self_attn.out_proj.bias"] = rng.normal(0, 0.02, D).astype(np.float32)
+        sd[p + ".linear1.weight"] = U((F, D), D)
+        sd[p + ".linear1.bias"] = rng.normal(0, 0.02, F).astype(np.float32)
+        sd[p + ".linear2.weight"] = U((D, F), F)
+        sd[p + ".linear2.bias"] = rng.normal(0, 0.02, D).astype(np.float32)
+        affine(p + ".norm1", D)
+        affine(p + ".norm2", D)
+    return sd
+
+
+DIMS_RAW = {"vit": 1024, "global": 9, "pose": 207, "beta": 10, "kp2d": 120}
+DIMS_DIFF = {"vit": 1024, "global": 3, "pose": 69, "beta": 10, "kp2d": 120}
+
+
+def save_checkpoint(path: str, sd: Dict[str, np.ndarray], d_model: int = 256, time_layers: int = 4,
+                    time_heads: int = 8) -> None:
+    """{model_state_dict, d_model, time_layers, time_heads, ...} as accepted by eval.py:136-160."""
+    import torch
+    torch.save({"model_state_dict": {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in sd.items()},
+                "d_model": d_model, "latent_dim": 128, "time_layers": time_layers,
+                "time_heads": time_heads, "dropout": 0.1}, path)
