@@ -1,0 +1,168 @@
+/*
+ * vge.h -- C ABI of libvge.so, the MI355X (gfx950) implementation of the Action-Consistency /
+ * Temporal-Coherence scoring path of XThomasBU/video-gen-evals.
+ *
+ * The reference has no FFI layer: its boundary is the set of Python functions eval.py composes.
+ * Each entry point below replaces one of them (reference file:line cited per function).
+ *
+ * Conventions
+ *   - Plain pointers and sizes; no torch types.  Pointers marked "device" are HBM buffers owned by
+ *     the caller (hipMalloc / torch), "host" pointers are ordinary host memory.
+ *   - Every compute call is asynchronous on the hipStream_t passed in (nullptr = default stream)
+ *     and never synchronises, allocates or frees inside (graph-capture safe), except the create /
+ *     reserve / destroy calls.
+ *   - Return value: 0 (VGE_OK) or a vge_status code; nothing throws across the ABI.
+ *     vge_last_error() returns a static description of the most recent failure on this thread.
+ *   - Feature-column order is the reference's feats layout (utils.py:496-514):
+ *       raw  = vit[1024] | global_orient[9] | pose[207] | betas[10] | kp2d[120]      (1370)
+ *       diff = vit[1024] | global_orient[3] | pose[69]  | betas[10] | kp2d[120]      (1226)
+ */
+#ifndef VGE_H
+#define VGE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t* vge_stream_t; /* == hipStream_t */
+
+typedef enum {
+  VGE_OK = 0,
+  VGE_ERR_ARG = 1,            /* bad argument / unsupported shape */
+  VGE_ERR_HIP = 2,            /* a HIP runtime call failed */
+  VGE_ERR_MISSING_WEIGHT = 3, /* a required state_dict key is absent (the reference's
+                                 load_state_dict(strict=False) would silently random-init it) */
+  VGE_ERR_WEIGHT_SHAPE = 4,   /* a state_dict tensor has the wrong shape */
+  VGE_ERR_NOMEM = 5,
+  VGE_ERR_WORKSPACE = 6       /* vge_encoder_reserve() was not called for this many windows */
+} vge_status;
+
+typedef enum { VGE_F32 = 0 } vge_dtype; /* compute type: f32 in / f32 accumulate (exact-f32 MFMA) */
+
+#define VGE_FEAT_DIM 2596
+#define VGE_RAW_DIM 1370
+#define VGE_CLIP_LEN 32
+#define VGE_D_MODEL 256
+
+/* Model shape (infer_dims_from_stats, eval.py:104-133; HumanActionScorer, model.py:102-148).
+ * The kernels are built for the reference configuration: 5 modalities in the order
+ * vit, global, pose, beta, kp2d with dims {1024,9,207,10,120} / {1024,3,69,10,120},
+ * d_model 256, 4 post-norm layers, 8 heads, FFN 1024, clip_len 32. */
+typedef struct {
+  int n_modalities;
+  int dims_raw[8];
+  int dims_diff[8];
+  int d_model;
+  int time_layers;
+  int time_heads;
+  int clip_len;
+} vge_dims;
+
+/* A named host tensor, named exactly as the reference state_dict key (model.py parameter names),
+ * e.g. "state_enc.vit.blocks.0.conv1.weight" [256,256,5] or "temporal.layers.3.norm2.bias" [256]. */
+typedef struct {
+  const char* name;
+  const float* data; /* host, contiguous float32 */
+  int ndim;
+  int64_t shape[4];
+} vge_tensor_view;
+
+typedef struct vge_encoder vge_encoder;
+
+/* ---- frame store: the per-frame features of a set of videos, resident in HBM ----------------
+ * Replaces the npz/keypoints.npy reads of WindowDataset._try_one (utils.py:383-425).
+ * videos[v] = {frame_off, n_frames, kp_off, kp_frames} (int32, device); kp_frames = 0 means the
+ * video has no keypoint file. */
+typedef struct {
+  const float* pose;   /* device [F,207] (23 rotmats) */
+  const float* gori;   /* device [F,9]                */
+  const float* betas;  /* device [F,10]               */
+  const float* vit;    /* device [F,1024]             */
+  const float* kp;     /* device [Fk,120]             */
+  const int32_t* videos; /* device [V,4]              */
+  int n_videos;
+} vge_frame_store;
+
+/* ---------------------------------------------------------------------------------------------
+ * Featurisation.  Replaces WindowDataset._try_one (utils.py:383-516) incl. _slice_or_pad
+ * (366-381), _vit_delta (142-147), _rotmat_delta/_log_so3 (130-140,165-174), _betas_delta
+ * (161-163), _procrustes_kp_delta with LAPACK-convention 2x2 SVD (177-217) and the z-norm
+ * (x-mean)/(std+1e-6) (472-494).
+ *   windows : device int32 [n_windows,2] = {video index, start frame}
+ *   mean,std: device float [2596] (ModalityStats in feats column order)
+ *   feats   : device float [n_windows,32,2596]
+ */
+int vge_featurize(const vge_frame_store* store, const int32_t* windows, int n_windows,
+                  const float* mean, const float* std, float* feats, vge_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * ModalityStats.  Replaces compute_stats_from_npz (utils.py:595-801) with _update_sum_sum2
+ * (589-593): float64 per-column sum / sum of squares over all frames of the selected videos,
+ * diffs on the full sequences; keypoint columns over keypoint frames only.
+ *   host_videos    : host copy of store->videos [V,4] (tile planning happens on the host)
+ *   host_video_sel : host int32 [n_sel] video indices into the store
+ *   sums      : device double [2,2596] (sum, sum of squares) -- ACCUMULATED INTO (zero it first)
+ *   counts    : host int64 [2] += {mesh frames, keypoint frames} of the selection
+ *   workspace : device scratch of >= vge_stats_workspace_bytes(1) bytes; videos are processed in
+ *               chunks of as many 32-frame tiles as fit (this call may synchronise the stream)
+ * vge_stats_finalize turns (sums, counts) into float32 mean/std (std = sqrt(max(var,0)+1e-6),
+ * utils.py:746-750).  Sums are the RCCL exchange payload when the real set is sharded.
+ */
+size_t vge_stats_workspace_bytes(int chunk_tiles);
+int vge_stats_accumulate(const vge_frame_store* store, const int32_t* host_videos, const int32_t* host_video_sel,
+                         int n_sel, double* sums, int64_t* counts, void* workspace, size_t workspace_bytes,
+                         vge_stream_t stream);
+int vge_stats_finalize(const double* sums, const int64_t* counts, float* mean, float* std, vge_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Encoder.  Replaces load_model (eval.py:136-165) + HumanActionScorer.forward (model.py:162-193).
+ * create: validates every required key (missing -> VGE_ERR_MISSING_WEIGHT) and repacks the
+ * weights into the library's MFMA panel layout in HBM (the handle owns them).
+ * reserve: allocates the activation workspace for up to max_windows windows (outside timed
+ * regions; compute calls never allocate).
+ * encode: feats device [B,T,2596] -> seq_embed device [B,256] (L2-normalised CLS),
+ *   frame_embed device [B,T+1,256] or NULL, tc_window device [B] (per-window temporal coherence,
+ *   eval.py:216-224) or NULL.
+ */
+int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int n_weights, vge_dtype compute,
+                       vge_encoder** out);
+int vge_encoder_reserve(vge_encoder* enc, int max_windows);
+int vge_encoder_destroy(vge_encoder* enc);
+int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_embed, float* frame_embed,
+               float* tc_window, vge_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Metrics.
+ * vge_tc_windows: compute_temporal_coherence_scores' per-window term (eval.py:216-224):
+ *   tc[w] = mean_t ||f[w,t+1]-f[w,t]||_2 over rows 1..T of frame_embed [B,T+1,d] (CLS dropped).
+ * vge_score_videos: per-video AC (eval.py:229-257) and TC (np.mean over windows, eval.py:226):
+ *   windows of video v are [video_first_win[v], video_first_win[v+1]) (device int32 [V+1]);
+ *   video_class[v] = centroid row or -1 (class not in label_dict -> ac[v] = NaN, no "ac" key).
+ *   ac: device float [V]; tc: device double [V].
+ */
+int vge_tc_windows(const float* frame_embed, int B, int T1, int d, float* tc, vge_stream_t stream);
+int vge_score_videos(const float* seq_embed, const float* tc_window, const int32_t* video_first_win,
+                     const int32_t* video_class, const float* centroids, int V, int d, float* ac, double* tc,
+                     vge_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Real-class centroids.  Replaces build_train_centroids_subset (utils.py:1018-1045):
+ * sums.index_add_(0, y, z); counts.index_add_ -- accumulated in window order (bit-identical
+ * sequential f32 sums); finalize = normalize(sums / counts.clamp_min(1)).
+ * sums [C,d] / counts [C] (device float) are ACCUMULATED INTO and are the RCCL all-gather payload.
+ */
+int vge_centroid_accumulate(const float* seq_embed, const int32_t* class_id, int n_windows, int C, int d,
+                            float* sums, float* counts, vge_stream_t stream);
+int vge_centroid_finalize(const float* sums, const float* counts, int C, int d, float* centroids,
+                          vge_stream_t stream);
+
+const char* vge_last_error(void);
+const char* vge_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* VGE_H */

@@ -1,0 +1,178 @@
+"""GPU parity: libvge.so (through its C ABI) against the golden vectors of the reference and the oracle.
+
+Tolerances (fp32 path; north star: scores within 1e-4 of the reference eval.py):
+  feats 1e-4 abs (z-normalised features), stats 1e-6 rel, embeddings 2e-5 abs,
+  AC / TC 1e-4 abs (the bar), centroid counts exact.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+@pytest.fixture(scope="module")
+def vg():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vge import eval as VE
+    from vge import ops
+    return VE, ops
+
+
+@pytest.fixture(scope="module")
+def real_setup(vg, golden_dataset):
+    VE, ops = vg
+    from vge.data import ACTION_CLASSES, NpzVideoDataset, train_test_split
+    paths, ckpt = golden_dataset
+    real_ds = NpzVideoDataset(paths["real"], filter_classes=ACTION_CLASSES)
+    train_ds, _ = train_test_split(real_ds, train_ratio=0.8, seed=1337)
+    store = ops.DeviceFrameStore.from_host(VE.load_frame_store(train_ds.items, paths["real_kp"], False), DEV)
+    stats = VE.compute_stats_from_npz(train_ds.items, paths["real_kp"], device=DEV, store=store)
+    model = VE.load_model(ckpt, device=DEV)
+    return paths, real_ds, train_ds, store, stats, model
+
+
+def test_stats_match_reference(real_setup, golden_flow):
+    _, _, _, _, stats, _ = real_setup
+    mean = stats.mean.cpu().numpy()
+    std = stats.std.cpu().numpy()
+    np.testing.assert_allclose(mean, golden_flow["stats_mean"], rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(std, golden_flow["stats_std"], rtol=1e-6, atol=1e-7)
+
+
+def test_featurize_matches_reference(vg, real_setup, golden_flow):
+    VE, ops = vg
+    from vge.data import create_dataset_from_generated_meshes, sample_all_windows_npz
+    paths, _, _, _, stats, _ = real_setup
+    ds = create_dataset_from_generated_meshes(paths["generated_meshes"])
+    store = ops.DeviceFrameStore.from_host(VE.load_frame_store(ds.items, paths["generated_kps"], True), DEV)
+    samples = sample_all_windows_npz(ds)
+    idx = {it.path: i for i, it in enumerate(ds.items)}
+    win = VE._window_tensor(samples, idx, DEV)
+    feats = ops.featurize(store, win, stats.mean, stats.std).cpu().numpy()
+    for wi, ref in zip(golden_flow["feat_windows"], golden_flow["feats_sel"]):
+        err = np.abs(feats[wi] - ref).max()
+        assert err < 1e-4, (wi, err)
+    absmean = np.abs(feats).mean(axis=(1, 2))
+    np.testing.assert_allclose(absmean, golden_flow["feats_absmean"], rtol=1e-5)
+
+
+def test_featurize_matches_oracle_all_windows(vg, real_setup):
+    """Every generated window (short clips, tail padding, kp shorter than mesh) vs the oracle."""
+    VE, ops = vg
+    from oracle import featurize as OF
+    from oracle.featurize import Stats
+    from vge.data import create_dataset_from_generated_meshes, load_clip, sample_all_windows_npz
+    paths, _, _, _, stats, _ = real_setup
+    ds = create_dataset_from_generated_meshes(paths["generated_meshes"])
+    store = ops.DeviceFrameStore.from_host(VE.load_frame_store(ds.items, paths["generated_kps"], True), DEV)
+    samples = sample_all_windows_npz(ds)
+    idx = {it.path: i for i, it in enumerate(ds.items)}
+    feats = ops.featurize(store, VE._window_tensor(samples, idx, DEV), stats.mean, stats.std).cpu().numpy()
+    mean, std = stats.mean.cpu().numpy(), stats.std.cpu().numpy()
+    for wi, (it, s) in enumerate(samples):
+        c = load_clip(it, paths["generated_kps"], True)
+        ref = OF.featurize_window(c["pose"], c["global_orient"], c["betas"], c["vit"], c["keypoints"], s, None)
+        ref = (ref - mean) / (std + np.float32(1e-6))
+        err = np.abs(feats[wi] - ref).max()
+        assert err < 1e-4, (wi, it.name, s, err)
+
+
+def test_encoder_matches_reference(vg, real_setup, golden_flow):
+    VE, ops = vg
+    from vge.data import create_dataset_from_generated_meshes
+    paths, _, _, _, stats, model = real_setup
+    ds = create_dataset_from_generated_meshes(paths["generated_meshes"])
+    f = VE.extract_window_features(model, ds, paths["generated_kps"], stats, device=DEV, frame_embed=True)
+    seq = f["seq_embeds"].cpu().numpy()
+    fe = f["frame_embeds"].cpu().numpy()
+    assert np.abs(seq - golden_flow["seq_embeds"]).max() < 2e-5
+    assert np.abs(fe[:4] - golden_flow["frame_embeds_first4"]).max() < 2e-5
+
+
+def test_encoder_vs_oracle_random_batch(vg, golden_state_dict):
+    """Odd batch (last conv workgroup half empty), random z-scored input, vs the torch-fp32 oracle."""
+    VE, ops = vg
+    from oracle.encoder import OracleEncoder
+    from vge import synth
+    torch.manual_seed(0)
+    x = torch.randn(37, 32, 2596)
+    model = VE.load_model(golden_state_dict, device=DEV)
+    seq, fe, tcw = model.encode(x.to(DEV), frame_embed=True, tc=True)
+    o = OracleEncoder(golden_state_dict, synth.DIMS_RAW, synth.DIMS_DIFF)
+    rs, rf, _ = o.forward(x)
+    assert (seq.cpu() - rs).abs().max().item() < 2e-5
+    assert (fe.cpu() - rf).abs().max().item() < 2e-5
+    f = rf[:, 1:]
+    ref_tc = (f[:, 1:] - f[:, :-1]).pow(2).sum(-1).sqrt().mean(-1)
+    assert (tcw.cpu() - ref_tc).abs().max().item() < 1e-5
+    # the standalone TC kernel on the same frame embeddings
+    assert (ops.tc_windows(fe).cpu() - ref_tc).abs().max().item() < 1e-5
+
+
+def test_centroids_match_reference(vg, real_setup, golden_flow, golden_meta):
+    VE, ops = vg
+    paths, real_ds, train_ds, store, stats, model = real_setup
+    label_dict = {c: i for i, c in enumerate(sorted({it.cls for it in real_ds.items}))}
+    assert label_dict == golden_meta["label_dict"]
+    cents, ld, counts = VE.build_real_centroids(model, paths["real"], paths["real_kp"], stats, device=DEV,
+                                                train_items=train_ds.items, label_dict=label_dict, store=store)
+    assert np.array_equal(counts.cpu().numpy(), golden_flow["counts"])
+    assert np.abs(cents.cpu().numpy() - golden_flow["centroids"]).max() < 2e-5
+
+
+def test_video_scores_match_reference(vg, golden_dataset, golden_meta, tmp_path):
+    """The whole eval.py flow -> video_scores.json within 1e-4 of the reference."""
+    VE, ops = vg
+    paths, ckpt = golden_dataset
+    out = tmp_path / "video_scores.json"
+    combined = VE.run_eval(paths["generated_meshes"], paths["real"], ckpt, paths["generated_kps"], paths["real_kp"],
+                           out_json=str(out), device=DEV)
+    ref = golden_meta["video_scores"]
+    assert sorted(combined) == sorted(ref)
+    worst = 0.0
+    for v, e in ref.items():
+        assert set(e) == set(combined[v]), v          # "Testmodel" video: tc only, no ac
+        for k in e:
+            worst = max(worst, abs(e[k] - combined[v][k]))
+    assert worst < 1e-4, worst
+    import json
+    assert json.loads(out.read_text()) == combined
+
+
+def test_featurize_edge_cases_vs_oracle(vg):
+    """Static / all-invisible / partly invisible keypoints, start past the end, single-frame clip."""
+    VE, ops = vg
+    from oracle import featurize as OF
+    from vge import synth
+    from vge.data import pack_frame_store
+    rng = np.random.default_rng(5)
+    clips = []
+    base = synth.make_clip(11, 0, 40)
+    for variant in range(5):
+        c = synth.make_clip(11, variant, 40 if variant != 4 else 1)
+        kp = c.keypoints.copy()
+        if variant == 0:
+            kp = np.repeat(kp[:1], kp.shape[0], 0)        # static: H = X^T X
+        elif variant == 1:
+            kp[:] = -1.0                                  # all invisible: H = 0 -> R = I
+        elif variant == 2:
+            kp[3] = -1.0                                  # one fully invisible frame
+        clips.append({"pose": c.pose, "global_orient": c.global_orient, "betas": c.betas, "vit": c.vit,
+                      "keypoints": kp})
+    st = pack_frame_store(clips, [f"c{i}" for i in range(5)], ["X"] * 5)
+    store = ops.DeviceFrameStore.from_host(st, DEV)
+    wins = [(0, 0), (0, 8), (1, 0), (2, 0), (3, 8), (3, 39), (3, 100), (4, 0)]
+    w = torch.tensor(wins, dtype=torch.int32, device=DEV)
+    mean = torch.zeros(2596, device=DEV)
+    std = torch.full((2596,), 1.0 - 1e-6, device=DEV)
+    feats = ops.featurize(store, w, mean, std).cpu().numpy()
+    for k, (v, s) in enumerate(wins):
+        c = clips[v]
+        ref = OF.featurize_window(c["pose"], c["global_orient"], c["betas"], c["vit"], c["keypoints"], s, None)
+        ref = ref / (np.float32(1.0 - 1e-6) + np.float32(1e-6))
+        err = np.abs(feats[k] - ref).max()
+        assert err < 1e-4, (v, s, err)

@@ -1,0 +1,524 @@
+// C ABI of libvge.so (include/vge.h): argument checking, weight repacking into the MFMA panel layout,
+// workspace management and the launch sequences.  No exception crosses the ABI.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/vge.h"
+
+namespace vge {
+// launchers (vge_featurize.hip / vge_encoder.hip / vge_score.hip)
+hipError_t launch_featurize_tiles(const float*, const float*, const float*, const float*, const float*, const int*,
+                                  const void*, const int*, int, const float*, const float*, float*, hipStream_t);
+hipError_t launch_stats_colsum(const float*, const void*, int, int, int, double*, double*, hipStream_t);
+hipError_t launch_stats_finalize(const double*, long long, long long, float*, float*, hipStream_t);
+struct EncDescHost {
+  const float* stem; const float* conv; const float* proj; const float* gn_w; const float* gn_b;
+  int in_col, d_in, n_stem_panels, pad;
+};
+struct FuseParamsHost {
+  const float* kv_w; const float* kv_b; const float* u;
+  float inv_tau[8]; float bias[8]; int n_mod; int has_motion[8];
+};
+struct GemmArgsHost {
+  const float* A; int lda; const float* W; float* out; int ldo; int M, K, N;
+  const float* bias; const float* res; int ldr; const float* ln_w; const float* ln_b; const float* pe; const float* cls;
+};
+hipError_t encoder_kernel_setup();
+hipError_t launch_conv_encoders(const float*, int, const void*, int, float*, hipStream_t);
+hipError_t launch_fuse(const float*, int, const FuseParamsHost&, float*, hipStream_t);
+hipError_t launch_gemm(int, const GemmArgsHost&, hipStream_t);
+hipError_t launch_attn(const float*, int, float*, hipStream_t);
+hipError_t launch_embed_tc(const float*, int, float*, float*, float*, hipStream_t);
+hipError_t launch_centroid_accum(const float*, const int*, int, int, int, float*, float*, hipStream_t);
+hipError_t launch_centroid_final(const float*, const float*, int, int, float*, hipStream_t);
+hipError_t launch_tc_windows(const float*, int, int, int, float*, hipStream_t);
+hipError_t launch_score_videos(const float*, const float*, const int*, const int*, const float*, int, int, float*,
+                               double*, hipStream_t);
+enum { EPI_TOKENS = 0, EPI_BIAS = 1, EPI_BIAS_RELU = 2, EPI_BIAS_RES_LN = 3 };
+}  // namespace vge
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(expr)                                                                         \
+  do {                                                                                       \
+    hipError_t _e = (expr);                                                                  \
+    if (_e != hipSuccess) return fail(VGE_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+hipStream_t S(vge_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+const char* kMods[5] = {"vit", "global", "pose", "beta", "kp2d"};
+const int kDimsRaw[5] = {1024, 9, 207, 10, 120};
+const int kDimsDiff[5] = {1024, 3, 69, 10, 120};
+constexpr int CHUNK_F = 4096;
+
+size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+// Pack W[N][K] (row-major, K_real valid columns, row stride ldk) into [N/256][P][16][4096] chunks:
+// chunk(nb, p, c)[(g*256 + n)*4 + q] = W[nb*256 + n][p*256 + 64g + 4c + q]
+void pack_linear(const float* W, int N, int K_real, int ldk, int P, std::vector<float>& out) {
+  const size_t base = out.size();
+  out.resize(base + (size_t)(N / 256) * P * 16 * CHUNK_F, 0.f);
+  float* o = out.data() + base;
+  for (int nb = 0; nb < N / 256; ++nb)
+    for (int p = 0; p < P; ++p)
+      for (int c = 0; c < 16; ++c) {
+        float* ch = o + (((size_t)nb * P + p) * 16 + c) * CHUNK_F;
+        for (int g = 0; g < 4; ++g)
+          for (int n = 0; n < 256; ++n)
+            for (int q = 0; q < 4; ++q) {
+              const int k = p * 256 + 64 * g + 4 * c + q;
+              ch[(g * 256 + n) * 4 + q] = (k < K_real) ? W[(size_t)(nb * 256 + n) * ldk + k] : 0.f;
+            }
+      }
+}
+
+// Conv1d weight [256][256][5] -> 5 taps x 16 chunks: chunk(tap, c)[(g*256+n)*4+q] = W[n][64g+4c+q][tap]
+void pack_conv(const float* W, std::vector<float>& out) {
+  const size_t base = out.size();
+  out.resize(base + (size_t)5 * 16 * CHUNK_F, 0.f);
+  float* o = out.data() + base;
+  for (int tap = 0; tap < 5; ++tap)
+    for (int c = 0; c < 16; ++c) {
+      float* ch = o + ((size_t)tap * 16 + c) * CHUNK_F;
+      for (int g = 0; g < 4; ++g)
+        for (int n = 0; n < 256; ++n)
+          for (int q = 0; q < 4; ++q) {
+            const int ci = 64 * g + 4 * c + q;
+            ch[(g * 256 + n) * 4 + q] = W[((size_t)n * 256 + ci) * 5 + tap];
+          }
+    }
+}
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+};
+
+}  // namespace
+
+struct vge_encoder {
+  int n_layers = 4;
+  // weights
+  float* wbuf = nullptr;          // all packed weights (one allocation)
+  vge::EncDescHost* d_encs = nullptr;
+  vge::FuseParamsHost fuse{};
+  const float* Wov = nullptr;     // packed [1][1]
+  struct Layer {
+    const float *in_w, *in_b, *out_w, *out_b, *l1_w, *l1_b, *l2_w, *l2_b, *n1_w, *n1_b, *n2_w, *n2_b;
+  };
+  std::vector<Layer> layers;
+  const float* cls = nullptr;
+  const float* pe = nullptr;
+  // workspace
+  int cap = 0;
+  float* ws = nullptr;
+  float *enc_out = nullptr, *pooled = nullptr, *x = nullptr, *qkv = nullptr, *att = nullptr, *x1 = nullptr,
+        *h = nullptr;
+};
+
+extern "C" {
+
+const char* vge_last_error(void) { return g_err.c_str(); }
+const char* vge_version(void) { return "vge 0.1 (gfx950, f32 MFMA)"; }
+
+// ------------------------------------------------------------------ featurise
+int vge_featurize(const vge_frame_store* st, const int32_t* windows, int n_windows, const float* mean, const float* std_,
+                  float* feats, vge_stream_t stream) {
+  if (!st || !windows || !feats || n_windows < 0 || !mean || !std_) return fail(VGE_ERR_ARG, "vge_featurize: null argument");
+  HIPCHK(vge::launch_featurize_tiles(st->pose, st->gori, st->betas, st->vit, st->kp, st->videos, nullptr, windows,
+                                     n_windows, mean, std_, feats, S(stream)));
+  return VGE_OK;
+}
+
+// ------------------------------------------------------------------ stats
+static const int kColChunk = 64;  // tiles per column-sum partial
+
+size_t vge_stats_workspace_bytes(int ct) {
+  if (ct < 1) ct = 1;
+  const size_t nch = (ct + kColChunk - 1) / kColChunk;
+  return align_up((size_t)ct * 32, 256) + align_up((size_t)ct * 32 * VGE_FEAT_DIM * 4, 256) +
+         align_up(nch * 2 * VGE_FEAT_DIM * 8, 256);
+}
+
+int vge_stats_accumulate(const vge_frame_store* st, const int32_t* host_videos, const int32_t* sel, int n_sel,
+                         double* sums, int64_t* counts, void* workspace, size_t wsb, vge_stream_t stream) {
+  if (!st || !host_videos || (!sel && n_sel) || !sums || !counts || !workspace) return fail(VGE_ERR_ARG, "vge_stats_accumulate: null argument");
+  // largest chunk of tiles that fits the workspace
+  int ct = 1;
+  while (vge_stats_workspace_bytes(ct * 2) <= wsb && ct < (1 << 20)) ct *= 2;
+  while (vge_stats_workspace_bytes(ct + 1) <= wsb && ct < (1 << 20)) ++ct;
+  if (vge_stats_workspace_bytes(ct) > wsb) return fail(VGE_ERR_WORKSPACE, "vge_stats_accumulate: workspace too small");
+  char* w = static_cast<char*>(workspace);
+  int32_t* d_tiles = reinterpret_cast<int32_t*>(w);
+  float* d_feats = reinterpret_cast<float*>(w + align_up((size_t)ct * 32, 256));
+  double* d_part = reinterpret_cast<double*>(w + align_up((size_t)ct * 32, 256) + align_up((size_t)ct * 32 * VGE_FEAT_DIM * 4, 256));
+  std::vector<int32_t> tiles;
+  tiles.reserve((size_t)ct * 8);
+  auto flush = [&]() -> int {
+    const int n = (int)(tiles.size() / 8);
+    if (n == 0) return VGE_OK;
+    HIPCHK(hipMemcpyAsync(d_tiles, tiles.data(), tiles.size() * 4, hipMemcpyHostToDevice, S(stream)));
+    HIPCHK(vge::launch_featurize_tiles(st->pose, st->gori, st->betas, st->vit, st->kp, st->videos, d_tiles, nullptr, n,
+                                       nullptr, nullptr, d_feats, S(stream)));
+    const int nch = (n + kColChunk - 1) / kColChunk;
+    HIPCHK(vge::launch_stats_colsum(d_feats, d_tiles, n, kColChunk, nch, d_part, sums, S(stream)));
+    HIPCHK(hipStreamSynchronize(S(stream)));  // host tile buffer is reused
+    tiles.clear();
+    return VGE_OK;
+  };
+  for (int s = 0; s < n_sel; ++s) {
+    const int v = sel[s];
+    if (v < 0 || v >= st->n_videos) return fail(VGE_ERR_ARG, "vge_stats_accumulate: video index out of range");
+    const int T = host_videos[4 * v + 1], Tk = host_videos[4 * v + 3];
+    counts[0] += T;
+    counts[1] += Tk;
+    const int nt = (std::max(T, Tk) + 31) / 32;
+    for (int i = 0; i < nt; ++i) {
+      if ((int)(tiles.size() / 8) == ct) {
+        int r = flush();
+        if (r) return r;
+      }
+      const int out_row = (int)(tiles.size() / 8) * 32;
+      const int mc = std::min(32, std::max(0, T - 32 * i)), kc = std::min(32, std::max(0, Tk - 32 * i));
+      const int32_t td[8] = {v, 1, 32 * i, mc, 32 * i, kc, out_row, 0};
+      tiles.insert(tiles.end(), td, td + 8);
+    }
+  }
+  return flush();
+}
+
+int vge_stats_finalize(const double* sums, const int64_t* counts, float* mean, float* std_, vge_stream_t stream) {
+  if (!sums || !counts || !mean || !std_) return fail(VGE_ERR_ARG, "vge_stats_finalize: null argument");
+  HIPCHK(vge::launch_stats_finalize(sums, counts[0], counts[1], mean, std_, S(stream)));
+  return VGE_OK;
+}
+
+// ------------------------------------------------------------------ encoder
+int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int n_weights, vge_dtype compute,
+                       vge_encoder** out) {
+  if (!dims || !weights || !out) return fail(VGE_ERR_ARG, "vge_encoder_create: null argument");
+  *out = nullptr;
+  if (compute != VGE_F32) return fail(VGE_ERR_ARG, "vge_encoder_create: unsupported compute dtype");
+  if (dims->n_modalities != 5 || dims->d_model != 256 || dims->time_heads != 8 || dims->clip_len != 32 ||
+      dims->time_layers < 1)
+    return fail(VGE_ERR_ARG, "vge_encoder_create: kernels are built for 5 modalities, d_model 256, 8 heads, clip 32");
+  for (int m = 0; m < 5; ++m)
+    if (dims->dims_raw[m] != kDimsRaw[m] || dims->dims_diff[m] != kDimsDiff[m])
+      return fail(VGE_ERR_ARG, std::string("vge_encoder_create: unsupported dims for modality ") + kMods[m]);
+
+  std::unordered_map<std::string, const vge_tensor_view*> wm;
+  for (int i = 0; i < n_weights; ++i)
+    if (weights[i].name) wm[weights[i].name] = &weights[i];
+  std::string err;
+  auto get = [&](const std::string& k, std::initializer_list<int64_t> shape) -> const float* {
+    auto it = wm.find(k);
+    if (it == wm.end()) {
+      if (err.empty()) err = "missing weight: " + k;
+      return nullptr;
+    }
+    const vge_tensor_view* t = it->second;
+    int i = 0;
+    bool ok = t->ndim == (int)shape.size() && t->data != nullptr;
+    for (int64_t s : shape) ok = ok && i < t->ndim && t->shape[i++] == s;
+    if (!ok && err.empty()) err = "bad shape for weight: " + k;
+    return ok ? t->data : nullptr;
+  };
+
+  const int L = dims->time_layers;
+  std::vector<float> pk;  // packed device image (floats), offsets recorded below
+  struct Off { size_t stem, conv, proj, gnw, gnb; int in_col, d_in, P; };
+  std::vector<Off> eoff(10);
+  int col_raw = 0, col_diff = VGE_RAW_DIM;
+  for (int kind = 0; kind < 2; ++kind) {
+    for (int m = 0; m < 5; ++m) {
+      const int e = kind * 5 + m;
+      const std::string pre = std::string(kind == 0 ? "state_enc." : "motion_enc.") + kMods[m];
+      const int d_in = kind == 0 ? kDimsRaw[m] : kDimsDiff[m];
+      Off& o = eoff[e];
+      o.d_in = d_in;
+      o.P = (d_in + 255) / 256;
+      o.in_col = kind == 0 ? col_raw : col_diff;
+      if (kind == 0) col_raw += d_in; else col_diff += d_in;
+      const float* stem = get(pre + ".stem.weight", {256, d_in, 1});
+      o.stem = pk.size();
+      if (stem) pack_linear(stem, 256, d_in, d_in, o.P, pk);
+      o.conv = pk.size();
+      for (int b = 0; b < 4; ++b)
+        for (int cv = 1; cv <= 2; ++cv) {
+          const float* w = get(pre + ".blocks." + std::to_string(b) + ".conv" + std::to_string(cv) + ".weight", {256, 256, 5});
+          if (w) pack_conv(w, pk);
+        }
+      const float* proj = get(pre + ".proj.weight", {256, 256});
+      o.proj = pk.size();
+      if (proj) pack_linear(proj, 256, 256, 256, 1, pk);
+      o.gnw = pk.size();
+      for (int b = 0; b < 4; ++b) {
+        const float* w = get(pre + ".blocks." + std::to_string(b) + ".norm.weight", {256});
+        if (w) pk.insert(pk.end(), w, w + 256);
+      }
+      o.gnb = pk.size();
+      for (int b = 0; b < 4; ++b) {
+        const float* w = get(pre + ".blocks." + std::to_string(b) + ".norm.bias", {256});
+        if (w) pk.insert(pk.end(), w, w + 256);
+      }
+      if (!err.empty()) return fail(err.rfind("missing", 0) == 0 ? VGE_ERR_MISSING_WEIGHT : VGE_ERR_WEIGHT_SHAPE, err);
+    }
+  }
+  // fusion: fold the constant query  u = Wk^T (Wq q_ln(latent)),  Wov = Wo Wv
+  const float* latent = get("fusion.latent", {1, 1, 256});
+  const float* qw = get("fusion.q_ln.weight", {256});
+  const float* qb = get("fusion.q_ln.bias", {256});
+  const float* kvw = get("fusion.kv_ln.weight", {256});
+  const float* kvb = get("fusion.kv_ln.bias", {256});
+  const float* Wq = get("fusion.Wq.weight", {256, 256});
+  const float* Wk = get("fusion.Wk.weight", {256, 256});
+  const float* Wv = get("fusion.Wv.weight", {256, 256});
+  const float* Wo = get("fusion.Wo.weight", {256, 256});
+  const float* ltemp = get("fusion.logit_temp", {5});
+  const float* lbias = get("fusion.logit_bias", {5});
+  const float* cls = get("cls", {1, 1, 256});
+  auto pe_it = wm.find("pos_enc.pe");
+  if (pe_it == wm.end() && err.empty()) err = "missing weight: pos_enc.pe";
+  const float* pe = nullptr;
+  if (pe_it != wm.end()) {
+    const vge_tensor_view* t = pe_it->second;
+    if (t->ndim == 3 && t->shape[0] == 1 && t->shape[1] >= 33 && t->shape[2] == 256 && t->data) pe = t->data;
+    else if (err.empty()) err = "bad shape for weight: pos_enc.pe";
+  }
+  if (!err.empty()) return fail(err.rfind("missing", 0) == 0 ? VGE_ERR_MISSING_WEIGHT : VGE_ERR_WEIGHT_SHAPE, err);
+
+  std::vector<double> q(256), Q(256);
+  {
+    double mu = 0, var = 0;
+    for (int i = 0; i < 256; ++i) mu += latent[i];
+    mu /= 256;
+    for (int i = 0; i < 256; ++i) var += (latent[i] - mu) * (latent[i] - mu);
+    var /= 256;
+    const double rstd = 1.0 / std::sqrt(var + 1e-5);
+    for (int i = 0; i < 256; ++i) q[i] = (latent[i] - mu) * rstd * qw[i] + qb[i];
+    for (int j = 0; j < 256; ++j) {
+      double a = 0;
+      for (int i = 0; i < 256; ++i) a += q[i] * Wq[(size_t)j * 256 + i];
+      Q[j] = a;
+    }
+  }
+  const size_t off_u = pk.size();
+  for (int i = 0; i < 256; ++i) {
+    double a = 0;
+    for (int j = 0; j < 256; ++j) a += Q[j] * Wk[(size_t)j * 256 + i];
+    pk.push_back((float)a);
+  }
+  const size_t off_kvw = pk.size();
+  pk.insert(pk.end(), kvw, kvw + 256);
+  const size_t off_kvb = pk.size();
+  pk.insert(pk.end(), kvb, kvb + 256);
+  std::vector<float> wov(256 * 256);
+  for (int i = 0; i < 256; ++i)
+    for (int j = 0; j < 256; ++j) {
+      double a = 0;
+      for (int k = 0; k < 256; ++k) a += (double)Wo[(size_t)i * 256 + k] * Wv[(size_t)k * 256 + j];
+      wov[(size_t)i * 256 + j] = (float)a;
+    }
+  const size_t off_wov = pk.size();
+  pack_linear(wov.data(), 256, 256, 256, 1, pk);
+  const size_t off_cls = pk.size();
+  pk.insert(pk.end(), cls, cls + 256);
+  const size_t off_pe = pk.size();
+  pk.insert(pk.end(), pe, pe + 33 * 256);
+
+  struct LOff { size_t in_w, in_b, out_w, out_b, l1_w, l1_b, l2_w, l2_b, n1_w, n1_b, n2_w, n2_b; };
+  std::vector<LOff> loff(L);
+  for (int l = 0; l < L; ++l) {
+    const std::string p = "temporal.layers." + std::to_string(l);
+    const float* inw = get(p + ".self_attn.in_proj_weight", {768, 256});
+    const float* inb = get(p + ".self_attn.in_proj_bias", {768});
+    const float* ow = get(p + ".self_attn.out_proj.weight", {256, 256});
+    const float* ob = get(p + ".self_attn.out_proj.bias", {256});
+    const float* l1w = get(p + ".linear1.weight", {1024, 256});
+    const float* l1b = get(p + ".linear1.bias", {1024});
+    const float* l2w = get(p + ".linear2.weight", {256, 1024});
+    const float* l2b = get(p + ".linear2.bias", {256});
+    const float* n1w = get(p + ".norm1.weight", {256});
+    const float* n1b = get(p + ".norm1.bias", {256});
+    const float* n2w = get(p + ".norm2.weight", {256});
+    const float* n2b = get(p + ".norm2.bias", {256});
+    if (!err.empty()) return fail(err.rfind("missing", 0) == 0 ? VGE_ERR_MISSING_WEIGHT : VGE_ERR_WEIGHT_SHAPE, err);
+    LOff& o = loff[l];
+    o.in_w = pk.size(); pack_linear(inw, 768, 256, 256, 1, pk);
+    o.out_w = pk.size(); pack_linear(ow, 256, 256, 256, 1, pk);
+    o.l1_w = pk.size(); pack_linear(l1w, 1024, 256, 256, 1, pk);
+    o.l2_w = pk.size(); pack_linear(l2w, 256, 1024, 1024, 4, pk);
+    o.in_b = pk.size(); pk.insert(pk.end(), inb, inb + 768);
+    o.out_b = pk.size(); pk.insert(pk.end(), ob, ob + 256);
+    o.l1_b = pk.size(); pk.insert(pk.end(), l1b, l1b + 1024);
+    o.l2_b = pk.size(); pk.insert(pk.end(), l2b, l2b + 256);
+    o.n1_w = pk.size(); pk.insert(pk.end(), n1w, n1w + 256);
+    o.n1_b = pk.size(); pk.insert(pk.end(), n1b, n1b + 256);
+    o.n2_w = pk.size(); pk.insert(pk.end(), n2w, n2w + 256);
+    o.n2_b = pk.size(); pk.insert(pk.end(), n2b, n2b + 256);
+  }
+
+  vge_encoder* enc = new vge_encoder();
+  enc->n_layers = L;
+  hipError_t he = vge::encoder_kernel_setup();
+  if (he == hipSuccess) he = hipMalloc(&enc->wbuf, pk.size() * sizeof(float));
+  if (he == hipSuccess) he = hipMemcpy(enc->wbuf, pk.data(), pk.size() * sizeof(float), hipMemcpyHostToDevice);
+  if (he != hipSuccess) {
+    vge_encoder_destroy(enc);
+    return fail(VGE_ERR_HIP, std::string("vge_encoder_create: ") + hipGetErrorString(he));
+  }
+  float* wb = enc->wbuf;
+  std::vector<vge::EncDescHost> descs(10);
+  for (int e = 0; e < 10; ++e) {
+    descs[e] = vge::EncDescHost{wb + eoff[e].stem, wb + eoff[e].conv, wb + eoff[e].proj, wb + eoff[e].gnw,
+                                wb + eoff[e].gnb, eoff[e].in_col, eoff[e].d_in, eoff[e].P, 0};
+  }
+  he = hipMalloc(&enc->d_encs, sizeof(vge::EncDescHost) * 10);
+  if (he == hipSuccess) he = hipMemcpy(enc->d_encs, descs.data(), sizeof(vge::EncDescHost) * 10, hipMemcpyHostToDevice);
+  if (he != hipSuccess) {
+    vge_encoder_destroy(enc);
+    return fail(VGE_ERR_HIP, std::string("vge_encoder_create: ") + hipGetErrorString(he));
+  }
+  enc->fuse.kv_w = wb + off_kvw;
+  enc->fuse.kv_b = wb + off_kvb;
+  enc->fuse.u = wb + off_u;
+  enc->fuse.n_mod = 5;
+  for (int m = 0; m < 5; ++m) {
+    const float x = ltemp[m];
+    const float sp = x > 20.0f ? x : log1pf(expf(x));  // F.softplus (beta 1, threshold 20)
+    enc->fuse.inv_tau[m] = 1.0f / (sp + 1e-3f);
+    enc->fuse.bias[m] = lbias[m];
+    enc->fuse.has_motion[m] = 1;
+  }
+  enc->Wov = wb + off_wov;
+  enc->cls = wb + off_cls;
+  enc->pe = wb + off_pe;
+  enc->layers.resize(L);
+  for (int l = 0; l < L; ++l) {
+    const LOff& o = loff[l];
+    enc->layers[l] = vge_encoder::Layer{wb + o.in_w, wb + o.in_b, wb + o.out_w, wb + o.out_b, wb + o.l1_w, wb + o.l1_b,
+                                        wb + o.l2_w, wb + o.l2_b, wb + o.n1_w, wb + o.n1_b, wb + o.n2_w, wb + o.n2_b};
+  }
+  *out = enc;
+  return VGE_OK;
+}
+
+int vge_encoder_reserve(vge_encoder* enc, int B) {
+  if (!enc || B < 1) return fail(VGE_ERR_ARG, "vge_encoder_reserve: bad argument");
+  if (B <= enc->cap) return VGE_OK;
+  if (enc->ws) {
+    (void)hipFree(enc->ws);
+    enc->ws = nullptr;
+    enc->cap = 0;
+  }
+  const size_t frames = (size_t)B * 32, tok = align_up((size_t)B * 33, 32);
+  const size_t n_enc_out = 10 * frames * 256, n_pooled = frames * 256, n_x = tok * 256, n_qkv = tok * 768,
+               n_att = tok * 256, n_x1 = tok * 256, n_h = tok * 1024;
+  const size_t total = n_enc_out + n_pooled + n_x + n_qkv + n_att + n_x1 + n_h;
+  hipError_t he = hipMalloc(&enc->ws, total * sizeof(float));
+  if (he == hipSuccess) he = hipMemset(enc->ws, 0, total * sizeof(float));
+  if (he != hipSuccess) return fail(VGE_ERR_NOMEM, std::string("vge_encoder_reserve: ") + hipGetErrorString(he));
+  float* p = enc->ws;
+  enc->enc_out = p; p += n_enc_out;
+  enc->pooled = p; p += n_pooled;
+  enc->x = p; p += n_x;
+  enc->qkv = p; p += n_qkv;
+  enc->att = p; p += n_att;
+  enc->x1 = p; p += n_x1;
+  enc->h = p;
+  enc->cap = B;
+  return VGE_OK;
+}
+
+int vge_encoder_destroy(vge_encoder* enc) {
+  if (!enc) return VGE_OK;
+  if (enc->ws) (void)hipFree(enc->ws);
+  if (enc->d_encs) (void)hipFree(enc->d_encs);
+  if (enc->wbuf) (void)hipFree(enc->wbuf);
+  delete enc;
+  return VGE_OK;
+}
+
+int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_embed, float* frame_embed, float* tc_window,
+               vge_stream_t stream) {
+  if (!enc || !feats || !seq_embed) return fail(VGE_ERR_ARG, "vge_encode: null argument");
+  if (T != 32) return fail(VGE_ERR_ARG, "vge_encode: clip_len must be 32");
+  if (B <= 0) return VGE_OK;
+  if (B > enc->cap) return fail(VGE_ERR_WORKSPACE, "vge_encode: call vge_encoder_reserve(B) first");
+  hipStream_t s = S(stream);
+  const int frames = B * 32, M = B * 33;
+  HIPCHK(vge::launch_conv_encoders(feats, B, enc->d_encs, 10, enc->enc_out, s));
+  HIPCHK(vge::launch_fuse(enc->enc_out, frames, enc->fuse, enc->pooled, s));
+  vge::GemmArgsHost g{};
+  g.A = enc->pooled; g.lda = 256; g.W = enc->Wov; g.out = enc->x; g.ldo = 256; g.M = frames; g.K = 256; g.N = 256;
+  g.pe = enc->pe; g.cls = enc->cls;
+  HIPCHK(vge::launch_gemm(vge::EPI_TOKENS, g, s));
+  for (int l = 0; l < enc->n_layers; ++l) {
+    const vge_encoder::Layer& Ly = enc->layers[l];
+    vge::GemmArgsHost a{};
+    a.A = enc->x; a.lda = 256; a.W = Ly.in_w; a.out = enc->qkv; a.ldo = 768; a.M = M; a.K = 256; a.N = 768; a.bias = Ly.in_b;
+    HIPCHK(vge::launch_gemm(vge::EPI_BIAS, a, s));
+    HIPCHK(vge::launch_attn(enc->qkv, B, enc->att, s));
+    vge::GemmArgsHost o{};
+    o.A = enc->att; o.lda = 256; o.W = Ly.out_w; o.out = enc->x1; o.ldo = 256; o.M = M; o.K = 256; o.N = 256;
+    o.bias = Ly.out_b; o.res = enc->x; o.ldr = 256; o.ln_w = Ly.n1_w; o.ln_b = Ly.n1_b;
+    HIPCHK(vge::launch_gemm(vge::EPI_BIAS_RES_LN, o, s));
+    vge::GemmArgsHost f1{};
+    f1.A = enc->x1; f1.lda = 256; f1.W = Ly.l1_w; f1.out = enc->h; f1.ldo = 1024; f1.M = M; f1.K = 256; f1.N = 1024;
+    f1.bias = Ly.l1_b;
+    HIPCHK(vge::launch_gemm(vge::EPI_BIAS_RELU, f1, s));
+    vge::GemmArgsHost f2{};
+    f2.A = enc->h; f2.lda = 1024; f2.W = Ly.l2_w; f2.out = enc->x; f2.ldo = 256; f2.M = M; f2.K = 1024; f2.N = 256;
+    f2.bias = Ly.l2_b; f2.res = enc->x1; f2.ldr = 256; f2.ln_w = Ly.n2_w; f2.ln_b = Ly.n2_b;
+    HIPCHK(vge::launch_gemm(vge::EPI_BIAS_RES_LN, f2, s));
+  }
+  HIPCHK(vge::launch_embed_tc(enc->x, B, seq_embed, frame_embed, tc_window, s));
+  return VGE_OK;
+}
+
+// ------------------------------------------------------------------ metrics / centroids
+int vge_tc_windows(const float* fe, int B, int T1, int d, float* tc, vge_stream_t stream) {
+  if (!fe || !tc || B < 0 || T1 < 1 || d < 1) return fail(VGE_ERR_ARG, "vge_tc_windows: bad argument");
+  if (B == 0) return VGE_OK;
+  HIPCHK(vge::launch_tc_windows(fe, B, T1, d, tc, S(stream)));
+  return VGE_OK;
+}
+
+int vge_score_videos(const float* seq, const float* tcw, const int32_t* first, const int32_t* vcls, const float* cent, int V,
+                     int d, float* ac, double* tc, vge_stream_t stream) {
+  if (!seq || !tcw || !first || !vcls || !ac || !tc || V < 0 || d < 1 || d > 256)
+    return fail(VGE_ERR_ARG, "vge_score_videos: bad argument");
+  if (V == 0) return VGE_OK;
+  HIPCHK(vge::launch_score_videos(seq, tcw, first, vcls, cent, V, d, ac, tc, S(stream)));
+  return VGE_OK;
+}
+
+int vge_centroid_accumulate(const float* seq, const int32_t* cls, int n, int C, int d, float* sums, float* counts,
+                            vge_stream_t stream) {
+  if (!seq || !cls || !sums || !counts || n < 0 || C < 1 || d < 1) return fail(VGE_ERR_ARG, "vge_centroid_accumulate: bad argument");
+  if (n == 0) return VGE_OK;
+  HIPCHK(vge::launch_centroid_accum(seq, cls, n, C, d, sums, counts, S(stream)));
+  return VGE_OK;
+}
+
+int vge_centroid_finalize(const float* sums, const float* counts, int C, int d, float* cent, vge_stream_t stream) {
+  if (!sums || !counts || !cent || C < 1 || d < 1 || d > 256) return fail(VGE_ERR_ARG, "vge_centroid_finalize: bad argument");
+  HIPCHK(vge::launch_centroid_final(sums, counts, C, d, cent, S(stream)));
+  return VGE_OK;
+}
+
+}  // extern "C"

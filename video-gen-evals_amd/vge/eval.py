@@ -1,0 +1,304 @@
+"""The scoring driver: eval.py's flow (reference eval.py:350-466) on libvge.
+
+Same function names, argument meaning and outputs as the reference:
+  load_model                          eval.py:136-165   (torch.load(weights_only=True); plain state_dict or
+                                                         {model_state_dict|state_dict, d_model, ...}; a missing
+                                                         key is an error here -- see INTEGRATION.md)
+  compute_stats_from_npz              utils.py:595-801  (HIP featurise in stats mode + float64 column sums)
+  build_real_centroids                eval.py:260-286   (+ build_train_centroids_subset utils.py:1018-1045)
+  extract_window_features             eval.py:168-206
+  compute_action_consistency_scores   eval.py:229-257
+  compute_temporal_coherence_scores   eval.py:209-226
+  compute_spearman_correlation        eval.py:297-347
+  run_eval                            eval.py:350-454 (writes video_scores.json)
+Per-frame features are decoded on the host (npz/zlib) into a frame store that lives in HBM; every
+numeric step after that runs in the HIP kernels of libvge.so.
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+from collections import defaultdict
+from concurrent.futures import ThreadPoolExecutor
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import ops
+from .data import (ACTION_CLASSES, FrameStore, NpzVideoDataset, VideoItem, _canonicalize_class,
+                   create_dataset_from_generated_meshes, enumerate_test_windows, load_clip, pack_frame_store,
+                   sample_all_windows_npz, train_test_split)
+
+
+# ----------------------------------------------------------------------------- loading
+
+def load_frame_store(items: Sequence[VideoItem], keypoint_dir: Optional[str], require_kp: bool,
+                     workers: int = 8) -> FrameStore:
+    """Decode the npz + keypoints.npy of `items` (thread pool: zlib releases the GIL) and pack them."""
+    with ThreadPoolExecutor(max_workers=max(1, workers)) as ex:
+        clips = list(ex.map(lambda it: load_clip(it, keypoint_dir, require_kp), items))
+    return pack_frame_store(clips, [it.name for it in items], [it.cls for it in items])
+
+
+class ModalityStatsGPU:
+    """mean/std [2596] f32 on device (feats column order) + the float64 sufficient statistics."""
+
+    def __init__(self, mean, std, sums, counts):
+        self.mean, self.std, self.sums, self.counts = mean, std, sums, counts
+
+
+def compute_stats_from_npz(train_items: Sequence[VideoItem], keypoint_dir: str, device="cuda",
+                           store: Optional[ops.DeviceFrameStore] = None, reduce_fn=None) -> ModalityStatsGPU:
+    """utils.py:595-801.  `reduce_fn(sums, counts)` (optional) all-reduces the sufficient statistics
+    across ranks before finalising (sharded real set)."""
+    assert len(train_items) > 0, "compute_stats_from_npz: train_items is empty"
+    if store is None:
+        store = ops.DeviceFrameStore.from_host(load_frame_store(train_items, keypoint_dir, require_kp=False), device)
+    sums = torch.zeros((2, ops.FEAT_DIM), device=device, dtype=torch.float64)
+    counts = np.zeros(2, np.int64)
+    ops.stats_accumulate(store, range(store.n_videos), sums, counts)
+    if reduce_fn is not None:
+        sums, counts = reduce_fn(sums, counts)
+    mean, std = ops.stats_finalize(sums, counts)
+    return ModalityStatsGPU(mean, std, sums, counts)
+
+
+def _load_state_dict(model_path: str):
+    ck = torch.load(model_path, map_location="cpu", weights_only=True)
+    hp = {"d_model": 256, "latent_dim": 128, "time_layers": 4, "time_heads": 8, "dropout": 0.1}
+    if isinstance(ck, dict):
+        for k in hp:
+            if k in ck and not isinstance(ck[k], torch.Tensor):
+                hp[k] = ck[k]
+    if isinstance(ck, dict) and "model_state_dict" in ck:
+        sd = ck["model_state_dict"]
+    elif isinstance(ck, dict) and "state_dict" in ck:
+        sd = ck["state_dict"]
+    else:
+        sd = ck
+    sd = {k: v.detach().float().cpu().numpy() for k, v in sd.items() if isinstance(v, torch.Tensor)}
+    return sd, hp
+
+
+def load_model(model_path, dims_map_raw=None, dims_map_diff=None, device="cuda") -> ops.Encoder:
+    """eval.py:136-165 -> a libvge encoder handle (weights repacked into HBM)."""
+    if dims_map_raw is not None:
+        if tuple(dims_map_raw.values()) != ops.DIMS_RAW or tuple(dims_map_diff.values()) != ops.DIMS_DIFF:
+            raise ValueError(f"unsupported modality dims {dims_map_raw} / {dims_map_diff}")
+    if isinstance(model_path, dict):
+        sd, hp = model_path, {"d_model": 256, "time_layers": 4, "time_heads": 8}
+    else:
+        sd, hp = _load_state_dict(model_path)
+    return ops.Encoder(sd, time_layers=int(hp["time_layers"]), time_heads=int(hp["time_heads"]),
+                       d_model=int(hp["d_model"]), device=device)
+
+
+def infer_dims_from_stats(stats) -> Tuple[Dict[str, int], Dict[str, int]]:
+    return dict(zip(ops.MODALITIES, ops.DIMS_RAW)), dict(zip(ops.MODALITIES, ops.DIMS_DIFF))
+
+
+# ----------------------------------------------------------------------------- windows -> embeddings
+
+def _window_tensor(samples, name_to_idx, device):
+    w = np.array([[name_to_idx[it.path], s] for it, s in samples], np.int32).reshape(-1, 2)
+    return torch.from_numpy(w).to(device)
+
+
+def encode_windows(model: ops.Encoder, store: ops.DeviceFrameStore, windows: torch.Tensor, stats: ModalityStatsGPU,
+                   batch: int = 1024, frame_embed: bool = False):
+    """featurise + encode windows in batches; returns (seq [N,256], frame [N,33,256] | None, tc [N])."""
+    n = int(windows.shape[0])
+    dev = windows.device
+    seq = torch.empty((n, ops.D_MODEL), device=dev)
+    tcw = torch.empty((n,), device=dev)
+    fe = torch.empty((n, 33, ops.D_MODEL), device=dev) if frame_embed else None
+    model.reserve(min(batch, max(n, 1)))
+    feats = torch.empty((min(batch, max(n, 1)), 32, ops.FEAT_DIM), device=dev)
+    for b0 in range(0, n, batch):
+        b1 = min(n, b0 + batch)
+        f = ops.featurize(store, windows[b0:b1], stats.mean, stats.std, out=feats[: b1 - b0])
+        s, fr, t = model.encode(f, frame_embed=frame_embed, tc=True)
+        seq[b0:b1] = s
+        tcw[b0:b1] = t
+        if frame_embed:
+            fe[b0:b1] = fr
+    return seq, fe, tcw
+
+
+def build_real_centroids(model: ops.Encoder, real_meshes_dir: str, real_kp_dir: str, stats: ModalityStatsGPU,
+                         clip_len: int = 32, stride: int = 8, device="cuda", train_items=None, label_dict=None,
+                         store: Optional[ops.DeviceFrameStore] = None, reduce_fn=None):
+    """eval.py:260-286 / utils.py:1018-1045 -> (centroids [C,256] device, label_dict, counts)."""
+    if train_items is None or label_dict is None:
+        real_ds = NpzVideoDataset(real_meshes_dir, filter_classes=ACTION_CLASSES)
+        train_ds, _ = train_test_split(real_ds, train_ratio=0.8, seed=1337)
+        train_items = train_ds.items
+        label_dict = {cls: i for i, cls in enumerate(sorted({it.cls for it in real_ds.items}))}
+    C_ = len(label_dict)
+    sums = torch.zeros((C_, ops.D_MODEL), device=device)
+    counts = torch.zeros((C_,), device=device)
+    if len(train_items):
+        samples = enumerate_test_windows(NpzVideoDataset("", items=list(train_items)), clip_len, stride)
+        if store is None:
+            store = ops.DeviceFrameStore.from_host(load_frame_store(train_items, real_kp_dir, require_kp=True), device)
+        idx = {it.path: i for i, it in enumerate(train_items)}
+        win = _window_tensor(samples, idx, device)
+        seq, _, _ = encode_windows(model, store, win, stats)
+        y = torch.as_tensor([label_dict[it.cls] for it, _ in samples], dtype=torch.int32, device=device)
+        ops.centroid_accumulate(seq, y, sums, counts)
+    if reduce_fn is not None:
+        sums, counts = reduce_fn(sums, counts)
+    return ops.centroid_finalize(sums, counts), label_dict, counts
+
+
+def extract_window_features(model: ops.Encoder, dataset: NpzVideoDataset, keypoint_dir: str, stats: ModalityStatsGPU,
+                            clip_len: int = 32, stride: int = 8, device="cuda", frame_embed: bool = False,
+                            store: Optional[ops.DeviceFrameStore] = None):
+    """eval.py:168-206 over all windows of `dataset` (sample_all_windows_npz order)."""
+    samples = sample_all_windows_npz(dataset, clip_len, stride)
+    if store is None:
+        store = ops.DeviceFrameStore.from_host(load_frame_store(dataset.items, keypoint_dir, require_kp=True), device)
+    idx = {it.path: i for i, it in enumerate(dataset.items)}
+    win = _window_tensor(samples, idx, device)
+    seq, fe, tcw = encode_windows(model, store, win, stats, frame_embed=frame_embed)
+    return {"seq_embeds": seq, "frame_embeds": fe, "tc_window": tcw,
+            "cls_names": [it.cls for it, _ in samples], "vid_names": [it.name for it, _ in samples]}
+
+
+# ----------------------------------------------------------------------------- metrics
+
+def _video_index(features):
+    vids, first = [], []
+    for i, v in enumerate(features["vid_names"]):
+        vid = os.path.splitext(v)[0]
+        if not vids or vids[-1] != vid:
+            vids.append(vid)
+            first.append(i)
+    first.append(len(features["vid_names"]))
+    return vids, first
+
+
+def _score(features, centroids, label_dict):
+    if "_scores" in features:
+        return features["_scores"]
+    dev = features["seq_embeds"].device
+    vids, first = _video_index(features)
+    if len(set(vids)) != len(vids):
+        raise ValueError("windows of one video must be contiguous (sample_all_windows_npz order)")
+    vcls = []
+    for k in range(len(vids)):
+        c = _canonicalize_class(features["cls_names"][first[k]])
+        vcls.append(label_dict[c] if (label_dict is not None and c in label_dict and
+                                      centroids is not None and label_dict[c] < len(centroids)) else -1)
+    tcw = features["tc_window"]
+    if tcw is None:
+        tcw = ops.tc_windows(features["frame_embeds"])
+    ac, tc = ops.score_videos(features["seq_embeds"], tcw,
+                              torch.as_tensor(first, dtype=torch.int32, device=dev),
+                              torch.as_tensor(vcls, dtype=torch.int32, device=dev), centroids)
+    ac = ac.cpu().numpy()
+    tc = tc.cpu().numpy()
+    features["_scores"] = (vids, vcls, ac, tc)
+    return features["_scores"]
+
+
+def compute_action_consistency_scores(features, centroids, label_dict) -> Dict[str, float]:
+    vids, vcls, ac, _ = _score(features, centroids, label_dict)
+    return {v: float(ac[k]) for k, v in enumerate(vids) if vcls[k] >= 0}
+
+
+def compute_temporal_coherence_scores(features, centroids=None, label_dict=None) -> Dict[str, float]:
+    vids, _, _, tc = _score(features, centroids, label_dict)
+    return {v: float(tc[k]) for k, v in enumerate(vids)}
+
+
+def combine_scores(ac: Dict[str, float], tc: Dict[str, float]) -> Dict[str, dict]:
+    out = {}
+    for v in sorted(set(ac) | set(tc)):
+        e = {}
+        if v in ac:
+            e["ac"] = ac[v]
+        if v in tc:
+            e["tc"] = tc[v]
+        out[v] = e
+    return out
+
+
+def _norm_name(name: str) -> str:
+    stem = os.path.splitext(os.path.basename(name))[0]
+    return stem.replace("_videos_", "_").replace("videos_", "").replace("_video_", "_")
+
+
+def compute_spearman_correlation(model_scores: dict, human_scores_path: str, human_key: str):
+    """eval.py:297-347 (sign-inverted Spearman; exact then suffix name matching)."""
+    from scipy.stats import spearmanr
+    with open(human_scores_path) as f:
+        human = json.load(f)
+    by_name = {_norm_name(k): v for k, v in model_scores.items()}
+    mv, hv, matched = [], [], []
+    for hname, hdata in human.items():
+        if human_key not in hdata:
+            continue
+        hn = _norm_name(hname)
+        if hn in by_name:
+            mv.append(by_name[hn])
+            hv.append(hdata[human_key])
+            matched.append((hn, hname))
+            continue
+        hp = hn.split("_")
+        for mn, ms in by_name.items():
+            mp = mn.split("_")
+            if len(mp) >= 2 and len(hp) >= 2 and (mp[-2:] == hp[-2:] or mp[-1] == hp[-1]):
+                mv.append(ms)
+                hv.append(hdata[human_key])
+                matched.append((mn, hname))
+                break
+    if len(mv) < 2:
+        print(f"Warning: Only {len(mv)} matched videos for {human_key}. Need at least 2.")
+        return None, None, matched
+    corr, p = spearmanr(np.array(mv), np.array(hv))
+    if corr is not None and not np.isnan(corr):
+        corr = -float(corr)
+    return corr, p, matched
+
+
+def run_eval(generated_meshes_dir: str, real_meshes_dir: str, model_path, keypoint_dir: str, real_kp_dir: str,
+             human_scores_path: Optional[str] = None, clip_len: int = 32, stride: int = 8,
+             out_json: Optional[str] = "video_scores.json", device="cuda", timings: Optional[dict] = None):
+    """eval.py __main__ (350-466) on one GPU; returns the combined {video: {ac, tc}} dict."""
+    t0 = time.perf_counter()
+    real_ds = NpzVideoDataset(real_meshes_dir, filter_classes=ACTION_CLASSES)
+    train_ds, _ = train_test_split(real_ds, train_ratio=0.8, seed=1337)
+    real_store = ops.DeviceFrameStore.from_host(load_frame_store(train_ds.items, real_kp_dir, require_kp=False), device)
+    stats = compute_stats_from_npz(train_ds.items, real_kp_dir, device=device, store=real_store)
+    dims_raw, dims_diff = infer_dims_from_stats(stats)
+    model = load_model(model_path, dims_raw, dims_diff, device=device)
+    t1 = time.perf_counter()
+    label_dict = {cls: i for i, cls in enumerate(sorted({it.cls for it in real_ds.items}))}
+    # centroids need every real-train keypoint file (WindowDataset raises otherwise)
+    for i, it in enumerate(train_ds.items):
+        if real_store.host_videos[i, 3] == 0:
+            load_clip(it, real_kp_dir, require_kp=True)  # raises FileNotFoundError like utils.py:416-417
+    centroids, label_dict, _ = build_real_centroids(model, real_meshes_dir, real_kp_dir, stats, clip_len, stride, device,
+                                                    train_items=train_ds.items, label_dict=label_dict, store=real_store)
+    t2 = time.perf_counter()
+    dataset = create_dataset_from_generated_meshes(generated_meshes_dir)
+    feats = extract_window_features(model, dataset, keypoint_dir, stats, clip_len, stride, device)
+    ac = compute_action_consistency_scores(feats, centroids, label_dict)
+    tc = compute_temporal_coherence_scores(feats, centroids, label_dict)
+    combined = combine_scores(ac, tc)
+    torch.cuda.synchronize(device)
+    t3 = time.perf_counter()
+    if out_json:
+        with open(out_json, "w") as f:
+            json.dump(combined, f, indent=2)
+    if human_scores_path and os.path.exists(human_scores_path):
+        for key, sc in (("ac", ac), ("tc", tc)):
+            corr, p, m = compute_spearman_correlation(sc, human_scores_path, key)
+            if corr is not None:
+                print(f"{key.upper()} Spearman: {corr:.4f} (p={p:.4e}, matched {len(m)})")
+    if timings is not None:
+        timings.update(stats_s=t1 - t0, centroids_s=t2 - t1, gen_s=t3 - t2, n_windows=len(feats["vid_names"]))
+    return combined

@@ -1,0 +1,82 @@
+"""ctypes binding of libvge.so (include/vge.h).  The product path has no fallback: if the HIP
+library cannot be loaded every compute call raises VgeError."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+_HERE = Path(__file__).resolve().parent
+LIB_PATH = Path(os.environ.get("VGE_LIB", _HERE / "libvge.so"))
+
+VGE_OK = 0
+STATUS = {0: "VGE_OK", 1: "VGE_ERR_ARG", 2: "VGE_ERR_HIP", 3: "VGE_ERR_MISSING_WEIGHT", 4: "VGE_ERR_WEIGHT_SHAPE",
+          5: "VGE_ERR_NOMEM", 6: "VGE_ERR_WORKSPACE"}
+
+EXPORTS = ["vge_featurize", "vge_stats_workspace_bytes", "vge_stats_accumulate", "vge_stats_finalize",
+           "vge_encoder_create", "vge_encoder_reserve", "vge_encoder_destroy", "vge_encode", "vge_tc_windows",
+           "vge_score_videos", "vge_centroid_accumulate", "vge_centroid_finalize", "vge_last_error", "vge_version"]
+
+
+class VgeError(RuntimeError):
+    pass
+
+
+class Dims(C.Structure):
+    _fields_ = [("n_modalities", C.c_int), ("dims_raw", C.c_int * 8), ("dims_diff", C.c_int * 8),
+                ("d_model", C.c_int), ("time_layers", C.c_int), ("time_heads", C.c_int), ("clip_len", C.c_int)]
+
+
+class TensorView(C.Structure):
+    _fields_ = [("name", C.c_char_p), ("data", C.c_void_p), ("ndim", C.c_int), ("shape", C.c_int64 * 4)]
+
+
+class FrameStoreC(C.Structure):
+    _fields_ = [("pose", C.c_void_p), ("gori", C.c_void_p), ("betas", C.c_void_p), ("vit", C.c_void_p),
+                ("kp", C.c_void_p), ("videos", C.c_void_p), ("n_videos", C.c_int)]
+
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load libvge.so once; raise VgeError (no CPU fallback) when it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not LIB_PATH.exists():
+        raise VgeError(f"libvge.so not found at {LIB_PATH}: build it with `make -C video-gen-evals_amd/csrc` "
+                       "(or __graft_entry__.build()); there is no CPU fallback")
+    lib = C.CDLL(str(LIB_PATH))
+    vp, i32, i64p = C.c_void_p, C.c_int, C.POINTER(C.c_int64)
+    sig = {
+        "vge_featurize": [C.POINTER(FrameStoreC), vp, i32, vp, vp, vp, vp],
+        "vge_stats_workspace_bytes": [i32],
+        "vge_stats_accumulate": [C.POINTER(FrameStoreC), vp, vp, i32, vp, i64p, vp, C.c_size_t, vp],
+        "vge_stats_finalize": [vp, i64p, vp, vp, vp],
+        "vge_encoder_create": [C.POINTER(Dims), C.POINTER(TensorView), i32, i32, C.POINTER(vp)],
+        "vge_encoder_reserve": [vp, i32],
+        "vge_encoder_destroy": [vp],
+        "vge_encode": [vp, vp, i32, i32, vp, vp, vp, vp],
+        "vge_tc_windows": [vp, i32, i32, i32, vp, vp],
+        "vge_score_videos": [vp, vp, vp, vp, vp, i32, i32, vp, vp, vp],
+        "vge_centroid_accumulate": [vp, vp, i32, i32, i32, vp, vp, vp],
+        "vge_centroid_finalize": [vp, vp, i32, i32, vp, vp],
+        "vge_last_error": [],
+        "vge_version": [],
+    }
+    for name, args in sig.items():
+        f = getattr(lib, name)
+        f.argtypes = args
+        f.restype = C.c_int
+    lib.vge_stats_workspace_bytes.restype = C.c_size_t
+    lib.vge_last_error.restype = C.c_char_p
+    lib.vge_version.restype = C.c_char_p
+    _lib = lib
+    return lib
+
+
+def check(status: int, what: str) -> None:
+    if status != VGE_OK:
+        msg = load().vge_last_error().decode(errors="replace")
+        raise VgeError(f"{what} failed: {STATUS.get(status, status)}: {msg}")

@@ -1,0 +1,199 @@
+"""Torch-facing wrappers over libvge.so.  torch supplies device memory and the current HIP stream;
+all arithmetic happens in the HIP kernels behind the C ABI (vge.lib)."""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Dict, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from . import lib as L
+from .data import FrameStore
+
+FEAT_DIM = 2596
+D_MODEL = 256
+MODALITIES = ("vit", "global", "pose", "beta", "kp2d")
+DIMS_RAW = (1024, 9, 207, 10, 120)
+DIMS_DIFF = (1024, 3, 69, 10, 120)
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise L.VgeError("vge ops need device (cuda/HIP) tensors")
+    if not t.is_contiguous():
+        raise L.VgeError("vge ops need contiguous tensors")
+    return t.data_ptr()
+
+
+def _stream(device=None) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+@dataclass
+class DeviceFrameStore:
+    """The frame store resident in HBM (see vge.data.FrameStore) + its C view."""
+    pose: torch.Tensor
+    gori: torch.Tensor
+    betas: torch.Tensor
+    vit: torch.Tensor
+    kp: torch.Tensor
+    videos: torch.Tensor            # int32 [V,4] on device
+    host_videos: np.ndarray         # int32 [V,4]
+    names: list
+    classes: list
+
+    @classmethod
+    def from_host(cls, st: FrameStore, device) -> "DeviceFrameStore":
+        def dev(a, dtype=torch.float32):
+            return torch.from_numpy(np.ascontiguousarray(a)).to(device=device, dtype=dtype)
+        return cls(pose=dev(st.pose), gori=dev(st.gori), betas=dev(st.betas), vit=dev(st.vit), kp=dev(st.kp),
+                   videos=dev(st.videos, torch.int32), host_videos=np.ascontiguousarray(st.videos, np.int32),
+                   names=list(st.names), classes=list(st.classes))
+
+    @property
+    def n_videos(self) -> int:
+        return int(self.host_videos.shape[0])
+
+    def cview(self) -> L.FrameStoreC:
+        return L.FrameStoreC(_ptr(self.pose), _ptr(self.gori), _ptr(self.betas), _ptr(self.vit), _ptr(self.kp),
+                             _ptr(self.videos), self.n_videos)
+
+
+def featurize(store: DeviceFrameStore, windows: torch.Tensor, mean: torch.Tensor, std: torch.Tensor,
+              out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """WindowDataset._try_one for a batch of windows -> feats [Nw,32,2596] (utils.py:383-516)."""
+    lib = L.load()
+    n = int(windows.shape[0])
+    if out is None:
+        out = torch.empty((n, 32, FEAT_DIM), device=windows.device, dtype=torch.float32)
+    if n:
+        hv = store.host_videos
+        cv = store.cview()
+        L.check(lib.vge_featurize(C.byref(cv), _ptr(windows), n, _ptr(mean), _ptr(std), _ptr(out),
+                                  _stream(windows.device)), "vge_featurize")
+    return out
+
+
+def stats_accumulate(store: DeviceFrameStore, video_sel: Sequence[int], sums: torch.Tensor, counts: np.ndarray,
+                     workspace_tiles: int = 512) -> None:
+    """compute_stats_from_npz's float64 sum / sum-of-squares (utils.py:595-744), accumulated into
+    sums [2,2596] f64 (device) and counts int64[2] (host)."""
+    lib = L.load()
+    sel = np.ascontiguousarray(np.asarray(video_sel, np.int32))
+    wsb = lib.vge_stats_workspace_bytes(workspace_tiles)
+    ws = torch.empty(wsb, dtype=torch.uint8, device=sums.device)
+    cnt = (C.c_int64 * 2)(int(counts[0]), int(counts[1]))
+    cv = store.cview()
+    L.check(lib.vge_stats_accumulate(C.byref(cv), store.host_videos.ctypes.data, sel.ctypes.data, len(sel),
+                                      _ptr(sums), cnt, _ptr(ws), wsb, _stream(sums.device)), "vge_stats_accumulate")
+    counts[0], counts[1] = cnt[0], cnt[1]
+
+
+def stats_finalize(sums: torch.Tensor, counts: np.ndarray) -> Tuple[torch.Tensor, torch.Tensor]:
+    lib = L.load()
+    mean = torch.empty(FEAT_DIM, device=sums.device, dtype=torch.float32)
+    std = torch.empty_like(mean)
+    cnt = (C.c_int64 * 2)(int(counts[0]), int(counts[1]))
+    L.check(lib.vge_stats_finalize(_ptr(sums), cnt, _ptr(mean), _ptr(std), _stream(sums.device)), "vge_stats_finalize")
+    return mean, std
+
+
+class Encoder:
+    """HumanActionScorer (model.py:102-193) as a libvge encoder handle owning repacked HBM weights."""
+
+    def __init__(self, state_dict: Dict[str, np.ndarray], time_layers: int = 4, time_heads: int = 8,
+                 d_model: int = 256, device=None):
+        lib = L.load()
+        self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+        dims = L.Dims()
+        dims.n_modalities = 5
+        for i in range(5):
+            dims.dims_raw[i] = DIMS_RAW[i]
+            dims.dims_diff[i] = DIMS_DIFF[i]
+        dims.d_model, dims.time_layers, dims.time_heads, dims.clip_len = d_model, time_layers, time_heads, 32
+        keep = []
+        views = (L.TensorView * len(state_dict))()
+        for i, (k, v) in enumerate(state_dict.items()):
+            a = np.ascontiguousarray(np.asarray(v, np.float32))
+            keep.append(a)
+            views[i].name = k.encode()
+            views[i].data = a.ctypes.data
+            views[i].ndim = a.ndim
+            for j, s in enumerate(a.shape[:4]):
+                views[i].shape[j] = s
+        h = C.c_void_p()
+        with torch.cuda.device(self.device):
+            L.check(lib.vge_encoder_create(C.byref(dims), views, len(state_dict), 0, C.byref(h)), "vge_encoder_create")
+        self._h = h
+        self._lib = lib
+        self.capacity = 0
+
+    def reserve(self, max_windows: int) -> None:
+        if max_windows > self.capacity:
+            with torch.cuda.device(self.device):
+                L.check(self._lib.vge_encoder_reserve(self._h, int(max_windows)), "vge_encoder_reserve")
+            self.capacity = int(max_windows)
+
+    def encode(self, feats: torch.Tensor, frame_embed: bool = False, tc: bool = True):
+        """feats [B,32,2596] -> (seq_embed [B,256], frame_embeds [B,33,256] | None, tc_window [B] | None)."""
+        B, T, D = feats.shape
+        if D != FEAT_DIM:
+            raise L.VgeError(f"feats last dim {D} != {FEAT_DIM}")
+        self.reserve(B)
+        seq = torch.empty((B, D_MODEL), device=feats.device, dtype=torch.float32)
+        fe = torch.empty((B, T + 1, D_MODEL), device=feats.device, dtype=torch.float32) if frame_embed else None
+        tcw = torch.empty((B,), device=feats.device, dtype=torch.float32) if tc else None
+        L.check(self._lib.vge_encode(self._h, _ptr(feats), B, T, _ptr(seq), _ptr(fe), _ptr(tcw), _stream(feats.device)),
+                "vge_encode")
+        return seq, fe, tcw
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                self._lib.vge_encoder_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+
+def tc_windows(frame_embeds: torch.Tensor) -> torch.Tensor:
+    lib = L.load()
+    B, T1, d = frame_embeds.shape
+    out = torch.empty((B,), device=frame_embeds.device, dtype=torch.float32)
+    L.check(lib.vge_tc_windows(_ptr(frame_embeds), B, T1, d, _ptr(out), _stream(frame_embeds.device)), "vge_tc_windows")
+    return out
+
+
+def score_videos(seq: torch.Tensor, tc_window: torch.Tensor, video_first_win: torch.Tensor, video_class: torch.Tensor,
+                 centroids: Optional[torch.Tensor]) -> Tuple[torch.Tensor, torch.Tensor]:
+    lib = L.load()
+    V = int(video_class.shape[0])
+    d = int(seq.shape[1])
+    ac = torch.empty((V,), device=seq.device, dtype=torch.float32)
+    tc = torch.empty((V,), device=seq.device, dtype=torch.float64)
+    if centroids is None:
+        centroids = torch.zeros((1, d), device=seq.device, dtype=torch.float32)
+    L.check(lib.vge_score_videos(_ptr(seq), _ptr(tc_window), _ptr(video_first_win), _ptr(video_class), _ptr(centroids),
+                                 V, d, _ptr(ac), _ptr(tc), _stream(seq.device)), "vge_score_videos")
+    return ac, tc
+
+
+def centroid_accumulate(seq: torch.Tensor, class_id: torch.Tensor, sums: torch.Tensor, counts: torch.Tensor) -> None:
+    lib = L.load()
+    C_, d = sums.shape
+    L.check(lib.vge_centroid_accumulate(_ptr(seq), _ptr(class_id), int(seq.shape[0]), C_, d, _ptr(sums), _ptr(counts),
+                                        _stream(seq.device)), "vge_centroid_accumulate")
+
+
+def centroid_finalize(sums: torch.Tensor, counts: torch.Tensor) -> torch.Tensor:
+    lib = L.load()
+    C_, d = sums.shape
+    out = torch.empty_like(sums)
+    L.check(lib.vge_centroid_finalize(_ptr(sums), _ptr(counts), C_, d, _ptr(out), _stream(sums.device)),
+            "vge_centroid_finalize")
+    return out

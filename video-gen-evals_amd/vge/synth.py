@@ -3,9 +3,10 @@
 There are no datasets, checkpoints or extractors offline, so every test, fixture and benchmark
 runs on data from this generator.  Values are shaped like the real extractor outputs:
 
-* pose / global_orient: valid SO(3) matrices from Rodrigues of a per-joint axis-angle random walk
-  (24 joints, base ~ N(0, 0.5^2), per-frame step ~ N(0, 0.05^2)); joint 0 -> global_orient
-  [T,1,3,3], joints 1..23 -> pose [T,23,3,3]  (layout written by extract_mesh.py:18-43).
+* pose / global_orient: valid SO(3) matrices from a per-joint random walk on unit quaternions
+  (uniform start, per-frame step ~ N(0, 0.025^2) per component, ~0.05 rad); joint 0 ->
+  global_orient [T,1,3,3], joints 1..23 -> pose [T,23,3,3]  (layout of extract_mesh.py:18-43).
+  Bit-reproducible on any host CPU (no SIMD transcendental functions).
 * betas ~ N(0,1) [T,10];  vit ~ N(0,1) [T,1024]  (token_head.py token_out).
 * keypoints ~ U[0,1] [T',120] with ~5% coordinates set to -1 (dwpose_init.py:57-60 marks
   low-score points -1) and an optional T' < T (process_video.py drops frames).
@@ -31,7 +32,8 @@ GEN_MODELS = ["Hunyuan", "Opensora_768", "wan21", "RunwayGen4", "Wan2.2"]
 
 
 def _rodrigues(aa: np.ndarray) -> np.ndarray:
-    """axis-angle [...,3] (float64) -> rotation matrices [...,3,3] (float64)."""
+    """axis-angle [...,3] (float64) -> rotation matrices [...,3,3] (float64).  Test helper only: uses
+    SIMD sin/cos, so its last bits can differ between host CPUs (never used for fixture inputs)."""
     theta = np.linalg.norm(aa, axis=-1, keepdims=True)
     k = aa / np.maximum(theta, 1e-12)
     kx, ky, kz = k[..., 0], k[..., 1], k[..., 2]
@@ -42,6 +44,33 @@ def _rodrigues(aa: np.ndarray) -> np.ndarray:
     c = np.cos(theta)[..., None]
     eye = np.broadcast_to(np.eye(3), K.shape)
     return eye + s * K + (1.0 - c) * (K @ K)
+
+
+def _quat_walk(rng: np.random.Generator, T: int, J: int, step: float = 0.025) -> np.ndarray:
+    """Smooth random SO(3) sequences [T,J,3,3] from a random walk on unit quaternions.
+
+    Only element-wise +,-,*,/ and sqrt (IEEE correctly rounded) are used, so the bits are identical on
+    every host CPU -- the golden fixtures are regenerated from seeds on the GPU box."""
+    def unit(q):
+        n = np.sqrt(q[..., 0] * q[..., 0] + q[..., 1] * q[..., 1] + q[..., 2] * q[..., 2] + q[..., 3] * q[..., 3])
+        return q / n[..., None]
+    q = np.empty((T, J, 4))
+    q[0] = unit(rng.normal(0.0, 1.0, size=(J, 4)))
+    noise = rng.normal(0.0, step, size=(T, J, 4))
+    for t in range(1, T):
+        q[t] = unit(q[t - 1] + noise[t])
+    w, x, y, z = q[..., 0], q[..., 1], q[..., 2], q[..., 3]
+    R = np.empty((T, J, 3, 3))
+    R[..., 0, 0] = 1 - 2 * (y * y + z * z)
+    R[..., 0, 1] = 2 * (x * y - w * z)
+    R[..., 0, 2] = 2 * (x * z + w * y)
+    R[..., 1, 0] = 2 * (x * y + w * z)
+    R[..., 1, 1] = 1 - 2 * (x * x + z * z)
+    R[..., 1, 2] = 2 * (y * z - w * x)
+    R[..., 2, 0] = 2 * (x * z - w * y)
+    R[..., 2, 1] = 2 * (y * z + w * x)
+    R[..., 2, 2] = 1 - 2 * (x * x + y * y)
+    return R
 
 
 @dataclass
@@ -56,10 +85,7 @@ class SynthClip:
 def make_clip(seed: int, index: int, T: int, kp_len: Optional[int] = None, vit_dim: int = 1024,
               kp_seed: int = SEED_KP) -> SynthClip:
     rng = np.random.default_rng([seed, index])
-    base = rng.normal(0.0, 0.5, size=(1, 24, 3))
-    steps = rng.normal(0.0, 0.05, size=(T, 24, 3))
-    aa = base + np.cumsum(steps, axis=0)
-    R = _rodrigues(aa).astype(np.float32)                       # [T,24,3,3]
+    R = _quat_walk(rng, T, 24).astype(np.float32)               # [T,24,3,3]
     betas = rng.normal(0.0, 1.0, size=(T, 10)).astype(np.float32)
     vit = rng.normal(0.0, 1.0, size=(T, vit_dim)).astype(np.float32)
     krng = np.random.default_rng([kp_seed, seed, index])
@@ -128,15 +154,18 @@ def write_dataset(root: str, n_real_per_class: int = 5, n_gen: int = 4, T_real: 
 # ----------------------------------------------------------------------------- weights
 
 def _sinusoidal_pe(d_model: int, max_len: int = 5000) -> np.ndarray:
-    """Same formula and float32 evaluation order as model.py:9-16 (computed with torch)."""
+    """The model.py:9-16 formula (pe[p, 2i] = sin(p / 10000^(2i/d)), pe[p, 2i+1] = cos(...)), evaluated
+    with the scalar libm in float64 so the buffer is bit-identical on every host (it is loaded from
+    the state_dict, so the reference uses exactly these values too)."""
     import math
-    import torch
-    pe = torch.zeros(max_len, d_model)
-    pos = torch.arange(0, max_len, dtype=torch.float32).unsqueeze(1)
-    div = torch.exp(torch.arange(0, d_model, 2, dtype=torch.float32) * (-math.log(10000.0) / d_model))
-    pe[:, 0::2] = torch.sin(pos * div)
-    pe[:, 1::2] = torch.cos(pos * div)
-    return pe.unsqueeze(0).numpy()
+    pe = np.zeros((max_len, d_model), np.float64)
+    for i in range(0, d_model, 2):
+        div = math.exp(i * (-math.log(10000.0) / d_model))
+        for p in range(max_len):
+            pe[p, i] = math.sin(p * div)
+            if i + 1 < d_model:
+                pe[p, i + 1] = math.cos(p * div)
+    return pe.astype(np.float32)[None]
 
 
 def make_state_dict(dims_raw: Dict[str, int], dims_diff: Dict[str, int], d_model: int = 256,
