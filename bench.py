@@ -1,0 +1,262 @@
+#!/usr/bin/env python3
+"""AC/TC scoring throughput on MI355X -- BASELINE.json's metric on its configs[1] workload.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (config 2 of BASELINE.json): 256 synthetic 32-frame clips per GPU with pre-extracted
+per-frame features (SMPL rotations, betas, 1024-d token, 120-d keypoints) resident in HBM.  One
+step = featurise all windows (HIP) -> HumanActionScorer forward (f32 MFMA) -> per-video AC + TC
+(HIP reductions) -> scores copied to pinned host memory.  ModalityStats and the real-class
+centroids (the real set is sharded over ranks, sufficient statistics all-reduced over RCCL) are
+built once in the setup phase and reported separately (`setup_s`).  Weak scaling: every rank
+scores its own 256 clips; no collective in the step.
+
+Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (conv_encoder_kernel, the 10
+MovementConvEncoders, f32 MFMA-bound): achieved = its algorithmic FLOPs per launch / its average
+duration from hipEvents recorded around it on its stream inside the timed steps.  `cpu_baseline`
+is the oracle CPU restatement of eval.py (torch-fp32 encoder + numpy featuriser, same work split as
+the reference) timed on this host on a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "video-gen-evals_amd"))
+sys.path.insert(0, str(ROOT))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = json.loads((ROOT / "BASELINE.json").read_text())["metric"]
+CLIP_LEN = 32
+# algorithmic FLOPs of conv_encoder_kernel per 32-frame window: stems (K = sum of the 10 input dims =
+# 2596) + 80 dilated k=5 convs 256->256 + 10 proj 256->256, 2 FLOP per MAC
+CONV_FLOP_PER_WINDOW = 2 * 32 * 256 * 2596 + 80 * 2 * 32 * 256 * 256 * 5 + 10 * 2 * 32 * 256 * 256
+ENCODER_FLOP_PER_WINDOW = 2.0203e9          # FlopCounterMode on model.py at T=32
+F32_MFMA_PEAK_TFLOPS = 157.3                # MI355X_MICROARCH.md: v_mfma_f32_* = FP32 vector peak
+HBM_PEAK_GBS = 8000.0
+FEAT_BYTES_PER_WINDOW = 32 * (1024 + 207 + 9 + 10 + 120) * 4 + 32 * 2596 * 4   # read + write
+
+
+def make_clips(seed, start, n, T, kp_len=None):
+    from vge import synth
+    clips = []
+    for i in range(start, start + n):
+        c = synth.make_clip(seed, i, T, kp_len)
+        clips.append({"pose": c.pose, "global_orient": c.global_orient, "betas": c.betas, "vit": c.vit,
+                      "keypoints": c.keypoints})
+    return clips
+
+
+def setup_dist():
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(0)
+    return world, rank, torch.device("cuda", torch.cuda.current_device())
+
+
+def allreduce_sum(t, world):
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return t
+
+
+def cpu_baseline(seconds: float, clips_per_batch: int = 32):
+    """Oracle CPU restatement of eval.py's generated-set pass (featurise + encode + AC/TC), timed on
+    this host.  Bounded: whole batches of 32 clips until `seconds` have elapsed."""
+    from oracle import evalflow
+    from oracle.encoder import OracleEncoder
+    from oracle.featurize import featurize_window
+    from vge import synth
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    torch.set_num_threads(threads)
+    sd = synth.make_state_dict(synth.DIMS_RAW, synth.DIMS_DIFF)
+    enc = OracleEncoder(sd, synth.DIMS_RAW, synth.DIMS_DIFF)
+    rng = np.random.default_rng(0)
+    mean = rng.normal(0, 0.1, 2596).astype(np.float32)
+    std = rng.uniform(0.5, 2.0, 2596).astype(np.float32)
+    cents = torch.nn.functional.normalize(torch.randn(10, 256), dim=-1)
+    label = {c: i for i, c in enumerate(evalflow.ACTION_CLASSES)}
+    n_done, t_used, b = 0, 0.0, 0
+    while t_used < seconds or n_done == 0:
+        clips = make_clips(synth.SEED_GEN, 10_000 + b * clips_per_batch, clips_per_batch, CLIP_LEN)
+        names = [synth.generated_name(10_000 + b * clips_per_batch + i) + ".npz" for i in range(clips_per_batch)]
+        t0 = time.perf_counter()
+        feats = torch.from_numpy(np.stack([
+            (featurize_window(c["pose"], c["global_orient"], c["betas"], c["vit"], c["keypoints"], 0, None) - mean)
+            / (std + np.float32(1e-6)) for c in clips]))
+        seq, fe, _ = enc.forward(feats)
+        cls = [evalflow.ACTION_CLASSES[((10_000 + b * clips_per_batch + i) // 5) % 10] for i in range(clips_per_batch)]
+        evalflow.ac_scores(seq, cls, names, cents, label)
+        evalflow.tc_scores(fe, names)
+        t_used += time.perf_counter() - t0
+        n_done += clips_per_batch
+        b += 1
+    return {"value": n_done / t_used, "unit": "videos/s", "cores": threads, "kind": "port",
+            "sample": f"{n_done} synthetic 32-frame clips (in-memory features, no npz decode), oracle "
+                      f"featurise (numpy, 1 thread) + torch-fp32 encoder ({threads} threads) + AC/TC, "
+                      f"{t_used:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--clips", type=int, default=256, help="32-frame clips per GPU per step (config 2: 256)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world, rank, dev = setup_dist()
+    from vge import eval as VE
+    from vge import ops, synth
+    from vge.data import ACTION_CLASSES, pack_frame_store
+
+    # ---------------- setup: frame stores in HBM, stats + centroids over the (sharded) real set
+    t_setup = time.perf_counter()
+    n_real_per_class, T_real = 8, 64
+    real_idx = [i for i in range(10 * n_real_per_class) if i % world == rank]
+    real_clips = [make_clips(synth.SEED_REAL, i, 1, T_real)[0] for i in real_idx]
+    real_cls = [ACTION_CLASSES[i // n_real_per_class] for i in real_idx]
+    real_store = ops.DeviceFrameStore.from_host(pack_frame_store(real_clips, [f"r{i}" for i in real_idx], real_cls), dev)
+    sums = torch.zeros((2, ops.FEAT_DIM), device=dev, dtype=torch.float64)
+    counts = np.zeros(2, np.int64)
+    ops.stats_accumulate(real_store, range(real_store.n_videos), sums, counts)
+    allreduce_sum(sums, world)
+    cnt_t = allreduce_sum(torch.tensor(counts, device=dev), world)
+    counts = cnt_t.cpu().numpy()
+    mean, std = ops.stats_finalize(sums, counts)
+    stats = VE.ModalityStatsGPU(mean, std, sums, counts)
+    sd = synth.make_state_dict(synth.DIMS_RAW, synth.DIMS_DIFF)
+    enc = ops.Encoder(sd, device=dev)
+    B = args.clips
+    enc.reserve(max(B, 64))
+    real_win = torch.tensor([[v, s] for v in range(real_store.n_videos) for s in range(0, T_real - CLIP_LEN + 1, 8)],
+                            dtype=torch.int32, device=dev)
+    rseq, _, _ = VE.encode_windows(enc, real_store, real_win, stats, batch=B)
+    label = {c: i for i, c in enumerate(ACTION_CLASSES)}
+    y = torch.tensor([label[real_cls[v]] for v in range(real_store.n_videos) for _ in range(0, T_real - CLIP_LEN + 1, 8)],
+                     dtype=torch.int32, device=dev)
+    csum = torch.zeros((10, 256), device=dev)
+    ccnt = torch.zeros((10,), device=dev)
+    ops.centroid_accumulate(rseq, y, csum, ccnt)
+    allreduce_sum(csum, world)
+    allreduce_sum(ccnt, world)
+    centroids = ops.centroid_finalize(csum, ccnt)
+
+    gen_clips = make_clips(synth.SEED_GEN, rank * B, B, CLIP_LEN)
+    names = [synth.generated_name(rank * B + i) for i in range(B)]
+    gstore = ops.DeviceFrameStore.from_host(pack_frame_store(gen_clips, names, ["X"] * B), dev)
+    windows = torch.tensor([[v, 0] for v in range(B)], dtype=torch.int32, device=dev)   # 32f clip = 1 window
+    first = torch.arange(B + 1, dtype=torch.int32, device=dev)
+    vcls = torch.tensor([label[ACTION_CLASSES[((rank * B + i) // 5) % 10]] for i in range(B)], dtype=torch.int32,
+                        device=dev)
+    feats = torch.empty((B, CLIP_LEN, ops.FEAT_DIM), device=dev)
+    host_ac = torch.empty((B,), dtype=torch.float32, pin_memory=True)
+    host_tc = torch.empty((B,), dtype=torch.float64, pin_memory=True)
+    torch.cuda.synchronize()
+    setup_s = time.perf_counter() - t_setup
+
+    fe0 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+    fe1 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
+
+    def step(i=None):
+        if i is not None:
+            fe0[i].record()
+        ops.featurize(gstore, windows, stats.mean, stats.std, out=feats)
+        if i is not None:
+            fe1[i].record()
+        seq, _, tcw = enc.encode(feats, frame_embed=False, tc=True)
+        ac, tc = ops.score_videos(seq, tcw, first, vcls, centroids)
+        host_ac.copy_(ac, non_blocking=True)
+        host_tc.copy_(tc, non_blocking=True)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    enc.profile_begin(args.steps)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    dt_t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
+    dt = float(dt_t.item())
+    stage_ms, ncalls = enc.profile_read()
+    feat_ms = sum(a.elapsed_time(b) for a, b in zip(fe0, fe1)) / args.steps
+    assert np.isfinite(host_ac.numpy()).all() and np.isfinite(host_tc.numpy()).all()
+
+    if rank == 0:
+        conv_ms = stage_ms["conv_encoders"] / max(ncalls, 1)
+        achieved = CONV_FLOP_PER_WINDOW * B / (conv_ms * 1e-3) / 1e12
+        traffic = None
+        pmc = ROOT / "profiles" / "pmc_conv_encoder.json"
+        if pmc.exists():
+            try:
+                pj = json.loads(pmc.read_text())
+                traffic = pj["hbm_bytes_per_window"] * B
+            except Exception:
+                traffic = None
+        total_videos = world * B * args.steps
+        out = {
+            "metric": METRIC,
+            "value": total_videos / dt,
+            "unit": "videos/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (deterministic generator vge.synth: quaternion-walk SMPL rotations, N(0,1) betas/tokens, "
+                    "U[0,1] keypoints with 5% invisible; random-init weights of the reference architecture)",
+            "config": {"workload": "BASELINE config 2: fusion-encoder fwd + AC/TC metrics, 256 clips x 32 frames per GPU, "
+                                   "pre-extracted features resident in HBM (featurise included in the step)",
+                       "clips_per_gpu": B, "frames_per_clip": CLIP_LEN, "windows_per_step_per_gpu": B,
+                       "parallelism": f"video-sharded x{world}"},
+            "roofline": {"bound": "mfma", "kernel": "conv_encoder_kernel (10 MovementConvEncoders, f32 MFMA)",
+                         "achieved": achieved, "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": achieved / F32_MFMA_PEAK_TFLOPS, "traffic": traffic,
+                         "flop_per_launch": CONV_FLOP_PER_WINDOW * B, "avg_launch_ms": conv_ms},
+            "stage_ms": {k: v / max(ncalls, 1) for k, v in stage_ms.items()},
+            "featurize": {"avg_ms": feat_ms, "bound": "hbm",
+                          "achieved_GBs": FEAT_BYTES_PER_WINDOW * B / (feat_ms * 1e-3) / 1e9, "peak_GBs": HBM_PEAK_GBS},
+            "encoder_tflops_2.0203GF_per_window": ENCODER_FLOP_PER_WINDOW * world * B * args.steps / dt / 1e12 / world,
+            "setup_s": setup_s,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -134,6 +134,16 @@ int vge_encoder_destroy(vge_encoder* enc);
 int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_embed, float* frame_embed,
                float* tc_window, vge_stream_t stream);
 
+/* Per-stage device time of vge_encode, measured with hipEvents recorded on the encode stream around
+ * each stage (used by bench.py for the roofline line).  profile_begin pre-creates events for up to
+ * max_calls subsequent vge_encode calls (no allocation inside encode); profile_read synchronises on
+ * the recorded events and returns the summed milliseconds per stage and the number of calls seen.
+ * Stages: 0 conv encoders (MovementConvEncoder x10), 1 fusion pool, 2 token GEMM (+CLS/PE),
+ *         3 transformer layers, 4 output normalisation + per-window TC. */
+#define VGE_N_STAGES 5
+int vge_encoder_profile_begin(vge_encoder* enc, int max_calls);
+int vge_encoder_profile_read(vge_encoder* enc, double* stage_ms, int* n_calls);
+
 /* ---------------------------------------------------------------------------------------------
  * Metrics.
  * vge_tc_windows: compute_temporal_coherence_scores' per-window term (eval.py:216-224):

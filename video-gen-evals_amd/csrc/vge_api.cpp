@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <string>
 #include <unordered_map>
 #include <vector>
@@ -123,6 +124,9 @@ struct vge_encoder {
   std::vector<Layer> layers;
   const float* cls = nullptr;
   const float* pe = nullptr;
+  // profiling (hipEvents recorded around the stages of vge_encode)
+  std::vector<hipEvent_t> prof_ev;   // (VGE_N_STAGES + 1) per call
+  int prof_max = 0, prof_calls = 0;
   // workspace
   int cap = 0;
   float* ws = nullptr;
@@ -444,8 +448,40 @@ int vge_encoder_reserve(vge_encoder* enc, int B) {
   return VGE_OK;
 }
 
+int vge_encoder_profile_begin(vge_encoder* enc, int max_calls) {
+  if (!enc || max_calls < 0) return fail(VGE_ERR_ARG, "vge_encoder_profile_begin: bad argument");
+  const size_t need = (size_t)max_calls * (VGE_N_STAGES + 1);
+  while (enc->prof_ev.size() < need) {
+    hipEvent_t e;
+    HIPCHK(hipEventCreate(&e));
+    enc->prof_ev.push_back(e);
+  }
+  enc->prof_max = max_calls;
+  enc->prof_calls = 0;
+  return VGE_OK;
+}
+
+int vge_encoder_profile_read(vge_encoder* enc, double* stage_ms, int* n_calls) {
+  if (!enc || !stage_ms || !n_calls) return fail(VGE_ERR_ARG, "vge_encoder_profile_read: bad argument");
+  for (int k = 0; k < VGE_N_STAGES; ++k) stage_ms[k] = 0.0;
+  const int n = std::min(enc->prof_calls, enc->prof_max);
+  for (int c = 0; c < n; ++c) {
+    hipEvent_t* ev = enc->prof_ev.data() + (size_t)c * (VGE_N_STAGES + 1);
+    HIPCHK(hipEventSynchronize(ev[VGE_N_STAGES]));
+    for (int k = 0; k < VGE_N_STAGES; ++k) {
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
+      stage_ms[k] += ms;
+    }
+  }
+  *n_calls = n;
+  enc->prof_max = 0;
+  return VGE_OK;
+}
+
 int vge_encoder_destroy(vge_encoder* enc) {
   if (!enc) return VGE_OK;
+  for (hipEvent_t e : enc->prof_ev) (void)hipEventDestroy(e);
   if (enc->ws) (void)hipFree(enc->ws);
   if (enc->d_encs) (void)hipFree(enc->d_encs);
   if (enc->wbuf) (void)hipFree(enc->wbuf);
@@ -461,12 +497,19 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
   if (B > enc->cap) return fail(VGE_ERR_WORKSPACE, "vge_encode: call vge_encoder_reserve(B) first");
   hipStream_t s = S(stream);
   const int frames = B * 32, M = B * 33;
+  hipEvent_t* ev = nullptr;
+  if (enc->prof_calls < enc->prof_max) ev = enc->prof_ev.data() + (size_t)(enc->prof_calls++) * (VGE_N_STAGES + 1);
+  auto mark = [&](int k) -> hipError_t { return ev ? hipEventRecord(ev[k], s) : hipSuccess; };
+  HIPCHK(mark(0));
   HIPCHK(vge::launch_conv_encoders(feats, B, enc->d_encs, 10, enc->enc_out, s));
+  HIPCHK(mark(1));
   HIPCHK(vge::launch_fuse(enc->enc_out, frames, enc->fuse, enc->pooled, s));
+  HIPCHK(mark(2));
   vge::GemmArgsHost g{};
   g.A = enc->pooled; g.lda = 256; g.W = enc->Wov; g.out = enc->x; g.ldo = 256; g.M = frames; g.K = 256; g.N = 256;
   g.pe = enc->pe; g.cls = enc->cls;
   HIPCHK(vge::launch_gemm(vge::EPI_TOKENS, g, s));
+  HIPCHK(mark(3));
   for (int l = 0; l < enc->n_layers; ++l) {
     const vge_encoder::Layer& Ly = enc->layers[l];
     vge::GemmArgsHost a{};
@@ -486,7 +529,9 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
     f2.bias = Ly.l2_b; f2.res = enc->x1; f2.ldr = 256; f2.ln_w = Ly.n2_w; f2.ln_b = Ly.n2_b;
     HIPCHK(vge::launch_gemm(vge::EPI_BIAS_RES_LN, f2, s));
   }
+  HIPCHK(mark(4));
   HIPCHK(vge::launch_embed_tc(enc->x, B, seq_embed, frame_embed, tc_window, s));
+  HIPCHK(mark(5));
   return VGE_OK;
 }
 

@@ -15,7 +15,8 @@ STATUS = {0: "VGE_OK", 1: "VGE_ERR_ARG", 2: "VGE_ERR_HIP", 3: "VGE_ERR_MISSING_W
 
 EXPORTS = ["vge_featurize", "vge_stats_workspace_bytes", "vge_stats_accumulate", "vge_stats_finalize",
            "vge_encoder_create", "vge_encoder_reserve", "vge_encoder_destroy", "vge_encode", "vge_tc_windows",
-           "vge_score_videos", "vge_centroid_accumulate", "vge_centroid_finalize", "vge_last_error", "vge_version"]
+           "vge_score_videos", "vge_centroid_accumulate", "vge_centroid_finalize", "vge_last_error", "vge_version",
+           "vge_encoder_profile_begin", "vge_encoder_profile_read"]
 
 
 class VgeError(RuntimeError):
@@ -62,6 +63,8 @@ def load() -> C.CDLL:
         "vge_score_videos": [vp, vp, vp, vp, vp, i32, i32, vp, vp, vp],
         "vge_centroid_accumulate": [vp, vp, i32, i32, i32, vp, vp, vp],
         "vge_centroid_finalize": [vp, vp, i32, i32, vp, vp],
+        "vge_encoder_profile_begin": [vp, i32],
+        "vge_encoder_profile_read": [vp, C.POINTER(C.c_double), C.POINTER(C.c_int)],
         "vge_last_error": [],
         "vge_version": [],
     }

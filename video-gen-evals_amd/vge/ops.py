@@ -151,6 +151,18 @@ class Encoder:
                 "vge_encode")
         return seq, fe, tcw
 
+    STAGES = ("conv_encoders", "fusion_pool", "token_gemm", "transformer", "outputs_tc")
+
+    def profile_begin(self, max_calls: int) -> None:
+        L.check(self._lib.vge_encoder_profile_begin(self._h, int(max_calls)), "vge_encoder_profile_begin")
+
+    def profile_read(self):
+        """-> ({stage: summed ms}, n_calls) for the encode calls since profile_begin."""
+        ms = (C.c_double * 5)()
+        n = C.c_int(0)
+        L.check(self._lib.vge_encoder_profile_read(self._h, ms, C.byref(n)), "vge_encoder_profile_read")
+        return dict(zip(self.STAGES, list(ms))), int(n.value)
+
     def __del__(self):
         h = getattr(self, "_h", None)
         if h is not None and h.value:
