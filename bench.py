@@ -120,6 +120,8 @@ def main():
     ap.add_argument("--clips", type=int, default=256, help="32-frame clips per GPU per step (config 2: 256)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--compute", default="f32x3", choices=["f32x3", "f32"],
+                    help="f32x3: 3xfp16 split-precision MFMA (f32-class, default); f32: exact f32 MFMA")
     args = ap.parse_args()
 
     world, rank, dev = setup_dist()
@@ -143,7 +145,7 @@ def main():
     mean, std = ops.stats_finalize(sums, counts)
     stats = VE.ModalityStatsGPU(mean, std, sums, counts)
     sd = synth.make_state_dict(synth.DIMS_RAW, synth.DIMS_DIFF)
-    enc = ops.Encoder(sd, device=dev)
+    enc = ops.Encoder(sd, device=dev, compute=args.compute)
     B = args.clips
     enc.reserve(max(B, 64))
     real_win = torch.tensor([[v, s] for v in range(real_store.n_videos) for s in range(0, T_real - CLIP_LEN + 1, 8)],

@@ -40,7 +40,11 @@ typedef enum {
   VGE_ERR_WORKSPACE = 6       /* vge_encoder_reserve() was not called for this many windows */
 } vge_status;
 
-typedef enum { VGE_F32 = 0 } vge_dtype; /* compute type: f32 in / f32 accumulate (exact-f32 MFMA) */
+/* Encoder compute modes.  VGE_F32: exact f32 MFMA (v_mfma_f32_16x16x4_f32, bitwise an fmaf chain).
+ * VGE_F32X3: f32-class split precision -- every GEMM operand carried as fp16 hi + fp16 lo*2^11 and
+ * each product formed as hi*hi + 2^-11 (hi*lo + lo*hi) on v_mfma_f32_32x32x16_f16 with f32
+ * accumulation (relative error ~2^-21 per product; AC/TC within ~1e-7 of the f32 mode). */
+typedef enum { VGE_F32 = 0, VGE_F32X3 = 1 } vge_dtype;
 
 #define VGE_FEAT_DIM 2596
 #define VGE_RAW_DIM 1370

@@ -22,8 +22,11 @@ def vg():
     return VE, ops
 
 
-@pytest.fixture(scope="module")
-def real_setup(vg, golden_dataset):
+MODES = ["f32", "f32x3"]
+
+
+@pytest.fixture(scope="module", params=MODES)
+def real_setup(vg, golden_dataset, request):
     VE, ops = vg
     from vge.data import ACTION_CLASSES, NpzVideoDataset, train_test_split
     paths, ckpt = golden_dataset
@@ -31,7 +34,7 @@ def real_setup(vg, golden_dataset):
     train_ds, _ = train_test_split(real_ds, train_ratio=0.8, seed=1337)
     store = ops.DeviceFrameStore.from_host(VE.load_frame_store(train_ds.items, paths["real_kp"], False), DEV)
     stats = VE.compute_stats_from_npz(train_ds.items, paths["real_kp"], device=DEV, store=store)
-    model = VE.load_model(ckpt, device=DEV)
+    model = VE.load_model(ckpt, device=DEV, compute=request.param)
     return paths, real_ds, train_ds, store, stats, model
 
 
@@ -93,14 +96,15 @@ def test_encoder_matches_reference(vg, real_setup, golden_flow):
     assert np.abs(fe[:4] - golden_flow["frame_embeds_first4"]).max() < 2e-5
 
 
-def test_encoder_vs_oracle_random_batch(vg, golden_state_dict):
+@pytest.mark.parametrize("compute", MODES)
+def test_encoder_vs_oracle_random_batch(vg, golden_state_dict, compute):
     """Odd batch (last conv workgroup half empty), random z-scored input, vs the torch-fp32 oracle."""
     VE, ops = vg
     from oracle.encoder import OracleEncoder
     from vge import synth
     torch.manual_seed(0)
     x = torch.randn(37, 32, 2596)
-    model = VE.load_model(golden_state_dict, device=DEV)
+    model = VE.load_model(golden_state_dict, device=DEV, compute=compute)
     seq, fe, tcw = model.encode(x.to(DEV), frame_embed=True, tc=True)
     o = OracleEncoder(golden_state_dict, synth.DIMS_RAW, synth.DIMS_DIFF)
     rs, rf, _ = o.forward(x)
@@ -124,13 +128,14 @@ def test_centroids_match_reference(vg, real_setup, golden_flow, golden_meta):
     assert np.abs(cents.cpu().numpy() - golden_flow["centroids"]).max() < 2e-5
 
 
-def test_video_scores_match_reference(vg, golden_dataset, golden_meta, tmp_path):
+@pytest.mark.parametrize("compute", MODES)
+def test_video_scores_match_reference(vg, golden_dataset, golden_meta, tmp_path, compute):
     """The whole eval.py flow -> video_scores.json within 1e-4 of the reference."""
     VE, ops = vg
     paths, ckpt = golden_dataset
     out = tmp_path / "video_scores.json"
     combined = VE.run_eval(paths["generated_meshes"], paths["real"], ckpt, paths["generated_kps"], paths["real_kp"],
-                           out_json=str(out), device=DEV)
+                           out_json=str(out), device=DEV, compute=compute)
     ref = golden_meta["video_scores"]
     assert sorted(combined) == sorted(ref)
     worst = 0.0

@@ -31,6 +31,17 @@ struct GemmArgsHost {
   const float* bias; const float* res; int ldr; const float* ln_w; const float* ln_b; const float* pe; const float* cls;
 };
 hipError_t encoder_kernel_setup();
+hipError_t encoder_x3_kernel_setup();
+struct EncDescX3Host {
+  const _Float16* stem; const _Float16* conv; const _Float16* proj; const float* gn_w; const float* gn_b;
+  int in_col, d_in, n_stem_panels, pad;
+};
+struct GemmArgsX3Host {
+  const float* A; int lda; const _Float16* W; float* out; int ldo; int M, K, N;
+  const float* bias; const float* res; int ldr; const float* ln_w; const float* ln_b; const float* pe; const float* cls;
+};
+hipError_t launch_conv_encoders_x3(const float*, int, const void*, int, float*, hipStream_t);
+hipError_t launch_gemm_x3(int, const GemmArgsX3Host&, hipStream_t);
 hipError_t launch_conv_encoders(const float*, int, const void*, int, float*, hipStream_t);
 hipError_t launch_fuse(const float*, int, const FuseParamsHost&, float*, hipStream_t);
 hipError_t launch_gemm(int, const GemmArgsHost&, hipStream_t);
@@ -104,22 +115,44 @@ void pack_conv(const float* W, std::vector<float>& out) {
     }
 }
 
-struct DevBuf {
-  void* p = nullptr;
-  size_t bytes = 0;
-};
+// 3xfp16 image: W[N][K] -> chunks [N/256][ceil(K/16)][plane 2][h 2][n 256][8] fp16, plane 0 = hi = f16(w),
+// plane 1 = lo = f16((w - hi) * 2^11); chunk c covers k = 16c + 8h + j (zero past K_real)
+template <class Get>
+void pack_linear_x3(Get W, int N, int K_real, std::vector<_Float16>& out) {
+  const int nch = (K_real + 15) / 16;
+  const size_t base = out.size();
+  out.resize(base + (size_t)(N / 256) * nch * 8192, (_Float16)0.0f);
+  _Float16* o = out.data() + base;
+  for (int nb = 0; nb < N / 256; ++nb)
+    for (int c = 0; c < nch; ++c) {
+      _Float16* ch = o + ((size_t)nb * nch + c) * 8192;
+      for (int h = 0; h < 2; ++h)
+        for (int n = 0; n < 256; ++n)
+          for (int j = 0; j < 8; ++j) {
+            const int k = 16 * c + 8 * h + j;
+            const float w = (k < K_real) ? W(nb * 256 + n, k) : 0.0f;
+            const _Float16 hi = (_Float16)w;
+            const _Float16 lo = (_Float16)((w - (float)hi) * 2048.0f);
+            ch[((0 * 2 + h) * 256 + n) * 8 + j] = hi;
+            ch[((1 * 2 + h) * 256 + n) * 8 + j] = lo;
+          }
+    }
+}
 
 }  // namespace
 
 struct vge_encoder {
+  int mode = VGE_F32;
   int n_layers = 4;
-  // weights
-  float* wbuf = nullptr;          // all packed weights (one allocation)
-  vge::EncDescHost* d_encs = nullptr;
+  // weights: f32 image (all modes: norms, biases, constants; f32-mode matrices) + fp16 hi/lo chunks (x3 mode)
+  float* wbuf = nullptr;
+  _Float16* hbuf = nullptr;
+  void* d_encs = nullptr;         // EncDescHost[10] or EncDescX3Host[10]
   vge::FuseParamsHost fuse{};
-  const float* Wov = nullptr;     // packed [1][1]
+  const void* Wov = nullptr;      // packed (f32 chunks or fp16 chunks)
   struct Layer {
-    const float *in_w, *in_b, *out_w, *out_b, *l1_w, *l1_b, *l2_w, *l2_b, *n1_w, *n1_b, *n2_w, *n2_b;
+    const void *in_w, *out_w, *l1_w, *l2_w;  // packed matrices
+    const float *in_b, *out_b, *l1_b, *l2_b, *n1_w, *n1_b, *n2_w, *n2_b;
   };
   std::vector<Layer> layers;
   const float* cls = nullptr;
@@ -137,7 +170,7 @@ struct vge_encoder {
 extern "C" {
 
 const char* vge_last_error(void) { return g_err.c_str(); }
-const char* vge_version(void) { return "vge 0.1 (gfx950, f32 MFMA)"; }
+const char* vge_version(void) { return "vge 0.2 (gfx950: f32 MFMA + 3xfp16 split MFMA)"; }
 
 // ------------------------------------------------------------------ featurise
 int vge_featurize(const vge_frame_store* st, const int32_t* windows, int n_windows, const float* mean, const float* std_,
@@ -216,7 +249,8 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
                        vge_encoder** out) {
   if (!dims || !weights || !out) return fail(VGE_ERR_ARG, "vge_encoder_create: null argument");
   *out = nullptr;
-  if (compute != VGE_F32) return fail(VGE_ERR_ARG, "vge_encoder_create: unsupported compute dtype");
+  if (compute != VGE_F32 && compute != VGE_F32X3) return fail(VGE_ERR_ARG, "vge_encoder_create: unsupported compute dtype");
+  const bool x3 = compute == VGE_F32X3;
   if (dims->n_modalities != 5 || dims->d_model != 256 || dims->time_heads != 8 || dims->clip_len != 32 ||
       dims->time_layers < 1)
     return fail(VGE_ERR_ARG, "vge_encoder_create: kernels are built for 5 modalities, d_model 256, 8 heads, clip 32");
@@ -237,14 +271,40 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
     const vge_tensor_view* t = it->second;
     int i = 0;
     bool ok = t->ndim == (int)shape.size() && t->data != nullptr;
-    for (int64_t s : shape) ok = ok && i < t->ndim && t->shape[i++] == s;
+    for (int64_t sh : shape) ok = ok && i < t->ndim && t->shape[i++] == sh;
     if (!ok && err.empty()) err = "bad shape for weight: " + k;
     return ok ? t->data : nullptr;
   };
+  auto bail = [&]() { return fail(err.rfind("missing", 0) == 0 ? VGE_ERR_MISSING_WEIGHT : VGE_ERR_WEIGHT_SHAPE, err); };
 
   const int L = dims->time_layers;
-  std::vector<float> pk;  // packed device image (floats), offsets recorded below
-  struct Off { size_t stem, conv, proj, gnw, gnb; int in_col, d_in, P; };
+  std::vector<float> pk;      // f32 device image
+  std::vector<_Float16> ph;   // fp16 device image (x3)
+  // a packed matrix lives in pk (f32 mode) or ph (x3 mode); record (is_half, offset)
+  struct Mat { size_t off; };
+  auto pack_lin = [&](const float* W, int N, int K_real, int ldk, int P) -> Mat {
+    if (x3) {
+      const size_t o = ph.size();
+      pack_linear_x3([&](int n, int k) { return W[(size_t)n * ldk + k]; }, N, K_real, ph);
+      return {o};
+    }
+    const size_t o = pk.size();
+    pack_linear(W, N, K_real, ldk, P, pk);
+    return {o};
+  };
+  auto pack_cv = [&](const float* W) -> Mat {
+    if (x3) {
+      const size_t o = ph.size();
+      // K index = tap * 256 + ci (tap-major panels)
+      pack_linear_x3([&](int n, int k) { return W[((size_t)n * 256 + (k & 255)) * 5 + (k >> 8)]; }, 256, 5 * 256, ph);
+      return {o};
+    }
+    const size_t o = pk.size();
+    pack_conv(W, pk);
+    return {o};
+  };
+
+  struct Off { Mat stem, conv, proj; size_t gnw, gnb; int in_col, d_in, P; };
   std::vector<Off> eoff(10);
   int col_raw = 0, col_diff = VGE_RAW_DIM;
   for (int kind = 0; kind < 2; ++kind) {
@@ -258,28 +318,25 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
       o.in_col = kind == 0 ? col_raw : col_diff;
       if (kind == 0) col_raw += d_in; else col_diff += d_in;
       const float* stem = get(pre + ".stem.weight", {256, d_in, 1});
-      o.stem = pk.size();
-      if (stem) pack_linear(stem, 256, d_in, d_in, o.P, pk);
-      o.conv = pk.size();
+      const float* cw[8];
       for (int b = 0; b < 4; ++b)
-        for (int cv = 1; cv <= 2; ++cv) {
-          const float* w = get(pre + ".blocks." + std::to_string(b) + ".conv" + std::to_string(cv) + ".weight", {256, 256, 5});
-          if (w) pack_conv(w, pk);
-        }
+        for (int cv = 0; cv < 2; ++cv)
+          cw[b * 2 + cv] = get(pre + ".blocks." + std::to_string(b) + ".conv" + std::to_string(cv + 1) + ".weight", {256, 256, 5});
       const float* proj = get(pre + ".proj.weight", {256, 256});
-      o.proj = pk.size();
-      if (proj) pack_linear(proj, 256, 256, 256, 1, pk);
+      const float *gw[4], *gb[4];
+      for (int b = 0; b < 4; ++b) {
+        gw[b] = get(pre + ".blocks." + std::to_string(b) + ".norm.weight", {256});
+        gb[b] = get(pre + ".blocks." + std::to_string(b) + ".norm.bias", {256});
+      }
+      if (!err.empty()) return bail();
+      o.stem = pack_lin(stem, 256, d_in, d_in, o.P);
+      o.conv = pack_cv(cw[0]);
+      for (int c = 1; c < 8; ++c) pack_cv(cw[c]);
+      o.proj = pack_lin(proj, 256, 256, 256, 1);
       o.gnw = pk.size();
-      for (int b = 0; b < 4; ++b) {
-        const float* w = get(pre + ".blocks." + std::to_string(b) + ".norm.weight", {256});
-        if (w) pk.insert(pk.end(), w, w + 256);
-      }
+      for (int b = 0; b < 4; ++b) pk.insert(pk.end(), gw[b], gw[b] + 256);
       o.gnb = pk.size();
-      for (int b = 0; b < 4; ++b) {
-        const float* w = get(pre + ".blocks." + std::to_string(b) + ".norm.bias", {256});
-        if (w) pk.insert(pk.end(), w, w + 256);
-      }
-      if (!err.empty()) return fail(err.rfind("missing", 0) == 0 ? VGE_ERR_MISSING_WEIGHT : VGE_ERR_WEIGHT_SHAPE, err);
+      for (int b = 0; b < 4; ++b) pk.insert(pk.end(), gb[b], gb[b] + 256);
     }
   }
   // fusion: fold the constant query  u = Wk^T (Wq q_ln(latent)),  Wov = Wo Wv
@@ -303,7 +360,7 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
     if (t->ndim == 3 && t->shape[0] == 1 && t->shape[1] >= 33 && t->shape[2] == 256 && t->data) pe = t->data;
     else if (err.empty()) err = "bad shape for weight: pos_enc.pe";
   }
-  if (!err.empty()) return fail(err.rfind("missing", 0) == 0 ? VGE_ERR_MISSING_WEIGHT : VGE_ERR_WEIGHT_SHAPE, err);
+  if (!err.empty()) return bail();
 
   std::vector<double> q(256), Q(256);
   {
@@ -337,14 +394,13 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
       for (int k = 0; k < 256; ++k) a += (double)Wo[(size_t)i * 256 + k] * Wv[(size_t)k * 256 + j];
       wov[(size_t)i * 256 + j] = (float)a;
     }
-  const size_t off_wov = pk.size();
-  pack_linear(wov.data(), 256, 256, 256, 1, pk);
+  const Mat m_wov = pack_lin(wov.data(), 256, 256, 256, 1);
   const size_t off_cls = pk.size();
   pk.insert(pk.end(), cls, cls + 256);
   const size_t off_pe = pk.size();
   pk.insert(pk.end(), pe, pe + 33 * 256);
 
-  struct LOff { size_t in_w, in_b, out_w, out_b, l1_w, l1_b, l2_w, l2_b, n1_w, n1_b, n2_w, n2_b; };
+  struct LOff { Mat in_w, out_w, l1_w, l2_w; size_t in_b, out_b, l1_b, l2_b, n1_w, n1_b, n2_w, n2_b; };
   std::vector<LOff> loff(L);
   for (int l = 0; l < L; ++l) {
     const std::string p = "temporal.layers." + std::to_string(l);
@@ -360,12 +416,12 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
     const float* n1b = get(p + ".norm1.bias", {256});
     const float* n2w = get(p + ".norm2.weight", {256});
     const float* n2b = get(p + ".norm2.bias", {256});
-    if (!err.empty()) return fail(err.rfind("missing", 0) == 0 ? VGE_ERR_MISSING_WEIGHT : VGE_ERR_WEIGHT_SHAPE, err);
+    if (!err.empty()) return bail();
     LOff& o = loff[l];
-    o.in_w = pk.size(); pack_linear(inw, 768, 256, 256, 1, pk);
-    o.out_w = pk.size(); pack_linear(ow, 256, 256, 256, 1, pk);
-    o.l1_w = pk.size(); pack_linear(l1w, 1024, 256, 256, 1, pk);
-    o.l2_w = pk.size(); pack_linear(l2w, 256, 1024, 1024, 4, pk);
+    o.in_w = pack_lin(inw, 768, 256, 256, 1);
+    o.out_w = pack_lin(ow, 256, 256, 256, 1);
+    o.l1_w = pack_lin(l1w, 1024, 256, 256, 1);
+    o.l2_w = pack_lin(l2w, 256, 1024, 1024, 4);
     o.in_b = pk.size(); pk.insert(pk.end(), inb, inb + 768);
     o.out_b = pk.size(); pk.insert(pk.end(), ob, ob + 256);
     o.l1_b = pk.size(); pk.insert(pk.end(), l1b, l1b + 1024);
@@ -377,26 +433,37 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
   }
 
   vge_encoder* enc = new vge_encoder();
+  enc->mode = compute;
   enc->n_layers = L;
-  hipError_t he = vge::encoder_kernel_setup();
+  auto hipfail = [&](hipError_t he) {
+    vge_encoder_destroy(enc);
+    return fail(VGE_ERR_HIP, std::string("vge_encoder_create: ") + hipGetErrorString(he));
+  };
+  hipError_t he = x3 ? vge::encoder_x3_kernel_setup() : vge::encoder_kernel_setup();
   if (he == hipSuccess) he = hipMalloc(&enc->wbuf, pk.size() * sizeof(float));
   if (he == hipSuccess) he = hipMemcpy(enc->wbuf, pk.data(), pk.size() * sizeof(float), hipMemcpyHostToDevice);
-  if (he != hipSuccess) {
-    vge_encoder_destroy(enc);
-    return fail(VGE_ERR_HIP, std::string("vge_encoder_create: ") + hipGetErrorString(he));
-  }
+  if (he == hipSuccess && x3) he = hipMalloc(&enc->hbuf, ph.size() * sizeof(_Float16));
+  if (he == hipSuccess && x3) he = hipMemcpy(enc->hbuf, ph.data(), ph.size() * sizeof(_Float16), hipMemcpyHostToDevice);
+  if (he != hipSuccess) return hipfail(he);
   float* wb = enc->wbuf;
-  std::vector<vge::EncDescHost> descs(10);
-  for (int e = 0; e < 10; ++e) {
-    descs[e] = vge::EncDescHost{wb + eoff[e].stem, wb + eoff[e].conv, wb + eoff[e].proj, wb + eoff[e].gnw,
-                                wb + eoff[e].gnb, eoff[e].in_col, eoff[e].d_in, eoff[e].P, 0};
+  _Float16* hb = enc->hbuf;
+  auto mat = [&](const Mat& m) -> const void* { return x3 ? (const void*)(hb + m.off) : (const void*)(wb + m.off); };
+  if (x3) {
+    std::vector<vge::EncDescX3Host> descs(10);
+    for (int e = 0; e < 10; ++e)
+      descs[e] = vge::EncDescX3Host{hb + eoff[e].stem.off, hb + eoff[e].conv.off, hb + eoff[e].proj.off,
+                                    wb + eoff[e].gnw, wb + eoff[e].gnb, eoff[e].in_col, eoff[e].d_in, eoff[e].P, 0};
+    he = hipMalloc(&enc->d_encs, sizeof(vge::EncDescX3Host) * 10);
+    if (he == hipSuccess) he = hipMemcpy(enc->d_encs, descs.data(), sizeof(vge::EncDescX3Host) * 10, hipMemcpyHostToDevice);
+  } else {
+    std::vector<vge::EncDescHost> descs(10);
+    for (int e = 0; e < 10; ++e)
+      descs[e] = vge::EncDescHost{wb + eoff[e].stem.off, wb + eoff[e].conv.off, wb + eoff[e].proj.off, wb + eoff[e].gnw,
+                                  wb + eoff[e].gnb, eoff[e].in_col, eoff[e].d_in, eoff[e].P, 0};
+    he = hipMalloc(&enc->d_encs, sizeof(vge::EncDescHost) * 10);
+    if (he == hipSuccess) he = hipMemcpy(enc->d_encs, descs.data(), sizeof(vge::EncDescHost) * 10, hipMemcpyHostToDevice);
   }
-  he = hipMalloc(&enc->d_encs, sizeof(vge::EncDescHost) * 10);
-  if (he == hipSuccess) he = hipMemcpy(enc->d_encs, descs.data(), sizeof(vge::EncDescHost) * 10, hipMemcpyHostToDevice);
-  if (he != hipSuccess) {
-    vge_encoder_destroy(enc);
-    return fail(VGE_ERR_HIP, std::string("vge_encoder_create: ") + hipGetErrorString(he));
-  }
+  if (he != hipSuccess) return hipfail(he);
   enc->fuse.kv_w = wb + off_kvw;
   enc->fuse.kv_b = wb + off_kvb;
   enc->fuse.u = wb + off_u;
@@ -408,14 +475,14 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
     enc->fuse.bias[m] = lbias[m];
     enc->fuse.has_motion[m] = 1;
   }
-  enc->Wov = wb + off_wov;
+  enc->Wov = mat(m_wov);
   enc->cls = wb + off_cls;
   enc->pe = wb + off_pe;
   enc->layers.resize(L);
   for (int l = 0; l < L; ++l) {
     const LOff& o = loff[l];
-    enc->layers[l] = vge_encoder::Layer{wb + o.in_w, wb + o.in_b, wb + o.out_w, wb + o.out_b, wb + o.l1_w, wb + o.l1_b,
-                                        wb + o.l2_w, wb + o.l2_b, wb + o.n1_w, wb + o.n1_b, wb + o.n2_w, wb + o.n2_b};
+    enc->layers[l] = vge_encoder::Layer{mat(o.in_w), mat(o.out_w), mat(o.l1_w), mat(o.l2_w), wb + o.in_b, wb + o.out_b,
+                                        wb + o.l1_b, wb + o.l2_b, wb + o.n1_w, wb + o.n1_b, wb + o.n2_w, wb + o.n2_b};
   }
   *out = enc;
   return VGE_OK;
@@ -429,7 +496,7 @@ int vge_encoder_reserve(vge_encoder* enc, int B) {
     enc->ws = nullptr;
     enc->cap = 0;
   }
-  const size_t frames = (size_t)B * 32, tok = align_up((size_t)B * 33, 32);
+  const size_t frames = (size_t)B * 32, tok = align_up((size_t)B * 33, 64);
   const size_t n_enc_out = 10 * frames * 256, n_pooled = frames * 256, n_x = tok * 256, n_qkv = tok * 768,
                n_att = tok * 256, n_x1 = tok * 256, n_h = tok * 1024;
   const size_t total = n_enc_out + n_pooled + n_x + n_qkv + n_att + n_x1 + n_h;
@@ -485,6 +552,7 @@ int vge_encoder_destroy(vge_encoder* enc) {
   if (enc->ws) (void)hipFree(enc->ws);
   if (enc->d_encs) (void)hipFree(enc->d_encs);
   if (enc->wbuf) (void)hipFree(enc->wbuf);
+  if (enc->hbuf) (void)hipFree(enc->hbuf);
   delete enc;
   return VGE_OK;
 }
@@ -500,34 +568,32 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
   hipEvent_t* ev = nullptr;
   if (enc->prof_calls < enc->prof_max) ev = enc->prof_ev.data() + (size_t)(enc->prof_calls++) * (VGE_N_STAGES + 1);
   auto mark = [&](int k) -> hipError_t { return ev ? hipEventRecord(ev[k], s) : hipSuccess; };
+  const bool x3 = enc->mode == VGE_F32X3;
+  // one GEMM launcher for both modes (same epilogues; x3 = 3xfp16 split MFMA, f32 = exact f32 MFMA)
+  auto gemm = [&](int epi, const float* A, int lda, const void* W, float* o, int ldo, int Mr, int K, int N,
+                  const float* bias, const float* res, const float* lw, const float* lb) -> hipError_t {
+    if (x3) {
+      vge::GemmArgsX3Host g{A, lda, (const _Float16*)W, o, ldo, Mr, K, N, bias, res, 256, lw, lb, enc->pe, enc->cls};
+      return vge::launch_gemm_x3(epi, g, s);
+    }
+    vge::GemmArgsHost g{A, lda, (const float*)W, o, ldo, Mr, K, N, bias, res, 256, lw, lb, enc->pe, enc->cls};
+    return vge::launch_gemm(epi, g, s);
+  };
   HIPCHK(mark(0));
-  HIPCHK(vge::launch_conv_encoders(feats, B, enc->d_encs, 10, enc->enc_out, s));
+  if (x3) HIPCHK(vge::launch_conv_encoders_x3(feats, B, enc->d_encs, 10, enc->enc_out, s));
+  else HIPCHK(vge::launch_conv_encoders(feats, B, enc->d_encs, 10, enc->enc_out, s));
   HIPCHK(mark(1));
   HIPCHK(vge::launch_fuse(enc->enc_out, frames, enc->fuse, enc->pooled, s));
   HIPCHK(mark(2));
-  vge::GemmArgsHost g{};
-  g.A = enc->pooled; g.lda = 256; g.W = enc->Wov; g.out = enc->x; g.ldo = 256; g.M = frames; g.K = 256; g.N = 256;
-  g.pe = enc->pe; g.cls = enc->cls;
-  HIPCHK(vge::launch_gemm(vge::EPI_TOKENS, g, s));
+  HIPCHK(gemm(vge::EPI_TOKENS, enc->pooled, 256, enc->Wov, enc->x, 256, frames, 256, 256, nullptr, nullptr, nullptr, nullptr));
   HIPCHK(mark(3));
   for (int l = 0; l < enc->n_layers; ++l) {
     const vge_encoder::Layer& Ly = enc->layers[l];
-    vge::GemmArgsHost a{};
-    a.A = enc->x; a.lda = 256; a.W = Ly.in_w; a.out = enc->qkv; a.ldo = 768; a.M = M; a.K = 256; a.N = 768; a.bias = Ly.in_b;
-    HIPCHK(vge::launch_gemm(vge::EPI_BIAS, a, s));
+    HIPCHK(gemm(vge::EPI_BIAS, enc->x, 256, Ly.in_w, enc->qkv, 768, M, 256, 768, Ly.in_b, nullptr, nullptr, nullptr));
     HIPCHK(vge::launch_attn(enc->qkv, B, enc->att, s));
-    vge::GemmArgsHost o{};
-    o.A = enc->att; o.lda = 256; o.W = Ly.out_w; o.out = enc->x1; o.ldo = 256; o.M = M; o.K = 256; o.N = 256;
-    o.bias = Ly.out_b; o.res = enc->x; o.ldr = 256; o.ln_w = Ly.n1_w; o.ln_b = Ly.n1_b;
-    HIPCHK(vge::launch_gemm(vge::EPI_BIAS_RES_LN, o, s));
-    vge::GemmArgsHost f1{};
-    f1.A = enc->x1; f1.lda = 256; f1.W = Ly.l1_w; f1.out = enc->h; f1.ldo = 1024; f1.M = M; f1.K = 256; f1.N = 1024;
-    f1.bias = Ly.l1_b;
-    HIPCHK(vge::launch_gemm(vge::EPI_BIAS_RELU, f1, s));
-    vge::GemmArgsHost f2{};
-    f2.A = enc->h; f2.lda = 1024; f2.W = Ly.l2_w; f2.out = enc->x; f2.ldo = 256; f2.M = M; f2.K = 1024; f2.N = 256;
-    f2.bias = Ly.l2_b; f2.res = enc->x1; f2.ldr = 256; f2.ln_w = Ly.n2_w; f2.ln_b = Ly.n2_b;
-    HIPCHK(vge::launch_gemm(vge::EPI_BIAS_RES_LN, f2, s));
+    HIPCHK(gemm(vge::EPI_BIAS_RES_LN, enc->att, 256, Ly.out_w, enc->x1, 256, M, 256, 256, Ly.out_b, enc->x, Ly.n1_w, Ly.n1_b));
+    HIPCHK(gemm(vge::EPI_BIAS_RELU, enc->x1, 256, Ly.l1_w, enc->h, 1024, M, 256, 1024, Ly.l1_b, nullptr, nullptr, nullptr));
+    HIPCHK(gemm(vge::EPI_BIAS_RES_LN, enc->h, 1024, Ly.l2_w, enc->x, 256, M, 1024, 256, Ly.l2_b, enc->x1, Ly.n2_w, Ly.n2_b));
   }
   HIPCHK(mark(4));
   HIPCHK(vge::launch_embed_tc(enc->x, B, seq_embed, frame_embed, tc_window, s));

@@ -82,7 +82,7 @@ def _load_state_dict(model_path: str):
     return sd, hp
 
 
-def load_model(model_path, dims_map_raw=None, dims_map_diff=None, device="cuda") -> ops.Encoder:
+def load_model(model_path, dims_map_raw=None, dims_map_diff=None, device="cuda", compute="f32x3") -> ops.Encoder:
     """eval.py:136-165 -> a libvge encoder handle (weights repacked into HBM)."""
     if dims_map_raw is not None:
         if tuple(dims_map_raw.values()) != ops.DIMS_RAW or tuple(dims_map_diff.values()) != ops.DIMS_DIFF:
@@ -92,7 +92,7 @@ def load_model(model_path, dims_map_raw=None, dims_map_diff=None, device="cuda")
     else:
         sd, hp = _load_state_dict(model_path)
     return ops.Encoder(sd, time_layers=int(hp["time_layers"]), time_heads=int(hp["time_heads"]),
-                       d_model=int(hp["d_model"]), device=device)
+                       d_model=int(hp["d_model"]), device=device, compute=compute)
 
 
 def infer_dims_from_stats(stats) -> Tuple[Dict[str, int], Dict[str, int]]:
@@ -266,7 +266,8 @@ def compute_spearman_correlation(model_scores: dict, human_scores_path: str, hum
 
 def run_eval(generated_meshes_dir: str, real_meshes_dir: str, model_path, keypoint_dir: str, real_kp_dir: str,
              human_scores_path: Optional[str] = None, clip_len: int = 32, stride: int = 8,
-             out_json: Optional[str] = "video_scores.json", device="cuda", timings: Optional[dict] = None):
+             out_json: Optional[str] = "video_scores.json", device="cuda", timings: Optional[dict] = None,
+             compute: str = "f32x3"):
     """eval.py __main__ (350-466) on one GPU; returns the combined {video: {ac, tc}} dict."""
     t0 = time.perf_counter()
     real_ds = NpzVideoDataset(real_meshes_dir, filter_classes=ACTION_CLASSES)
@@ -274,7 +275,7 @@ def run_eval(generated_meshes_dir: str, real_meshes_dir: str, model_path, keypoi
     real_store = ops.DeviceFrameStore.from_host(load_frame_store(train_ds.items, real_kp_dir, require_kp=False), device)
     stats = compute_stats_from_npz(train_ds.items, real_kp_dir, device=device, store=real_store)
     dims_raw, dims_diff = infer_dims_from_stats(stats)
-    model = load_model(model_path, dims_raw, dims_diff, device=device)
+    model = load_model(model_path, dims_raw, dims_diff, device=device, compute=compute)
     t1 = time.perf_counter()
     label_dict = {cls: i for i, cls in enumerate(sorted({it.cls for it in real_ds.items}))}
     # centroids need every real-train keypoint file (WindowDataset raises otherwise)

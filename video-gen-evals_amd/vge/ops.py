@@ -102,11 +102,17 @@ def stats_finalize(sums: torch.Tensor, counts: np.ndarray) -> Tuple[torch.Tensor
     return mean, std
 
 
+COMPUTE = {"f32": 0, "f32x3": 1}
+
+
 class Encoder:
-    """HumanActionScorer (model.py:102-193) as a libvge encoder handle owning repacked HBM weights."""
+    """HumanActionScorer (model.py:102-193) as a libvge encoder handle owning repacked HBM weights.
+
+    compute="f32x3" (default): split-precision 3xfp16 MFMA, f32-class results (~1e-7 from exact f32);
+    compute="f32": exact f32 MFMA."""
 
     def __init__(self, state_dict: Dict[str, np.ndarray], time_layers: int = 4, time_heads: int = 8,
-                 d_model: int = 256, device=None):
+                 d_model: int = 256, device=None, compute: str = "f32x3"):
         lib = L.load()
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         dims = L.Dims()
@@ -127,7 +133,9 @@ class Encoder:
                 views[i].shape[j] = s
         h = C.c_void_p()
         with torch.cuda.device(self.device):
-            L.check(lib.vge_encoder_create(C.byref(dims), views, len(state_dict), 0, C.byref(h)), "vge_encoder_create")
+            L.check(lib.vge_encoder_create(C.byref(dims), views, len(state_dict), COMPUTE[compute], C.byref(h)),
+                    "vge_encoder_create")
+        self.compute = compute
         self._h = h
         self._lib = lib
         self.capacity = 0
