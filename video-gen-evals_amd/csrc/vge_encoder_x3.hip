@@ -63,61 +63,76 @@ __device__ __forceinline__ void acc_zero(Acc<NT>& a) {
   }
 }
 
-// one 16-K chunk: A fragments (hi, lo) of this lane, B from the ring slot, NT n-tiles from column nb0
+// A and B fragments of one 16-K chunk for NT n-tiles
 template <int NT>
-__device__ __forceinline__ void mma_chunk_x3(Acc<NT>& acc, const half8 ah, const half8 al, const _Float16* slot, int nb0,
-                                             int lane) {
-  const int i = lane & 31, h = lane >> 5;
+struct Frag {
+  half8 ah, al;
   half8 bh[NT], bl[NT];
+};
+
+template <int NT>
+__device__ __forceinline__ void load_b(Frag<NT>& f, const _Float16* slot, int nb0, int lane) {
+  const int i = lane & 31, h = lane >> 5;
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
     const int col = nb0 + n * 32 + i;
-    bh[n] = *reinterpret_cast<const half8*>(slot + ((0 * 2 + h) * 256 + col) * 8);
-    bl[n] = *reinterpret_cast<const half8*>(slot + ((1 * 2 + h) * 256 + col) * 8);
-  }
-#pragma unroll
-  for (int n = 0; n < NT; ++n) {
-    acc.hh[n] = mfma32(ah, bh[n], acc.hh[n]);
-    acc.x[n] = mfma32(ah, bl[n], acc.x[n]);
-    acc.x[n] = mfma32(al, bh[n], acc.x[n]);
+    f.bh[n] = *reinterpret_cast<const half8*>(slot + ((0 * 2 + h) * 256 + col) * 8);
+    f.bl[n] = *reinterpret_cast<const half8*>(slot + ((1 * 2 + h) * 256 + col) * 8);
   }
 }
 
-// Stream nchunks chunks through the NSLOT-deep ring.  afn(c, ah, al) loads this lane's A fragments.
-// Chunk c+NSLOT-1 is issued at iteration c; the end-of-iteration wait retires chunk c+1 (issued
-// NSLOT-2 iterations earlier) with a counted vmcnt, so the DMA never drains at a barrier.
+template <int NT>
+__device__ __forceinline__ void mma_frag(Acc<NT>& acc, const Frag<NT>& f) {
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    acc.hh[n] = mfma32(f.ah, f.bh[n], acc.hh[n]);
+    acc.x[n] = mfma32(f.ah, f.bl[n], acc.x[n]);
+    acc.x[n] = mfma32(f.al, f.bh[n], acc.x[n]);
+  }
+}
+
+// vmcnt(4 * k) for a runtime k in [0, 3]
+__device__ __forceinline__ void vmcnt_chunks(int k) {
+  if (k >= 3) vmcnt<12>();
+  else if (k == 2) vmcnt<8>();
+  else if (k == 1) vmcnt<4>();
+  else vmcnt<0>();
+}
+
+// Stream nchunks 16 KB weight chunks through the NSLOT-deep LDS ring.  afn(c, ah, al) loads this lane's
+// A fragments of chunk c.  Fragments are double-buffered in registers: iteration c multiplies chunk c
+// from registers while the ds_reads of chunk c+1 and the DMA of chunk c+NSLOT are in flight.  One
+// counted vmcnt (retire chunk c+1, leave the newer DMA in flight) + raw s_barrier per chunk.
+template <int NT, class AFn>
+__device__ __forceinline__ void stream_step(Acc<NT>& acc, Frag<NT>& use, Frag<NT>& nxt, const _Float16* __restrict__ chunks,
+                                            int nchunks, _Float16* ring, AFn& afn, int nb0, int wave, int lane, int c) {
+  // retire chunk c+1 (issued chunks newer than it: c+2 .. min(c+NSLOT-1, n-1))
+  vmcnt_chunks(min(c + NSLOT - 1, nchunks - 1) - (c + 1));
+  lds_barrier();  // every wave's reads of chunk c's slot are done; chunk c+1 visible
+  if (c + NSLOT < nchunks) stage_chunk16(chunks + (size_t)(c + NSLOT) * CHUNK_H, ring + (c % NSLOT) * CHUNK_H, wave, lane);
+  if (c + 1 < nchunks) {
+    afn(c + 1, nxt.ah, nxt.al);
+    load_b(nxt, ring + ((c + 1) % NSLOT) * CHUNK_H, nb0, lane);
+  }
+  mma_frag(acc, use);
+}
+
 template <int NT, class AFn>
 __device__ __forceinline__ void run_stream_x3(Acc<NT>& acc, const _Float16* __restrict__ chunks, int nchunks, _Float16* ring,
                                               AFn afn, int nb0, int wave, int lane) {
-  const int pre = min(nchunks, NSLOT - 1);
+  const int pre = min(nchunks, NSLOT);
   for (int c = 0; c < pre; ++c) stage_chunk16(chunks + (size_t)c * CHUNK_H, ring + c * CHUNK_H, wave, lane);
-  // retire chunk 0 (4 instructions per chunk per wave; the newer pre-1 chunks may stay in flight)
-  switch (pre) {
-    case 1: vmcnt<0>(); break;
-    case 2: vmcnt<4>(); break;
-    case 3: vmcnt<8>(); break;
-    default: vmcnt<12>(); break;
-  }
+  vmcnt_chunks(pre - 1);  // chunk 0 landed
   lds_barrier();
-  int slot = 0;
-  for (int c = 0; c < nchunks; ++c) {
-    const int ahead = c + NSLOT - 1;
-    if (ahead < nchunks) {
-      const int s2 = (slot == 0) ? NSLOT - 1 : slot - 1;  // (slot + NSLOT - 1) % NSLOT
-      stage_chunk16(chunks + (size_t)ahead * CHUNK_H, ring + s2 * CHUNK_H, wave, lane);
-    }
-    half8 ah, al;
-    afn(c, ah, al);
-    mma_chunk_x3<NT>(acc, ah, al, ring + slot * CHUNK_H, nb0, lane);
-    // chunks issued after c+1: min(nchunks-1, c+NSLOT-1) - (c+1)
-    const int newer = min(nchunks - 1, c + NSLOT - 1) - (c + 1);
-    if (newer >= 3) vmcnt<12>();
-    else if (newer == 2) vmcnt<8>();
-    else if (newer == 1) vmcnt<4>();
-    else vmcnt<0>();
-    lds_barrier();
-    slot = (slot == NSLOT - 1) ? 0 : slot + 1;
+  Frag<NT> f0, f1;
+  afn(0, f0.ah, f0.al);
+  load_b(f0, ring, nb0, lane);
+  for (int c = 0; c < nchunks; c += 2) {
+    stream_step(acc, f0, f1, chunks, nchunks, ring, afn, nb0, wave, lane, c);
+    if (c + 1 < nchunks) stream_step(acc, f1, f0, chunks, nchunks, ring, afn, nb0, wave, lane, c + 1);
   }
+  vmcnt<0>();
+  lds_barrier();  // ring and X free for the caller
 }
 
 // ------------------------------------------------------------------ conv encoder chain
@@ -130,15 +145,16 @@ struct EncDescX3 {
   int in_col, d_in, n_stem_panels, pad;
 };
 
-constexpr int CONVX3_LDS_BYTES = 2 * 64 * XS * 2 + NSLOT * CHUNK_H * 2 + 64 * 4;
+constexpr int XROWS = 65;  // 64 activation rows + one all-zero row that masked (out-of-window) taps read
+constexpr int CONVX3_LDS_BYTES = 2 * XROWS * XS * 2 + NSLOT * CHUNK_H * 2 + 64 * 4;
 
 __global__ void __launch_bounds__(256, 1) conv_encoder_x3_kernel(const float* __restrict__ feats, int n_windows,
                                                                   const EncDescX3* __restrict__ encs, int n_enc,
                                                                   float* __restrict__ enc_out) {
   extern __shared__ __attribute__((aligned(16))) _Float16 ldsh[];
-  _Float16* Xh = ldsh;                       // [64][XS]
-  _Float16* Xl = ldsh + 64 * XS;             // [64][XS]
-  _Float16* ring = ldsh + 2 * 64 * XS;       // NSLOT x CHUNK_H
+  _Float16* Xh = ldsh;                       // [65][XS]
+  _Float16* Xl = ldsh + XROWS * XS;          // [65][XS]
+  _Float16* ring = ldsh + 2 * XROWS * XS;    // NSLOT x CHUNK_H
   float* red = reinterpret_cast<float*>(ring + NSLOT * CHUNK_H);  // [16]
 
   const int n_pairs = (n_windows + 1) >> 1;
@@ -158,6 +174,10 @@ __global__ void __launch_bounds__(256, 1) conv_encoder_x3_kernel(const float* __
 
   Acc<4> acc;
   floatx16 res[4];
+  for (int c = threadIdx.x; c < XS; c += 256) {  // the zero row
+    Xh[64 * XS + c] = (_Float16)0.0f;
+    Xl[64 * XS + c] = (_Float16)0.0f;
+  }
 
   auto store_x = [&](const floatx16 (&v)[4]) {
 #pragma unroll
@@ -207,14 +227,10 @@ __global__ void __launch_bounds__(256, 1) conv_encoder_x3_kernel(const float* __
       auto afn = [&](int c, half8& ah, half8& al) {
         const int tap = c >> 4, cc = c & 15;
         const int tt = i + (tap - 2) * dil;
-        const bool ok = (unsigned)tt < 32u;
-        const int off = (rt * 32 + (ok ? tt : 0)) * XS + 16 * cc + 8 * h;
+        const int row = ((unsigned)tt < 32u) ? rt * 32 + tt : 64;  // out of the window -> zero row
+        const int off = row * XS + 16 * cc + 8 * h;
         ah = *reinterpret_cast<const half8*>(Xh + off);
         al = *reinterpret_cast<const half8*>(Xl + off);
-        if (!ok) {
-          ah = half8{0, 0, 0, 0, 0, 0, 0, 0};
-          al = half8{0, 0, 0, 0, 0, 0, 0, 0};
-        }
       };
       run_stream_x3<4>(acc, ed.conv + (size_t)(blk * 2 + cv) * 5 * 16 * CHUNK_H, 5 * 16, ring, afn, nb0, wave, lane);
       floatx16 (&v)[4] = acc.hh;  // combine in place: hh + 2^-11 x
