@@ -24,6 +24,9 @@ namespace {
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
+#ifndef VGE_ABL
+#define VGE_ABL 0  // kernel ablation builds (tools/time_encoder.py); 0 = the product
+#endif
 constexpr int XS = 264;              // fp16 per LDS activation row (256 + 8 pad: conflict-free b128 reads)
 constexpr int CHUNK_H = 8192;        // fp16 per weight chunk (16 KB)
 constexpr int NSLOT = 5;             // LDS ring depth
@@ -109,12 +112,20 @@ __device__ __forceinline__ void stream_step(Acc<NT>& acc, Frag<NT>& use, Frag<NT
   // retire chunk c+1 (issued chunks newer than it: c+2 .. min(c+NSLOT-1, n-1))
   vmcnt_chunks(min(c + NSLOT - 1, nchunks - 1) - (c + 1));
   lds_barrier();  // every wave's reads of chunk c's slot are done; chunk c+1 visible
+#if VGE_ABL != 2
   if (c + NSLOT < nchunks) stage_chunk16(chunks + (size_t)(c + NSLOT) * CHUNK_H, ring + (c % NSLOT) * CHUNK_H, wave, lane);
+#endif
   if (c + 1 < nchunks) {
     afn(c + 1, nxt.ah, nxt.al);
+#if VGE_ABL != 3
     load_b(nxt, ring + ((c + 1) % NSLOT) * CHUNK_H, nb0, lane);
+#endif
   }
+#if VGE_ABL != 1
   mma_frag(acc, use);
+#else
+  asm volatile("" ::"v"(use.ah), "v"(use.bh[0]), "v"(use.bl[NT - 1]));
+#endif
 }
 
 template <int NT, class AFn>
