@@ -7,15 +7,17 @@
 
 Workload (config 2 of BASELINE.json): 256 synthetic 32-frame clips per GPU with pre-extracted
 per-frame features (SMPL rotations, betas, 1024-d token, 120-d keypoints) resident in HBM.  One
-step = featurise all windows (HIP) -> HumanActionScorer forward (f32 MFMA) -> per-video AC + TC
+step = featurise all windows (HIP) -> HumanActionScorer forward (MFMA) -> per-video AC + TC
 (HIP reductions) -> scores copied to pinned host memory.  ModalityStats and the real-class
 centroids (the real set is sharded over ranks, sufficient statistics all-reduced over RCCL) are
 built once in the setup phase and reported separately (`setup_s`).  Weak scaling: every rank
 scores its own 256 clips; no collective in the step.
 
-Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (conv_encoder_kernel, the 10
-MovementConvEncoders, f32 MFMA-bound): achieved = its algorithmic FLOPs per launch / its average
-duration from hipEvents recorded around it on its stream inside the timed steps.  `cpu_baseline`
+Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (the 10 MovementConvEncoders,
+MFMA-bound): achieved = its algorithmic (f32) FLOPs per launch / its average duration from hipEvents
+recorded around it on its stream inside the timed steps; peak = the MFMA ceiling of the compute mode
+(exact f32: 157.3 TF; 3xfp16 split: dense F16 / 3 = 838.9 TF).  `traffic` = HBM bytes per launch from
+the committed PMC pass (profiles/pmc_conv_encoder.json, FETCH_SIZE x2 + WRITE_SIZE per the guide).  `cpu_baseline`
 is the oracle CPU restatement of eval.py (torch-fp32 encoder + numpy featuriser, same work split as
 the reference) timed on this host on a bounded sample of the same workload.
 """
@@ -43,6 +45,12 @@ CLIP_LEN = 32
 CONV_FLOP_PER_WINDOW = 2 * 32 * 256 * 2596 + 80 * 2 * 32 * 256 * 256 * 5 + 10 * 2 * 32 * 256 * 256
 ENCODER_FLOP_PER_WINDOW = 2.0203e9          # FlopCounterMode on model.py at T=32
 F32_MFMA_PEAK_TFLOPS = 157.3                # MI355X_MICROARCH.md: v_mfma_f32_* = FP32 vector peak
+# dense F16 MFMA peak: 256 CUs x 4 SIMDs x 1024 FLOP/clk x 2.4 GHz (MI355X_MICROARCH.md "~2.5 PF dense");
+# the 3xfp16 path issues 3 f16 MFMAs per f32 product, so its ceiling in algorithmic f32 FLOP/s is 1/3 of it
+F16_MFMA_PEAK_TFLOPS = 2516.6
+PEAK_BY_COMPUTE = {"f32": (F32_MFMA_PEAK_TFLOPS, "conv_encoder_kernel (10 MovementConvEncoders, exact f32 MFMA)"),
+                   "f32x3": (F16_MFMA_PEAK_TFLOPS / 3, "conv_encoder_x3_kernel (10 MovementConvEncoders, "
+                                                      "3xfp16 split MFMA, peak = dense F16 MFMA / 3)")}
 HBM_PEAK_GBS = 8000.0
 FEAT_BYTES_PER_WINDOW = 32 * (1024 + 207 + 9 + 10 + 120) * 4 + 32 * 2596 * 4   # read + write
 
@@ -169,6 +177,16 @@ def main():
     vcls = torch.tensor([label[ACTION_CLASSES[((rank * B + i) // 5) % 10]] for i in range(B)], dtype=torch.int32,
                         device=dev)
     feats = torch.empty((B, CLIP_LEN, ops.FEAT_DIM), device=dev)
+    # precision evidence for the timed mode: one pass against the exact-f32 MFMA encoder on the same input
+    ops.featurize(gstore, windows, stats.mean, stats.std, out=feats)
+    seq_a, _, tc_a = enc.encode(feats, frame_embed=False, tc=True)
+    ac_a, tc_a = ops.score_videos(seq_a, tc_a, first, vcls, centroids)
+    enc_ref = ops.Encoder(sd, device=dev, compute="f32")
+    enc_ref.reserve(B)
+    seq_r, _, tc_r = enc_ref.encode(feats, frame_embed=False, tc=True)
+    ac_r, tc_r = ops.score_videos(seq_r, tc_r, first, vcls, centroids)
+    score_dev = max((ac_a - ac_r).abs().max().item(), (tc_a - tc_r).abs().max().item())
+    del enc_ref, seq_r, tc_r, ac_r
     host_ac = torch.empty((B,), dtype=torch.float32, pin_memory=True)
     host_tc = torch.empty((B,), dtype=torch.float64, pin_memory=True)
     torch.cuda.synchronize()
@@ -213,12 +231,13 @@ def main():
     if rank == 0:
         conv_ms = stage_ms["conv_encoders"] / max(ncalls, 1)
         achieved = CONV_FLOP_PER_WINDOW * B / (conv_ms * 1e-3) / 1e12
+        peak, kname = PEAK_BY_COMPUTE[args.compute]
         traffic = None
         pmc = ROOT / "profiles" / "pmc_conv_encoder.json"
         if pmc.exists():
             try:
                 pj = json.loads(pmc.read_text())
-                traffic = pj["hbm_bytes_per_window"] * B
+                traffic = pj[args.compute]["hbm_bytes_per_window"] * B
             except Exception:
                 traffic = None
         total_videos = world * B * args.steps
@@ -233,16 +252,19 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f32",
+            "dtype": args.compute,
+            "precision": {"arith": "f32 in, f32 accumulate (v_mfma_f32_16x16x4_f32)" if args.compute == "f32" else
+                          "f32 operands split into fp16 hi + 2^11-scaled fp16 lo, 3 f16 MFMAs per product, f32 accumulate",
+                          "max_abs_score_dev_vs_exact_f32": score_dev, "north_star_tolerance": 1e-4},
             "data": "synthetic (deterministic generator vge.synth: quaternion-walk SMPL rotations, N(0,1) betas/tokens, "
                     "U[0,1] keypoints with 5% invisible; random-init weights of the reference architecture)",
             "config": {"workload": "BASELINE config 2: fusion-encoder fwd + AC/TC metrics, 256 clips x 32 frames per GPU, "
                                    "pre-extracted features resident in HBM (featurise included in the step)",
                        "clips_per_gpu": B, "frames_per_clip": CLIP_LEN, "windows_per_step_per_gpu": B,
                        "parallelism": f"video-sharded x{world}"},
-            "roofline": {"bound": "mfma", "kernel": "conv_encoder_kernel (10 MovementConvEncoders, f32 MFMA)",
-                         "achieved": achieved, "peak": F32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": achieved / F32_MFMA_PEAK_TFLOPS, "traffic": traffic,
+            "roofline": {"bound": "mfma", "kernel": kname,
+                         "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                         "frac": achieved / peak, "traffic": traffic,
                          "flop_per_launch": CONV_FLOP_PER_WINDOW * B, "avg_launch_ms": conv_ms},
             "stage_ms": {k: v / max(ncalls, 1) for k, v in stage_ms.items()},
             "featurize": {"avg_ms": feat_ms, "bound": "hbm",

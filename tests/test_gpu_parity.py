@@ -181,3 +181,34 @@ def test_featurize_edge_cases_vs_oracle(vg):
         ref = ref / (np.float32(1.0 - 1e-6) + np.float32(1e-6))
         err = np.abs(feats[k] - ref).max()
         assert err < 1e-4, (v, s, err)
+
+
+def test_x3_stem_out_of_fp16_range(vg, golden_state_dict):
+    """z-scored columns far outside the fp16 range (train-set std ~ 0): the split path scales stem rows by
+    powers of two, so it must still match the torch-fp32 oracle."""
+    VE, ops = vg
+    from oracle.encoder import OracleEncoder
+    from vge import synth
+    torch.manual_seed(1)
+    x = torch.randn(6, 32, 2596)
+    x[:, :, 100:110] *= 3e5          # pose block (raw), beyond 65504
+    x[1, 5, 1500] = 2e6               # one diff feature
+    x[2] *= 1e-6                      # a whole window of tiny values
+    model = VE.load_model(golden_state_dict, device=DEV, compute="f32x3")
+    seq, fe, _ = model.encode(x.to(DEV), frame_embed=True, tc=True)
+    o = OracleEncoder(golden_state_dict, synth.DIMS_RAW, synth.DIMS_DIFF)
+    rs, rf, _ = o.forward(x)
+    assert torch.isfinite(seq).all()
+    assert (seq.cpu() - rs).abs().max().item() < 1e-4
+    assert (fe.cpu() - rf).abs().max().item() < 1e-4
+
+
+def test_x3_rejects_weights_outside_split_range(vg, golden_state_dict):
+    VE, ops = vg
+    from vge.lib import VgeError
+    sd = {k: v.copy() for k, v in golden_state_dict.items()}
+    k = next(k for k in sd if k.endswith("proj.weight"))
+    sd[k][0, 0] = 1e5
+    with pytest.raises(VgeError, match="split range"):
+        VE.load_model(sd, device=DEV, compute="f32x3")
+    VE.load_model(sd, device=DEV, compute="f32")   # the exact-f32 path accepts it

@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Condense the rocprofv3 passes of tools/profile_round.sh into profiles/pmc_conv_encoder.json (read by
+bench.py for roofline.traffic) and a per-kernel stats CSV under profiles/.
+
+    python tools/pmc_to_json.py TAG COMPUTE [--windows 256]
+
+Only the timed-workload dispatches are kept: the conv-encoder launch whose grid is 10 encoders x
+windows/2 workgroups.  HBM bytes = FETCH_SIZE x 2 (gfx950 reports half of wide streaming reads,
+MI355X_MICROARCH.md HBM section) + WRITE_SIZE, both in KB as rocprofv3 reports them.
+"""
+import argparse
+import collections
+import csv
+import glob
+import json
+import shutil
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+ap = argparse.ArgumentParser()
+ap.add_argument("tag")
+ap.add_argument("compute")
+ap.add_argument("--windows", type=int, default=256)
+a = ap.parse_args()
+out_dir = ROOT / "gpurun_out"
+KNAME = {"f32x3": "conv_encoder_x3_kernel", "f32": "conv_encoder_kernel("}[a.compute]
+threads = {"f32x3": 512, "f32": 256}[a.compute]
+grid = 10 * ((a.windows + 1) // 2) * threads
+
+
+def rows(kind):
+    for f in glob.glob(str(out_dir / f"prof_{a.tag}_{kind}" / "**" / "*counter_collection.csv"), recursive=True):
+        yield from csv.DictReader(open(f))
+
+
+def counters(kind):
+    vals = collections.defaultdict(list)
+    dur = []
+    for r in rows(kind):
+        if KNAME in r["Kernel_Name"] and int(r["Grid_Size"]) == grid:
+            vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
+            dur.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    return {k: sum(v) / len(v) for k, v in vals.items()}, len(dur)
+
+
+fetch, nf = counters("fetch")
+write, nw = counters("write")
+l2, _ = counters("l2")
+sq, _ = counters("sq")
+# kernel-trace average of the same dispatches
+tr = []
+for f in glob.glob(str(out_dir / f"prof_{a.tag}_trace" / "**" / "*kernel_trace.csv"), recursive=True):
+    for r in csv.DictReader(open(f)):
+        if KNAME in r["Kernel_Name"] and int(r["Grid_Size_X"]) == grid:
+            tr.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+hbm = fetch["FETCH_SIZE"] * 1024 * 2 + write["WRITE_SIZE"] * 1024
+res = {
+    "kernel": KNAME.rstrip("("), "windows_per_launch": a.windows, "dispatches": {"fetch": nf, "write": nw},
+    "fetch_size_kb_raw": fetch["FETCH_SIZE"], "write_size_kb": write["WRITE_SIZE"],
+    "hbm_bytes_per_launch": hbm, "hbm_bytes_per_window": hbm / a.windows,
+    "l2_hit_rate": l2["TCC_HIT_sum"] / (l2["TCC_HIT_sum"] + l2["TCC_MISS_sum"]) if l2 else None,
+    "kernel_trace_avg_ms": sum(tr) / len(tr) / 1e6 if tr else None,
+    "sq": sq, "source": f"gpurun_out/prof_{a.tag}_*/ (tools/profile_round.sh {a.tag} {a.compute})",
+}
+if sq.get("GRBM_GUI_ACTIVE") and tr:
+    res["clock_ghz_est"] = sq["GRBM_GUI_ACTIVE"] / 8 / (sum(tr) / len(tr))   # GRBM counts summed over 8 XCDs
+pj = ROOT / "profiles" / "pmc_conv_encoder.json"
+allj = json.loads(pj.read_text()) if pj.exists() else {}
+allj[a.compute] = res
+pj.write_text(json.dumps(allj, indent=1) + "\n")
+for f in glob.glob(str(out_dir / f"prof_{a.tag}_trace" / "**" / "*kernel_stats.csv"), recursive=True):
+    shutil.copy(f, ROOT / "profiles" / f"rocprof_{a.tag}_kernel_stats.csv")
+print(json.dumps(res, indent=1))

@@ -439,6 +439,10 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
     vge_encoder_destroy(enc);
     return fail(VGE_ERR_HIP, std::string("vge_encoder_create: ") + hipGetErrorString(he));
   };
+  // the fp16 hi plane overflows for |w| >= 65520: refuse rather than score with inf/NaN
+  for (const _Float16 v : ph)
+    if (!std::isfinite((float)v))
+      return fail(VGE_ERR_ARG, "vge_encoder_create: a weight exceeds the 3xfp16 split range (|w| >= 65520); use VGE_F32");
   hipError_t he = x3 ? vge::encoder_x3_kernel_setup() : vge::encoder_kernel_setup();
   if (he == hipSuccess) he = hipMalloc(&enc->wbuf, pk.size() * sizeof(float));
   if (he == hipSuccess) he = hipMemcpy(enc->wbuf, pk.data(), pk.size() * sizeof(float), hipMemcpyHostToDevice);

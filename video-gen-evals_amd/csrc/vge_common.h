@@ -38,7 +38,11 @@ __device__ __forceinline__ float group16_sum(float v) {
 }
 
 // exact-erf GELU (nn.GELU() default; ATen: x * 0.5 * (1 + erf(x * M_SQRT1_2)))
+#if defined(VGE_ABL) && VGE_ABL == 5
+__device__ __forceinline__ float gelu_erf(float x) { return x; }
+#else
 __device__ __forceinline__ float gelu_erf(float x) { return x * 0.5f * (1.0f + erff(x * 0.70710678118654752440f)); }
+#endif
 
 // v_mfma_f32_16x16x4_f32: exact f32 (bitwise an fmaf chain over k).  Lane l supplies
 // A[i = l&15][k = l>>4] and B[k = l>>4][j = l&15]; C/D: col = l&15, row = (l>>4)*4 + r.

@@ -7,11 +7,12 @@
 // deviation from the exact f32 path ~1e-7, see tests/test_gpu_parity.py), at 3 f16 MFMAs per K=16
 // step instead of 4 f32 MFMAs per K=4 step: 5.3x the f32 MFMA rate.
 //
-//   conv_encoder_x3_kernel   MovementConvEncoder x10 (model.py:21-58), one workgroup = 1 encoder x 2 windows,
-//                            activations in LDS as hi/lo planes for the whole chain, weights streamed through
-//                            a 5-slot LDS ring of 16 KB chunks by global_load_lds (chunk c+4 in flight while
-//                            chunk c is multiplied; counted vmcnt + raw s_barrier).
-//   gemm_x3_kernel<EPI>      transformer / token GEMMs with the same fused epilogues as the f32 path.
+//   conv_encoder_x3_kernel   MovementConvEncoder x10 (model.py:21-58): one workgroup = 1 encoder x 2 windows
+//                            (64 rows), 8 waves = 2 row tiles x 4 column quarters.  Activations stay in LDS
+//                            as hi/lo planes for the whole chain; weights stream through a 5-slot LDS ring of
+//                            16 KB chunks by global_load_lds (chunk c+5 issued while chunk c is multiplied;
+//                            counted vmcnt + raw s_barrier; fragments double-buffered in registers).
+//   gemm_x3_kernel<EPI>      transformer / token GEMMs, same tiling, with the fused epilogues of the f32 path.
 //
 // MFMA maps (v_mfma_f32_32x32x16_f16): lane l (i = l&31, h = l>>5) supplies A[row i][k = 8h + j] and
 // B[k = 8h + j][col i], j = 0..7; C/D: col = l&31, row = (r&3) + 8(r>>2) + 4(l>>5), r = 0..15.
@@ -19,17 +20,24 @@
 #include "vge_common.h"
 #include <cstring>
 
+#ifndef VGE_ABL
+#define VGE_ABL 0  // timing-only ablation builds (tools/ablate.sh): 1 no MFMA, 2 no DMA, 3 no B reads,
+                   // 4 no stream barriers, 5 identity GELU; 0 = the product
+#endif
+
 namespace {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
-#ifndef VGE_ABL
-#define VGE_ABL 0  // kernel ablation builds (tools/time_encoder.py); 0 = the product
-#endif
 constexpr int XS = 264;              // fp16 per LDS activation row (256 + 8 pad: conflict-free b128 reads)
-constexpr int CHUNK_H = 8192;        // fp16 per weight chunk (16 KB)
-constexpr int NSLOT = 5;             // LDS ring depth
+constexpr int XSB = XS * 2;          // bytes per activation row
+constexpr int XROWS = 65;            // 64 activation rows + one all-zero row that masked conv taps read
+constexpr int CHUNK_B = 16384;       // bytes per weight chunk
+constexpr int PLANE_B = 8192;        // bytes between the hi and lo planes of a chunk
+constexpr int NSLOT = 5;             // LDS ring depth (chunks)
+constexpr int NWAVE = 8;             // waves per workgroup
+constexpr int NT = 2;                // 32-column n-tiles per wave
 constexpr float LO_SCALE = 2048.0f;  // 2^11
 constexpr float LO_INV = 1.0f / 2048.0f;
 
@@ -43,22 +51,12 @@ __device__ __forceinline__ void split_store(_Float16* hi, _Float16* lo, float v)
   *lo = (_Float16)((v - (float)h) * LO_SCALE);
 }
 
-__device__ __forceinline__ void stage_chunk16(const _Float16* __restrict__ chunk, _Float16* slot, int wave, int lane) {
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int piece = wave * 4 + i;  // 1 KB = 512 fp16 per wave-instruction
-    glds16(chunk + piece * 512 + lane * 8, slot + piece * 512);
-  }
-}
-
-template <int NT>
 struct Acc {
   floatx16 hh[NT];
   floatx16 x[NT];
 };
 
-template <int NT>
-__device__ __forceinline__ void acc_zero(Acc<NT>& a) {
+__device__ __forceinline__ void acc_zero(Acc& a) {
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
 #pragma unroll
@@ -66,26 +64,13 @@ __device__ __forceinline__ void acc_zero(Acc<NT>& a) {
   }
 }
 
-// A and B fragments of one 16-K chunk for NT n-tiles
-template <int NT>
+// A and B fragments of one 16-K chunk
 struct Frag {
   half8 ah, al;
   half8 bh[NT], bl[NT];
 };
 
-template <int NT>
-__device__ __forceinline__ void load_b(Frag<NT>& f, const _Float16* slot, int nb0, int lane) {
-  const int i = lane & 31, h = lane >> 5;
-#pragma unroll
-  for (int n = 0; n < NT; ++n) {
-    const int col = nb0 + n * 32 + i;
-    f.bh[n] = *reinterpret_cast<const half8*>(slot + ((0 * 2 + h) * 256 + col) * 8);
-    f.bl[n] = *reinterpret_cast<const half8*>(slot + ((1 * 2 + h) * 256 + col) * 8);
-  }
-}
-
-template <int NT>
-__device__ __forceinline__ void mma_frag(Acc<NT>& acc, const Frag<NT>& f) {
+__device__ __forceinline__ void mma_frag(Acc& acc, const Frag& f) {
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
     acc.hh[n] = mfma32(f.ah, f.bh[n], acc.hh[n]);
@@ -94,32 +79,60 @@ __device__ __forceinline__ void mma_frag(Acc<NT>& acc, const Frag<NT>& f) {
   }
 }
 
-// vmcnt(4 * k) for a runtime k in [0, 3]
-__device__ __forceinline__ void vmcnt_chunks(int k) {
-  if (k >= 3) vmcnt<12>();
-  else if (k == 2) vmcnt<8>();
-  else if (k == 1) vmcnt<4>();
+// One workgroup's weight stream: n 16 KB chunks in HBM, a 5-slot ring in LDS.
+struct Ring {
+  const char* g;   // chunk 0 of the stream
+  char* lds;       // ring base
+  int n;           // chunks in the stream
+  int wave;        // wave id (scalar)
+  int lane;
+  unsigned boff;   // this lane's B-fragment byte offset inside a chunk (n-tile 0, hi plane)
+
+  // a chunk is 16 x 1 KB wave-pieces, 2 per wave (the LDS destination of a piece is wave-uniform)
+  __device__ __forceinline__ void stage(int c, int slot) const {
+#if VGE_ABL != 2
+    const char* src = g + (size_t)c * CHUNK_B + wave * 1024 + lane * 16;
+    char* dst = lds + slot * CHUNK_B + wave * 1024;
+    glds16(src, dst);
+    glds16(src + NWAVE * 1024, dst + NWAVE * 1024);
+#endif
+  }
+  __device__ __forceinline__ void load_b(Frag& f, int slot) const {
+#if VGE_ABL != 3
+    const char* p = lds + slot * CHUNK_B + boff;
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+      f.bh[n] = *reinterpret_cast<const half8*>(p + n * 512);
+      f.bl[n] = *reinterpret_cast<const half8*>(p + n * 512 + PLANE_B);
+    }
+#endif
+  }
+};
+
+// leave k newer chunks (2 DMA instructions each) in flight, k in [0, 3]
+__device__ __forceinline__ void vm_wait_chunks(int k) {
+  if (k >= 3) vmcnt<6>();
+  else if (k == 2) vmcnt<4>();
+  else if (k == 1) vmcnt<2>();
   else vmcnt<0>();
 }
 
-// Stream nchunks 16 KB weight chunks through the NSLOT-deep LDS ring.  afn(c, ah, al) loads this lane's
-// A fragments of chunk c.  Fragments are double-buffered in registers: iteration c multiplies chunk c
-// from registers while the ds_reads of chunk c+1 and the DMA of chunk c+NSLOT are in flight.  One
-// counted vmcnt (retire chunk c+1, leave the newer DMA in flight) + raw s_barrier per chunk.
-template <int NT, class AFn>
-__device__ __forceinline__ void stream_step(Acc<NT>& acc, Frag<NT>& use, Frag<NT>& nxt, const _Float16* __restrict__ chunks,
-                                            int nchunks, _Float16* ring, AFn& afn, int nb0, int wave, int lane, int c) {
-  // retire chunk c+1 (issued chunks newer than it: c+2 .. min(c+NSLOT-1, n-1))
-  vmcnt_chunks(min(c + NSLOT - 1, nchunks - 1) - (c + 1));
-  lds_barrier();  // every wave's reads of chunk c's slot are done; chunk c+1 visible
-#if VGE_ABL != 2
-  if (c + NSLOT < nchunks) stage_chunk16(chunks + (size_t)(c + NSLOT) * CHUNK_H, ring + (c % NSLOT) * CHUNK_H, wave, lane);
+__device__ __forceinline__ int next_slot(int s) { return s == NSLOT - 1 ? 0 : s + 1; }
+
+// One chunk step: retire chunk c+1, barrier, issue chunk c+NSLOT into chunk c's slot, read chunk c+1's
+// fragments, multiply chunk c from registers.  STEADY: chunks c+2..c+4 are in flight (constant vmcnt).
+template <bool STEADY, class AFn>
+__device__ __forceinline__ void stream_step(Acc& acc, const Frag& use, Frag& nxt, const Ring& R, AFn& afn, int c,
+                                            int slot) {
+  if (STEADY) vmcnt<6>();
+  else vm_wait_chunks(min(c + NSLOT - 1, R.n - 1) - (c + 1));
+#if VGE_ABL != 4
+  lds_barrier();  // every wave's reads of chunk c's slot are done; chunk c+1 has landed for all waves
 #endif
-  if (c + 1 < nchunks) {
-    afn(c + 1, nxt.ah, nxt.al);
-#if VGE_ABL != 3
-    load_b(nxt, ring + ((c + 1) % NSLOT) * CHUNK_H, nb0, lane);
-#endif
+  if (c + NSLOT < R.n) R.stage(c + NSLOT, slot);
+  if (STEADY || c + 1 < R.n) {
+    afn(c + 1, nxt);
+    R.load_b(nxt, next_slot(slot));
   }
 #if VGE_ABL != 1
   mma_frag(acc, use);
@@ -128,27 +141,39 @@ __device__ __forceinline__ void stream_step(Acc<NT>& acc, Frag<NT>& use, Frag<NT
 #endif
 }
 
-template <int NT, class AFn>
-__device__ __forceinline__ void run_stream_x3(Acc<NT>& acc, const _Float16* __restrict__ chunks, int nchunks, _Float16* ring,
-                                              AFn afn, int nb0, int wave, int lane) {
-  const int pre = min(nchunks, NSLOT);
-  for (int c = 0; c < pre; ++c) stage_chunk16(chunks + (size_t)c * CHUNK_H, ring + c * CHUNK_H, wave, lane);
-  vmcnt_chunks(pre - 1);  // chunk 0 landed
+// afn(c, frag) loads this lane's A fragments of chunk c
+template <class AFn>
+__device__ __forceinline__ void run_stream(Acc& acc, const Ring& R, AFn afn) {
+  const int n = R.n;
+  const int pre = min(n, NSLOT);
+  for (int c = 0; c < pre; ++c) R.stage(c, c);
+  vm_wait_chunks(pre - 1);  // chunk 0 landed
   lds_barrier();
-  Frag<NT> f0, f1;
-  afn(0, f0.ah, f0.al);
-  load_b(f0, ring, nb0, lane);
-  for (int c = 0; c < nchunks; c += 2) {
-    stream_step(acc, f0, f1, chunks, nchunks, ring, afn, nb0, wave, lane, c);
-    if (c + 1 < nchunks) stream_step(acc, f1, f0, chunks, nchunks, ring, afn, nb0, wave, lane, c + 1);
+  Frag f0, f1;
+  afn(0, f0);
+  R.load_b(f0, 0);
+  int c = 0, slot = 0;
+  for (; c + 1 <= n - NSLOT; c += 2) {
+    stream_step<true>(acc, f0, f1, R, afn, c, slot);
+    slot = next_slot(slot);
+    stream_step<true>(acc, f1, f0, R, afn, c + 1, slot);
+    slot = next_slot(slot);
+  }
+  for (; c < n; c += 2) {
+    stream_step<false>(acc, f0, f1, R, afn, c, slot);
+    slot = next_slot(slot);
+    if (c + 1 < n) {
+      stream_step<false>(acc, f1, f0, R, afn, c + 1, slot);
+      slot = next_slot(slot);
+    }
   }
   vmcnt<0>();
-  lds_barrier();  // ring and X free for the caller
+  lds_barrier();  // ring and activations free for the caller
 }
 
 // ------------------------------------------------------------------ conv encoder chain
 struct EncDescX3 {
-  const _Float16* stem;  // stem chunks, panel-major: panel p has stem_chunks_p chunks
+  const _Float16* stem;  // stem chunks; panel p (256 K) starts at chunk 16p, the last panel may be short
   const _Float16* conv;  // 8 convs x 5 taps x 16 chunks
   const _Float16* proj;  // 16 chunks
   const float* gn_w;     // [4][256]
@@ -156,18 +181,19 @@ struct EncDescX3 {
   int in_col, d_in, n_stem_panels, pad;
 };
 
-constexpr int XROWS = 65;  // 64 activation rows + one all-zero row that masked (out-of-window) taps read
-constexpr int CONVX3_LDS_BYTES = 2 * XROWS * XS * 2 + NSLOT * CHUNK_H * 2 + 64 * 4;
+constexpr int CONVX3_LDS_BYTES = 2 * XROWS * XSB + NSLOT * CHUNK_B + (24 + 64) * 4;
 
-__global__ void __launch_bounds__(256, 1) conv_encoder_x3_kernel(const float* __restrict__ feats, int n_windows,
+__global__ void __launch_bounds__(512, 1) conv_encoder_x3_kernel(const float* __restrict__ feats, int n_windows,
                                                                   const EncDescX3* __restrict__ encs, int n_enc,
                                                                   float* __restrict__ enc_out) {
-  extern __shared__ __attribute__((aligned(16))) _Float16 ldsh[];
-  _Float16* Xh = ldsh;                       // [65][XS]
-  _Float16* Xl = ldsh + XROWS * XS;          // [65][XS]
-  _Float16* ring = ldsh + 2 * XROWS * XS;    // NSLOT x CHUNK_H
-  float* red = reinterpret_cast<float*>(ring + NSLOT * CHUNK_H);  // [16]
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  _Float16* Xh = reinterpret_cast<_Float16*>(lds_raw);            // [65][XS]
+  _Float16* Xl = Xh + XROWS * XS;                                 // [65][XS]
+  char* ring = lds_raw + 2 * XROWS * XSB;                         // NSLOT x 16 KB
+  float* red = reinterpret_cast<float*>(ring + NSLOT * CHUNK_B);  // [24]: GN sums, GN squares, |x| maxima
+  int* rexp = reinterpret_cast<int*>(red + 24);                   // [64] stem row scale exponents
 
+  // XCD-aware remap: the 8 XCDs take contiguous work ranges, so co-resident blocks of an XCD share an encoder
   const int n_pairs = (n_windows + 1) >> 1;
   const int nblk = n_enc * n_pairs;
   const int b = blockIdx.x;
@@ -176,58 +202,93 @@ __global__ void __launch_bounds__(256, 1) conv_encoder_x3_kernel(const float* __
   const int e = work / n_pairs, pair = work % n_pairs;
   const EncDescX3 ed = encs[e];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int rt = wave >> 1;          // row tile = window within the pair
-  const int nb0 = (wave & 1) * 128;  // this wave's 128 output columns
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int rt = wave >> 2;         // row tile = window within the pair
+  const int nb0 = (wave & 3) * 64;  // this wave's 64 output columns
   const int i = lane & 31, h = lane >> 5;
   const int win = pair * 2 + rt;
-  const bool win_valid = win < n_windows;
+  const unsigned boff = (unsigned)((h * 256 + nb0 + i) * 16);
+  const char* xa = reinterpret_cast<const char*>(Xh) + h * 16;  // this lane's 8 k-values of a 16-K chunk column
 
-  Acc<4> acc;
-  floatx16 res[4];
-  for (int c = threadIdx.x; c < XS; c += 256) {  // the zero row
-    Xh[64 * XS + c] = (_Float16)0.0f;
-    Xl[64 * XS + c] = (_Float16)0.0f;
+  Acc acc;
+  floatx16 res[NT];
+  if (tid < XS) {  // the zero row
+    Xh[64 * XS + tid] = (_Float16)0.0f;
+    Xl[64 * XS + tid] = (_Float16)0.0f;
   }
 
-  auto store_x = [&](const floatx16 (&v)[4]) {
+  // Store the next conv's input as window * 2^-e (exact) with the window's largest |value| in [2^8, 2^9), so
+  // the fp16 planes neither overflow nor lose small values; returns e (the same for the row tile's 4 waves)
+  // for the consumer to multiply its accumulators back by.  Caller guarantees X is no longer being read.
+  auto store_x = [&](const floatx16 (&v)[NT]) -> int {
+    float m = 0.f;
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
+    for (int n = 0; n < NT; ++n)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) m = fmaxf(m, fabsf(v[n][r]));
+    m = wave_max(m);
+    if (lane == 0) red[16 + wave] = m;
+    __syncthreads();
+    const float* rm = red + 16 + rt * 4;
+    const float mm = fmaxf(fmaxf(rm[0], rm[1]), fmaxf(rm[2], rm[3]));
+    const int e = (mm > 0.f && mm <= 3.0e38f) ? ilogbf(mm) - 8 : 0;
+#pragma unroll
+    for (int n = 0; n < NT; ++n)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         const int col = nb0 + n * 32 + i;
-        split_store(Xh + row * XS + col, Xl + row * XS + col, v[n][r]);
+        split_store(Xh + row * XS + col, Xl + row * XS + col, ldexpf(v[n][r], -e));
       }
+    return e;
   };
+  auto a_at = [&](int row_byte, int cc, Frag& f) {
+    const char* p = xa + row_byte + cc * 32;
+    f.ah = *reinterpret_cast<const half8*>(p);
+    f.al = *reinterpret_cast<const half8*>(p + XROWS * XSB);
+  };
+  const int own_row_b = (rt * 32 + i) * XSB;
 
   // ---------------- stem: Conv1d(d_in -> 256, k=1, no bias), K streamed in 256-wide panels
+  // Per-row power-of-two scale: z-scored features leave the fp16 range when a column's train-set std is ~0
+  // ((x - mean) / (std + 1e-6)), so row m is split as A[m,:] * 2^-e_m (exact) with its largest |value| in
+  // [2^8, 2^9), and the row's accumulators are multiplied back by 2^e_m (exact).
+  for (int r = wave * 8; r < wave * 8 + 8; ++r) {
+    const int w = pair * 2 + (r >> 5);
+    float m = 0.f;
+    if (w < n_windows) {
+      const float* src = feats + ((size_t)w * VGE_T + (r & 31)) * VGE_FD + ed.in_col;
+      for (int c = lane; c < ed.d_in; c += 64) m = fmaxf(m, fabsf(src[c]));
+    }
+    m = wave_max(m);
+    if (lane == 0) rexp[r] = (m > 0.f && m <= 3.0e38f) ? ilogbf(m) - 8 : 0;
+  }
   acc_zero(acc);
-  const _Float16* stem_chunks = ed.stem;
   for (int p = 0; p < ed.n_stem_panels; ++p) {
     const int kw = min(256, ed.d_in - p * 256);
-    const int nch = (kw + 15) >> 4;
     __syncthreads();
-    for (int r = 0; r < 64; ++r) {
-      const int w = pair * 2 + (r >> 5);
-      float v = 0.f;
-      if (tid < kw && w < n_windows) v = feats[((size_t)w * VGE_T + (r & 31)) * VGE_FD + ed.in_col + p * 256 + tid];
-      split_store(Xh + r * XS + tid, Xl + r * XS + tid, v);
+    {
+      const int c = tid & 255;
+      for (int r = tid >> 8; r < 64; r += 2) {
+        const int w = pair * 2 + (r >> 5);
+        float v = 0.f;
+        if (c < kw && w < n_windows) v = feats[((size_t)w * VGE_T + (r & 31)) * VGE_FD + ed.in_col + p * 256 + c];
+        split_store(Xh + r * XS + c, Xl + r * XS + c, ldexpf(v, -rexp[r]));
+      }
     }
     __syncthreads();
-    auto afn = [&](int c, half8& ah, half8& al) {
-      const int off = (rt * 32 + i) * XS + 16 * c + 8 * h;
-      ah = *reinterpret_cast<const half8*>(Xh + off);
-      al = *reinterpret_cast<const half8*>(Xl + off);
-    };
-    run_stream_x3<4>(acc, stem_chunks, nch, ring, afn, nb0, wave, lane);
-    stem_chunks += (size_t)nch * CHUNK_H;
+    auto afn = [&](int c, Frag& f) { a_at(own_row_b, c, f); };
+    const Ring R{reinterpret_cast<const char*>(ed.stem) + (size_t)p * 16 * CHUNK_B, ring, (kw + 15) >> 4, wave, lane,
+                 boff};
+    run_stream(acc, R, afn);
   }
 #pragma unroll
-  for (int n = 0; n < 4; ++n)
+  for (int n = 0; n < NT; ++n)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) res[n][r] = acc.hh[n][r] + acc.x[n][r] * LO_INV;
-  store_x(res);
+    for (int r = 0; r < 16; ++r)
+      res[n][r] = ldexpf(acc.hh[n][r] + acc.x[n][r] * LO_INV, rexp[rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h]);
+  int xexp = store_x(res);
   __syncthreads();
 
   // ---------------- 4 TemporalConvBlocks
@@ -235,49 +296,52 @@ __global__ void __launch_bounds__(256, 1) conv_encoder_x3_kernel(const float* __
     const int dil = 1 << blk;
     for (int cv = 0; cv < 2; ++cv) {
       acc_zero(acc);
-      auto afn = [&](int c, half8& ah, half8& al) {
+      auto afn = [&](int c, Frag& f) {
         const int tap = c >> 4, cc = c & 15;
         const int tt = i + (tap - 2) * dil;
         const int row = ((unsigned)tt < 32u) ? rt * 32 + tt : 64;  // out of the window -> zero row
-        const int off = row * XS + 16 * cc + 8 * h;
-        ah = *reinterpret_cast<const half8*>(Xh + off);
-        al = *reinterpret_cast<const half8*>(Xl + off);
+        a_at(row * XSB, cc, f);
       };
-      run_stream_x3<4>(acc, ed.conv + (size_t)(blk * 2 + cv) * 5 * 16 * CHUNK_H, 5 * 16, ring, afn, nb0, wave, lane);
-      floatx16 (&v)[4] = acc.hh;  // combine in place: hh + 2^-11 x
+      const Ring R{reinterpret_cast<const char*>(ed.conv) + (size_t)(blk * 2 + cv) * 5 * 16 * CHUNK_B, ring, 5 * 16,
+                   wave, lane, boff};
+      run_stream(acc, R, afn);
+      floatx16 (&v)[NT] = acc.hh;  // combine in place: (hh + 2^-11 x) * 2^xexp
+      const float xs = ldexpf(1.0f, xexp);
       if (cv == 0) {
 #pragma unroll
-        for (int n = 0; n < 4; ++n)
+        for (int n = 0; n < NT; ++n)
 #pragma unroll
-          for (int r = 0; r < 16; ++r) v[n][r] = gelu_erf(acc.hh[n][r] + acc.x[n][r] * LO_INV);
+          for (int r = 0; r < 16; ++r) v[n][r] = gelu_erf((acc.hh[n][r] + acc.x[n][r] * LO_INV) * xs);
       } else {
+        // GroupNorm(1, 256) over the window: 32 x 256 values held by the row tile's 4 waves
         float s = 0.f;
 #pragma unroll
-        for (int n = 0; n < 4; ++n)
+        for (int n = 0; n < NT; ++n)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            v[n][r] = gelu_erf(acc.hh[n][r] + acc.x[n][r] * LO_INV + res[n][r]);
+            v[n][r] = gelu_erf((acc.hh[n][r] + acc.x[n][r] * LO_INV) * xs + res[n][r]);
             s += v[n][r];
           }
         s = wave_sum(s);
         if (lane == 0) red[wave] = s;
         __syncthreads();
-        const float mean = (red[rt * 2] + red[rt * 2 + 1]) / 8192.0f;
+        const float mean = (red[rt * 4] + red[rt * 4 + 1] + red[rt * 4 + 2] + red[rt * 4 + 3]) / 8192.0f;
         float q = 0.f;
 #pragma unroll
-        for (int n = 0; n < 4; ++n)
+        for (int n = 0; n < NT; ++n)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const float d = v[n][r] - mean;
             q += d * d;
           }
         q = wave_sum(q);
-        if (lane == 0) red[4 + wave] = q;
+        if (lane == 0) red[8 + wave] = q;
         __syncthreads();
-        const float var = (red[4 + rt * 2] + red[4 + rt * 2 + 1]) / 8192.0f;
+        const float var =
+            (red[8 + rt * 4] + red[8 + rt * 4 + 1] + red[8 + rt * 4 + 2] + red[8 + rt * 4 + 3]) / 8192.0f;
         const float rstd = 1.0f / sqrtf(var + 1e-5f);
 #pragma unroll
-        for (int n = 0; n < 4; ++n) {
+        for (int n = 0; n < NT; ++n) {
           const int col = nb0 + n * 32 + i;
           const float w_ = ed.gn_w[blk * 256 + col], b_ = ed.gn_b[blk * 256 + col];
 #pragma unroll
@@ -287,7 +351,7 @@ __global__ void __launch_bounds__(256, 1) conv_encoder_x3_kernel(const float* __
           }
         }
       }
-      store_x(v);  // the stream's final barrier retired every read of X
+      xexp = store_x(v);  // the stream's final barrier retired every read of X
       __syncthreads();
     }
   }
@@ -295,21 +359,19 @@ __global__ void __launch_bounds__(256, 1) conv_encoder_x3_kernel(const float* __
   // ---------------- proj: Linear(256 -> 256, no bias)
   acc_zero(acc);
   {
-    auto afn = [&](int c, half8& ah, half8& al) {
-      const int off = (rt * 32 + i) * XS + 16 * c + 8 * h;
-      ah = *reinterpret_cast<const half8*>(Xh + off);
-      al = *reinterpret_cast<const half8*>(Xl + off);
-    };
-    run_stream_x3<4>(acc, ed.proj, 16, ring, afn, nb0, wave, lane);
+    auto afn = [&](int c, Frag& f) { a_at(own_row_b, c, f); };
+    const Ring R{reinterpret_cast<const char*>(ed.proj), ring, 16, wave, lane, boff};
+    run_stream(acc, R, afn);
   }
-  if (win_valid) {
+  if (win < n_windows) {
+    const float xs = ldexpf(1.0f, xexp);
     float* o = enc_out + ((size_t)e * n_windows * VGE_T + (size_t)win * VGE_T) * VGE_D;
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
+    for (int n = 0; n < NT; ++n)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-        o[row * VGE_D + nb0 + n * 32 + i] = acc.hh[n][r] + acc.x[n][r] * LO_INV;
+        o[row * VGE_D + nb0 + n * 32 + i] = (acc.hh[n][r] + acc.x[n][r] * LO_INV) * xs;
       }
   }
 }
@@ -319,7 +381,7 @@ enum Epi { EPI_TOKENS = 0, EPI_BIAS = 1, EPI_BIAS_RELU = 2, EPI_BIAS_RES_LN = 3 
 
 struct GemmArgsX3 {
   const float* A;  int lda;
-  const _Float16* W;            // chunks [N/256][K/16][CHUNK_H]
+  const _Float16* W;            // chunks [N/256][K/16][16 KB]
   float* out;      int ldo;
   int M, K, N;
   const float* bias;
@@ -329,57 +391,87 @@ struct GemmArgsX3 {
   const float* cls;
 };
 
-// block = 4 waves = 2 row tiles (32 rows) x 2 column halves (128 cols): BM = 64, BN = 256
-constexpr int GEMMX3_LDS_BYTES = 2 * 64 * XS * 2 + NSLOT * CHUNK_H * 2 + 128 * 4;
+// block = 8 waves = 2 row tiles (32 rows) x 4 column quarters (64 cols): BM = 64, BN = 256
+constexpr int GEMMX3_LDS_BYTES = 2 * 64 * XSB + NSLOT * CHUNK_B + (64 * 4 + 8) * 4;
 
 template <int EPI>
-__global__ void __launch_bounds__(256, 1) gemm_x3_kernel(GemmArgsX3 ga) {
-  extern __shared__ __attribute__((aligned(16))) _Float16 ldsh[];
-  _Float16* Xh = ldsh;
-  _Float16* Xl = ldsh + 64 * XS;
-  _Float16* ring = ldsh + 2 * 64 * XS;
-  float* red = reinterpret_cast<float*>(ring + NSLOT * CHUNK_H);  // [64 rows][2]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int rt = wave >> 1, nb0 = (wave & 1) * 128;
+__global__ void __launch_bounds__(512, 1) gemm_x3_kernel(GemmArgsX3 ga) {
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  _Float16* Xh = reinterpret_cast<_Float16*>(lds_raw);
+  _Float16* Xl = Xh + 64 * XS;
+  char* ring = lds_raw + 2 * 64 * XSB;
+  float* red = reinterpret_cast<float*>(ring + NSLOT * CHUNK_B);  // [64 rows][4 column quarters] + [8] maxima
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int rt = wave >> 2, cq = wave & 3, nb0 = cq * 64;
   const int i = lane & 31, h = lane >> 5;
   const int row0 = blockIdx.x * 64, nb = blockIdx.y;
   const int n_panels = ga.K / 256;
+  const unsigned boff = (unsigned)((h * 256 + nb0 + i) * 16);
+  const char* xa = reinterpret_cast<const char*>(Xh) + (rt * 32 + i) * XSB + h * 16;
 
-  Acc<4> acc;
+  Acc acc;
   acc_zero(acc);
+  int aexp = 0;  // the accumulators hold C * 2^-aexp
   for (int p = 0; p < n_panels; ++p) {
-    __syncthreads();
-    // stage the 64 x 256 A panel as hi/lo planes (rows >= M read as 0)
-    for (int r = 0; r < 64; ++r) {
-      const int row = row0 + r;
-      const float v = (row < ga.M) ? ga.A[(size_t)row * ga.lda + p * 256 + tid] : 0.f;
-      split_store(Xh + r * XS + tid, Xl + r * XS + tid, v);
+    // the 64 x 256 A panel (rows >= M read as 0) as hi/lo planes of panel * 2^-e, its largest |value| in
+    // [2^8, 2^9): exact power-of-two scaling that keeps fp16 in range; the accumulators are rescaled to match
+    const int c = tid & 255;
+    float a[32];
+    float m = 0.f;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      const int row = row0 + (tid >> 8) + 2 * j;
+      a[j] = (row < ga.M) ? ga.A[(size_t)row * ga.lda + p * 256 + c] : 0.f;
+      m = fmaxf(m, fabsf(a[j]));
+    }
+    m = wave_max(m);
+    if (lane == 0) red[256 + wave] = m;
+    __syncthreads();  // also: every wave is past the previous panel's stream
+    float mm = red[256];
+#pragma unroll
+    for (int w = 1; w < NWAVE; ++w) mm = fmaxf(mm, red[256 + w]);
+    const int e = (mm > 0.f && mm <= 3.0e38f) ? ilogbf(mm) - 8 : 0;
+    if (p > 0 && e != aexp) {
+      const float f = ldexpf(1.0f, aexp - e);
+#pragma unroll
+      for (int n = 0; n < NT; ++n)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { acc.hh[n][r] *= f; acc.x[n][r] *= f; }
+    }
+    aexp = e;
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      const int r = (tid >> 8) + 2 * j;
+      split_store(Xh + r * XS + c, Xl + r * XS + c, ldexpf(a[j], -e));
     }
     __syncthreads();
-    auto afn = [&](int c, half8& ah, half8& al) {
-      const int off = (rt * 32 + i) * XS + 16 * c + 8 * h;
-      ah = *reinterpret_cast<const half8*>(Xh + off);
-      al = *reinterpret_cast<const half8*>(Xl + off);
+    auto afn = [&](int cc, Frag& f) {
+      f.ah = *reinterpret_cast<const half8*>(xa + cc * 32);
+      f.al = *reinterpret_cast<const half8*>(xa + cc * 32 + 64 * XSB);
     };
-    run_stream_x3<4>(acc, ga.W + ((size_t)nb * (ga.K / 16) + p * 16) * CHUNK_H, 16, ring, afn, nb0, wave, lane);
+    const Ring R{reinterpret_cast<const char*>(ga.W) + ((size_t)nb * (ga.K / 16) + p * 16) * CHUNK_B, ring, 16, wave,
+                 lane, boff};
+    run_stream(acc, R, afn);
   }
 
-  float v[4][16];
+  float v[NT][16];
+  const float as = ldexpf(1.0f, aexp);
 #pragma unroll
-  for (int n = 0; n < 4; ++n)
+  for (int n = 0; n < NT; ++n)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[n][r] = acc.hh[n][r] + acc.x[n][r] * LO_INV;
+    for (int r = 0; r < 16; ++r) v[n][r] = (acc.hh[n][r] + acc.x[n][r] * LO_INV) * as;
   const int colb = nb * 256 + nb0;
-  auto rowof = [&](int r) { return row0 + rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h; };
+  auto lrow = [&](int r) { return rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h; };
 
   if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) {
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
+    for (int n = 0; n < NT; ++n) {
       const int col = colb + n * 32 + i;
       const float bb = ga.bias[col];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = rowof(r);
+        const int row = row0 + lrow(r);
         float x = v[n][r] + bb;
         if (EPI == EPI_BIAS_RELU) x = fmaxf(x, 0.f);
         if (row < ga.M) ga.out[(size_t)row * ga.ldo + col] = x;
@@ -387,11 +479,11 @@ __global__ void __launch_bounds__(256, 1) gemm_x3_kernel(GemmArgsX3 ga) {
     }
   } else if constexpr (EPI == EPI_TOKENS) {
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
+    for (int n = 0; n < NT; ++n) {
       const int col = colb + n * 32 + i;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = rowof(r);
+        const int row = row0 + lrow(r);
         if (row < ga.M) {
           const int w = row >> 5, t = row & 31;
           ga.out[((size_t)w * VGE_TOK + 1 + t) * ga.ldo + col] = v[n][r] + ga.pe[(1 + t) * VGE_D + col];
@@ -400,44 +492,43 @@ __global__ void __launch_bounds__(256, 1) gemm_x3_kernel(GemmArgsX3 ga) {
       }
     }
   } else {  // EPI_BIAS_RES_LN over the 256 columns (N == 256, one column block)
-    float s[16];
+    float s[16], q[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) s[r] = 0.f;
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
+    for (int n = 0; n < NT; ++n) {
       const int col = colb + n * 32 + i;
       const float bb = ga.bias[col];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = rowof(r);
+        const int row = row0 + lrow(r);
         v[n][r] += bb + ((row < ga.M) ? ga.res[(size_t)row * ga.ldr + col] : 0.f);
         s[r] += v[n][r];
       }
     }
-    // row sums: reduce over the 32 lanes that share h (xor 1..16 stays inside a 32-lane half)
+    // row sums: reduce over the 32 lanes that share h (xor 1..16 stays inside a 32-lane half), then over
+    // the 4 column-quarter waves through LDS
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
 #pragma unroll
       for (int o = 16; o >= 1; o >>= 1) s[r] += __shfl_xor(s[r], o, 64);
     }
-    __syncthreads();
     if (i == 0) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) red[(rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * 2 + (wave & 1)] = s[r];
+      for (int r = 0; r < 16; ++r) red[lrow(r) * 4 + cq] = s[r];
     }
     __syncthreads();
-    float mean[16], q[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int lr = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      mean[r] = (red[lr * 2] + red[lr * 2 + 1]) / 256.0f;
+      const float* rr = red + lrow(r) * 4;
+      s[r] = (rr[0] + rr[1] + rr[2] + rr[3]) / 256.0f;  // mean
       q[r] = 0.f;
     }
 #pragma unroll
-    for (int n = 0; n < 4; ++n)
+    for (int n = 0; n < NT; ++n)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float d = v[n][r] - mean[r];
+        const float d = v[n][r] - s[r];
         q[r] += d * d;
       }
 #pragma unroll
@@ -445,25 +536,25 @@ __global__ void __launch_bounds__(256, 1) gemm_x3_kernel(GemmArgsX3 ga) {
 #pragma unroll
       for (int o = 16; o >= 1; o >>= 1) q[r] += __shfl_xor(q[r], o, 64);
     }
-    __syncthreads();
+    __syncthreads();  // every wave has read the sums
     if (i == 0) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) red[(rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * 2 + (wave & 1)] = q[r];
+      for (int r = 0; r < 16; ++r) red[lrow(r) * 4 + cq] = q[r];
     }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const int lr = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-      q[r] = 1.0f / sqrtf((red[lr * 2] + red[lr * 2 + 1]) / 256.0f + 1e-5f);
+      const float* rr = red + lrow(r) * 4;
+      q[r] = 1.0f / sqrtf((rr[0] + rr[1] + rr[2] + rr[3]) / 256.0f + 1e-5f);
     }
 #pragma unroll
-    for (int n = 0; n < 4; ++n) {
+    for (int n = 0; n < NT; ++n) {
       const int col = colb + n * 32 + i;
       const float lw = ga.ln_w[col], lb = ga.ln_b[col];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = rowof(r);
-        if (row < ga.M) ga.out[(size_t)row * ga.ldo + col] = (v[n][r] - mean[r]) * q[r] * lw + lb;
+        const int row = row0 + lrow(r);
+        if (row < ga.M) ga.out[(size_t)row * ga.ldo + col] = (v[n][r] - s[r]) * q[r] * lw + lb;
       }
     }
   }
@@ -502,7 +593,7 @@ hipError_t encoder_x3_kernel_setup() {
 hipError_t launch_conv_encoders_x3(const float* feats, int n_windows, const void* encs, int n_enc, float* enc_out,
                                    hipStream_t s) {
   const int n_pairs = (n_windows + 1) / 2;
-  hipLaunchKernelGGL(conv_encoder_x3_kernel, dim3(n_enc * n_pairs), dim3(256), CONVX3_LDS_BYTES, s, feats, n_windows,
+  hipLaunchKernelGGL(conv_encoder_x3_kernel, dim3(n_enc * n_pairs), dim3(512), CONVX3_LDS_BYTES, s, feats, n_windows,
                      reinterpret_cast<const EncDescX3*>(encs), n_enc, enc_out);
   return hipGetLastError();
 }
@@ -512,10 +603,10 @@ hipError_t launch_gemm_x3(int epi, const GemmArgsX3Host& a, hipStream_t s) {
   memcpy(&g, &a, sizeof(g));
   dim3 grid((a.M + 63) / 64, a.N / 256);
   switch (epi) {
-    case EPI_TOKENS: hipLaunchKernelGGL(gemm_x3_kernel<EPI_TOKENS>, grid, dim3(256), GEMMX3_LDS_BYTES, s, g); break;
-    case EPI_BIAS: hipLaunchKernelGGL(gemm_x3_kernel<EPI_BIAS>, grid, dim3(256), GEMMX3_LDS_BYTES, s, g); break;
-    case EPI_BIAS_RELU: hipLaunchKernelGGL(gemm_x3_kernel<EPI_BIAS_RELU>, grid, dim3(256), GEMMX3_LDS_BYTES, s, g); break;
-    default: hipLaunchKernelGGL(gemm_x3_kernel<EPI_BIAS_RES_LN>, grid, dim3(256), GEMMX3_LDS_BYTES, s, g); break;
+    case EPI_TOKENS: hipLaunchKernelGGL(gemm_x3_kernel<EPI_TOKENS>, grid, dim3(512), GEMMX3_LDS_BYTES, s, g); break;
+    case EPI_BIAS: hipLaunchKernelGGL(gemm_x3_kernel<EPI_BIAS>, grid, dim3(512), GEMMX3_LDS_BYTES, s, g); break;
+    case EPI_BIAS_RELU: hipLaunchKernelGGL(gemm_x3_kernel<EPI_BIAS_RELU>, grid, dim3(512), GEMMX3_LDS_BYTES, s, g); break;
+    default: hipLaunchKernelGGL(gemm_x3_kernel<EPI_BIAS_RES_LN>, grid, dim3(512), GEMMX3_LDS_BYTES, s, g); break;
   }
   return hipGetLastError();
 }
