@@ -38,7 +38,7 @@ __device__ __forceinline__ float group16_sum(float v) {
 }
 
 // exact-erf GELU (nn.GELU() default; ATen: x * 0.5 * (1 + erf(x * M_SQRT1_2)))
-#if defined(VGE_ABL) && VGE_ABL == 5
+#if defined(VGE_ABL) && (VGE_ABL & 16)
 __device__ __forceinline__ float gelu_erf(float x) { return x; }
 #else
 __device__ __forceinline__ float gelu_erf(float x) { return x * 0.5f * (1.0f + erff(x * 0.70710678118654752440f)); }

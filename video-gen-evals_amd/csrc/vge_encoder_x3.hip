@@ -21,8 +21,8 @@
 #include <cstring>
 
 #ifndef VGE_ABL
-#define VGE_ABL 0  // timing-only ablation builds (tools/ablate.sh): 1 no MFMA, 2 no DMA, 3 no B reads,
-                   // 4 no stream barriers, 5 identity GELU; 0 = the product
+#define VGE_ABL 0  // timing-only ablation builds (tools/ablate.sh), a bit mask: 1 no MFMA, 2 no DMA after the
+                   // prologue, 4 no B reads, 8 no stream barriers, 16 identity GELU; 0 = the product
 #endif
 
 namespace {
@@ -90,7 +90,7 @@ struct Ring {
 
   // a chunk is 16 x 1 KB wave-pieces, 2 per wave (the LDS destination of a piece is wave-uniform)
   __device__ __forceinline__ void stage(int c, int slot) const {
-#if VGE_ABL != 2
+#if !(VGE_ABL & 2)
     const char* src = g + (size_t)c * CHUNK_B + wave * 1024 + lane * 16;
     char* dst = lds + slot * CHUNK_B + wave * 1024;
     glds16(src, dst);
@@ -98,7 +98,7 @@ struct Ring {
 #endif
   }
   __device__ __forceinline__ void load_b(Frag& f, int slot) const {
-#if VGE_ABL != 3
+#if !(VGE_ABL & 4)
     const char* p = lds + slot * CHUNK_B + boff;
 #pragma unroll
     for (int n = 0; n < NT; ++n) {
@@ -126,7 +126,7 @@ __device__ __forceinline__ void stream_step(Acc& acc, const Frag& use, Frag& nxt
                                             int slot) {
   if (STEADY) vmcnt<6>();
   else vm_wait_chunks(min(c + NSLOT - 1, R.n - 1) - (c + 1));
-#if VGE_ABL != 4
+#if !(VGE_ABL & 8)
   lds_barrier();  // every wave's reads of chunk c's slot are done; chunk c+1 has landed for all waves
 #endif
   if (c + NSLOT < R.n) R.stage(c + NSLOT, slot);
@@ -134,7 +134,7 @@ __device__ __forceinline__ void stream_step(Acc& acc, const Frag& use, Frag& nxt
     afn(c + 1, nxt);
     R.load_b(nxt, next_slot(slot));
   }
-#if VGE_ABL != 1
+#if !(VGE_ABL & 1)
   mma_frag(acc, use);
 #else
   asm volatile("" ::"v"(use.ah), "v"(use.bh[0]), "v"(use.bl[NT - 1]));
@@ -181,7 +181,7 @@ struct EncDescX3 {
   int in_col, d_in, n_stem_panels, pad;
 };
 
-constexpr int CONVX3_LDS_BYTES = 2 * XROWS * XSB + NSLOT * CHUNK_B + (24 + 64) * 4;
+constexpr int CONVX3_LDS_BYTES = 2 * XROWS * XSB + NSLOT * CHUNK_B + (24 + 128) * 4;
 
 __global__ void __launch_bounds__(512, 1) conv_encoder_x3_kernel(const float* __restrict__ feats, int n_windows,
                                                                   const EncDescX3* __restrict__ encs, int n_enc,
@@ -191,7 +191,7 @@ __global__ void __launch_bounds__(512, 1) conv_encoder_x3_kernel(const float* __
   _Float16* Xl = Xh + XROWS * XS;                                 // [65][XS]
   char* ring = lds_raw + 2 * XROWS * XSB;                         // NSLOT x 16 KB
   float* red = reinterpret_cast<float*>(ring + NSLOT * CHUNK_B);  // [24]: GN sums, GN squares, |x| maxima
-  int* rexp = reinterpret_cast<int*>(red + 24);                   // [64] stem row scale exponents
+  int* rexp = reinterpret_cast<int*>(red + 24);                   // [2][64] stem row scale exponents
 
   // XCD-aware remap: the 8 XCDs take contiguous work ranges, so co-resident blocks of an XCD share an encoder
   const int n_pairs = (n_windows + 1) >> 1;
@@ -252,42 +252,63 @@ __global__ void __launch_bounds__(512, 1) conv_encoder_x3_kernel(const float* __
 
   // ---------------- stem: Conv1d(d_in -> 256, k=1, no bias), K streamed in 256-wide panels
   // Per-row power-of-two scale: z-scored features leave the fp16 range when a column's train-set std is ~0
-  // ((x - mean) / (std + 1e-6)), so row m is split as A[m,:] * 2^-e_m (exact) with its largest |value| in
-  // [2^8, 2^9), and the row's accumulators are multiplied back by 2^e_m (exact).
-  for (int r = wave * 8; r < wave * 8 + 8; ++r) {
-    const int w = pair * 2 + (r >> 5);
-    float m = 0.f;
-    if (w < n_windows) {
-      const float* src = feats + ((size_t)w * VGE_T + (r & 31)) * VGE_FD + ed.in_col;
-      for (int c = lane; c < ed.d_in; c += 64) m = fmaxf(m, fabsf(src[c]));
-    }
-    m = wave_max(m);
-    if (lane == 0) rexp[r] = (m > 0.f && m <= 3.0e38f) ? ilogbf(m) - 8 : 0;
-  }
+  // ((x - mean) / (std + 1e-6)), so row m of panel p is split as A[m,:] * 2^-e (exact) with the panel row's
+  // largest |value| in [2^8, 2^9); the accumulators (held as C * 2^-e per row) are rescaled when e changes
+  // between panels and multiplied back by 2^e at the end (all exact).  rexp[parity][row] holds e.
   acc_zero(acc);
   for (int p = 0; p < ed.n_stem_panels; ++p) {
     const int kw = min(256, ed.d_in - p * 256);
-    __syncthreads();
-    {
-      const int c = tid & 255;
-      for (int r = tid >> 8; r < 64; r += 2) {
-        const int w = pair * 2 + (r >> 5);
-        float v = 0.f;
-        if (c < kw && w < n_windows) v = feats[((size_t)w * VGE_T + (r & 31)) * VGE_FD + ed.in_col + p * 256 + c];
-        split_store(Xh + r * XS + c, Xl + r * XS + c, ldexpf(v, -rexp[r]));
+    int* ecur = rexp + (p & 1) * 64;
+    // wave w stages rows 8w..8w+7, lane l columns l, l+64, l+128, l+192: 32 independent coalesced loads
+    float a[8][4];
+#pragma unroll
+    for (int jr = 0; jr < 8; ++jr) {
+      const int r = wave * 8 + jr;
+      const int w = pair * 2 + (r >> 5);
+      const float* src = feats + ((size_t)w * VGE_T + (r & 31)) * VGE_FD + ed.in_col + p * 256;
+#pragma unroll
+      for (int jc = 0; jc < 4; ++jc) {
+        const int c = lane + 64 * jc;
+        a[jr][jc] = (c < kw && w < n_windows) ? src[c] : 0.f;
       }
     }
-    __syncthreads();
+#pragma unroll
+    for (int jr = 0; jr < 8; ++jr) {
+      float m = fmaxf(fmaxf(fabsf(a[jr][0]), fabsf(a[jr][1])), fmaxf(fabsf(a[jr][2]), fabsf(a[jr][3])));
+      m = wave_max(m);
+      const int e = (m > 0.f && m <= 3.0e38f) ? ilogbf(m) - 8 : 0;
+      const int r = wave * 8 + jr;
+      if (lane == 0) ecur[r] = e;
+#pragma unroll
+      for (int jc = 0; jc < 4; ++jc) {
+        const int c = lane + 64 * jc;
+        split_store(Xh + r * XS + c, Xl + r * XS + c, ldexpf(a[jr][jc], -e));
+      }
+    }
+    __syncthreads();  // X and ecur complete (the previous stream's final barrier retired every read of X)
+    if (p > 0) {
+      const int* eprev = rexp + ((p - 1) & 1) * 64;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const float f = ldexpf(1.0f, eprev[row] - ecur[row]);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) { acc.hh[n][r] *= f; acc.x[n][r] *= f; }
+      }
+    }
     auto afn = [&](int c, Frag& f) { a_at(own_row_b, c, f); };
     const Ring R{reinterpret_cast<const char*>(ed.stem) + (size_t)p * 16 * CHUNK_B, ring, (kw + 15) >> 4, wave, lane,
                  boff};
     run_stream(acc, R, afn);
   }
+  {
+    const int* efin = rexp + ((ed.n_stem_panels - 1) & 1) * 64;
 #pragma unroll
-  for (int n = 0; n < NT; ++n)
+    for (int n = 0; n < NT; ++n)
 #pragma unroll
-    for (int r = 0; r < 16; ++r)
-      res[n][r] = ldexpf(acc.hh[n][r] + acc.x[n][r] * LO_INV, rexp[rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h]);
+      for (int r = 0; r < 16; ++r)
+        res[n][r] = ldexpf(acc.hh[n][r] + acc.x[n][r] * LO_INV, efin[rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h]);
+  }
   int xexp = store_x(res);
   __syncthreads();
 
