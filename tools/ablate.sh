@@ -1,13 +1,21 @@
 #!/bin/bash
-# Build timing-only ablation variants of the 3xfp16 encoder kernels (VGE_ABL bit masks given as arguments,
-# see vge_encoder_x3.hip) into video-gen-evals_amd/csrc/build/ablN/libvge.so.  Run them on the GPU box with:
-#   for v in MASKS; do VGE_LIB=... python tools/time_encoder.py --tag abl$v; done
+# Build timing-only variants of the 3xfp16 encoder kernels into video-gen-evals_amd/csrc/build/:
+#   ablN/libvge.so  for each VGE_ABL bit mask N given as an argument (see vge_encoder_x3.hip)
+#   trace/libvge.so with VGE_TRACE (s_memtime phase stamps, read by tools/trace_encoder.py)
+# Run them on the GPU box with VGE_LIB=<that path> python tools/time_encoder.py / trace_encoder.py.
 set -e
 cd "$(dirname "$0")/../video-gen-evals_amd/csrc"
 make -s ARCH=gfx950
+HIPCC="/opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950"
+link() {
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$1/libvge.so" build/vge_featurize.o \
+    build/vge_encoder.o "$1/x3.o" build/vge_score.o build/vge_api.o
+}
 for v in "$@"; do
   mkdir -p build/abl$v
-  /opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 -DVGE_ABL=$v -c vge_encoder_x3.hip -o build/abl$v/x3.o
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build/abl$v/libvge.so build/vge_featurize.o \
-    build/vge_encoder.o build/abl$v/x3.o build/vge_score.o build/vge_api.o
+  $HIPCC -DVGE_ABL=$v -c vge_encoder_x3.hip -o build/abl$v/x3.o
+  link build/abl$v
 done
+mkdir -p build/trace
+$HIPCC -DVGE_TRACE -c vge_encoder_x3.hip -o build/trace/x3.o
+link build/trace

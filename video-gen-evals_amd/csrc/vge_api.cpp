@@ -118,8 +118,8 @@ void pack_conv(const float* W, std::vector<float>& out) {
 // 3xfp16 image: W[N][K] -> chunks [N/256][ceil(K/16)][plane 2][h 2][n 256][8] fp16, plane 0 = hi = f16(w),
 // plane 1 = lo = f16((w - hi) * 2^11); chunk c covers k = 16c + 8h + j (zero past K_real)
 template <class Get>
-void pack_linear_x3(Get W, int N, int K_real, std::vector<_Float16>& out) {
-  const int nch = (K_real + 15) / 16;
+void pack_linear_x3(Get W, int N, int K_real, std::vector<_Float16>& out, int chunk_mult = 1) {
+  const int nch = ((K_real + 15) / 16 + chunk_mult - 1) / chunk_mult * chunk_mult;  // streams run in groups of chunk_mult
   const size_t base = out.size();
   out.resize(base + (size_t)(N / 256) * nch * 8192, (_Float16)0.0f);
   _Float16* o = out.data() + base;
@@ -285,7 +285,8 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
   auto pack_lin = [&](const float* W, int N, int K_real, int ldk, int P) -> Mat {
     if (x3) {
       const size_t o = ph.size();
-      pack_linear_x3([&](int n, int k) { return W[(size_t)n * ldk + k]; }, N, K_real, ph);
+      // the x3 kernels stream weights in groups of 8 chunks (zero chunks pad a short last panel)
+      pack_linear_x3([&](int n, int k) { return W[(size_t)n * ldk + k]; }, N, K_real, ph, 8);
       return {o};
     }
     const size_t o = pk.size();

@@ -5,24 +5,42 @@
 // (f32 accumulate; two accumulators, combined in the epilogue).  The dropped lo*lo term and the fp16
 // rounding of lo leave a relative error of ~2^-21 per product, i.e. f32-class results (measured AC/TC
 // deviation from the exact f32 path ~1e-7, see tests/test_gpu_parity.py), at 3 f16 MFMAs per K=16
-// step instead of 4 f32 MFMAs per K=4 step: 5.3x the f32 MFMA rate.
+// step instead of 4 f32 MFMAs per K=4 step: 5.3x the f32 MFMA rate.  Operands are scaled by powers of
+// two (exact) so the fp16 planes never overflow: per row of a stem panel, per window inside the conv
+// chain, per 64-row tile and panel in the GEMMs.
 //
 //   conv_encoder_x3_kernel   MovementConvEncoder x10 (model.py:21-58): one workgroup = 1 encoder x 2 windows
-//                            (64 rows), 8 waves = 2 row tiles x 4 column quarters.  Activations stay in LDS
-//                            as hi/lo planes for the whole chain; weights stream through a 5-slot LDS ring of
-//                            16 KB chunks by global_load_lds (chunk c+5 issued while chunk c is multiplied;
-//                            counted vmcnt + raw s_barrier; fragments double-buffered in registers).
-//   gemm_x3_kernel<EPI>      transformer / token GEMMs, same tiling, with the fused epilogues of the f32 path.
+//                            (64 rows), 8 waves, wave w owns output columns 32w..32w+31 of all 64 rows.
+//                            Activations stay in LDS as hi/lo planes for the whole chain (the A operand);
+//                            each wave streams its own 32 weight columns (the B operand) straight from
+//                            L2 into registers, PF chunks deep, so the K loop has no barrier and no LDS
+//                            traffic besides the A fragment reads.
+//   gemm_x3_kernel<EPI>      transformer / token GEMMs, same tiling (BM = 64, BN = 256), with the fused
+//                            epilogues of the f32 path.
 //
 // MFMA maps (v_mfma_f32_32x32x16_f16): lane l (i = l&31, h = l>>5) supplies A[row i][k = 8h + j] and
 // B[k = 8h + j][col i], j = 0..7; C/D: col = l&31, row = (r&3) + 8(r>>2) + 4(l>>5), r = 0..15.
-// A chunk = 16 K x 256 columns: [plane][h][n][8] fp16 = 16 KB, the exact LDS image the B reads use.
+// A weight chunk = 16 K x 256 columns: [plane][h][n][8] fp16 = 16 KB, so a lane's B fragment of a chunk
+// is one 16-B load per plane and a wave's 32 columns are two contiguous 512-B runs per plane.
 #include "vge_common.h"
 #include <cstring>
 
 #ifndef VGE_ABL
-#define VGE_ABL 0  // timing-only ablation builds (tools/ablate.sh), a bit mask: 1 no MFMA, 2 no DMA after the
-                   // prologue, 4 no B reads, 8 no stream barriers, 16 identity GELU; 0 = the product
+#define VGE_ABL 0  // timing-only ablation builds (tools/ablate.sh), a bit mask: 1 no MFMA, 2 no B loads after the
+                   // prologue, 4 no A reads, 16 identity GELU; 0 = the product
+#endif
+
+#ifdef VGE_TRACE  // timing-only builds (tools/trace_encoder.py): s_memtime stamps of every wave of blocks 0..63
+__device__ long long g_vge_trace[64 * 8 * 32];
+#define STAMP(k)                                                                                        \
+  do {                                                                                                  \
+    if (blockIdx.x < 64 && (threadIdx.x & 63) == 0)                                                     \
+      g_vge_trace[(blockIdx.x * 8 + (threadIdx.x >> 6)) * 32 + (k)] = __builtin_amdgcn_s_memtime();     \
+  } while (0)
+#else
+#define STAMP(k) \
+  do {           \
+  } while (0)
 #endif
 
 namespace {
@@ -35,9 +53,9 @@ constexpr int XSB = XS * 2;          // bytes per activation row
 constexpr int XROWS = 65;            // 64 activation rows + one all-zero row that masked conv taps read
 constexpr int CHUNK_B = 16384;       // bytes per weight chunk
 constexpr int PLANE_B = 8192;        // bytes between the hi and lo planes of a chunk
-constexpr int NSLOT = 5;             // LDS ring depth (chunks)
 constexpr int NWAVE = 8;             // waves per workgroup
-constexpr int NT = 2;                // 32-column n-tiles per wave
+constexpr int RT = 2;                // 32-row tiles per wave (all 64 rows)
+constexpr int PF = 8;                // weight chunks in flight per wave; streams are multiples of PF chunks
 constexpr float LO_SCALE = 2048.0f;  // 2^11
 constexpr float LO_INV = 1.0f / 2048.0f;
 
@@ -51,129 +69,83 @@ __device__ __forceinline__ void split_store(_Float16* hi, _Float16* lo, float v)
   *lo = (_Float16)((v - (float)h) * LO_SCALE);
 }
 
+__device__ __forceinline__ int fp16_range_exp(float m) {  // 2^-e brings m into [2^8, 2^9); 2^+-e stays normal
+  return (m > 0.f && m <= 3.0e38f) ? max(ilogbf(m) - 8, -100) : 0;
+}
+
 struct Acc {
-  floatx16 hh[NT];
-  floatx16 x[NT];
+  floatx16 hh[RT];
+  floatx16 x[RT];
 };
 
 __device__ __forceinline__ void acc_zero(Acc& a) {
 #pragma unroll
-  for (int n = 0; n < NT; ++n) {
+  for (int t = 0; t < RT; ++t) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) { a.hh[n][r] = 0.f; a.x[n][r] = 0.f; }
+    for (int r = 0; r < 16; ++r) { a.hh[t][r] = 0.f; a.x[t][r] = 0.f; }
   }
 }
 
-// A and B fragments of one 16-K chunk
-struct Frag {
-  half8 ah, al;
-  half8 bh[NT], bl[NT];
+struct AFrag {
+  half8 h[RT], l[RT];
 };
 
-__device__ __forceinline__ void mma_frag(Acc& acc, const Frag& f) {
-#pragma unroll
-  for (int n = 0; n < NT; ++n) {
-    acc.hh[n] = mfma32(f.ah, f.bh[n], acc.hh[n]);
-    acc.x[n] = mfma32(f.ah, f.bl[n], acc.x[n]);
-    acc.x[n] = mfma32(f.al, f.bh[n], acc.x[n]);
-  }
-}
-
-// One workgroup's weight stream: n 16 KB chunks in HBM, a 5-slot ring in LDS.
-struct Ring {
-  const char* g;   // chunk 0 of the stream
-  char* lds;       // ring base
-  int n;           // chunks in the stream
-  int wave;        // wave id (scalar)
-  int lane;
-  unsigned boff;   // this lane's B-fragment byte offset inside a chunk (n-tile 0, hi plane)
-
-  // a chunk is 16 x 1 KB wave-pieces, 2 per wave (the LDS destination of a piece is wave-uniform)
-  __device__ __forceinline__ void stage(int c, int slot) const {
-#if !(VGE_ABL & 2)
-    const char* src = g + (size_t)c * CHUNK_B + wave * 1024 + lane * 16;
-    char* dst = lds + slot * CHUNK_B + wave * 1024;
-    glds16(src, dst);
-    glds16(src + NWAVE * 1024, dst + NWAVE * 1024);
-#endif
-  }
-  __device__ __forceinline__ void load_b(Frag& f, int slot) const {
-#if !(VGE_ABL & 4)
-    const char* p = lds + slot * CHUNK_B + boff;
-#pragma unroll
-    for (int n = 0; n < NT; ++n) {
-      f.bh[n] = *reinterpret_cast<const half8*>(p + n * 512);
-      f.bl[n] = *reinterpret_cast<const half8*>(p + n * 512 + PLANE_B);
-    }
-#endif
-  }
-};
-
-// leave k newer chunks (2 DMA instructions each) in flight, k in [0, 3]
-__device__ __forceinline__ void vm_wait_chunks(int k) {
-  if (k >= 3) vmcnt<6>();
-  else if (k == 2) vmcnt<4>();
-  else if (k == 1) vmcnt<2>();
-  else vmcnt<0>();
-}
-
-__device__ __forceinline__ int next_slot(int s) { return s == NSLOT - 1 ? 0 : s + 1; }
-
-// One chunk step: retire chunk c+1, barrier, issue chunk c+NSLOT into chunk c's slot, read chunk c+1's
-// fragments, multiply chunk c from registers.  STEADY: chunks c+2..c+4 are in flight (constant vmcnt).
-template <bool STEADY, class AFn>
-__device__ __forceinline__ void stream_step(Acc& acc, const Frag& use, Frag& nxt, const Ring& R, AFn& afn, int c,
-                                            int slot) {
-  if (STEADY) vmcnt<6>();
-  else vm_wait_chunks(min(c + NSLOT - 1, R.n - 1) - (c + 1));
-#if !(VGE_ABL & 8)
-  lds_barrier();  // every wave's reads of chunk c's slot are done; chunk c+1 has landed for all waves
-#endif
-  if (c + NSLOT < R.n) R.stage(c + NSLOT, slot);
-  if (STEADY || c + 1 < R.n) {
-    afn(c + 1, nxt);
-    R.load_b(nxt, next_slot(slot));
-  }
+__device__ __forceinline__ void mma_chunk(Acc& acc, const AFrag& a, half8 bh, half8 bl) {
 #if !(VGE_ABL & 1)
-  mma_frag(acc, use);
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    acc.hh[t] = mfma32(a.h[t], bh, acc.hh[t]);
+    acc.x[t] = mfma32(a.h[t], bl, acc.x[t]);
+    acc.x[t] = mfma32(a.l[t], bh, acc.x[t]);
+  }
 #else
-  asm volatile("" ::"v"(use.ah), "v"(use.bh[0]), "v"(use.bl[NT - 1]));
+  asm volatile("" ::"v"(a.h[0]), "v"(a.l[RT - 1]), "v"(bh), "v"(bl));
 #endif
 }
 
-// afn(c, frag) loads this lane's A fragments of chunk c
+typedef const __attribute__((address_space(1))) char* gchar;  // global (not flat) loads: counted by vmcnt only
+typedef const __attribute__((address_space(1))) half8* ghalf8;
+
+__device__ __forceinline__ void load_b(gchar g, int c, unsigned loff, half8& bh, half8& bl) {
+  gchar p = g + (size_t)c * CHUNK_B + loff;
+  bh = *reinterpret_cast<ghalf8>(p);
+  bl = *reinterpret_cast<ghalf8>(p + PLANE_B);
+}
+
+// Multiply this wave's 64 x 32 output tile by a stream of n weight chunks (n a multiple of PF, >= PF).
+// afn(c, AFrag&) reads the A fragments of chunk c from LDS.  B fragments are loaded PF - 1 chunks ahead
+// into a register ring; the loop is unrolled by PF so every ring index is static and the compiler's
+// counted vmcnt waits retire exactly the chunk being consumed.
 template <class AFn>
-__device__ __forceinline__ void run_stream(Acc& acc, const Ring& R, AFn afn) {
-  const int n = R.n;
-  const int pre = min(n, NSLOT);
-  for (int c = 0; c < pre; ++c) R.stage(c, c);
-  vm_wait_chunks(pre - 1);  // chunk 0 landed
-  lds_barrier();
-  Frag f0, f1;
-  afn(0, f0);
-  R.load_b(f0, 0);
-  int c = 0, slot = 0;
-  for (; c + 1 <= n - NSLOT; c += 2) {
-    stream_step<true>(acc, f0, f1, R, afn, c, slot);
-    slot = next_slot(slot);
-    stream_step<true>(acc, f1, f0, R, afn, c + 1, slot);
-    slot = next_slot(slot);
-  }
-  for (; c < n; c += 2) {
-    stream_step<false>(acc, f0, f1, R, afn, c, slot);
-    slot = next_slot(slot);
-    if (c + 1 < n) {
-      stream_step<false>(acc, f1, f0, R, afn, c + 1, slot);
-      slot = next_slot(slot);
+__device__ __forceinline__ void run_stream(Acc& acc, const void* gw, int n, unsigned loff, AFn afn) {
+  const gchar g = (gchar)gw;
+  half8 bh[PF], bl[PF];
+#pragma unroll
+  for (int j = 0; j < PF - 1; ++j) load_b(g, j, loff, bh[j], bl[j]);
+  AFrag a[2];
+  afn(0, a[0]);
+  for (int c0 = 0; c0 < n; c0 += PF) {
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      const int c = c0 + j;
+#if !(VGE_ABL & 2)
+      load_b(g, min(c + PF - 1, n - 1), loff, bh[(j + PF - 1) % PF], bl[(j + PF - 1) % PF]);
+#endif
+#if !(VGE_ABL & 4)
+      afn(min(c + 1, n - 1), a[(j + 1) & 1]);
+#endif
+      mma_chunk(acc, a[j & 1], bh[j], bl[j]);
+      // pin this step's loads in place: without it the compiler hoists every A read of the unrolled group
+      // and sinks the B loads next to their use, which collapses the prefetch to vmcnt(0) waits
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
-  vmcnt<0>();
-  lds_barrier();  // ring and activations free for the caller
 }
 
 // ------------------------------------------------------------------ conv encoder chain
 struct EncDescX3 {
-  const _Float16* stem;  // stem chunks; panel p (256 K) starts at chunk 16p, the last panel may be short
+  const _Float16* stem;  // stem chunks; panel p (256 K) starts at chunk 16p, padded to a multiple of PF chunks
   const _Float16* conv;  // 8 convs x 5 taps x 16 chunks
   const _Float16* proj;  // 16 chunks
   const float* gn_w;     // [4][256]
@@ -181,17 +153,16 @@ struct EncDescX3 {
   int in_col, d_in, n_stem_panels, pad;
 };
 
-constexpr int CONVX3_LDS_BYTES = 2 * XROWS * XSB + NSLOT * CHUNK_B + (24 + 128) * 4;
+constexpr int CONVX3_LDS_BYTES = 2 * XROWS * XSB + (4 * RT * NWAVE + 128) * 4;
 
 __global__ void __launch_bounds__(512, 1) conv_encoder_x3_kernel(const float* __restrict__ feats, int n_windows,
                                                                   const EncDescX3* __restrict__ encs, int n_enc,
                                                                   float* __restrict__ enc_out) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
-  _Float16* Xh = reinterpret_cast<_Float16*>(lds_raw);            // [65][XS]
-  _Float16* Xl = Xh + XROWS * XS;                                 // [65][XS]
-  char* ring = lds_raw + 2 * XROWS * XSB;                         // NSLOT x 16 KB
-  float* red = reinterpret_cast<float*>(ring + NSLOT * CHUNK_B);  // [24]: GN sums, GN squares, |x| maxima
-  int* rexp = reinterpret_cast<int*>(red + 24);                   // [2][64] stem row scale exponents
+  _Float16* Xh = reinterpret_cast<_Float16*>(lds_raw);                       // [65][XS]
+  _Float16* Xl = Xh + XROWS * XS;                                            // [65][XS]
+  float* red = reinterpret_cast<float*>(lds_raw + 2 * XROWS * XSB);          // [4 slots][RT][NWAVE] partials
+  int* rexp = reinterpret_cast<int*>(red + 4 * RT * NWAVE);                  // [2][64] stem row exponents
 
   // XCD-aware remap: the 8 XCDs take contiguous work ranges, so co-resident blocks of an XCD share an encoder
   const int n_pairs = (n_windows + 1) >> 1;
@@ -204,53 +175,78 @@ __global__ void __launch_bounds__(512, 1) conv_encoder_x3_kernel(const float* __
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int rt = wave >> 2;         // row tile = window within the pair
-  const int nb0 = (wave & 3) * 64;  // this wave's 64 output columns
   const int i = lane & 31, h = lane >> 5;
-  const int win = pair * 2 + rt;
-  const unsigned boff = (unsigned)((h * 256 + nb0 + i) * 16);
-  const char* xa = reinterpret_cast<const char*>(Xh) + h * 16;  // this lane's 8 k-values of a 16-K chunk column
+  const int col = wave * 32 + i;                               // this lane's output column
+  const unsigned loff = (unsigned)((h * 256 + col) * 16);      // its B fragment inside a chunk
+  const char* xa = reinterpret_cast<const char*>(Xh) + h * 16;  // its 8 k-values of a 16-K chunk column
+  auto crow = [&](int t, int r) { return t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h; };  // C-layout row
 
   Acc acc;
-  floatx16 res[NT];
+  floatx16 res[RT];
   if (tid < XS) {  // the zero row
     Xh[64 * XS + tid] = (_Float16)0.0f;
     Xl[64 * XS + tid] = (_Float16)0.0f;
   }
 
-  // Store the next conv's input as window * 2^-e (exact) with the window's largest |value| in [2^8, 2^9), so
-  // the fp16 planes neither overflow nor lose small values; returns e (the same for the row tile's 4 waves)
-  // for the consumer to multiply its accumulators back by.  Caller guarantees X is no longer being read.
-  auto store_x = [&](const floatx16 (&v)[NT]) -> int {
-    float m = 0.f;
+  // Combine one value per window over the 8 waves (each holds 32 of the 256 columns).  `slot` picks one
+  // of 4 partial buffers so back-to-back reductions need only the one barrier inside.
+  auto block_reduce = [&](const float (&v)[RT], int slot, bool is_max, float (&out)[RT]) {
 #pragma unroll
-    for (int n = 0; n < NT; ++n)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) m = fmaxf(m, fabsf(v[n][r]));
-    m = wave_max(m);
-    if (lane == 0) red[16 + wave] = m;
+    for (int t = 0; t < RT; ++t) {
+      const float w = is_max ? wave_max(v[t]) : wave_sum(v[t]);
+      if (lane == 0) red[(slot * RT + t) * NWAVE + wave] = w;
+    }
     __syncthreads();
-    const float* rm = red + 16 + rt * 4;
-    const float mm = fmaxf(fmaxf(rm[0], rm[1]), fmaxf(rm[2], rm[3]));
-    const int e = (mm > 0.f && mm <= 3.0e38f) ? ilogbf(mm) - 8 : 0;
 #pragma unroll
-    for (int n = 0; n < NT; ++n)
+    for (int t = 0; t < RT; ++t) {
+      const float* p = red + (slot * RT + t) * NWAVE;
+      float a = p[0];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int col = nb0 + n * 32 + i;
-        split_store(Xh + row * XS + col, Xl + row * XS + col, ldexpf(v[n][r], -e));
-      }
-    return e;
+      for (int w = 1; w < NWAVE; ++w) a = is_max ? fmaxf(a, p[w]) : a + p[w];
+      out[t] = a;
+    }
   };
-  auto a_at = [&](int row_byte, int cc, Frag& f) {
-    const char* p = xa + row_byte + cc * 32;
-    f.ah = *reinterpret_cast<const half8*>(p);
-    f.al = *reinterpret_cast<const half8*>(p + XROWS * XSB);
-  };
-  const int own_row_b = (rt * 32 + i) * XSB;
 
-  // ---------------- stem: Conv1d(d_in -> 256, k=1, no bias), K streamed in 256-wide panels
+  // Store the next conv's input as window * 2^-ex[t] (exact), the window's largest |value| in [2^8, 2^9);
+  // the consumer multiplies its accumulators back by 2^ex[t].  Caller guarantees X is no longer read.
+  auto store_x = [&](const floatx16 (&v)[RT], int (&ex)[RT]) {
+    float m[RT], mm[RT];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      m[t] = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) m[t] = fmaxf(m[t], fabsf(v[t][r]));
+    }
+    block_reduce(m, 3, true, mm);
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      ex[t] = fp16_range_exp(mm[t]);
+      const float sc = ldexpf(1.0f, -ex[t]);
+#pragma unroll
+      for (int r = 0; r < 16; r += 2) {
+        const floatx2 y = (floatx2){v[t][r], v[t][r + 1]} * sc;
+        const _Float16 h0 = (_Float16)y.x, h1 = (_Float16)y.y;
+        const floatx2 lo = (y - (floatx2){(float)h0, (float)h1}) * LO_SCALE;
+        const int row = crow(t, r);  // rows r and r + 1 of the tile are adjacent
+        Xh[row * XS + col] = h0;
+        Xh[(row + 1) * XS + col] = h1;
+        Xl[row * XS + col] = (_Float16)lo.x;
+        Xl[(row + 1) * XS + col] = (_Float16)lo.y;
+      }
+    }
+  };
+
+  auto afn_rows = [&](int c, AFrag& f) {  // A fragments of the block's own 64 rows
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      const char* q = xa + (t * 32 + i) * XSB + c * 32;
+      f.h[t] = *reinterpret_cast<const half8*>(q);
+      f.l[t] = *reinterpret_cast<const half8*>(q + XROWS * XSB);
+    }
+  };
+
+  STAMP(0);
+  // ---------------- stem: Conv1d(d_in -> 256, k=1, no bias), K streamed in 256-wide panels.
   // Per-row power-of-two scale: z-scored features leave the fp16 range when a column's train-set std is ~0
   // ((x - mean) / (std + 1e-6)), so row m of panel p is split as A[m,:] * 2^-e (exact) with the panel row's
   // largest |value| in [2^8, 2^9); the accumulators (held as C * 2^-e per row) are rescaled when e changes
@@ -276,125 +272,141 @@ __global__ void __launch_bounds__(512, 1) conv_encoder_x3_kernel(const float* __
     for (int jr = 0; jr < 8; ++jr) {
       float m = fmaxf(fmaxf(fabsf(a[jr][0]), fabsf(a[jr][1])), fmaxf(fabsf(a[jr][2]), fabsf(a[jr][3])));
       m = wave_max(m);
-      const int e = (m > 0.f && m <= 3.0e38f) ? ilogbf(m) - 8 : 0;
+      const int ex = fp16_range_exp(m);
       const int r = wave * 8 + jr;
-      if (lane == 0) ecur[r] = e;
+      if (lane == 0) ecur[r] = ex;
 #pragma unroll
       for (int jc = 0; jc < 4; ++jc) {
         const int c = lane + 64 * jc;
-        split_store(Xh + r * XS + c, Xl + r * XS + c, ldexpf(a[jr][jc], -e));
+        split_store(Xh + r * XS + c, Xl + r * XS + c, ldexpf(a[jr][jc], -ex));
       }
     }
-    __syncthreads();  // X and ecur complete (the previous stream's final barrier retired every read of X)
+    __syncthreads();  // X and ecur complete
+    if (p == 0) STAMP(1);
     if (p > 0) {
       const int* eprev = rexp + ((p - 1) & 1) * 64;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const float f = ldexpf(1.0f, eprev[row] - ecur[row]);
+      for (int t = 0; t < RT; ++t)
 #pragma unroll
-        for (int n = 0; n < NT; ++n) { acc.hh[n][r] *= f; acc.x[n][r] *= f; }
-      }
+        for (int r = 0; r < 16; ++r) {
+          const float f = ldexpf(1.0f, eprev[crow(t, r)] - ecur[crow(t, r)]);
+          acc.hh[t][r] *= f;
+          acc.x[t][r] *= f;
+        }
     }
-    auto afn = [&](int c, Frag& f) { a_at(own_row_b, c, f); };
-    const Ring R{reinterpret_cast<const char*>(ed.stem) + (size_t)p * 16 * CHUNK_B, ring, (kw + 15) >> 4, wave, lane,
-                 boff};
-    run_stream(acc, R, afn);
+    run_stream(acc, reinterpret_cast<const char*>(ed.stem) + (size_t)p * 16 * CHUNK_B, ((kw + 127) >> 7) * PF, loff,
+               afn_rows);
+    __syncthreads();  // every wave is done reading X
   }
   {
     const int* efin = rexp + ((ed.n_stem_panels - 1) & 1) * 64;
 #pragma unroll
-    for (int n = 0; n < NT; ++n)
+    for (int t = 0; t < RT; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        res[n][r] = ldexpf(acc.hh[n][r] + acc.x[n][r] * LO_INV, efin[rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h]);
+      for (int r = 0; r < 16; ++r) res[t][r] = ldexpf(acc.hh[t][r] + acc.x[t][r] * LO_INV, efin[crow(t, r)]);
   }
-  int xexp = store_x(res);
+  STAMP(2);
+  int xexp[RT];
+  store_x(res, xexp);
   __syncthreads();
+  STAMP(3);
 
   // ---------------- 4 TemporalConvBlocks
   for (int blk = 0; blk < 4; ++blk) {
     const int dil = 1 << blk;
+    const float gw = ed.gn_w[blk * 256 + col], gb = ed.gn_b[blk * 256 + col];
     for (int cv = 0; cv < 2; ++cv) {
       acc_zero(acc);
-      auto afn = [&](int c, Frag& f) {
+      auto afn = [&](int c, AFrag& f) {
         const int tap = c >> 4, cc = c & 15;
         const int tt = i + (tap - 2) * dil;
-        const int row = ((unsigned)tt < 32u) ? rt * 32 + tt : 64;  // out of the window -> zero row
-        a_at(row * XSB, cc, f);
+        const bool in = (unsigned)tt < 32u;
+#pragma unroll
+        for (int t = 0; t < RT; ++t) {
+          const int row = in ? t * 32 + tt : 64;  // out of the window -> zero row
+          const char* q = xa + row * XSB + cc * 32;
+          f.h[t] = *reinterpret_cast<const half8*>(q);
+          f.l[t] = *reinterpret_cast<const half8*>(q + XROWS * XSB);
+        }
       };
-      const Ring R{reinterpret_cast<const char*>(ed.conv) + (size_t)(blk * 2 + cv) * 5 * 16 * CHUNK_B, ring, 5 * 16,
-                   wave, lane, boff};
-      run_stream(acc, R, afn);
-      floatx16 (&v)[NT] = acc.hh;  // combine in place: (hh + 2^-11 x) * 2^xexp
-      const float xs = ldexpf(1.0f, xexp);
-      if (cv == 0) {
+      run_stream(acc, reinterpret_cast<const char*>(ed.conv) + (size_t)(blk * 2 + cv) * 5 * 16 * CHUNK_B, 5 * 16,
+                 loff, afn);
+      STAMP(4 + (blk * 2 + cv) * 2);
+      // epilogue in packed f32 (v_pk_fma_f32: two rows per instruction); combine in place:
+      // (hh + 2^-11 x) * 2^xexp -> [+ residual] -> GELU [-> GroupNorm]
+      floatx16 (&v)[RT] = acc.hh;
+      floatx2 s2[RT];
 #pragma unroll
-        for (int n = 0; n < NT; ++n)
+      for (int t = 0; t < RT; ++t) {
+        const float xs = ldexpf(1.0f, xexp[t]), xl = xs * LO_INV;
+        s2[t] = 0.f;
 #pragma unroll
-          for (int r = 0; r < 16; ++r) v[n][r] = gelu_erf((acc.hh[n][r] + acc.x[n][r] * LO_INV) * xs);
-      } else {
-        // GroupNorm(1, 256) over the window: 32 x 256 values held by the row tile's 4 waves
-        float s = 0.f;
+        for (int r = 0; r < 16; r += 2) {
+          floatx2 y = __builtin_elementwise_fma((floatx2){acc.x[t][r], acc.x[t][r + 1]}, (floatx2)xl,
+                                                (floatx2){acc.hh[t][r], acc.hh[t][r + 1]} * xs);
+          if (cv == 1) y += (floatx2){res[t][r], res[t][r + 1]};
+          y = gelu2(y);
+          s2[t] += y;
+          v[t][r] = y.x;
+          v[t][r + 1] = y.y;
+        }
+      }
+      STAMP(22 + blk * 2 + cv);
+      if (cv == 1) {
+        // GroupNorm(1, 256) per window over its 32 x 256 values, spread over the 8 waves
+        float s[RT], mean[RT], q[RT], var[RT];
 #pragma unroll
-        for (int n = 0; n < NT; ++n)
+        for (int t = 0; t < RT; ++t) s[t] = s2[t].x + s2[t].y;
+        block_reduce(s, 0, false, mean);
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            v[n][r] = gelu_erf((acc.hh[n][r] + acc.x[n][r] * LO_INV) * xs + res[n][r]);
-            s += v[n][r];
+        for (int t = 0; t < RT; ++t) {
+          mean[t] *= 1.0f / 8192.0f;
+          floatx2 q2 = 0.f;
+#pragma unroll
+          for (int r = 0; r < 16; r += 2) {
+            const floatx2 d = (floatx2){v[t][r], v[t][r + 1]} - mean[t];
+            q2 = __builtin_elementwise_fma(d, d, q2);
           }
-        s = wave_sum(s);
-        if (lane == 0) red[wave] = s;
-        __syncthreads();
-        const float mean = (red[rt * 4] + red[rt * 4 + 1] + red[rt * 4 + 2] + red[rt * 4 + 3]) / 8192.0f;
-        float q = 0.f;
+          q[t] = q2.x + q2.y;
+        }
+        block_reduce(q, 1, false, var);
 #pragma unroll
-        for (int n = 0; n < NT; ++n)
+        for (int t = 0; t < RT; ++t) {
+          const float rstd = 1.0f / sqrtf(var[t] * (1.0f / 8192.0f) + 1e-5f);
+          const float sc = rstd * gw, sh = gb - mean[t] * sc;  // (v - mean) * rstd * w + b
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const float d = v[n][r] - mean;
-            q += d * d;
-          }
-        q = wave_sum(q);
-        if (lane == 0) red[8 + wave] = q;
-        __syncthreads();
-        const float var =
-            (red[8 + rt * 4] + red[8 + rt * 4 + 1] + red[8 + rt * 4 + 2] + red[8 + rt * 4 + 3]) / 8192.0f;
-        const float rstd = 1.0f / sqrtf(var + 1e-5f);
-#pragma unroll
-        for (int n = 0; n < NT; ++n) {
-          const int col = nb0 + n * 32 + i;
-          const float w_ = ed.gn_w[blk * 256 + col], b_ = ed.gn_b[blk * 256 + col];
-#pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            v[n][r] = (v[n][r] - mean) * rstd * w_ + b_;
-            res[n][r] = v[n][r];
+          for (int r = 0; r < 16; r += 2) {
+            const floatx2 y = __builtin_elementwise_fma((floatx2){v[t][r], v[t][r + 1]}, (floatx2)sc, (floatx2)sh);
+            v[t][r] = res[t][r] = y.x;
+            v[t][r + 1] = res[t][r + 1] = y.y;
           }
         }
       }
-      xexp = store_x(v);  // the stream's final barrier retired every read of X
+      __syncthreads();  // every wave is done reading X (this conv's A operand)
+      store_x(v, xexp);
       __syncthreads();
+      STAMP(5 + (blk * 2 + cv) * 2);
     }
   }
 
   // ---------------- proj: Linear(256 -> 256, no bias)
   acc_zero(acc);
-  {
-    auto afn = [&](int c, Frag& f) { a_at(own_row_b, c, f); };
-    const Ring R{reinterpret_cast<const char*>(ed.proj), ring, 16, wave, lane, boff};
-    run_stream(acc, R, afn);
-  }
-  if (win < n_windows) {
-    const float xs = ldexpf(1.0f, xexp);
-    float* o = enc_out + ((size_t)e * n_windows * VGE_T + (size_t)win * VGE_T) * VGE_D;
+  run_stream(acc, reinterpret_cast<const char*>(ed.proj), 16, loff, afn_rows);
+  STAMP(20);
 #pragma unroll
-    for (int n = 0; n < NT; ++n)
+  for (int t = 0; t < RT; ++t) {
+    const int win = pair * 2 + t;
+    if (win < n_windows) {
+      const float xs = ldexpf(1.0f, xexp[t]);
+      float* o = enc_out + ((size_t)e * n_windows * VGE_T + (size_t)win * VGE_T) * VGE_D;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = (r & 3) + 8 * (r >> 2) + 4 * h;
-        o[row * VGE_D + nb0 + n * 32 + i] = (acc.hh[n][r] + acc.x[n][r] * LO_INV) * xs;
-      }
+      for (int r = 0; r < 16; ++r) o[crow(0, r) * VGE_D + col] = (acc.hh[t][r] + acc.x[t][r] * LO_INV) * xs;
+    }
   }
+  STAMP(21);
+#ifdef VGE_TRACE
+  if (blockIdx.x < 64 && threadIdx.x == 0) g_vge_trace[blockIdx.x * 8 * 32 + 31] = e;
+#endif
 }
 
 // ------------------------------------------------------------------ panel GEMM (3xfp16) with fused epilogues
@@ -412,24 +424,23 @@ struct GemmArgsX3 {
   const float* cls;
 };
 
-// block = 8 waves = 2 row tiles (32 rows) x 4 column quarters (64 cols): BM = 64, BN = 256
-constexpr int GEMMX3_LDS_BYTES = 2 * 64 * XSB + NSLOT * CHUNK_B + (64 * 4 + 8) * 4;
+// block = 8 waves, BM = 64 rows x BN = 256 columns, wave w owns columns 32w..32w+31 of all 64 rows
+constexpr int GEMMX3_LDS_BYTES = 2 * 64 * XSB + (64 * NWAVE + NWAVE) * 4;
 
 template <int EPI>
 __global__ void __launch_bounds__(512, 1) gemm_x3_kernel(GemmArgsX3 ga) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   _Float16* Xh = reinterpret_cast<_Float16*>(lds_raw);
   _Float16* Xl = Xh + 64 * XS;
-  char* ring = lds_raw + 2 * 64 * XSB;
-  float* red = reinterpret_cast<float*>(ring + NSLOT * CHUNK_B);  // [64 rows][4 column quarters] + [8] maxima
+  float* red = reinterpret_cast<float*>(lds_raw + 2 * 64 * XSB);  // [64 rows][8 waves] + [8] maxima
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int rt = wave >> 2, cq = wave & 3, nb0 = cq * 64;
   const int i = lane & 31, h = lane >> 5;
   const int row0 = blockIdx.x * 64, nb = blockIdx.y;
   const int n_panels = ga.K / 256;
-  const unsigned boff = (unsigned)((h * 256 + nb0 + i) * 16);
-  const char* xa = reinterpret_cast<const char*>(Xh) + (rt * 32 + i) * XSB + h * 16;
+  const unsigned loff = (unsigned)((h * 256 + wave * 32 + i) * 16);
+  const char* xa = reinterpret_cast<const char*>(Xh) + i * XSB + h * 16;
+  auto lrow = [&](int t, int r) { return t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h; };
 
   Acc acc;
   acc_zero(acc);
@@ -447,18 +458,18 @@ __global__ void __launch_bounds__(512, 1) gemm_x3_kernel(GemmArgsX3 ga) {
       m = fmaxf(m, fabsf(a[j]));
     }
     m = wave_max(m);
-    if (lane == 0) red[256 + wave] = m;
+    if (lane == 0) red[64 * NWAVE + wave] = m;
     __syncthreads();  // also: every wave is past the previous panel's stream
-    float mm = red[256];
+    float mm = red[64 * NWAVE];
 #pragma unroll
-    for (int w = 1; w < NWAVE; ++w) mm = fmaxf(mm, red[256 + w]);
-    const int e = (mm > 0.f && mm <= 3.0e38f) ? ilogbf(mm) - 8 : 0;
+    for (int w = 1; w < NWAVE; ++w) mm = fmaxf(mm, red[64 * NWAVE + w]);
+    const int e = fp16_range_exp(mm);
     if (p > 0 && e != aexp) {
       const float f = ldexpf(1.0f, aexp - e);
 #pragma unroll
-      for (int n = 0; n < NT; ++n)
+      for (int t = 0; t < RT; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) { acc.hh[n][r] *= f; acc.x[n][r] *= f; }
+        for (int r = 0; r < 16; ++r) { acc.hh[t][r] *= f; acc.x[t][r] *= f; }
     }
     aexp = e;
 #pragma unroll
@@ -467,117 +478,101 @@ __global__ void __launch_bounds__(512, 1) gemm_x3_kernel(GemmArgsX3 ga) {
       split_store(Xh + r * XS + c, Xl + r * XS + c, ldexpf(a[j], -e));
     }
     __syncthreads();
-    auto afn = [&](int cc, Frag& f) {
-      f.ah = *reinterpret_cast<const half8*>(xa + cc * 32);
-      f.al = *reinterpret_cast<const half8*>(xa + cc * 32 + 64 * XSB);
+    auto afn = [&](int cc, AFrag& f) {
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        const char* q = xa + t * 32 * XSB + cc * 32;
+        f.h[t] = *reinterpret_cast<const half8*>(q);
+        f.l[t] = *reinterpret_cast<const half8*>(q + 64 * XSB);
+      }
     };
-    const Ring R{reinterpret_cast<const char*>(ga.W) + ((size_t)nb * (ga.K / 16) + p * 16) * CHUNK_B, ring, 16, wave,
-                 lane, boff};
-    run_stream(acc, R, afn);
+    run_stream(acc, reinterpret_cast<const char*>(ga.W) + ((size_t)nb * (ga.K / 16) + p * 16) * CHUNK_B, 16, loff,
+               afn);
+    __syncthreads();  // every wave is done reading the panel
   }
 
-  float v[NT][16];
+  float v[RT][16];
   const float as = ldexpf(1.0f, aexp);
 #pragma unroll
-  for (int n = 0; n < NT; ++n)
+  for (int t = 0; t < RT; ++t)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[n][r] = (acc.hh[n][r] + acc.x[n][r] * LO_INV) * as;
-  const int colb = nb * 256 + nb0;
-  auto lrow = [&](int r) { return rt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h; };
+    for (int r = 0; r < 16; ++r) v[t][r] = (acc.hh[t][r] + acc.x[t][r] * LO_INV) * as;
+  const int col = nb * 256 + wave * 32 + i;
 
   if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) {
+    const float bb = ga.bias[col];
 #pragma unroll
-    for (int n = 0; n < NT; ++n) {
-      const int col = colb + n * 32 + i;
-      const float bb = ga.bias[col];
+    for (int t = 0; t < RT; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = row0 + lrow(r);
-        float x = v[n][r] + bb;
+        const int row = row0 + lrow(t, r);
+        float x = v[t][r] + bb;
         if (EPI == EPI_BIAS_RELU) x = fmaxf(x, 0.f);
         if (row < ga.M) ga.out[(size_t)row * ga.ldo + col] = x;
       }
-    }
   } else if constexpr (EPI == EPI_TOKENS) {
 #pragma unroll
-    for (int n = 0; n < NT; ++n) {
-      const int col = colb + n * 32 + i;
+    for (int t = 0; t < RT; ++t)
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = row0 + lrow(r);
+        const int row = row0 + lrow(t, r);
         if (row < ga.M) {
-          const int w = row >> 5, t = row & 31;
-          ga.out[((size_t)w * VGE_TOK + 1 + t) * ga.ldo + col] = v[n][r] + ga.pe[(1 + t) * VGE_D + col];
-          if (t == 0) ga.out[(size_t)w * VGE_TOK * ga.ldo + col] = ga.cls[col] + ga.pe[col];
+          const int w = row >> 5, tt = row & 31;
+          ga.out[((size_t)w * VGE_TOK + 1 + tt) * ga.ldo + col] = v[t][r] + ga.pe[(1 + tt) * VGE_D + col];
+          if (tt == 0) ga.out[(size_t)w * VGE_TOK * ga.ldo + col] = ga.cls[col] + ga.pe[col];
         }
       }
-    }
-  } else {  // EPI_BIAS_RES_LN over the 256 columns (N == 256, one column block)
-    float s[16], q[16];
-#pragma unroll
-    for (int r = 0; r < 16; ++r) s[r] = 0.f;
-#pragma unroll
-    for (int n = 0; n < NT; ++n) {
-      const int col = colb + n * 32 + i;
-      const float bb = ga.bias[col];
+  } else {  // EPI_BIAS_RES_LN over the 256 columns (N == 256, one column block), one 32-row tile at a time
+    const float bb = ga.bias[col], lw = ga.ln_w[col], lb = ga.ln_b[col];
+    const int mrow = ga.M - 1 - row0;  // last valid local row (rows past M read it, their results are dropped)
+    // row sums (in place): over the 32 lanes that share h (xor 1..16 stays inside a 32-lane half), then over
+    // the 8 waves' column slices through LDS
+    auto row_reduce = [&](float (&q)[16], int t) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = row0 + lrow(r);
-        v[n][r] += bb + ((row < ga.M) ? ga.res[(size_t)row * ga.ldr + col] : 0.f);
-        s[r] += v[n][r];
+#pragma unroll
+        for (int o = 16; o >= 1; o >>= 1) q[r] += __shfl_xor(q[r], o, 64);
       }
-    }
-    // row sums: reduce over the 32 lanes that share h (xor 1..16 stays inside a 32-lane half), then over
-    // the 4 column-quarter waves through LDS
+      if (i == 0) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-#pragma unroll
-      for (int o = 16; o >= 1; o >>= 1) s[r] += __shfl_xor(s[r], o, 64);
-    }
-    if (i == 0) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) red[lrow(r) * 4 + cq] = s[r];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float* rr = red + lrow(r) * 4;
-      s[r] = (rr[0] + rr[1] + rr[2] + rr[3]) / 256.0f;  // mean
-      q[r] = 0.f;
-    }
-#pragma unroll
-    for (int n = 0; n < NT; ++n)
+        for (int r = 0; r < 16; ++r) red[lrow(t, r) * NWAVE + wave] = q[r];
+      }
+      __syncthreads();
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float d = v[n][r] - s[r];
-        q[r] += d * d;
+        const float* rr = red + lrow(t, r) * NWAVE;
+        float a = rr[0];
+#pragma unroll
+        for (int w = 1; w < NWAVE; ++w) a += rr[w];
+        q[r] = a;
       }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-#pragma unroll
-      for (int o = 16; o >= 1; o >>= 1) q[r] += __shfl_xor(q[r], o, 64);
-    }
-    __syncthreads();  // every wave has read the sums
-    if (i == 0) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) red[lrow(r) * 4 + cq] = q[r];
-    }
-    __syncthreads();
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float* rr = red + lrow(r) * 4;
-      q[r] = 1.0f / sqrtf((rr[0] + rr[1] + rr[2] + rr[3]) / 256.0f + 1e-5f);
-    }
-#pragma unroll
-    for (int n = 0; n < NT; ++n) {
-      const int col = colb + n * 32 + i;
-      const float lw = ga.ln_w[col], lb = ga.ln_b[col];
+      __syncthreads();  // every wave has read the partials before they are reused
+    };
+    auto tile = [&](float (&vt)[16], int t) {
+      const float* rbase = ga.res + (size_t)(row0 + t * 32) * ga.ldr + col;
+      float s[16], q[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const int row = row0 + lrow(r);
-        if (row < ga.M) ga.out[(size_t)row * ga.ldo + col] = (v[n][r] - s[r]) * q[r] * lw + lb;
+        vt[r] += bb + rbase[min(lrow(0, r), mrow - t * 32) * ga.ldr];
+        s[r] = vt[r];
       }
-    }
+      row_reduce(s, t);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        s[r] *= 1.0f / 256.0f;  // row means
+        const float d = vt[r] - s[r];
+        q[r] = d * d;
+      }
+      row_reduce(q, t);
+      float* obase = ga.out + (size_t)(row0 + t * 32) * ga.ldo + col;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float rstd = 1.0f / sqrtf(q[r] * (1.0f / 256.0f) + 1e-5f);
+        if (lrow(0, r) <= mrow - t * 32) obase[lrow(0, r) * ga.ldo] = (vt[r] - s[r]) * rstd * lw + lb;
+      }
+    };
+    tile(v[0], 0);
+    tile(v[1], 1);
   }
 }
 
@@ -633,3 +628,9 @@ hipError_t launch_gemm_x3(int epi, const GemmArgsX3Host& a, hipStream_t s) {
 }
 
 }  // namespace vge
+
+#ifdef VGE_TRACE
+extern "C" int vge_debug_x3_trace(long long* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_vge_trace), sizeof(long long) * (size_t)n);
+}
+#endif
