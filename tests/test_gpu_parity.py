@@ -203,12 +203,20 @@ def test_x3_stem_out_of_fp16_range(vg, golden_state_dict):
     assert (fe.cpu() - rf).abs().max().item() < 1e-4
 
 
-def test_x3_rejects_weights_outside_split_range(vg, golden_state_dict):
+def test_x3_large_weights_and_nonfinite(vg, golden_state_dict):
+    """Per-column power-of-two weight scaling: a weight far outside the fp16 range still matches the exact-f32
+    path; a non-finite weight cannot be split and is refused loudly (the f32 path takes it)."""
     VE, ops = vg
     from vge.lib import VgeError
     sd = {k: v.copy() for k, v in golden_state_dict.items()}
     k = next(k for k in sd if k.endswith("proj.weight"))
     sd[k][0, 0] = 1e5
-    with pytest.raises(VgeError, match="split range"):
+    torch.manual_seed(2)
+    x = torch.randn(5, 32, 2596, device=DEV)
+    s3, f3, _ = VE.load_model(sd, device=DEV, compute="f32x3").encode(x, frame_embed=True)
+    s1, f1, _ = VE.load_model(sd, device=DEV, compute="f32").encode(x, frame_embed=True)
+    assert (s3 - s1).abs().max().item() < 2e-5
+    assert (f3 - f1).abs().max().item() < 2e-5
+    sd[k][0, 1] = np.inf
+    with pytest.raises(VgeError, match="non-finite"):
         VE.load_model(sd, device=DEV, compute="f32x3")
-    VE.load_model(sd, device=DEV, compute="f32")   # the exact-f32 path accepts it

@@ -34,11 +34,13 @@ hipError_t encoder_kernel_setup();
 hipError_t encoder_x3_kernel_setup();
 struct EncDescX3Host {
   const _Float16* stem; const _Float16* conv; const _Float16* proj; const float* gn_w; const float* gn_b;
+  const float* cs;
   int in_col, d_in, n_stem_panels, pad;
 };
 struct GemmArgsX3Host {
   const float* A; int lda; const _Float16* W; float* out; int ldo; int M, K, N;
   const float* bias; const float* res; int ldr; const float* ln_w; const float* ln_b; const float* pe; const float* cls;
+  const float* cs;
 };
 hipError_t launch_conv_encoders_x3(const float*, int, const void*, int, float*, hipStream_t);
 hipError_t launch_gemm_x3(int, const GemmArgsX3Host&, hipStream_t);
@@ -115,11 +117,20 @@ void pack_conv(const float* W, std::vector<float>& out) {
     }
 }
 
-// 3xfp16 image: W[N][K] -> chunks [N/256][ceil(K/16)][plane 2][h 2][n 256][8] fp16, plane 0 = hi = f16(w),
-// plane 1 = lo = f16((w - hi) * 2^11); chunk c covers k = 16c + 8h + j (zero past K_real)
+// 3xfp16 image: W[N][K] -> chunks [N/256][ceil(K/16)][plane 2][h 2][n 256][8] fp16 of w' = w * 2^s_n, the
+// power-of-two column scale s_n bringing column n's largest |w| into [2^8, 2^9); plane 0 = hi = f16(w'),
+// plane 1 = lo = f16(w' - hi) (an fp16 residual, subnormals kept by the MFMA); chunk c covers
+// k = 16c + 8h + j (zero past K_real).  cs receives 2^-s_n per column (the kernels' epilogue factor).
 template <class Get>
-void pack_linear_x3(Get W, int N, int K_real, std::vector<_Float16>& out, int chunk_mult = 1) {
+void pack_linear_x3(Get W, int N, int K_real, std::vector<_Float16>& out, std::vector<float>& cs, int chunk_mult = 1) {
   const int nch = ((K_real + 15) / 16 + chunk_mult - 1) / chunk_mult * chunk_mult;  // streams run in groups of chunk_mult
+  std::vector<int> sh(N);
+  for (int n = 0; n < N; ++n) {
+    float m = 0.f;
+    for (int k = 0; k < K_real; ++k) m = std::max(m, std::fabs(W(n, k)));
+    sh[n] = (m > 0.f) ? std::min(8 - std::ilogb(m), 100) : 0;
+    cs.push_back(std::ldexp(1.0f, -sh[n]));
+  }
   const size_t base = out.size();
   out.resize(base + (size_t)(N / 256) * nch * 8192, (_Float16)0.0f);
   _Float16* o = out.data() + base;
@@ -130,9 +141,9 @@ void pack_linear_x3(Get W, int N, int K_real, std::vector<_Float16>& out, int ch
         for (int n = 0; n < 256; ++n)
           for (int j = 0; j < 8; ++j) {
             const int k = 16 * c + 8 * h + j;
-            const float w = (k < K_real) ? W(nb * 256 + n, k) : 0.0f;
+            const float w = (k < K_real) ? std::ldexp(W(nb * 256 + n, k), sh[nb * 256 + n]) : 0.0f;
             const _Float16 hi = (_Float16)w;
-            const _Float16 lo = (_Float16)((w - (float)hi) * 2048.0f);
+            const _Float16 lo = (_Float16)(w - (float)hi);
             ch[((0 * 2 + h) * 256 + n) * 8 + j] = hi;
             ch[((1 * 2 + h) * 256 + n) * 8 + j] = lo;
           }
@@ -150,9 +161,11 @@ struct vge_encoder {
   void* d_encs = nullptr;         // EncDescHost[10] or EncDescX3Host[10]
   vge::FuseParamsHost fuse{};
   const void* Wov = nullptr;      // packed (f32 chunks or fp16 chunks)
+  const float* Wov_cs = nullptr;  // x3: its column scales
   struct Layer {
     const void *in_w, *out_w, *l1_w, *l2_w;  // packed matrices
     const float *in_b, *out_b, *l1_b, *l2_b, *n1_w, *n1_b, *n2_w, *n2_b;
+    const float *in_cs, *out_cs, *l1_cs, *l2_cs;  // x3: per-column weight scales
   };
   std::vector<Layer> layers;
   const float* cls = nullptr;
@@ -281,28 +294,28 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
   std::vector<float> pk;      // f32 device image
   std::vector<_Float16> ph;   // fp16 device image (x3)
   // a packed matrix lives in pk (f32 mode) or ph (x3 mode); record (is_half, offset)
-  struct Mat { size_t off; };
+  struct Mat { size_t off, cs; };  // packed matrix (pk or ph offset); x3: column scales at pk[cs]
   auto pack_lin = [&](const float* W, int N, int K_real, int ldk, int P) -> Mat {
     if (x3) {
-      const size_t o = ph.size();
+      const Mat m{ph.size(), pk.size()};
       // the x3 kernels stream weights in groups of 8 chunks (zero chunks pad a short last panel)
-      pack_linear_x3([&](int n, int k) { return W[(size_t)n * ldk + k]; }, N, K_real, ph, 8);
-      return {o};
+      pack_linear_x3([&](int n, int k) { return W[(size_t)n * ldk + k]; }, N, K_real, ph, pk, 8);
+      return m;
     }
     const size_t o = pk.size();
     pack_linear(W, N, K_real, ldk, P, pk);
-    return {o};
+    return {o, 0};
   };
   auto pack_cv = [&](const float* W) -> Mat {
     if (x3) {
-      const size_t o = ph.size();
+      const Mat m{ph.size(), pk.size()};
       // K index = tap * 256 + ci (tap-major panels)
-      pack_linear_x3([&](int n, int k) { return W[((size_t)n * 256 + (k & 255)) * 5 + (k >> 8)]; }, 256, 5 * 256, ph);
-      return {o};
+      pack_linear_x3([&](int n, int k) { return W[((size_t)n * 256 + (k & 255)) * 5 + (k >> 8)]; }, 256, 5 * 256, ph, pk);
+      return m;
     }
     const size_t o = pk.size();
     pack_conv(W, pk);
-    return {o};
+    return {o, 0};
   };
 
   struct Off { Mat stem, conv, proj; size_t gnw, gnb; int in_col, d_in, P; };
@@ -440,10 +453,10 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
     vge_encoder_destroy(enc);
     return fail(VGE_ERR_HIP, std::string("vge_encoder_create: ") + hipGetErrorString(he));
   };
-  // the fp16 hi plane overflows for |w| >= 65520: refuse rather than score with inf/NaN
+  // column scaling keeps every finite weight in the fp16 planes' range; a non-finite one cannot be split
   for (const _Float16 v : ph)
     if (!std::isfinite((float)v))
-      return fail(VGE_ERR_ARG, "vge_encoder_create: a weight exceeds the 3xfp16 split range (|w| >= 65520); use VGE_F32");
+      return fail(VGE_ERR_ARG, "vge_encoder_create: non-finite weight, not representable by the 3xfp16 split; use VGE_F32");
   hipError_t he = x3 ? vge::encoder_x3_kernel_setup() : vge::encoder_kernel_setup();
   if (he == hipSuccess) he = hipMalloc(&enc->wbuf, pk.size() * sizeof(float));
   if (he == hipSuccess) he = hipMemcpy(enc->wbuf, pk.data(), pk.size() * sizeof(float), hipMemcpyHostToDevice);
@@ -457,7 +470,8 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
     std::vector<vge::EncDescX3Host> descs(10);
     for (int e = 0; e < 10; ++e)
       descs[e] = vge::EncDescX3Host{hb + eoff[e].stem.off, hb + eoff[e].conv.off, hb + eoff[e].proj.off,
-                                    wb + eoff[e].gnw, wb + eoff[e].gnb, eoff[e].in_col, eoff[e].d_in, eoff[e].P, 0};
+                                    wb + eoff[e].gnw, wb + eoff[e].gnb, wb + eoff[e].stem.cs,  // [10][256] scales
+                                    eoff[e].in_col, eoff[e].d_in, eoff[e].P, 0};
     he = hipMalloc(&enc->d_encs, sizeof(vge::EncDescX3Host) * 10);
     if (he == hipSuccess) he = hipMemcpy(enc->d_encs, descs.data(), sizeof(vge::EncDescX3Host) * 10, hipMemcpyHostToDevice);
   } else {
@@ -481,13 +495,16 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
     enc->fuse.has_motion[m] = 1;
   }
   enc->Wov = mat(m_wov);
+  enc->Wov_cs = x3 ? wb + m_wov.cs : nullptr;
   enc->cls = wb + off_cls;
   enc->pe = wb + off_pe;
   enc->layers.resize(L);
   for (int l = 0; l < L; ++l) {
     const LOff& o = loff[l];
+    auto csp = [&](const Mat& m) -> const float* { return x3 ? wb + m.cs : nullptr; };
     enc->layers[l] = vge_encoder::Layer{mat(o.in_w), mat(o.out_w), mat(o.l1_w), mat(o.l2_w), wb + o.in_b, wb + o.out_b,
-                                        wb + o.l1_b, wb + o.l2_b, wb + o.n1_w, wb + o.n1_b, wb + o.n2_w, wb + o.n2_b};
+                                        wb + o.l1_b, wb + o.l2_b, wb + o.n1_w, wb + o.n1_b, wb + o.n2_w, wb + o.n2_b,
+                                        csp(o.in_w), csp(o.out_w), csp(o.l1_w), csp(o.l2_w)};
   }
   *out = enc;
   return VGE_OK;
@@ -575,10 +592,10 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
   auto mark = [&](int k) -> hipError_t { return ev ? hipEventRecord(ev[k], s) : hipSuccess; };
   const bool x3 = enc->mode == VGE_F32X3;
   // one GEMM launcher for both modes (same epilogues; x3 = 3xfp16 split MFMA, f32 = exact f32 MFMA)
-  auto gemm = [&](int epi, const float* A, int lda, const void* W, float* o, int ldo, int Mr, int K, int N,
-                  const float* bias, const float* res, const float* lw, const float* lb) -> hipError_t {
+  auto gemm = [&](int epi, const float* A, int lda, const void* W, const float* cs, float* o, int ldo, int Mr, int K,
+                  int N, const float* bias, const float* res, const float* lw, const float* lb) -> hipError_t {
     if (x3) {
-      vge::GemmArgsX3Host g{A, lda, (const _Float16*)W, o, ldo, Mr, K, N, bias, res, 256, lw, lb, enc->pe, enc->cls};
+      vge::GemmArgsX3Host g{A, lda, (const _Float16*)W, o, ldo, Mr, K, N, bias, res, 256, lw, lb, enc->pe, enc->cls, cs};
       return vge::launch_gemm_x3(epi, g, s);
     }
     vge::GemmArgsHost g{A, lda, (const float*)W, o, ldo, Mr, K, N, bias, res, 256, lw, lb, enc->pe, enc->cls};
@@ -590,15 +607,20 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
   HIPCHK(mark(1));
   HIPCHK(vge::launch_fuse(enc->enc_out, frames, enc->fuse, enc->pooled, s));
   HIPCHK(mark(2));
-  HIPCHK(gemm(vge::EPI_TOKENS, enc->pooled, 256, enc->Wov, enc->x, 256, frames, 256, 256, nullptr, nullptr, nullptr, nullptr));
+  HIPCHK(gemm(vge::EPI_TOKENS, enc->pooled, 256, enc->Wov, enc->Wov_cs, enc->x, 256, frames, 256, 256, nullptr, nullptr,
+              nullptr, nullptr));
   HIPCHK(mark(3));
   for (int l = 0; l < enc->n_layers; ++l) {
     const vge_encoder::Layer& Ly = enc->layers[l];
-    HIPCHK(gemm(vge::EPI_BIAS, enc->x, 256, Ly.in_w, enc->qkv, 768, M, 256, 768, Ly.in_b, nullptr, nullptr, nullptr));
+    HIPCHK(gemm(vge::EPI_BIAS, enc->x, 256, Ly.in_w, Ly.in_cs, enc->qkv, 768, M, 256, 768, Ly.in_b, nullptr, nullptr,
+                nullptr));
     HIPCHK(vge::launch_attn(enc->qkv, B, enc->att, s));
-    HIPCHK(gemm(vge::EPI_BIAS_RES_LN, enc->att, 256, Ly.out_w, enc->x1, 256, M, 256, 256, Ly.out_b, enc->x, Ly.n1_w, Ly.n1_b));
-    HIPCHK(gemm(vge::EPI_BIAS_RELU, enc->x1, 256, Ly.l1_w, enc->h, 1024, M, 256, 1024, Ly.l1_b, nullptr, nullptr, nullptr));
-    HIPCHK(gemm(vge::EPI_BIAS_RES_LN, enc->h, 1024, Ly.l2_w, enc->x, 256, M, 1024, 256, Ly.l2_b, enc->x1, Ly.n2_w, Ly.n2_b));
+    HIPCHK(gemm(vge::EPI_BIAS_RES_LN, enc->att, 256, Ly.out_w, Ly.out_cs, enc->x1, 256, M, 256, 256, Ly.out_b, enc->x,
+                Ly.n1_w, Ly.n1_b));
+    HIPCHK(gemm(vge::EPI_BIAS_RELU, enc->x1, 256, Ly.l1_w, Ly.l1_cs, enc->h, 1024, M, 256, 1024, Ly.l1_b, nullptr,
+                nullptr, nullptr));
+    HIPCHK(gemm(vge::EPI_BIAS_RES_LN, enc->h, 1024, Ly.l2_w, Ly.l2_cs, enc->x, 256, M, 1024, 256, Ly.l2_b, enc->x1,
+                Ly.n2_w, Ly.n2_b));
   }
   HIPCHK(mark(4));
   HIPCHK(vge::launch_embed_tc(enc->x, B, seq_embed, frame_embed, tc_window, s));

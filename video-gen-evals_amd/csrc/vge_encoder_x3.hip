@@ -1,13 +1,14 @@
 // Split-precision ("3xfp16") MFMA path of the fusion encoder (gfx950).
 //
-// Every GEMM operand x is carried as two fp16 planes, hi = f16(x) and lo = f16((x - hi) * 2^11), and
-// each product is formed as hi_a*hi_b + 2^-11 (hi_a*lo_b + lo_a*hi_b) with v_mfma_f32_32x32x16_f16
-// (f32 accumulate; two accumulators, combined in the epilogue).  The dropped lo*lo term and the fp16
-// rounding of lo leave a relative error of ~2^-21 per product, i.e. f32-class results (measured AC/TC
-// deviation from the exact f32 path ~1e-7, see tests/test_gpu_parity.py), at 3 f16 MFMAs per K=16
-// step instead of 4 f32 MFMAs per K=4 step: 5.3x the f32 MFMA rate.  Operands are scaled by powers of
-// two (exact) so the fp16 planes never overflow: per row of a stem panel, per window inside the conv
-// chain, per 64-row tile and panel in the GEMMs.
+// Every GEMM operand x is carried as two fp16 planes, hi = f16(x) and lo = f16(x - hi), and each product
+// is formed as hi_a*hi_b + hi_a*lo_b + lo_a*hi_b by three v_mfma_f32_32x32x16_f16 into one f32
+// accumulator.  The dropped lo*lo term and the fp16 rounding of lo leave a relative error of ~2^-21 per
+// product, i.e. f32-class results (AC/TC within ~1e-7 of the exact f32 path, tests/test_gpu_parity.py),
+// at 3 f16 MFMAs per K=16 step instead of 4 f32 MFMAs per K=4 step: 5.3x the f32 MFMA rate.  Both
+// operands are scaled by powers of two (exact) so that a block's largest |value| sits in [2^8, 2^9): the
+// planes never overflow and the residual lo keeps ~11 significant bits (fp16 subnormals are kept by the
+// MFMA).  Activations: per row of a stem panel, per window inside the conv chain, per 64-row tile and
+// panel in the GEMMs; weights: per output column at pack time (vge_api.cpp pack_linear_x3, factor `cs`).
 //
 //   conv_encoder_x3_kernel   MovementConvEncoder x10 (model.py:21-58): one workgroup = 1 encoder x 2 windows
 //                            (64 rows), 8 waves, wave w owns output columns 32w..32w+31 of all 64 rows.
@@ -56,8 +57,6 @@ constexpr int PLANE_B = 8192;        // bytes between the hi and lo planes of a 
 constexpr int NWAVE = 8;             // waves per workgroup
 constexpr int RT = 2;                // 32-row tiles per wave (all 64 rows)
 constexpr int PF = 8;                // weight chunks in flight per wave; streams are multiples of PF chunks
-constexpr float LO_SCALE = 2048.0f;  // 2^11
-constexpr float LO_INV = 1.0f / 2048.0f;
 
 __device__ __forceinline__ floatx16 mfma32(half8 a, half8 b, floatx16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
@@ -66,7 +65,7 @@ __device__ __forceinline__ floatx16 mfma32(half8 a, half8 b, floatx16 c) {
 __device__ __forceinline__ void split_store(_Float16* hi, _Float16* lo, float v) {
   const _Float16 h = (_Float16)v;
   *hi = h;
-  *lo = (_Float16)((v - (float)h) * LO_SCALE);
+  *lo = (_Float16)(v - (float)h);
 }
 
 __device__ __forceinline__ int fp16_range_exp(float m) {  // 2^-e brings m into [2^8, 2^9); 2^+-e stays normal
@@ -74,15 +73,14 @@ __device__ __forceinline__ int fp16_range_exp(float m) {  // 2^-e brings m into 
 }
 
 struct Acc {
-  floatx16 hh[RT];
-  floatx16 x[RT];
+  floatx16 c[RT];
 };
 
 __device__ __forceinline__ void acc_zero(Acc& a) {
 #pragma unroll
   for (int t = 0; t < RT; ++t) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) { a.hh[t][r] = 0.f; a.x[t][r] = 0.f; }
+    for (int r = 0; r < 16; ++r) a.c[t][r] = 0.f;
   }
 }
 
@@ -94,9 +92,9 @@ __device__ __forceinline__ void mma_chunk(Acc& acc, const AFrag& a, half8 bh, ha
 #if !(VGE_ABL & 1)
 #pragma unroll
   for (int t = 0; t < RT; ++t) {
-    acc.hh[t] = mfma32(a.h[t], bh, acc.hh[t]);
-    acc.x[t] = mfma32(a.h[t], bl, acc.x[t]);
-    acc.x[t] = mfma32(a.l[t], bh, acc.x[t]);
+    acc.c[t] = mfma32(a.h[t], bh, acc.c[t]);
+    acc.c[t] = mfma32(a.h[t], bl, acc.c[t]);
+    acc.c[t] = mfma32(a.l[t], bh, acc.c[t]);
   }
 #else
   asm volatile("" ::"v"(a.h[0]), "v"(a.l[RT - 1]), "v"(bh), "v"(bl));
@@ -150,6 +148,7 @@ struct EncDescX3 {
   const _Float16* proj;  // 16 chunks
   const float* gn_w;     // [4][256]
   const float* gn_b;     // [4][256]
+  const float* cs;       // [10][256] weight column scales: stem, conv 0..7, proj
   int in_col, d_in, n_stem_panels, pad;
 };
 
@@ -226,7 +225,7 @@ __global__ void __launch_bounds__(512, 1) conv_encoder_x3_kernel(const float* __
       for (int r = 0; r < 16; r += 2) {
         const floatx2 y = (floatx2){v[t][r], v[t][r + 1]} * sc;
         const _Float16 h0 = (_Float16)y.x, h1 = (_Float16)y.y;
-        const floatx2 lo = (y - (floatx2){(float)h0, (float)h1}) * LO_SCALE;
+        const floatx2 lo = y - (floatx2){(float)h0, (float)h1};
         const int row = crow(t, r);  // rows r and r + 1 of the tile are adjacent
         Xh[row * XS + col] = h0;
         Xh[(row + 1) * XS + col] = h1;
@@ -289,9 +288,7 @@ __global__ void __launch_bounds__(512, 1) conv_encoder_x3_kernel(const float* __
       for (int t = 0; t < RT; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const float f = ldexpf(1.0f, eprev[crow(t, r)] - ecur[crow(t, r)]);
-          acc.hh[t][r] *= f;
-          acc.x[t][r] *= f;
+          acc.c[t][r] *= ldexpf(1.0f, eprev[crow(t, r)] - ecur[crow(t, r)]);
         }
     }
     run_stream(acc, reinterpret_cast<const char*>(ed.stem) + (size_t)p * 16 * CHUNK_B, ((kw + 127) >> 7) * PF, loff,
@@ -300,10 +297,11 @@ __global__ void __launch_bounds__(512, 1) conv_encoder_x3_kernel(const float* __
   }
   {
     const int* efin = rexp + ((ed.n_stem_panels - 1) & 1) * 64;
+    const float wcs = ed.cs[col];
 #pragma unroll
     for (int t = 0; t < RT; ++t)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) res[t][r] = ldexpf(acc.hh[t][r] + acc.x[t][r] * LO_INV, efin[crow(t, r)]);
+      for (int r = 0; r < 16; ++r) res[t][r] = ldexpf(acc.c[t][r] * wcs, efin[crow(t, r)]);
   }
   STAMP(2);
   int xexp[RT];
@@ -315,6 +313,7 @@ __global__ void __launch_bounds__(512, 1) conv_encoder_x3_kernel(const float* __
   for (int blk = 0; blk < 4; ++blk) {
     const int dil = 1 << blk;
     const float gw = ed.gn_w[blk * 256 + col], gb = ed.gn_b[blk * 256 + col];
+    const float wcs0 = ed.cs[(1 + blk * 2) * 256 + col], wcs1 = ed.cs[(2 + blk * 2) * 256 + col];
     for (int cv = 0; cv < 2; ++cv) {
       acc_zero(acc);
       auto afn = [&](int c, AFrag& f) {
@@ -332,18 +331,17 @@ __global__ void __launch_bounds__(512, 1) conv_encoder_x3_kernel(const float* __
       run_stream(acc, reinterpret_cast<const char*>(ed.conv) + (size_t)(blk * 2 + cv) * 5 * 16 * CHUNK_B, 5 * 16,
                  loff, afn);
       STAMP(4 + (blk * 2 + cv) * 2);
-      // epilogue in packed f32 (v_pk_fma_f32: two rows per instruction); combine in place:
-      // (hh + 2^-11 x) * 2^xexp -> [+ residual] -> GELU [-> GroupNorm]
-      floatx16 (&v)[RT] = acc.hh;
+      // epilogue in packed f32 (v_pk_fma_f32: two rows per instruction), in place:
+      // acc * 2^xexp * column scale -> [+ residual] -> GELU [-> GroupNorm]
+      floatx16 (&v)[RT] = acc.c;
       floatx2 s2[RT];
 #pragma unroll
       for (int t = 0; t < RT; ++t) {
-        const float xs = ldexpf(1.0f, xexp[t]), xl = xs * LO_INV;
+        const float xs = ldexpf(1.0f, xexp[t]) * (cv == 0 ? wcs0 : wcs1);
         s2[t] = 0.f;
 #pragma unroll
         for (int r = 0; r < 16; r += 2) {
-          floatx2 y = __builtin_elementwise_fma((floatx2){acc.x[t][r], acc.x[t][r + 1]}, (floatx2)xl,
-                                                (floatx2){acc.hh[t][r], acc.hh[t][r + 1]} * xs);
+          floatx2 y = (floatx2){acc.c[t][r], acc.c[t][r + 1]} * xs;
           if (cv == 1) y += (floatx2){res[t][r], res[t][r + 1]};
           y = gelu2(y);
           s2[t] += y;
@@ -397,10 +395,10 @@ __global__ void __launch_bounds__(512, 1) conv_encoder_x3_kernel(const float* __
   for (int t = 0; t < RT; ++t) {
     const int win = pair * 2 + t;
     if (win < n_windows) {
-      const float xs = ldexpf(1.0f, xexp[t]);
+      const float xs = ldexpf(1.0f, xexp[t]) * ed.cs[9 * 256 + col];
       float* o = enc_out + ((size_t)e * n_windows * VGE_T + (size_t)win * VGE_T) * VGE_D;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) o[crow(0, r) * VGE_D + col] = (acc.hh[t][r] + acc.x[t][r] * LO_INV) * xs;
+      for (int r = 0; r < 16; ++r) o[crow(0, r) * VGE_D + col] = acc.c[t][r] * xs;
     }
   }
   STAMP(21);
@@ -422,6 +420,7 @@ struct GemmArgsX3 {
   const float* ln_w; const float* ln_b;
   const float* pe;
   const float* cls;
+  const float* cs;              // [N] weight column scales
 };
 
 // block = 8 waves, BM = 64 rows x BN = 256 columns, wave w owns columns 32w..32w+31 of all 64 rows
@@ -469,7 +468,7 @@ __global__ void __launch_bounds__(512, 1) gemm_x3_kernel(GemmArgsX3 ga) {
 #pragma unroll
       for (int t = 0; t < RT; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) { acc.hh[t][r] *= f; acc.x[t][r] *= f; }
+        for (int r = 0; r < 16; ++r) acc.c[t][r] *= f;
     }
     aexp = e;
 #pragma unroll
@@ -491,13 +490,13 @@ __global__ void __launch_bounds__(512, 1) gemm_x3_kernel(GemmArgsX3 ga) {
     __syncthreads();  // every wave is done reading the panel
   }
 
+  const int col = nb * 256 + wave * 32 + i;
   float v[RT][16];
-  const float as = ldexpf(1.0f, aexp);
+  const float as = ldexpf(1.0f, aexp) * ga.cs[col];
 #pragma unroll
   for (int t = 0; t < RT; ++t)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[t][r] = (acc.hh[t][r] + acc.x[t][r] * LO_INV) * as;
-  const int col = nb * 256 + wave * 32 + i;
+    for (int r = 0; r < 16; ++r) v[t][r] = acc.c[t][r] * as;
 
   if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) {
     const float bb = ga.bias[col];
@@ -583,6 +582,7 @@ namespace vge {
 
 struct EncDescX3Host {
   const _Float16* stem; const _Float16* conv; const _Float16* proj; const float* gn_w; const float* gn_b;
+  const float* cs;
   int in_col, d_in, n_stem_panels, pad;
 };
 static_assert(sizeof(EncDescX3Host) == sizeof(EncDescX3), "EncDescX3 layout");
@@ -590,6 +590,7 @@ static_assert(sizeof(EncDescX3Host) == sizeof(EncDescX3), "EncDescX3 layout");
 struct GemmArgsX3Host {
   const float* A; int lda; const _Float16* W; float* out; int ldo; int M, K, N;
   const float* bias; const float* res; int ldr; const float* ln_w; const float* ln_b; const float* pe; const float* cls;
+  const float* cs;
 };
 static_assert(sizeof(GemmArgsX3Host) == sizeof(GemmArgsX3), "GemmArgsX3 layout");
 
