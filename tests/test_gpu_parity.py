@@ -220,3 +220,19 @@ def test_x3_large_weights_and_nonfinite(vg, golden_state_dict):
     sd[k][0, 1] = np.inf
     with pytest.raises(VgeError, match="non-finite"):
         VE.load_model(sd, device=DEV, compute="f32x3")
+
+
+@pytest.mark.parametrize("n", [256, 293, 600])
+def test_x3_quad_and_pair_blocks_vs_f32(vg, golden_state_dict, n):
+    """Large batches run the conv chain in 4-window (quad) blocks with 2-window blocks filling the last round
+    (256: quads + a round of pairs; 293: quads + one half-empty pair; 600: quads only).  Checked against the
+    exact-f32 MFMA path (itself pinned to the oracle above) on the same input."""
+    VE, ops = vg
+    torch.manual_seed(n)
+    x = torch.randn(n, 32, 2596, device=DEV)
+    x[:, :, 40:48] *= 1e4   # a few large z-scores: per-row / per-window scaling at work
+    s3, f3, t3 = VE.load_model(golden_state_dict, device=DEV, compute="f32x3").encode(x, frame_embed=True, tc=True)
+    s1, f1, t1 = VE.load_model(golden_state_dict, device=DEV, compute="f32").encode(x, frame_embed=True, tc=True)
+    assert (s3 - s1).abs().max().item() < 2e-5
+    assert (f3 - f1).abs().max().item() < 2e-5
+    assert (t3 - t1).abs().max().item() < 1e-5

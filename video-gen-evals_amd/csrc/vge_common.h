@@ -30,6 +30,53 @@ __device__ __forceinline__ float wave_max(float v) {
   for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
   return v;
 }
+// ---- DPP reductions (no LDS round trips): the result is valid in the LAST lane of the group only ------
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ float dpp_f(float old, float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old), __builtin_bit_cast(int, x),
+                                                               CTRL, ROW_MASK, 0xf, false));
+}
+#define VGE_DPP_QP_XOR1 0xB1        // quad_perm [1,0,3,2]
+#define VGE_DPP_QP_XOR2 0x4E        // quad_perm [2,3,0,1]
+#define VGE_DPP_ROW_HALF_MIRROR 0x141
+#define VGE_DPP_ROW_MIRROR 0x140
+#define VGE_DPP_ROW_BCAST15 0x142
+#define VGE_DPP_ROW_BCAST31 0x143
+// sum over each 16-lane row, in every lane of the row
+__device__ __forceinline__ float row16_sum(float x) {
+  x += dpp_f<VGE_DPP_QP_XOR1, 0xf>(0.f, x);
+  x += dpp_f<VGE_DPP_QP_XOR2, 0xf>(0.f, x);
+  x += dpp_f<VGE_DPP_ROW_HALF_MIRROR, 0xf>(0.f, x);
+  x += dpp_f<VGE_DPP_ROW_MIRROR, 0xf>(0.f, x);
+  return x;
+}
+__device__ __forceinline__ float row16_max(float x) {
+  x = fmaxf(x, dpp_f<VGE_DPP_QP_XOR1, 0xf>(x, x));
+  x = fmaxf(x, dpp_f<VGE_DPP_QP_XOR2, 0xf>(x, x));
+  x = fmaxf(x, dpp_f<VGE_DPP_ROW_HALF_MIRROR, 0xf>(x, x));
+  x = fmaxf(x, dpp_f<VGE_DPP_ROW_MIRROR, 0xf>(x, x));
+  return x;
+}
+// sum over each 32-lane half: valid in lanes 31 and 63
+__device__ __forceinline__ float half_sum_last(float x) {
+  x = row16_sum(x);
+  return x + dpp_f<VGE_DPP_ROW_BCAST15, 0xa>(0.f, x);
+}
+// sum / max over the wave: valid in lane 63
+__device__ __forceinline__ float wave_sum_last(float x) {
+  x = half_sum_last(x);
+  return x + dpp_f<VGE_DPP_ROW_BCAST31, 0xc>(0.f, x);
+}
+__device__ __forceinline__ float wave_max_last(float x) {
+  x = row16_max(x);
+  x = fmaxf(x, dpp_f<VGE_DPP_ROW_BCAST15, 0xa>(x, x));
+  return fmaxf(x, dpp_f<VGE_DPP_ROW_BCAST31, 0xc>(x, x));
+}
+// wave max broadcast to every lane (lane 63's value via readlane)
+__device__ __forceinline__ float wave_max_all(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, wave_max_last(x)), 63));
+}
+
 // sum over the 16 lanes that share (lane >> 4): xor offsets 1..8 stay inside a 16-lane group
 __device__ __forceinline__ float group16_sum(float v) {
 #pragma unroll
@@ -37,47 +84,75 @@ __device__ __forceinline__ float group16_sum(float v) {
   return v;
 }
 
-// exact-erf GELU (nn.GELU() default; ATen: x * 0.5 * (1 + erf(x * M_SQRT1_2))), branch free.
-// erf(a), a = |z|: a + a q(a^2) for a < 1, 1 - exp(-p(a)) for a >= 1, with the minimax coefficients of the
-// ROCm device library's erff (ocml) but both pieces evaluated and selected (no divergent branches), and
-// exp via v_exp_f32.  Max |error| vs erf in double 7.4e-8 over [-8, 8] (tools: host check in
-// tests/test_lib_abi.py::test_erf_branch_free_accuracy); the packed form runs two values per v_pk_fma_f32.
-__device__ __forceinline__ floatx2 erf2(floatx2 z) {
-  const floatx2 a = __builtin_elementwise_abs(z);
-  const floatx2 s = a * a;
-  floatx2 q = __builtin_elementwise_fma(s, (floatx2)(-0x1.268bc20000000p-11f), (floatx2)(0x1.4208280000000p-8f));
-  q = __builtin_elementwise_fma(s, q, (floatx2)(-0x1.b593700000000p-6f));
-  q = __builtin_elementwise_fma(s, q, (floatx2)(0x1.ce077c0000000p-4f));
-  q = __builtin_elementwise_fma(s, q, (floatx2)(-0x1.8126600000000p-2f));
-  q = __builtin_elementwise_fma(s, q, (floatx2)(0x1.06eba00000000p-3f));
-  const floatx2 rs = __builtin_elementwise_fma(a, q, a);
-  floatx2 p = __builtin_elementwise_fma(a, (floatx2)(0x1.1d31560000000p-16f), (floatx2)(-0x1.8d12900000000p-12f));
-  p = __builtin_elementwise_fma(a, p, (floatx2)(0x1.f9a6d20000000p-9f));
-  p = __builtin_elementwise_fma(a, p, (floatx2)(-0x1.8c31640000000p-6f));
-  p = __builtin_elementwise_fma(a, p, (floatx2)(0x1.b4e9c80000000p-4f));
-  p = __builtin_elementwise_fma(a, p, (floatx2)(0x1.4515fa0000000p-1f));
-  p = __builtin_elementwise_fma(a, p, (floatx2)(0x1.078e500000000p-3f));
-  p = __builtin_elementwise_fma(a, p, a);
-  const floatx2 l = p * (floatx2)(-1.44269504f);
-  floatx2 t;
-  t.x = __builtin_amdgcn_exp2f(l.x);
-  t.y = __builtin_amdgcn_exp2f(l.y);
-  const floatx2 rb = 1.0f - t;
-  floatx2 r;
-  r.x = a.x < 1.0f ? rs.x : rb.x;
-  r.y = a.y < 1.0f ? rs.y : rb.y;
-  return __builtin_elementwise_copysign(r, z);
-}
+// exact-erf GELU (nn.GELU() default; ATen: x * 0.5 * (1 + erf(x * M_SQRT1_2))).  gelu_erf: scalar, ocml
+// erff (f32 path).  gelu2_many: branch free and packed (two values per v_pk_fma_f32): erf(a), a = |z|, is
+// a + a q(a^2) for a < 1 and 1 - exp(-p(a)) for a >= 1 with the minimax coefficients of ocml's erff, both
+// pieces evaluated and selected, exp via v_exp_f32.  Max |error| vs erf in double 7.4e-8 over [-8, 8]
+// (host restatement checked in tests/test_lib_abi.py::test_erf_branch_free_accuracy).
 #if defined(VGE_ABL) && (VGE_ABL & 16)
-__device__ __forceinline__ floatx2 gelu2(floatx2 x) { return x; }
 __device__ __forceinline__ float gelu_erf(float x) { return x; }
 #else
-__device__ __forceinline__ floatx2 gelu2(floatx2 x) {
-  const floatx2 hx = x * 0.5f;
-  return __builtin_elementwise_fma(hx, erf2(x * 0.70710678118654752440f), hx);
-}
 __device__ __forceinline__ float gelu_erf(float x) { return x * 0.5f * (1.0f + erff(x * 0.70710678118654752440f)); }
 #endif
+// K pairs at once, written stage by stage so K independent dependency chains interleave (one pair's
+// chain alone is ~20 dependent packed ops with hazard nops between them)
+template <int K>
+__device__ __forceinline__ void gelu2_many(floatx2 (&y)[K]) {
+#if !(defined(VGE_ABL) && (VGE_ABL & 16))
+  floatx2 z[K], a[K], s[K], q[K], p[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    z[k] = y[k] * 0.70710678118654752440f;
+    a[k] = __builtin_elementwise_abs(z[k]);
+    s[k] = a[k] * a[k];
+  }
+#define VGE_STAGE(dst, x, c1, c0)                                                                  \
+  _Pragma("unroll") for (int k = 0; k < K; ++k) dst[k] = __builtin_elementwise_fma(x[k], c1, c0);
+  VGE_STAGE(q, s, (floatx2)(-0x1.268bc2p-11f), (floatx2)(0x1.420828p-8f))
+  VGE_STAGE(p, a, (floatx2)(0x1.1d3156p-16f), (floatx2)(-0x1.8d129p-12f))
+#undef VGE_STAGE
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    q[k] = __builtin_elementwise_fma(s[k], q[k], (floatx2)(-0x1.b5937p-6f));
+    p[k] = __builtin_elementwise_fma(a[k], p[k], (floatx2)(0x1.f9a6d2p-9f));
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    q[k] = __builtin_elementwise_fma(s[k], q[k], (floatx2)(0x1.ce077cp-4f));
+    p[k] = __builtin_elementwise_fma(a[k], p[k], (floatx2)(-0x1.8c3164p-6f));
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    q[k] = __builtin_elementwise_fma(s[k], q[k], (floatx2)(-0x1.81266p-2f));
+    p[k] = __builtin_elementwise_fma(a[k], p[k], (floatx2)(0x1.b4e9c8p-4f));
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    q[k] = __builtin_elementwise_fma(s[k], q[k], (floatx2)(0x1.06eba0p-3f));
+    p[k] = __builtin_elementwise_fma(a[k], p[k], (floatx2)(0x1.4515fap-1f));
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    q[k] = __builtin_elementwise_fma(a[k], q[k], a[k]);  // erf(a), a < 1
+    p[k] = __builtin_elementwise_fma(a[k], p[k], (floatx2)(0x1.078e5p-3f));
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) p[k] = __builtin_elementwise_fma(a[k], p[k], a[k]) * (floatx2)(-1.44269504f);
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    p[k].x = __builtin_amdgcn_exp2f(p[k].x);
+    p[k].y = __builtin_amdgcn_exp2f(p[k].y);
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    floatx2 r;
+    r.x = a[k].x < 1.0f ? q[k].x : 1.0f - p[k].x;
+    r.y = a[k].y < 1.0f ? q[k].y : 1.0f - p[k].y;
+    const floatx2 hx = y[k] * 0.5f;
+    y[k] = __builtin_elementwise_fma(hx, __builtin_elementwise_copysign(r, z[k]), hx);
+  }
+#endif
+}
 
 // v_mfma_f32_16x16x4_f32: exact f32 (bitwise an fmaf chain over k).  Lane l supplies
 // A[i = l&15][k = l>>4] and B[k = l>>4][j = l&15]; C/D: col = l&15, row = (l>>4)*4 + r.

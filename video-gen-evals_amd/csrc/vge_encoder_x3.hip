@@ -24,6 +24,7 @@
 // A weight chunk = 16 K x 256 columns: [plane][h][n][8] fp16 = 16 KB, so a lane's B fragment of a chunk
 // is one 16-B load per plane and a wave's 32 columns are two contiguous 512-B runs per plane.
 #include "vge_common.h"
+#include <algorithm>
 #include <cstring>
 
 #ifndef VGE_ABL
@@ -51,12 +52,11 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr int XS = 264;              // fp16 per LDS activation row (256 + 8 pad: conflict-free b128 reads)
 constexpr int XSB = XS * 2;          // bytes per activation row
-constexpr int XROWS = 65;            // 64 activation rows + one all-zero row that masked conv taps read
 constexpr int CHUNK_B = 16384;       // bytes per weight chunk
 constexpr int PLANE_B = 8192;        // bytes between the hi and lo planes of a chunk
-constexpr int NWAVE = 8;             // waves per workgroup
-constexpr int RT = 2;                // 32-row tiles per wave (all 64 rows)
-constexpr int PF = 8;                // weight chunks in flight per wave; streams are multiples of PF chunks
+constexpr int STREAM_GROUP = 8;      // weight streams are packed as multiples of 8 chunks
+constexpr int CONV_PF = 4;           // weight chunks in flight per wave: conv (a quad wave holds 128 x 64 outputs)
+constexpr int GEMM_PF = 8;           // ... and GEMM waves (64 x 32 outputs)
 
 __device__ __forceinline__ floatx16 mfma32(half8 a, half8 b, floatx16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
@@ -72,78 +72,99 @@ __device__ __forceinline__ int fp16_range_exp(float m) {  // 2^-e brings m into 
   return (m > 0.f && m <= 3.0e38f) ? max(ilogbf(m) - 8, -100) : 0;
 }
 
+// A wave's output tile: R row tiles x N column tiles of 32 x 32, one f32 accumulator each
+template <int R, int N>
 struct Acc {
-  floatx16 c[RT];
-};
-
-__device__ __forceinline__ void acc_zero(Acc& a) {
+  floatx16 c[R][N];
+  __device__ __forceinline__ void zero() {
 #pragma unroll
-  for (int t = 0; t < RT; ++t) {
+    for (int t = 0; t < R; ++t)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) a.c[t][r] = 0.f;
+      for (int n = 0; n < N; ++n)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) c[t][n][r] = 0.f;
   }
-}
-
-struct AFrag {
-  half8 h[RT], l[RT];
 };
 
-__device__ __forceinline__ void mma_chunk(Acc& acc, const AFrag& a, half8 bh, half8 bl) {
+template <int R>
+struct AFrag {  // A fragments (hi, lo) of one 16-K chunk for R row tiles
+  half8 h[R], l[R];
+};
+
+template <int N>
+struct BFrag {  // B fragments (hi, lo) of one 16-K chunk for N column tiles
+  half8 h[N], l[N];
+};
+
+template <int R, int N>
+__device__ __forceinline__ void mma_chunk(Acc<R, N>& acc, const AFrag<R>& a, const BFrag<N>& b) {
 #if !(VGE_ABL & 1)
 #pragma unroll
-  for (int t = 0; t < RT; ++t) {
-    acc.c[t] = mfma32(a.h[t], bh, acc.c[t]);
-    acc.c[t] = mfma32(a.h[t], bl, acc.c[t]);
-    acc.c[t] = mfma32(a.l[t], bh, acc.c[t]);
-  }
+  for (int n = 0; n < N; ++n)
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+      acc.c[t][n] = mfma32(a.h[t], b.h[n], acc.c[t][n]);
+      acc.c[t][n] = mfma32(a.h[t], b.l[n], acc.c[t][n]);
+      acc.c[t][n] = mfma32(a.l[t], b.h[n], acc.c[t][n]);
+    }
 #else
-  asm volatile("" ::"v"(a.h[0]), "v"(a.l[RT - 1]), "v"(bh), "v"(bl));
+  asm volatile("" ::"v"(a.h[0]), "v"(a.l[R - 1]), "v"(b.h[0]), "v"(b.l[N - 1]));
 #endif
 }
 
 typedef const __attribute__((address_space(1))) char* gchar;  // global (not flat) loads: counted by vmcnt only
 typedef const __attribute__((address_space(1))) half8* ghalf8;
 
-__device__ __forceinline__ void load_b(gchar g, int c, unsigned loff, half8& bh, half8& bl) {
+// column tile n of this lane sits 32 columns (512 B) after tile n - 1
+template <int N>
+__device__ __forceinline__ void load_b(gchar g, int c, unsigned loff, BFrag<N>& b) {
   gchar p = g + (size_t)c * CHUNK_B + loff;
-  bh = *reinterpret_cast<ghalf8>(p);
-  bl = *reinterpret_cast<ghalf8>(p + PLANE_B);
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    b.h[n] = *reinterpret_cast<ghalf8>(p + n * 512);
+    b.l[n] = *reinterpret_cast<ghalf8>(p + n * 512 + PLANE_B);
+  }
 }
 
-// Multiply this wave's 64 x 32 output tile by a stream of n weight chunks (n a multiple of PF, >= PF).
-// afn(c, AFrag&) reads the A fragments of chunk c from LDS.  B fragments are loaded PF - 1 chunks ahead
-// into a register ring; the loop is unrolled by PF so every ring index is static and the compiler's
-// counted vmcnt waits retire exactly the chunk being consumed.
-template <class AFn>
-__device__ __forceinline__ void run_stream(Acc& acc, const void* gw, int n, unsigned loff, AFn afn) {
+// Multiply a wave's output tile by a stream of n weight chunks (n a multiple of PF, >= PF, PF | 8).  afn(c, AFrag&)
+// reads the A fragments of chunk c from LDS (one chunk ahead).  B fragments are loaded PF - 1 chunks ahead
+// into a register ring; the loop is unrolled by PF so every ring index is static and the compiler's counted
+// vmcnt waits retire exactly the chunk being consumed.
+template <int PF, int R, int N, class AFn>
+__device__ __forceinline__ void run_stream(Acc<R, N>& acc, const void* gw, int n, unsigned loff, AFn afn) {
   const gchar g = (gchar)gw;
-  half8 bh[PF], bl[PF];
+  BFrag<N> b[PF];
 #pragma unroll
-  for (int j = 0; j < PF - 1; ++j) load_b(g, j, loff, bh[j], bl[j]);
-  AFrag a[2];
+  for (int j = 0; j < PF - 1; ++j) load_b(g, j, loff, b[j]);
+  AFrag<R> a[2];
   afn(0, a[0]);
   for (int c0 = 0; c0 < n; c0 += PF) {
 #pragma unroll
     for (int j = 0; j < PF; ++j) {
       const int c = c0 + j;
 #if !(VGE_ABL & 2)
-      load_b(g, min(c + PF - 1, n - 1), loff, bh[(j + PF - 1) % PF], bl[(j + PF - 1) % PF]);
+      load_b(g, min(c + PF - 1, n - 1), loff, b[(j + PF - 1) % PF]);
 #endif
 #if !(VGE_ABL & 4)
       afn(min(c + 1, n - 1), a[(j + 1) & 1]);
 #endif
-      mma_chunk(acc, a[j & 1], bh[j], bl[j]);
+      mma_chunk(acc, a[j & 1], b[j]);
       // pin this step's loads in place: without it the compiler hoists every A read of the unrolled group
       // and sinks the B loads next to their use, which collapses the prefetch to vmcnt(0) waits
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
     }
+#if !(VGE_ABL & 8)
+    // keep the two waves of each SIMD abreast (a raw s_barrier: LDS reads retired, loads stay in flight);
+    // a wave left alone at the end of a stream has too few loads in flight to keep the MFMA pipe busy
+    lds_barrier();
+#endif
   }
 }
 
 // ------------------------------------------------------------------ conv encoder chain
 struct EncDescX3 {
-  const _Float16* stem;  // stem chunks; panel p (256 K) starts at chunk 16p, padded to a multiple of PF chunks
+  const _Float16* stem;  // stem chunks; panel p (256 K) starts at chunk 16p, padded to STREAM_GROUP chunks
   const _Float16* conv;  // 8 convs x 5 taps x 16 chunks
   const _Float16* proj;  // 16 chunks
   const float* gn_w;     // [4][256]
@@ -152,92 +173,101 @@ struct EncDescX3 {
   int in_col, d_in, n_stem_panels, pad;
 };
 
-constexpr int CONVX3_LDS_BYTES = 2 * XROWS * XSB + (4 * RT * NWAVE + 128) * 4;
+// One workgroup = one encoder x W windows (32 W rows), 8 waves (two per SIMD); wave w owns output columns
+// 32w..32w+31 of all rows, so every weight byte streamed into the CU feeds 32 W rows.
+constexpr int CONV_WAVES = 8;
+template <int W>
+constexpr int conv_lds_bytes() {
+  return 2 * (32 * W + 1) * XSB + (4 * W * CONV_WAVES + 2 * 32 * W) * 4;
+}
 
-__global__ void __launch_bounds__(512, 1) conv_encoder_x3_kernel(const float* __restrict__ feats, int n_windows,
-                                                                  const EncDescX3* __restrict__ encs, int n_enc,
-                                                                  float* __restrict__ enc_out) {
-  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
-  _Float16* Xh = reinterpret_cast<_Float16*>(lds_raw);                       // [65][XS]
-  _Float16* Xl = Xh + XROWS * XS;                                            // [65][XS]
-  float* red = reinterpret_cast<float*>(lds_raw + 2 * XROWS * XSB);          // [4 slots][RT][NWAVE] partials
-  int* rexp = reinterpret_cast<int*>(red + 4 * RT * NWAVE);                  // [2][64] stem row exponents
-
-  // XCD-aware remap: the 8 XCDs take contiguous work ranges, so co-resident blocks of an XCD share an encoder
-  const int n_pairs = (n_windows + 1) >> 1;
-  const int nblk = n_enc * n_pairs;
-  const int b = blockIdx.x;
-  const int q8 = nblk >> 3, r8 = nblk & 7, x8 = b & 7;
-  const int work = (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (b >> 3);
-  const int e = work / n_pairs, pair = work % n_pairs;
-  const EncDescX3 ed = encs[e];
+// blocks [0, n_quad) take 4 windows, the rest 2: quads stream each weight byte for twice the rows, pairs
+// fill the last round (see launch_conv_encoders_x3)
+template <int W>
+__device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feats, int n_windows, int win0,
+                                                  const EncDescX3& ed, int e, float* __restrict__ enc_out,
+                                                  char* lds_raw) {
+  constexpr int R = W, N = 1, ROWS = 32 * W, XROWS = ROWS + 1;
+  _Float16* Xh = reinterpret_cast<_Float16*>(lds_raw);                   // [XROWS][XS]
+  _Float16* Xl = Xh + XROWS * XS;                                        // [XROWS][XS]
+  float* red = reinterpret_cast<float*>(lds_raw + 2 * XROWS * XSB);      // [4 slots][W][waves] partials
+  int* rexp = reinterpret_cast<int*>(red + 4 * W * CONV_WAVES);          // [2][ROWS] stem row exponents
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int i = lane & 31, h = lane >> 5;
-  const int col = wave * 32 + i;                               // this lane's output column
-  const unsigned loff = (unsigned)((h * 256 + col) * 16);      // its B fragment inside a chunk
+  const int col0 = wave * 32 * N + i;                           // this lane's columns: col0 + 32 n
+  const unsigned loff = (unsigned)((h * 256 + col0) * 16);      // its B fragment (column tile 0) in a chunk
   const char* xa = reinterpret_cast<const char*>(Xh) + h * 16;  // its 8 k-values of a 16-K chunk column
   auto crow = [&](int t, int r) { return t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h; };  // C-layout row
 
-  Acc acc;
-  floatx16 res[RT];
+  Acc<R, N> acc;
+  floatx16 res[R][N];
   if (tid < XS) {  // the zero row
-    Xh[64 * XS + tid] = (_Float16)0.0f;
-    Xl[64 * XS + tid] = (_Float16)0.0f;
+    Xh[ROWS * XS + tid] = (_Float16)0.0f;
+    Xl[ROWS * XS + tid] = (_Float16)0.0f;
   }
 
-  // Combine one value per window over the 8 waves (each holds 32 of the 256 columns).  `slot` picks one
-  // of 4 partial buffers so back-to-back reductions need only the one barrier inside.
-  auto block_reduce = [&](const float (&v)[RT], int slot, bool is_max, float (&out)[RT]) {
+  // Combine one value per window over the 8 waves.  `slot` picks one of 4 partial buffers so back-to-back
+  // reductions need only the one barrier inside.
+  auto block_reduce = [&](const float (&v)[R], int slot, bool is_max, float (&out)[R]) {
 #pragma unroll
-    for (int t = 0; t < RT; ++t) {
-      const float w = is_max ? wave_max(v[t]) : wave_sum(v[t]);
-      if (lane == 0) red[(slot * RT + t) * NWAVE + wave] = w;
+    for (int t = 0; t < R; ++t) {
+      const float w = is_max ? wave_max_last(v[t]) : wave_sum_last(v[t]);
+      if (lane == 63) red[(slot * R + t) * CONV_WAVES + wave] = w;
     }
     __syncthreads();
 #pragma unroll
-    for (int t = 0; t < RT; ++t) {
-      const float* p = red + (slot * RT + t) * NWAVE;
+    for (int t = 0; t < R; ++t) {
+      const float* p = red + (slot * R + t) * CONV_WAVES;
       float a = p[0];
 #pragma unroll
-      for (int w = 1; w < NWAVE; ++w) a = is_max ? fmaxf(a, p[w]) : a + p[w];
+      for (int w = 1; w < CONV_WAVES; ++w) a = is_max ? fmaxf(a, p[w]) : a + p[w];
       out[t] = a;
     }
   };
 
   // Store the next conv's input as window * 2^-ex[t] (exact), the window's largest |value| in [2^8, 2^9);
   // the consumer multiplies its accumulators back by 2^ex[t].  Caller guarantees X is no longer read.
-  auto store_x = [&](const floatx16 (&v)[RT], int (&ex)[RT]) {
-    float m[RT], mm[RT];
+  auto store_x = [&](const floatx16 (&v)[R][N], int (&ex)[R]) {
+    float m[R], mm[R];
 #pragma unroll
-    for (int t = 0; t < RT; ++t) {
+    for (int t = 0; t < R; ++t) {
       m[t] = 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) m[t] = fmaxf(m[t], fabsf(v[t][r]));
+      for (int n = 0; n < N; ++n)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) m[t] = fmaxf(m[t], fabsf(v[t][n][r]));
     }
     block_reduce(m, 3, true, mm);
 #pragma unroll
-    for (int t = 0; t < RT; ++t) {
+    for (int t = 0; t < R; ++t) {
       ex[t] = fp16_range_exp(mm[t]);
       const float sc = ldexpf(1.0f, -ex[t]);
 #pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        const floatx2 y = (floatx2){v[t][r], v[t][r + 1]} * sc;
-        const _Float16 h0 = (_Float16)y.x, h1 = (_Float16)y.y;
-        const floatx2 lo = y - (floatx2){(float)h0, (float)h1};
-        const int row = crow(t, r);  // rows r and r + 1 of the tile are adjacent
-        Xh[row * XS + col] = h0;
-        Xh[(row + 1) * XS + col] = h1;
-        Xl[row * XS + col] = (_Float16)lo.x;
-        Xl[(row + 1) * XS + col] = (_Float16)lo.y;
+      for (int n = 0; n < N; ++n) {
+        // byte bases of this lane's column in row tile t (plane hi, lo); row r of the tile sits at a constant
+        // offset (an immediate of ds_write_b16), so no per-store address register stays live
+        char* bh = reinterpret_cast<char*>(Xh) + ((t * 32 + 4 * h) * XS + col0 + 32 * n) * 2;
+        char* bl = bh + XROWS * XSB;
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          const floatx2 y = (floatx2){v[t][n][r], v[t][n][r + 1]} * sc;
+          const _Float16 h0 = (_Float16)y.x, h1 = (_Float16)y.y;
+          const floatx2 lo = y - (floatx2){(float)h0, (float)h1};
+          const int off = ((r & 3) + 8 * (r >> 2)) * XSB;  // rows r and r + 1 of the tile are adjacent
+          *reinterpret_cast<_Float16*>(bh + off) = h0;
+          *reinterpret_cast<_Float16*>(bh + off + XSB) = h1;
+          *reinterpret_cast<_Float16*>(bl + off) = (_Float16)lo.x;
+          *reinterpret_cast<_Float16*>(bl + off + XSB) = (_Float16)lo.y;
+        }
       }
     }
   };
 
-  auto afn_rows = [&](int c, AFrag& f) {  // A fragments of the block's own 64 rows
+  auto afn_rows = [&](int c, AFrag<R>& f) {  // A fragments of the block's own rows
 #pragma unroll
-    for (int t = 0; t < RT; ++t) {
+    for (int t = 0; t < R; ++t) {
       const char* q = xa + (t * 32 + i) * XSB + c * 32;
       f.h[t] = *reinterpret_cast<const half8*>(q);
       f.l[t] = *reinterpret_cast<const half8*>(q + XROWS * XSB);
@@ -250,61 +280,69 @@ __global__ void __launch_bounds__(512, 1) conv_encoder_x3_kernel(const float* __
   // ((x - mean) / (std + 1e-6)), so row m of panel p is split as A[m,:] * 2^-e (exact) with the panel row's
   // largest |value| in [2^8, 2^9); the accumulators (held as C * 2^-e per row) are rescaled when e changes
   // between panels and multiplied back by 2^e at the end (all exact).  rexp[parity][row] holds e.
-  acc_zero(acc);
+  acc.zero();
   for (int p = 0; p < ed.n_stem_panels; ++p) {
     const int kw = min(256, ed.d_in - p * 256);
-    int* ecur = rexp + (p & 1) * 64;
-    // wave w stages rows 8w..8w+7, lane l columns l, l+64, l+128, l+192: 32 independent coalesced loads
-    float a[8][4];
+    int* ecur = rexp + (p & 1) * ROWS;
+    // wave w stages rows w*4W .. w*4W + 4W - 1 in groups of 4; lane l columns l, l+64, l+128, l+192
 #pragma unroll
-    for (int jr = 0; jr < 8; ++jr) {
-      const int r = wave * 8 + jr;
-      const int w = pair * 2 + (r >> 5);
-      const float* src = feats + ((size_t)w * VGE_T + (r & 31)) * VGE_FD + ed.in_col + p * 256;
+    for (int g8 = 0; g8 < W; ++g8) {
+      float a[4][4];
 #pragma unroll
-      for (int jc = 0; jc < 4; ++jc) {
-        const int c = lane + 64 * jc;
-        a[jr][jc] = (c < kw && w < n_windows) ? src[c] : 0.f;
+      for (int jr = 0; jr < 4; ++jr) {
+        const int r = wave * 4 * W + g8 * 4 + jr;
+        const int w = win0 + (r >> 5);
+        const float* src = feats + ((size_t)w * VGE_T + (r & 31)) * VGE_FD + ed.in_col + p * 256;
+#pragma unroll
+        for (int jc = 0; jc < 4; ++jc) {
+          const int c = lane + 64 * jc;
+          a[jr][jc] = (c < kw && w < n_windows) ? src[c] : 0.f;
+        }
       }
-    }
 #pragma unroll
-    for (int jr = 0; jr < 8; ++jr) {
-      float m = fmaxf(fmaxf(fabsf(a[jr][0]), fabsf(a[jr][1])), fmaxf(fabsf(a[jr][2]), fabsf(a[jr][3])));
-      m = wave_max(m);
-      const int ex = fp16_range_exp(m);
-      const int r = wave * 8 + jr;
-      if (lane == 0) ecur[r] = ex;
+      for (int jr = 0; jr < 4; ++jr) {
+        float m = fmaxf(fmaxf(fabsf(a[jr][0]), fabsf(a[jr][1])), fmaxf(fabsf(a[jr][2]), fabsf(a[jr][3])));
+        m = wave_max_all(m);
+        const int ex = fp16_range_exp(m);
+        const int r = wave * 4 * W + g8 * 4 + jr;
+        if (lane == 0) ecur[r] = ex;
 #pragma unroll
-      for (int jc = 0; jc < 4; ++jc) {
-        const int c = lane + 64 * jc;
-        split_store(Xh + r * XS + c, Xl + r * XS + c, ldexpf(a[jr][jc], -ex));
+        for (int jc = 0; jc < 4; ++jc) {
+          const int c = lane + 64 * jc;
+          split_store(Xh + r * XS + c, Xl + r * XS + c, ldexpf(a[jr][jc], -ex));
+        }
       }
     }
     __syncthreads();  // X and ecur complete
     if (p == 0) STAMP(1);
     if (p > 0) {
-      const int* eprev = rexp + ((p - 1) & 1) * 64;
+      const int* eprev = rexp + ((p - 1) & 1) * ROWS;
 #pragma unroll
-      for (int t = 0; t < RT; ++t)
+      for (int t = 0; t < R; ++t)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          acc.c[t][r] *= ldexpf(1.0f, eprev[crow(t, r)] - ecur[crow(t, r)]);
+          const float f = ldexpf(1.0f, eprev[crow(t, r)] - ecur[crow(t, r)]);
+#pragma unroll
+          for (int n = 0; n < N; ++n) acc.c[t][n][r] *= f;
         }
     }
-    run_stream(acc, reinterpret_cast<const char*>(ed.stem) + (size_t)p * 16 * CHUNK_B, ((kw + 127) >> 7) * PF, loff,
-               afn_rows);
+    run_stream<CONV_PF>(acc, reinterpret_cast<const char*>(ed.stem) + (size_t)p * 16 * CHUNK_B,
+                        ((kw + 127) >> 7) * STREAM_GROUP, loff, afn_rows);
     __syncthreads();  // every wave is done reading X
   }
   {
-    const int* efin = rexp + ((ed.n_stem_panels - 1) & 1) * 64;
-    const float wcs = ed.cs[col];
+    const int* efin = rexp + ((ed.n_stem_panels - 1) & 1) * ROWS;
 #pragma unroll
-    for (int t = 0; t < RT; ++t)
+    for (int n = 0; n < N; ++n) {
+      const float wcs = ed.cs[col0 + 32 * n];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) res[t][r] = ldexpf(acc.c[t][r] * wcs, efin[crow(t, r)]);
+      for (int t = 0; t < R; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) res[t][n][r] = ldexpf(acc.c[t][n][r] * wcs, efin[crow(t, r)]);
+    }
   }
   STAMP(2);
-  int xexp[RT];
+  int xexp[R];
   store_x(res, xexp);
   __syncthreads();
   STAMP(3);
@@ -312,71 +350,86 @@ __global__ void __launch_bounds__(512, 1) conv_encoder_x3_kernel(const float* __
   // ---------------- 4 TemporalConvBlocks
   for (int blk = 0; blk < 4; ++blk) {
     const int dil = 1 << blk;
-    const float gw = ed.gn_w[blk * 256 + col], gb = ed.gn_b[blk * 256 + col];
-    const float wcs0 = ed.cs[(1 + blk * 2) * 256 + col], wcs1 = ed.cs[(2 + blk * 2) * 256 + col];
     for (int cv = 0; cv < 2; ++cv) {
-      acc_zero(acc);
-      auto afn = [&](int c, AFrag& f) {
+      acc.zero();
+      auto afn = [&](int c, AFrag<R>& f) {
         const int tap = c >> 4, cc = c & 15;
         const int tt = i + (tap - 2) * dil;
         const bool in = (unsigned)tt < 32u;
 #pragma unroll
-        for (int t = 0; t < RT; ++t) {
-          const int row = in ? t * 32 + tt : 64;  // out of the window -> zero row
+        for (int t = 0; t < R; ++t) {
+          const int row = in ? t * 32 + tt : ROWS;  // out of the window -> zero row
           const char* q = xa + row * XSB + cc * 32;
           f.h[t] = *reinterpret_cast<const half8*>(q);
           f.l[t] = *reinterpret_cast<const half8*>(q + XROWS * XSB);
         }
       };
-      run_stream(acc, reinterpret_cast<const char*>(ed.conv) + (size_t)(blk * 2 + cv) * 5 * 16 * CHUNK_B, 5 * 16,
-                 loff, afn);
+      run_stream<CONV_PF>(acc, reinterpret_cast<const char*>(ed.conv) + (size_t)(blk * 2 + cv) * 5 * 16 * CHUNK_B,
+                          5 * 16, loff, afn);
       STAMP(4 + (blk * 2 + cv) * 2);
       // epilogue in packed f32 (v_pk_fma_f32: two rows per instruction), in place:
       // acc * 2^xexp * column scale -> [+ residual] -> GELU [-> GroupNorm]
-      floatx16 (&v)[RT] = acc.c;
-      floatx2 s2[RT];
+      floatx16 (&v)[R][N] = acc.c;
+      floatx2 s2[R];
 #pragma unroll
-      for (int t = 0; t < RT; ++t) {
-        const float xs = ldexpf(1.0f, xexp[t]) * (cv == 0 ? wcs0 : wcs1);
-        s2[t] = 0.f;
+      for (int t = 0; t < R; ++t) s2[t] = 0.f;
 #pragma unroll
-        for (int r = 0; r < 16; r += 2) {
-          floatx2 y = (floatx2){acc.c[t][r], acc.c[t][r + 1]} * xs;
-          if (cv == 1) y += (floatx2){res[t][r], res[t][r + 1]};
-          y = gelu2(y);
-          s2[t] += y;
-          v[t][r] = y.x;
-          v[t][r + 1] = y.y;
+      for (int n = 0; n < N; ++n) {
+        const float wcs = ed.cs[(1 + blk * 2 + cv) * 256 + col0 + 32 * n];
+#pragma unroll
+        for (int t = 0; t < R; ++t) {
+          const float xs = ldexpf(1.0f, xexp[t]) * wcs;
+          floatx2 y[8];
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            y[k] = (floatx2){v[t][n][2 * k], v[t][n][2 * k + 1]} * xs;
+            if (cv == 1) y[k] += (floatx2){res[t][n][2 * k], res[t][n][2 * k + 1]};
+          }
+          gelu2_many(y);  // 8 independent chains interleaved
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            s2[t] += y[k];
+            v[t][n][2 * k] = y[k].x;
+            v[t][n][2 * k + 1] = y[k].y;
+          }
+          __builtin_amdgcn_sched_barrier(0);  // one tile's temporaries at a time
         }
       }
       STAMP(22 + blk * 2 + cv);
       if (cv == 1) {
         // GroupNorm(1, 256) per window over its 32 x 256 values, spread over the 8 waves
-        float s[RT], mean[RT], q[RT], var[RT];
+        float s[R], mean[R], q[R], var[R];
 #pragma unroll
-        for (int t = 0; t < RT; ++t) s[t] = s2[t].x + s2[t].y;
+        for (int t = 0; t < R; ++t) s[t] = s2[t].x + s2[t].y;
         block_reduce(s, 0, false, mean);
 #pragma unroll
-        for (int t = 0; t < RT; ++t) {
+        for (int t = 0; t < R; ++t) {
           mean[t] *= 1.0f / 8192.0f;
           floatx2 q2 = 0.f;
 #pragma unroll
-          for (int r = 0; r < 16; r += 2) {
-            const floatx2 d = (floatx2){v[t][r], v[t][r + 1]} - mean[t];
-            q2 = __builtin_elementwise_fma(d, d, q2);
-          }
+          for (int n = 0; n < N; ++n)
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) {
+              const floatx2 d = (floatx2){v[t][n][r], v[t][n][r + 1]} - mean[t];
+              q2 = __builtin_elementwise_fma(d, d, q2);
+            }
           q[t] = q2.x + q2.y;
         }
         block_reduce(q, 1, false, var);
 #pragma unroll
-        for (int t = 0; t < RT; ++t) {
-          const float rstd = 1.0f / sqrtf(var[t] * (1.0f / 8192.0f) + 1e-5f);
-          const float sc = rstd * gw, sh = gb - mean[t] * sc;  // (v - mean) * rstd * w + b
+        for (int n = 0; n < N; ++n) {
+          const float gw = ed.gn_w[blk * 256 + col0 + 32 * n], gb = ed.gn_b[blk * 256 + col0 + 32 * n];
 #pragma unroll
-          for (int r = 0; r < 16; r += 2) {
-            const floatx2 y = __builtin_elementwise_fma((floatx2){v[t][r], v[t][r + 1]}, (floatx2)sc, (floatx2)sh);
-            v[t][r] = res[t][r] = y.x;
-            v[t][r + 1] = res[t][r + 1] = y.y;
+          for (int t = 0; t < R; ++t) {
+            const float rstd = 1.0f / sqrtf(var[t] * (1.0f / 8192.0f) + 1e-5f);
+            const float sc = rstd * gw, sh = gb - mean[t] * sc;  // (v - mean) * rstd * w + b
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) {
+              const floatx2 y =
+                  __builtin_elementwise_fma((floatx2){v[t][n][r], v[t][n][r + 1]}, (floatx2)sc, (floatx2)sh);
+              v[t][n][r] = res[t][n][r] = y.x;
+              v[t][n][r + 1] = res[t][n][r + 1] = y.y;
+            }
           }
         }
       }
@@ -388,23 +441,66 @@ __global__ void __launch_bounds__(512, 1) conv_encoder_x3_kernel(const float* __
   }
 
   // ---------------- proj: Linear(256 -> 256, no bias)
-  acc_zero(acc);
-  run_stream(acc, reinterpret_cast<const char*>(ed.proj), 16, loff, afn_rows);
+  acc.zero();
+  run_stream<CONV_PF>(acc, reinterpret_cast<const char*>(ed.proj), 16, loff, afn_rows);
   STAMP(20);
 #pragma unroll
-  for (int t = 0; t < RT; ++t) {
-    const int win = pair * 2 + t;
+  for (int t = 0; t < R; ++t) {
+    const int win = win0 + t;
     if (win < n_windows) {
-      const float xs = ldexpf(1.0f, xexp[t]) * ed.cs[9 * 256 + col];
       float* o = enc_out + ((size_t)e * n_windows * VGE_T + (size_t)win * VGE_T) * VGE_D;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) o[crow(0, r) * VGE_D + col] = acc.c[t][r] * xs;
+      for (int n = 0; n < N; ++n) {
+        const float xs = ldexpf(1.0f, xexp[t]) * ed.cs[9 * 256 + col0 + 32 * n];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[crow(0, r) * VGE_D + col0 + 32 * n] = acc.c[t][n][r] * xs;
+      }
     }
   }
   STAMP(21);
 #ifdef VGE_TRACE
   if (blockIdx.x < 64 && threadIdx.x == 0) g_vge_trace[blockIdx.x * 8 * 32 + 31] = e;
 #endif
+}
+
+// Persistent schedule.  Work units: Q quads (4 windows) then the pairs (2 windows) covering the rest of each
+// encoder's windows; encoder e takes q_e = qa + (e < qr) quads (windows [0, 4 q_e)) and the pairs after them.
+// Grid = G blocks (one per CU); unit u runs on block u % G in round u / G, so with Q a multiple of G every
+// CU does the same number of quads and at most one pair.  Within a round the block index is remapped so the
+// 8 XCDs (blocks dealt round robin) take contiguous units, i.e. the same encoders' weights in their L2.
+struct ConvSched {
+  int n_windows, n_enc, G, Q, qa, qr, n_units;
+};
+
+__device__ __forceinline__ int xcd_remap(int b, int nblk) {
+  const int q8 = nblk >> 3, r8 = nblk & 7, x8 = b & 7;
+  return (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (b >> 3);
+}
+
+__global__ void __launch_bounds__(512, 1) conv_encoder_x3_kernel(const float* __restrict__ feats,
+                                                                  const EncDescX3* __restrict__ encs, ConvSched cs,
+                                                                  float* __restrict__ enc_out) {
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  const int n = cs.n_windows;
+  const int p_big = (n - 4 * (cs.qa + 1) + 1) / 2, p_small = (n - 4 * cs.qa + 1) / 2;  // pairs per encoder
+  for (int round = 0; round * cs.G < cs.n_units; ++round) {
+    const int u = round * cs.G + xcd_remap(blockIdx.x, cs.G);
+    if (u >= cs.n_units) break;  // uniform over the block
+    if (round > 0) __syncthreads();  // the previous unit's LDS is free
+    if (u < cs.Q) {
+      const int big = cs.qr * (cs.qa + 1);
+      const int e = u < big ? u / (cs.qa + 1) : cs.qr + (u - big) / cs.qa;
+      const int j = u < big ? u % (cs.qa + 1) : (u - big) % cs.qa;
+      conv_encoder_body<4>(feats, n, 4 * j, encs[e], e, enc_out, lds_raw);
+    } else {
+      const int v = u - cs.Q;
+      const int big = cs.qr * p_big;
+      const int e = v < big ? v / p_big : cs.qr + (v - big) / p_small;
+      const int j = v < big ? v % p_big : (v - big) % p_small;
+      const int q_e = cs.qa + (e < cs.qr);
+      conv_encoder_body<2>(feats, n, 4 * q_e + 2 * j, encs[e], e, enc_out, lds_raw);
+    }
+  }
 }
 
 // ------------------------------------------------------------------ panel GEMM (3xfp16) with fused epilogues
@@ -424,6 +520,7 @@ struct GemmArgsX3 {
 };
 
 // block = 8 waves, BM = 64 rows x BN = 256 columns, wave w owns columns 32w..32w+31 of all 64 rows
+constexpr int NWAVE = 8, RT = 2;
 constexpr int GEMMX3_LDS_BYTES = 2 * 64 * XSB + (64 * NWAVE + NWAVE) * 4;
 
 template <int EPI>
@@ -441,8 +538,8 @@ __global__ void __launch_bounds__(512, 1) gemm_x3_kernel(GemmArgsX3 ga) {
   const char* xa = reinterpret_cast<const char*>(Xh) + i * XSB + h * 16;
   auto lrow = [&](int t, int r) { return t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h; };
 
-  Acc acc;
-  acc_zero(acc);
+  Acc<RT, 1> acc;
+  acc.zero();
   int aexp = 0;  // the accumulators hold C * 2^-aexp
   for (int p = 0; p < n_panels; ++p) {
     // the 64 x 256 A panel (rows >= M read as 0) as hi/lo planes of panel * 2^-e, its largest |value| in
@@ -456,8 +553,8 @@ __global__ void __launch_bounds__(512, 1) gemm_x3_kernel(GemmArgsX3 ga) {
       a[j] = (row < ga.M) ? ga.A[(size_t)row * ga.lda + p * 256 + c] : 0.f;
       m = fmaxf(m, fabsf(a[j]));
     }
-    m = wave_max(m);
-    if (lane == 0) red[64 * NWAVE + wave] = m;
+    m = wave_max_last(m);
+    if (lane == 63) red[64 * NWAVE + wave] = m;
     __syncthreads();  // also: every wave is past the previous panel's stream
     float mm = red[64 * NWAVE];
 #pragma unroll
@@ -468,7 +565,7 @@ __global__ void __launch_bounds__(512, 1) gemm_x3_kernel(GemmArgsX3 ga) {
 #pragma unroll
       for (int t = 0; t < RT; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc.c[t][r] *= f;
+        for (int r = 0; r < 16; ++r) acc.c[t][0][r] *= f;
     }
     aexp = e;
 #pragma unroll
@@ -477,7 +574,7 @@ __global__ void __launch_bounds__(512, 1) gemm_x3_kernel(GemmArgsX3 ga) {
       split_store(Xh + r * XS + c, Xl + r * XS + c, ldexpf(a[j], -e));
     }
     __syncthreads();
-    auto afn = [&](int cc, AFrag& f) {
+    auto afn = [&](int cc, AFrag<RT>& f) {
 #pragma unroll
       for (int t = 0; t < RT; ++t) {
         const char* q = xa + t * 32 * XSB + cc * 32;
@@ -485,8 +582,8 @@ __global__ void __launch_bounds__(512, 1) gemm_x3_kernel(GemmArgsX3 ga) {
         f.l[t] = *reinterpret_cast<const half8*>(q + 64 * XSB);
       }
     };
-    run_stream(acc, reinterpret_cast<const char*>(ga.W) + ((size_t)nb * (ga.K / 16) + p * 16) * CHUNK_B, 16, loff,
-               afn);
+    run_stream<GEMM_PF>(acc, reinterpret_cast<const char*>(ga.W) + ((size_t)nb * (ga.K / 16) + p * 16) * CHUNK_B, 16,
+                        loff, afn);
     __syncthreads();  // every wave is done reading the panel
   }
 
@@ -496,7 +593,7 @@ __global__ void __launch_bounds__(512, 1) gemm_x3_kernel(GemmArgsX3 ga) {
 #pragma unroll
   for (int t = 0; t < RT; ++t)
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[t][r] = acc.c[t][r] * as;
+    for (int r = 0; r < 16; ++r) v[t][r] = acc.c[t][0][r] * as;
 
   if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_RELU) {
     const float bb = ga.bias[col];
@@ -528,11 +625,8 @@ __global__ void __launch_bounds__(512, 1) gemm_x3_kernel(GemmArgsX3 ga) {
     // the 8 waves' column slices through LDS
     auto row_reduce = [&](float (&q)[16], int t) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-#pragma unroll
-        for (int o = 16; o >= 1; o >>= 1) q[r] += __shfl_xor(q[r], o, 64);
-      }
-      if (i == 0) {
+      for (int r = 0; r < 16; ++r) q[r] = half_sum_last(q[r]);  // valid in lanes 31 and 63
+      if (i == 31) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) red[lrow(t, r) * NWAVE + wave] = q[r];
       }
@@ -596,7 +690,7 @@ static_assert(sizeof(GemmArgsX3Host) == sizeof(GemmArgsX3), "GemmArgsX3 layout")
 
 hipError_t encoder_x3_kernel_setup() {
   hipError_t e = hipFuncSetAttribute((const void*)conv_encoder_x3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     CONVX3_LDS_BYTES);
+                                     conv_lds_bytes<4>());
   if (e != hipSuccess) return e;
   const void* gk[4] = {(const void*)gemm_x3_kernel<EPI_TOKENS>, (const void*)gemm_x3_kernel<EPI_BIAS>,
                        (const void*)gemm_x3_kernel<EPI_BIAS_RELU>, (const void*)gemm_x3_kernel<EPI_BIAS_RES_LN>};
@@ -607,11 +701,35 @@ hipError_t encoder_x3_kernel_setup() {
   return hipSuccess;
 }
 
+// Quads (4 windows per block) halve the weight bytes per row; pairs fill the remainder.  With G = min(CUs,
+// units) persistent blocks and m = ceil(pair units / G) per block, Q = G * floor(m / 2) quads (as many as
+// fit) make every block run floor(m / 2) quads and at most one pair.
 hipError_t launch_conv_encoders_x3(const float* feats, int n_windows, const void* encs, int n_enc, float* enc_out,
                                    hipStream_t s) {
-  const int n_pairs = (n_windows + 1) / 2;
-  hipLaunchKernelGGL(conv_encoder_x3_kernel, dim3(n_enc * n_pairs), dim3(512), CONVX3_LDS_BYTES, s, feats, n_windows,
-                     reinterpret_cast<const EncDescX3*>(encs), n_enc, enc_out);
+  static int n_cu = 0;
+  if (n_cu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu < 1)
+      n_cu = 256;
+  }
+  if (n_windows < 1 || n_enc < 1) return hipSuccess;
+  const int pair_units = n_enc * ((n_windows + 1) / 2);
+  const int G0 = std::min(n_cu, pair_units);
+  const int m = (pair_units + G0 - 1) / G0;
+  const int Q = std::min(G0 * (m / 2), n_enc * (n_windows / 4));
+  ConvSched cs;
+  cs.n_windows = n_windows;
+  cs.n_enc = n_enc;
+  cs.Q = Q;
+  cs.qa = Q / n_enc;
+  cs.qr = Q % n_enc;
+  int pairs = 0;
+  for (int e = 0; e < n_enc; ++e) pairs += (n_windows - 4 * (cs.qa + (e < cs.qr)) + 1) / 2;
+  cs.n_units = Q + pairs;
+  cs.G = std::min(n_cu, cs.n_units);
+  hipLaunchKernelGGL(conv_encoder_x3_kernel, dim3(cs.G), dim3(512), conv_lds_bytes<4>(), s, feats,
+                     reinterpret_cast<const EncDescX3*>(encs), cs, enc_out);
   return hipGetLastError();
 }
 
