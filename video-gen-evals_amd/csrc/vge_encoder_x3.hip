@@ -56,7 +56,7 @@ constexpr int CHUNK_B = 16384;       // bytes per weight chunk
 constexpr int PLANE_B = 8192;        // bytes between the hi and lo planes of a chunk
 constexpr int STREAM_GROUP = 8;      // weight streams are packed as multiples of 8 chunks
 constexpr int CONV_PF = 4;           // weight chunks in flight per wave: conv (a quad wave holds 128 x 64 outputs)
-constexpr int GEMM_PF = 8;           // ... and GEMM waves (64 x 32 outputs)
+constexpr int GEMM_PF = 4;           // ... and GEMM waves (32 x 32 outputs, 4 waves per SIMD)
 
 __device__ __forceinline__ floatx16 mfma32(half8 a, half8 b, floatx16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
@@ -519,20 +519,26 @@ struct GemmArgsX3 {
   const float* cs;              // [N] weight column scales
 };
 
-// block = 8 waves, BM = 64 rows x BN = 256 columns, wave w owns columns 32w..32w+31 of all 64 rows
-constexpr int NWAVE = 8, RT = 2;
-constexpr int GEMMX3_LDS_BYTES = 2 * 64 * XSB + (64 * NWAVE + NWAVE) * 4;
+// block = 8 waves, BM = 32 RT rows x BN = 256 columns, wave w owns columns 32w..32w+31 of all BM rows.
+// RT = 1: 32-row blocks, small enough (LDS 34 KB, <= 128 VGPRs) for several workgroups per CU, so one
+// workgroup's staging / epilogue latency hides behind another's MFMAs on these short (K <= 1024) GEMMs.
+constexpr int NWAVE = 8, GEMM_RT = 1;
+template <int RT>
+constexpr int gemm_lds_bytes() {
+  return 2 * 32 * RT * XSB + (32 * RT * NWAVE + NWAVE) * 4;
+}
 
-template <int EPI>
-__global__ void __launch_bounds__(512, 1) gemm_x3_kernel(GemmArgsX3 ga) {
+template <int EPI, int RT>
+__global__ void __launch_bounds__(512, 4) gemm_x3_kernel(GemmArgsX3 ga) {  // 4 waves per SIMD
+  constexpr int BM = 32 * RT;
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   _Float16* Xh = reinterpret_cast<_Float16*>(lds_raw);
-  _Float16* Xl = Xh + 64 * XS;
-  float* red = reinterpret_cast<float*>(lds_raw + 2 * 64 * XSB);  // [64 rows][8 waves] + [8] maxima
+  _Float16* Xl = Xh + BM * XS;
+  float* red = reinterpret_cast<float*>(lds_raw + 2 * BM * XSB);  // [BM rows][8 waves] + [8] maxima
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int i = lane & 31, h = lane >> 5;
-  const int row0 = blockIdx.x * 64, nb = blockIdx.y;
+  const int row0 = blockIdx.x * BM, nb = blockIdx.y;
   const int n_panels = ga.K / 256;
   const unsigned loff = (unsigned)((h * 256 + wave * 32 + i) * 16);
   const char* xa = reinterpret_cast<const char*>(Xh) + i * XSB + h * 16;
@@ -542,23 +548,23 @@ __global__ void __launch_bounds__(512, 1) gemm_x3_kernel(GemmArgsX3 ga) {
   acc.zero();
   int aexp = 0;  // the accumulators hold C * 2^-aexp
   for (int p = 0; p < n_panels; ++p) {
-    // the 64 x 256 A panel (rows >= M read as 0) as hi/lo planes of panel * 2^-e, its largest |value| in
+    // the BM x 256 A panel (rows >= M read as 0) as hi/lo planes of panel * 2^-e, its largest |value| in
     // [2^8, 2^9): exact power-of-two scaling that keeps fp16 in range; the accumulators are rescaled to match
     const int c = tid & 255;
-    float a[32];
+    float a[BM / 2];
     float m = 0.f;
 #pragma unroll
-    for (int j = 0; j < 32; ++j) {
+    for (int j = 0; j < BM / 2; ++j) {
       const int row = row0 + (tid >> 8) + 2 * j;
       a[j] = (row < ga.M) ? ga.A[(size_t)row * ga.lda + p * 256 + c] : 0.f;
       m = fmaxf(m, fabsf(a[j]));
     }
     m = wave_max_last(m);
-    if (lane == 63) red[64 * NWAVE + wave] = m;
+    if (lane == 63) red[BM * NWAVE + wave] = m;
     __syncthreads();  // also: every wave is past the previous panel's stream
-    float mm = red[64 * NWAVE];
+    float mm = red[BM * NWAVE];
 #pragma unroll
-    for (int w = 1; w < NWAVE; ++w) mm = fmaxf(mm, red[64 * NWAVE + w]);
+    for (int w = 1; w < NWAVE; ++w) mm = fmaxf(mm, red[BM * NWAVE + w]);
     const int e = fp16_range_exp(mm);
     if (p > 0 && e != aexp) {
       const float f = ldexpf(1.0f, aexp - e);
@@ -569,7 +575,7 @@ __global__ void __launch_bounds__(512, 1) gemm_x3_kernel(GemmArgsX3 ga) {
     }
     aexp = e;
 #pragma unroll
-    for (int j = 0; j < 32; ++j) {
+    for (int j = 0; j < BM / 2; ++j) {
       const int r = (tid >> 8) + 2 * j;
       split_store(Xh + r * XS + c, Xl + r * XS + c, ldexpf(a[j], -e));
     }
@@ -579,7 +585,7 @@ __global__ void __launch_bounds__(512, 1) gemm_x3_kernel(GemmArgsX3 ga) {
       for (int t = 0; t < RT; ++t) {
         const char* q = xa + t * 32 * XSB + cc * 32;
         f.h[t] = *reinterpret_cast<const half8*>(q);
-        f.l[t] = *reinterpret_cast<const half8*>(q + 64 * XSB);
+        f.l[t] = *reinterpret_cast<const half8*>(q + BM * XSB);
       }
     };
     run_stream<GEMM_PF>(acc, reinterpret_cast<const char*>(ga.W) + ((size_t)nb * (ga.K / 16) + p * 16) * CHUNK_B, 16,
@@ -619,8 +625,9 @@ __global__ void __launch_bounds__(512, 1) gemm_x3_kernel(GemmArgsX3 ga) {
         }
       }
   } else {  // EPI_BIAS_RES_LN over the 256 columns (N == 256, one column block), one 32-row tile at a time
+    // the token buffers are padded to whole 64-row tiles (vge_encoder_reserve): rows past M read and write
+    // that padding (never consumed; A staging zeroes them), so the epilogue needs no row guards
     const float bb = ga.bias[col], lw = ga.ln_w[col], lb = ga.ln_b[col];
-    const int mrow = ga.M - 1 - row0;  // last valid local row (rows past M read it, their results are dropped)
     // row sums (in place): over the 32 lanes that share h (xor 1..16 stays inside a 32-lane half), then over
     // the 8 waves' column slices through LDS
     auto row_reduce = [&](float (&q)[16], int t) {
@@ -646,7 +653,7 @@ __global__ void __launch_bounds__(512, 1) gemm_x3_kernel(GemmArgsX3 ga) {
       float s[16], q[16];
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        vt[r] += bb + rbase[min(lrow(0, r), mrow - t * 32) * ga.ldr];
+        vt[r] += bb + rbase[lrow(0, r) * ga.ldr];
         s[r] = vt[r];
       }
       row_reduce(s, t);
@@ -661,11 +668,11 @@ __global__ void __launch_bounds__(512, 1) gemm_x3_kernel(GemmArgsX3 ga) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const float rstd = 1.0f / sqrtf(q[r] * (1.0f / 256.0f) + 1e-5f);
-        if (lrow(0, r) <= mrow - t * 32) obase[lrow(0, r) * ga.ldo] = (vt[r] - s[r]) * rstd * lw + lb;
+        obase[lrow(0, r) * ga.ldo] = (vt[r] - s[r]) * rstd * lw + lb;
       }
     };
-    tile(v[0], 0);
-    tile(v[1], 1);
+#pragma unroll
+    for (int t = 0; t < RT; ++t) tile(v[t], t);
   }
 }
 
@@ -692,10 +699,11 @@ hipError_t encoder_x3_kernel_setup() {
   hipError_t e = hipFuncSetAttribute((const void*)conv_encoder_x3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      conv_lds_bytes<4>());
   if (e != hipSuccess) return e;
-  const void* gk[4] = {(const void*)gemm_x3_kernel<EPI_TOKENS>, (const void*)gemm_x3_kernel<EPI_BIAS>,
-                       (const void*)gemm_x3_kernel<EPI_BIAS_RELU>, (const void*)gemm_x3_kernel<EPI_BIAS_RES_LN>};
+  const void* gk[4] = {(const void*)gemm_x3_kernel<EPI_TOKENS, GEMM_RT>, (const void*)gemm_x3_kernel<EPI_BIAS, GEMM_RT>,
+                       (const void*)gemm_x3_kernel<EPI_BIAS_RELU, GEMM_RT>,
+                       (const void*)gemm_x3_kernel<EPI_BIAS_RES_LN, GEMM_RT>};
   for (auto k : gk) {
-    e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, GEMMX3_LDS_BYTES);
+    e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, gemm_lds_bytes<GEMM_RT>());
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
@@ -736,12 +744,13 @@ hipError_t launch_conv_encoders_x3(const float* feats, int n_windows, const void
 hipError_t launch_gemm_x3(int epi, const GemmArgsX3Host& a, hipStream_t s) {
   GemmArgsX3 g;
   memcpy(&g, &a, sizeof(g));
-  dim3 grid((a.M + 63) / 64, a.N / 256);
+  constexpr int BM = 32 * GEMM_RT, L = gemm_lds_bytes<GEMM_RT>();
+  dim3 grid((a.M + BM - 1) / BM, a.N / 256);
   switch (epi) {
-    case EPI_TOKENS: hipLaunchKernelGGL(gemm_x3_kernel<EPI_TOKENS>, grid, dim3(512), GEMMX3_LDS_BYTES, s, g); break;
-    case EPI_BIAS: hipLaunchKernelGGL(gemm_x3_kernel<EPI_BIAS>, grid, dim3(512), GEMMX3_LDS_BYTES, s, g); break;
-    case EPI_BIAS_RELU: hipLaunchKernelGGL(gemm_x3_kernel<EPI_BIAS_RELU>, grid, dim3(512), GEMMX3_LDS_BYTES, s, g); break;
-    default: hipLaunchKernelGGL(gemm_x3_kernel<EPI_BIAS_RES_LN>, grid, dim3(512), GEMMX3_LDS_BYTES, s, g); break;
+    case EPI_TOKENS: hipLaunchKernelGGL((gemm_x3_kernel<EPI_TOKENS, GEMM_RT>), grid, dim3(512), L, s, g); break;
+    case EPI_BIAS: hipLaunchKernelGGL((gemm_x3_kernel<EPI_BIAS, GEMM_RT>), grid, dim3(512), L, s, g); break;
+    case EPI_BIAS_RELU: hipLaunchKernelGGL((gemm_x3_kernel<EPI_BIAS_RELU, GEMM_RT>), grid, dim3(512), L, s, g); break;
+    default: hipLaunchKernelGGL((gemm_x3_kernel<EPI_BIAS_RES_LN, GEMM_RT>), grid, dim3(512), L, s, g); break;
   }
   return hipGetLastError();
 }
