@@ -254,7 +254,7 @@ def main():
             "vs_baseline": None,
             "dtype": args.compute,
             "precision": {"arith": "f32 in, f32 accumulate (v_mfma_f32_16x16x4_f32)" if args.compute == "f32" else
-                          "f32 operands split into fp16 hi + 2^11-scaled fp16 lo, 3 f16 MFMAs per product, f32 accumulate",
+                          "f32 operands as fp16 hi + fp16 residual lo (power-of-two scaled per row/window/column), 3 f16 MFMAs per product (hi*hi + hi*lo + lo*hi), f32 accumulate",
                           "max_abs_score_dev_vs_exact_f32": score_dev, "north_star_tolerance": 1e-4},
             "data": "synthetic (deterministic generator vge.synth: quaternion-walk SMPL rotations, N(0,1) betas/tokens, "
                     "U[0,1] keypoints with 5% invisible; random-init weights of the reference architecture)",

@@ -4,8 +4,8 @@ bench.py for roofline.traffic) and a per-kernel stats CSV under profiles/.
 
     python tools/pmc_to_json.py TAG COMPUTE [--windows 256]
 
-Only the timed-workload dispatches are kept: the conv-encoder launch whose grid is 10 encoders x
-windows/2 workgroups.  HBM bytes = FETCH_SIZE x 2 (gfx950 reports half of wide streaming reads,
+Only the timed-workload dispatches are kept: the last --last conv-encoder dispatches of the run (bench.py
+--steps in tools/profile_round.sh; setup launches come first).  HBM bytes = FETCH_SIZE x 2 (gfx950 reports half of wide streaming reads,
 MI355X_MICROARCH.md HBM section) + WRITE_SIZE, both in KB as rocprofv3 reports them.
 """
 import argparse
@@ -21,11 +21,10 @@ ap = argparse.ArgumentParser()
 ap.add_argument("tag")
 ap.add_argument("compute")
 ap.add_argument("--windows", type=int, default=256)
+ap.add_argument("--last", type=int, default=6)
 a = ap.parse_args()
 out_dir = ROOT / "gpurun_out"
 KNAME = {"f32x3": "conv_encoder_x3_kernel", "f32": "conv_encoder_kernel("}[a.compute]
-threads = {"f32x3": 512, "f32": 256}[a.compute]
-grid = 10 * ((a.windows + 1) // 2) * threads
 
 
 def rows(kind):
@@ -34,13 +33,17 @@ def rows(kind):
 
 
 def counters(kind):
-    vals = collections.defaultdict(list)
-    dur = []
+    per_dispatch = collections.defaultdict(dict)
     for r in rows(kind):
-        if KNAME in r["Kernel_Name"] and int(r["Grid_Size"]) == grid:
-            vals[r["Counter_Name"]].append(float(r["Counter_Value"]))
-            dur.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
-    return {k: sum(v) / len(v) for k, v in vals.items()}, len(dur)
+        if KNAME in r["Kernel_Name"]:
+            d = per_dispatch[int(r["Dispatch_Id"])]
+            d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    keep = [per_dispatch[k] for k in sorted(per_dispatch)[-a.last:]]
+    vals = collections.defaultdict(list)
+    for d in keep:
+        for k, v in d.items():
+            vals[k].append(v)
+    return {k: sum(v) / len(v) for k, v in vals.items()}, len(keep)
 
 
 fetch, nf = counters("fetch")
@@ -50,9 +53,9 @@ sq, _ = counters("sq")
 # kernel-trace average of the same dispatches
 tr = []
 for f in glob.glob(str(out_dir / f"prof_{a.tag}_trace" / "**" / "*kernel_trace.csv"), recursive=True):
-    for r in csv.DictReader(open(f)):
-        if KNAME in r["Kernel_Name"] and int(r["Grid_Size_X"]) == grid:
-            tr.append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+    rs = [r for r in csv.DictReader(open(f)) if KNAME in r["Kernel_Name"]]
+    rs.sort(key=lambda r: int(r["Dispatch_Id"]))
+    tr += [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rs[-a.last:]]
 hbm = fetch["FETCH_SIZE"] * 1024 * 2 + write["WRITE_SIZE"] * 1024
 res = {
     "kernel": KNAME.rstrip("("), "windows_per_launch": a.windows, "dispatches": {"fetch": nf, "write": nw},
