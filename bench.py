@@ -78,9 +78,9 @@ def setup_dist():
 
 
 def allreduce_sum(t, world):
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.SUM)
-    return t
+    # vge.dist: one all-gather + rank-ordered sum (deterministic, identical on every rank)
+    from vge.dist import allgather_sum
+    return allgather_sum(t) if world > 1 else t
 
 
 def cpu_baseline(seconds: float, clips_per_batch: int = 32):
@@ -140,14 +140,15 @@ def main():
     # ---------------- setup: frame stores in HBM, stats + centroids over the (sharded) real set
     t_setup = time.perf_counter()
     n_real_per_class, T_real = 8, 64
-    real_idx = [i for i in range(10 * n_real_per_class) if i % world == rank]
+    from vge.dist import shard
+    real_idx = shard(list(range(10 * n_real_per_class)), rank, world)     # contiguous block of the real set
     real_clips = [make_clips(synth.SEED_REAL, i, 1, T_real)[0] for i in real_idx]
     real_cls = [ACTION_CLASSES[i // n_real_per_class] for i in real_idx]
     real_store = ops.DeviceFrameStore.from_host(pack_frame_store(real_clips, [f"r{i}" for i in real_idx], real_cls), dev)
     sums = torch.zeros((2, ops.FEAT_DIM), device=dev, dtype=torch.float64)
     counts = np.zeros(2, np.int64)
     ops.stats_accumulate(real_store, range(real_store.n_videos), sums, counts)
-    allreduce_sum(sums, world)
+    sums = allreduce_sum(sums, world)
     cnt_t = allreduce_sum(torch.tensor(counts, device=dev), world)
     counts = cnt_t.cpu().numpy()
     mean, std = ops.stats_finalize(sums, counts)
@@ -165,8 +166,8 @@ def main():
     csum = torch.zeros((10, 256), device=dev)
     ccnt = torch.zeros((10,), device=dev)
     ops.centroid_accumulate(rseq, y, csum, ccnt)
-    allreduce_sum(csum, world)
-    allreduce_sum(ccnt, world)
+    csum = allreduce_sum(csum, world)
+    ccnt = allreduce_sum(ccnt, world)
     centroids = ops.centroid_finalize(csum, ccnt)
 
     gen_clips = make_clips(synth.SEED_GEN, rank * B, B, CLIP_LEN)

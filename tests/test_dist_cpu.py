@@ -1,0 +1,132 @@
+"""world_size-2 gloo (CPU) tests of the multi-GPU composition in vge/dist.py.
+
+The per-rank compute here is the oracle (the CPU restatement of eval.py); what is under test is the part
+the GPU path shares verbatim: contiguous sharding of the sorted video lists, the deterministic all-gather +
+rank-ordered sum of the stats / centroid sufficient statistics, and the gather of per-video scores to rank
+0.  The merged result must equal the single-process reference golden vectors.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def test_shard_bounds_partition():
+    from vge.dist import shard_bounds
+    for ws in range(1, 9):
+        for n in range(0, 41):
+            spans = [shard_bounds(n, r, ws) for r in range(ws)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            for (a, b), (c, d) in zip(spans, spans[1:]):
+                assert b == c
+            sizes = [b - a for a, b in spans]
+            assert max(sizes) - min(sizes) <= 1
+
+
+def _rank_main(rank, ws, port, paths, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.set_num_threads(2)
+    import torch.distributed as dist
+    import torch.nn.functional as F
+    from oracle import evalflow as EF
+    from oracle.encoder import OracleEncoder
+    from oracle.featurize import RAW_ORDER, StatsAccumulator
+    from vge import dist as VD
+    from vge import synth
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        real = EF.scan_real(paths["real"])
+        train = EF.split(real)
+        mine = VD.shard(train, rank, ws)
+        # ModalityStats: float64 sums / squares + frame counts, one all-gather, rank-ordered sum
+        acc = StatsAccumulator()
+        for cls, name, path, T in mine:
+            pose, gori, betas, vit, kp = EF.load(path, paths["real_kp"], cls, require_kp=False)
+            acc.add_video(pose, gori, betas, vit, kp)
+        keys = [(k, m) for m in RAW_ORDER for k in ("raw", "diff")]
+        dims = {}
+        for cls, name, path, T in train[:1]:
+            pose, gori, betas, vit, kp = EF.load(path, paths["real_kp"], cls, require_kp=False)
+            probe = StatsAccumulator()
+            probe.add_video(pose, gori, betas, vit, kp)
+            dims = {k: probe.s[k].shape[0] for k in keys}
+        flat_s = np.concatenate([acc.s.get(k, np.zeros(dims[k])) for k in keys] +
+                                [acc.ss.get(k, np.zeros(dims[k])) for k in keys])
+        n = np.array([acc.n.get(k, 0) for k in keys], np.int64)
+        S, N = VD.stats_reduce_fn(torch.from_numpy(flat_s), n)
+        S = S.numpy()
+        off = 0
+        tot = StatsAccumulator()
+        for k in keys:
+            tot.s[k] = S[off:off + dims[k]]
+            off += dims[k]
+        for k in keys:
+            tot.ss[k] = S[off:off + dims[k]]
+            off += dims[k]
+        for k, c in zip(keys, N):
+            tot.n[k] = int(c)
+        stats = tot.finalize()
+        mean, std = stats.concat()
+        # centroids: f32 sums [C,256] + counts [C], one all-gather, rank-ordered sum
+        sd = synth.make_state_dict(synth.DIMS_RAW, synth.DIMS_DIFF)
+        enc = OracleEncoder(sd, synth.DIMS_RAW, synth.DIMS_DIFF)
+        label_dict = {c: i for i, c in enumerate(sorted(real.keys()))}
+        samples = [(cls, name, path, s) for cls, name, path, T in mine if T > 0 for s in EF.windows_for(T)]
+        sums = torch.zeros(len(label_dict), 256)
+        counts = torch.zeros(len(label_dict))
+        if samples:
+            seq, _, clss, _ = EF.encode_samples(enc, samples, paths["real_kp"], stats, batch_size=64)
+            y = torch.as_tensor([label_dict[c] for c in clss], dtype=torch.long)
+            sums.index_add_(0, y, seq)
+            counts.index_add_(0, y, torch.ones_like(y, dtype=torch.float32))
+        sums, counts = VD.centroid_reduce_fn(sums, counts)
+        cents = F.normalize(sums / counts.clamp_min(1.0).unsqueeze(1), dim=-1)
+        # scoring: this rank's contiguous block of the sorted generated list, no collective
+        gen = sorted(EF.scan_generated(paths["generated_meshes"]), key=lambda it: it[2])
+        gmine = VD.shard(gen, rank, ws)
+        gs = [(cls, name, path, s) for cls, name, path, T in gmine for s in EF.windows_for(T)]
+        combined = {}
+        if gs:
+            seq, fe, clss, names = EF.encode_samples(enc, gs, paths["generated_kps"], stats)
+            ac = EF.ac_scores(seq, clss, names, cents, label_dict)
+            tc = EF.tc_scores(fe, names)
+            for v in sorted(set(ac) | set(tc)):
+                combined[v] = {**({"ac": ac[v]} if v in ac else {}), **({"tc": tc[v]} if v in tc else {})}
+        parts = VD.gather_to_rank0(combined)
+        if rank == 0:
+            q.put({"mean": mean, "std": std, "centroids": cents.numpy(), "counts": counts.numpy(),
+                   "scores": VD.merge_scores(parts), "n_parts": len(parts), "sizes": [len(p) for p in parts]})
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_gloo_flow_matches_single_process_golden(golden_dataset, golden_flow, golden_meta):
+    paths, _ = golden_dataset
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, paths, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=600)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    out = q.get()
+    assert out["n_parts"] == 2 and min(out["sizes"]) > 0          # both ranks scored videos
+    np.testing.assert_allclose(out["mean"], golden_flow["stats_mean"], rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(out["std"], golden_flow["stats_std"], rtol=1e-6, atol=1e-7)
+    assert np.array_equal(out["counts"], golden_flow["counts"])
+    assert np.abs(out["centroids"] - golden_flow["centroids"]).max() < 2e-5
+    ref = golden_meta["video_scores"]
+    assert sorted(out["scores"]) == sorted(ref)
+    worst = max(abs(ref[v][k] - out["scores"][v][k]) for v in ref for k in ref[v])
+    assert worst < 1e-4, worst

@@ -42,3 +42,34 @@ def test_error_path_without_gpu_work():
     h = C.c_void_p()
     dims = L.Dims()
     assert so.vge_encoder_create(C.byref(dims), None, 0, 0, C.byref(h)) == 1
+
+
+def _hexf(s):
+    return float.fromhex(s)
+
+
+def test_erf_branch_free_accuracy():
+    """Host restatement (float32 numpy) of the device GELU's branch-free erf (vge_common.h gelu2_many): the
+    ocml erff minimax pieces, both evaluated and selected.  |error| vs math.erf stays at f32 rounding level."""
+    import math
+    import numpy as np
+    f = np.float32
+    c = [f(_hexf(x)) for x in ("-0x1.268bc2p-11", "0x1.420828p-8", "-0x1.b5937p-6", "0x1.ce077cp-4",
+                               "-0x1.81266p-2", "0x1.06eba0p-3")]
+    d = [f(_hexf(x)) for x in ("0x1.1d3156p-16", "-0x1.8d129p-12", "0x1.f9a6d2p-9", "-0x1.8c3164p-6",
+                               "0x1.b4e9c8p-4", "0x1.4515fap-1", "0x1.078e5p-3")]
+    z = np.linspace(-6, 6, 200001, dtype=np.float32)
+    a = np.abs(z)
+    s = a * a
+    q = s * c[0] + c[1]
+    for k in c[2:]:
+        q = s * q + k
+    small = a * q + a
+    p = a * d[0] + d[1]
+    for k in d[2:]:
+        p = a * p + k
+    p = a * p + a
+    big = f(1) - np.exp2(p * f(-1.44269504))
+    erf = np.copysign(np.where(a < 1, small, big), z)
+    ref = np.array([math.erf(float(v)) for v in z])
+    assert np.abs(erf - ref).max() < 1.5e-7
