@@ -70,8 +70,15 @@ def setup_dist():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
+        # one process per GPU over RCCL ("nccl").  VGE_BENCH_BACKEND=gloo rehearses the multi-rank code path
+        # with ranks sharing the visible GPUs (a one-GPU box); the driver's scaling runs use the default.
+        backend = os.environ.get("VGE_BENCH_BACKEND", "nccl")
+        local = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(0)
     return world, rank, torch.device("cuda", torch.cuda.current_device())
@@ -221,7 +228,8 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    dt_t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    dt_t = torch.tensor([dt], dtype=torch.float64, device=dev if dist.is_initialized() and
+                        dist.get_backend() == "nccl" else "cpu")
     if world > 1:
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
     dt = float(dt_t.item())
