@@ -44,6 +44,13 @@ struct GemmArgsX3Host {
 };
 hipError_t launch_conv_encoders_x3(const float*, int, const void*, int, float*, hipStream_t);
 hipError_t launch_gemm_x3(int, const GemmArgsX3Host&, hipStream_t);
+struct FfnArgsX3Host {
+  const float* X1; float* out; int M;
+  const _Float16* W1; const float* cs1; const float* b1;
+  const _Float16* W2; const float* cs2; const float* b2;
+  const float* ln_w; const float* ln_b;
+};
+hipError_t launch_ffn_x3(const FfnArgsX3Host&, hipStream_t);
 hipError_t launch_conv_encoders(const float*, int, const void*, int, float*, hipStream_t);
 hipError_t launch_fuse(const float*, int, const FuseParamsHost&, float*, hipStream_t);
 hipError_t launch_gemm(int, const GemmArgsHost&, hipStream_t);
@@ -617,10 +624,16 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
     HIPCHK(vge::launch_attn(enc->qkv, B, enc->att, s));
     HIPCHK(gemm(vge::EPI_BIAS_RES_LN, enc->att, 256, Ly.out_w, Ly.out_cs, enc->x1, 256, M, 256, 256, Ly.out_b, enc->x,
                 Ly.n1_w, Ly.n1_b));
-    HIPCHK(gemm(vge::EPI_BIAS_RELU, enc->x1, 256, Ly.l1_w, Ly.l1_cs, enc->h, 1024, M, 256, 1024, Ly.l1_b, nullptr,
-                nullptr, nullptr));
-    HIPCHK(gemm(vge::EPI_BIAS_RES_LN, enc->h, 1024, Ly.l2_w, Ly.l2_cs, enc->x, 256, M, 1024, 256, Ly.l2_b, enc->x1,
-                Ly.n2_w, Ly.n2_b));
+    if (x3) {  // fused FFN block: the 1024-wide hidden stays on chip
+      const vge::FfnArgsX3Host fa{enc->x1, enc->x, M, (const _Float16*)Ly.l1_w, Ly.l1_cs, Ly.l1_b,
+                                  (const _Float16*)Ly.l2_w, Ly.l2_cs, Ly.l2_b, Ly.n2_w, Ly.n2_b};
+      HIPCHK(vge::launch_ffn_x3(fa, s));
+    } else {
+      HIPCHK(gemm(vge::EPI_BIAS_RELU, enc->x1, 256, Ly.l1_w, Ly.l1_cs, enc->h, 1024, M, 256, 1024, Ly.l1_b, nullptr,
+                  nullptr, nullptr));
+      HIPCHK(gemm(vge::EPI_BIAS_RES_LN, enc->h, 1024, Ly.l2_w, Ly.l2_cs, enc->x, 256, M, 1024, 256, Ly.l2_b, enc->x1,
+                  Ly.n2_w, Ly.n2_b));
+    }
   }
   HIPCHK(mark(4));
   HIPCHK(vge::launch_embed_tc(enc->x, B, seq_embed, frame_embed, tc_window, s));

@@ -676,6 +676,159 @@ __global__ void __launch_bounds__(512, 4) gemm_x3_kernel(GemmArgsX3 ga) {  // 4 
   }
 }
 
+// ------------------------------------------------------------------ fused FFN block (3xfp16)
+// out = LN2(X1 + relu(X1 W1^T + b1) W2^T + b2)  (TransformerEncoderLayer post-norm FFN, model.py:145-146)
+// for a 32-row block, with the 1024-wide hidden activation never leaving the CU: the hidden dimension is
+// processed in 4 chunks of 256; each chunk's relu(X1 W1_chunk^T + b1) is split into LDS hi/lo planes and
+// immediately multiplied into the running FFN2 accumulator (K panel = that chunk).
+struct FfnArgsX3 {
+  const float* X1;  // [M (padded to 64)][256] input, also the residual
+  float* out;       // [M][256]
+  int M;
+  const _Float16* W1; const float* cs1; const float* b1;  // linear1 [1024][256]: 4 column blocks x 16 chunks
+  const _Float16* W2; const float* cs2; const float* b2;  // linear2 [256][1024]: 64 chunks (4 K panels)
+  const float* ln_w; const float* ln_b;
+};
+
+constexpr int FFN_LDS_BYTES = 4 * 32 * XSB + (32 * NWAVE + 2 * NWAVE) * 4;
+
+__global__ void __launch_bounds__(512, 4) ffn_x3_kernel(FfnArgsX3 fa) {
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  _Float16* Xh = reinterpret_cast<_Float16*>(lds_raw);
+  _Float16* Xl = Xh + 32 * XS;
+  _Float16* Hh = Xl + 32 * XS;  // Hl = Hh + 32 * XS
+  float* red = reinterpret_cast<float*>(lds_raw + 4 * 32 * XSB);  // [32 rows][8 waves] + 2 x [8] maxima
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i = lane & 31, h = lane >> 5;
+  const int row0 = blockIdx.x * 32;
+  const int col = wave * 32 + i;  // this lane's column of every 256-wide block
+  const unsigned loff = (unsigned)((h * 256 + col) * 16);
+  auto lrow = [&](int r) { return (r & 3) + 8 * (r >> 2) + 4 * h; };
+  auto block_max = [&](float m, int slot) {  // over the 512 threads, every thread gets it
+    m = wave_max_last(m);
+    if (lane == 63) red[32 * NWAVE + slot * NWAVE + wave] = m;
+    __syncthreads();
+    float mm = red[32 * NWAVE + slot * NWAVE];
+#pragma unroll
+    for (int w = 1; w < NWAVE; ++w) mm = fmaxf(mm, red[32 * NWAVE + slot * NWAVE + w]);
+    return mm;
+  };
+
+  // ---- X1 panel (32 x 256) as hi/lo planes of X1 * 2^-ex (exact)
+  int ex;
+  {
+    const int c = tid & 255;
+    float a[16];
+    float m = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int row = row0 + (tid >> 8) + 2 * j;
+      a[j] = (row < fa.M) ? fa.X1[(size_t)row * 256 + c] : 0.f;
+      m = fmaxf(m, fabsf(a[j]));
+    }
+    ex = fp16_range_exp(block_max(m, 0));
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int r = (tid >> 8) + 2 * j;
+      split_store(Xh + r * XS + c, Xl + r * XS + c, ldexpf(a[j], -ex));
+    }
+  }
+  __syncthreads();
+  const char* xa = reinterpret_cast<const char*>(Xh) + i * XSB + h * 16;
+  const char* ha = reinterpret_cast<const char*>(Hh) + i * XSB + h * 16;
+  auto afn_x = [&](int cc, AFrag<1>& f) {
+    f.h[0] = *reinterpret_cast<const half8*>(xa + cc * 32);
+    f.l[0] = *reinterpret_cast<const half8*>(xa + cc * 32 + 32 * XSB);
+  };
+  auto afn_h = [&](int cc, AFrag<1>& f) {
+    f.h[0] = *reinterpret_cast<const half8*>(ha + cc * 32);
+    f.l[0] = *reinterpret_cast<const half8*>(ha + cc * 32 + 32 * XSB);
+  };
+  char* hb = reinterpret_cast<char*>(Hh) + (4 * h * XS + col) * 2;  // this lane's H column, C-layout rows
+
+  Acc<1, 1> acc2;
+  acc2.zero();
+  int hexp = 0;  // acc2 holds (H W2^T) * 2^-hexp
+  for (int hc = 0; hc < 4; ++hc) {
+    Acc<1, 1> acc1;
+    acc1.zero();
+    run_stream<GEMM_PF, 1>(acc1, reinterpret_cast<const char*>(fa.W1) + (size_t)hc * 16 * CHUNK_B, 16, loff, afn_x);
+    // hidden chunk: relu(acc1 * 2^ex * cs1 + b1)
+    const float s1 = ldexpf(1.0f, ex) * fa.cs1[hc * 256 + col], bb = fa.b1[hc * 256 + col];
+    float v[16];
+    float m = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      v[r] = fmaxf(acc1.c[0][0][r] * s1 + bb, 0.f);
+      m = fmaxf(m, v[r]);
+    }
+    const int e = fp16_range_exp(block_max(m, 1));  // its barrier also retires the previous chunk's H reads
+    if (hc > 0 && e != hexp) {
+      const float f = ldexpf(1.0f, hexp - e);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc2.c[0][0][r] *= f;
+    }
+    hexp = e;
+    const float sc = ldexpf(1.0f, -e);
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {
+      const floatx2 y = (floatx2){v[r], v[r + 1]} * sc;
+      const _Float16 h0 = (_Float16)y.x, h1 = (_Float16)y.y;
+      const floatx2 lo = y - (floatx2){(float)h0, (float)h1};
+      const int off = ((r & 3) + 8 * (r >> 2)) * XSB;
+      *reinterpret_cast<_Float16*>(hb + off) = h0;
+      *reinterpret_cast<_Float16*>(hb + off + XSB) = h1;
+      *reinterpret_cast<_Float16*>(hb + off + 32 * XSB) = (_Float16)lo.x;  // the Hl plane: 32 rows on
+      *reinterpret_cast<_Float16*>(hb + off + XSB + 32 * XSB) = (_Float16)lo.y;
+    }
+    __syncthreads();
+    run_stream<GEMM_PF, 1>(acc2, reinterpret_cast<const char*>(fa.W2) + (size_t)hc * 16 * CHUNK_B, 16, loff, afn_h);
+  }
+
+  // ---- epilogue: LN2(X1 + acc2 * 2^hexp * cs2 + b2), one row tile, no row guards (padded token buffers)
+  const float s2 = ldexpf(1.0f, hexp) * fa.cs2[col], bb2 = fa.b2[col], lw = fa.ln_w[col], lb = fa.ln_b[col];
+  const float* rbase = fa.X1 + (size_t)row0 * 256 + col;
+  float vt[16], s[16], q[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    vt[r] = acc2.c[0][0][r] * s2 + bb2 + rbase[lrow(r) * 256];
+    s[r] = vt[r];
+  }
+  auto row_reduce = [&](float (&x)[16]) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) x[r] = half_sum_last(x[r]);  // valid in lanes 31 and 63
+    if (i == 31) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) red[lrow(r) * NWAVE + wave] = x[r];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float* rr = red + lrow(r) * NWAVE;
+      float a = rr[0];
+#pragma unroll
+      for (int w = 1; w < NWAVE; ++w) a += rr[w];
+      x[r] = a;
+    }
+    __syncthreads();
+  };
+  row_reduce(s);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    s[r] *= 1.0f / 256.0f;
+    const float d = vt[r] - s[r];
+    q[r] = d * d;
+  }
+  row_reduce(q);
+  float* obase = fa.out + (size_t)row0 * 256 + col;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float rstd = 1.0f / sqrtf(q[r] * (1.0f / 256.0f) + 1e-5f);
+    obase[lrow(r) * 256] = (vt[r] - s[r]) * rstd * lw + lb;
+  }
+}
+
 }  // namespace
 
 // ================================================================== host launchers
@@ -706,7 +859,7 @@ hipError_t encoder_x3_kernel_setup() {
     e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, gemm_lds_bytes<GEMM_RT>());
     if (e != hipSuccess) return e;
   }
-  return hipSuccess;
+  return hipFuncSetAttribute((const void*)ffn_x3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, FFN_LDS_BYTES);
 }
 
 // Quads (4 windows per block) halve the weight bytes per row; pairs fill the remainder.  With G = min(CUs,
@@ -752,6 +905,21 @@ hipError_t launch_gemm_x3(int epi, const GemmArgsX3Host& a, hipStream_t s) {
     case EPI_BIAS_RELU: hipLaunchKernelGGL((gemm_x3_kernel<EPI_BIAS_RELU, GEMM_RT>), grid, dim3(512), L, s, g); break;
     default: hipLaunchKernelGGL((gemm_x3_kernel<EPI_BIAS_RES_LN, GEMM_RT>), grid, dim3(512), L, s, g); break;
   }
+  return hipGetLastError();
+}
+
+struct FfnArgsX3Host {
+  const float* X1; float* out; int M;
+  const _Float16* W1; const float* cs1; const float* b1;
+  const _Float16* W2; const float* cs2; const float* b2;
+  const float* ln_w; const float* ln_b;
+};
+static_assert(sizeof(FfnArgsX3Host) == sizeof(FfnArgsX3), "FfnArgsX3 layout");
+
+hipError_t launch_ffn_x3(const FfnArgsX3Host& a, hipStream_t s) {
+  FfnArgsX3 f;
+  memcpy(&f, &a, sizeof(f));
+  hipLaunchKernelGGL(ffn_x3_kernel, dim3((a.M + 31) / 32), dim3(512), FFN_LDS_BYTES, s, f);
   return hipGetLastError();
 }
 
