@@ -1,5 +1,5 @@
 #!/bin/bash
-# Build timing-only variants of the 3xfp16 encoder kernels into video-gen-evals_amd/csrc/build/:
+# Build timing-only variants of the 3xfp16 encoder + transformer kernels into video-gen-evals_amd/csrc/build/:
 #   ablN/libvge.so  for each VGE_ABL bit mask N given as an argument (see vge_encoder_x3.hip)
 #   trace/libvge.so with VGE_TRACE (s_memtime phase stamps, read by tools/trace_encoder.py)
 # Run them on the GPU box with VGE_LIB=<that path> python tools/time_encoder.py / trace_encoder.py.
@@ -9,13 +9,15 @@ make -s ARCH=gfx950
 HIPCC="/opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950"
 link() {
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$1/libvge.so" build/vge_featurize.o \
-    build/vge_encoder.o "$1/x3.o" build/vge_score.o build/vge_api.o
+    build/vge_encoder.o "$1/x3.o" "$1/tx.o" build/vge_score.o build/vge_api.o
 }
 for v in "$@"; do
   mkdir -p build/abl$v
   $HIPCC -DVGE_ABL=$v -c vge_encoder_x3.hip -o build/abl$v/x3.o
+  $HIPCC -DVGE_ABL=$v -c vge_transformer_x3.hip -o build/abl$v/tx.o
   link build/abl$v
 done
 mkdir -p build/trace
 $HIPCC -DVGE_TRACE -c vge_encoder_x3.hip -o build/trace/x3.o
+$HIPCC -DVGE_TRACE -c vge_transformer_x3.hip -o build/trace/tx.o
 link build/trace

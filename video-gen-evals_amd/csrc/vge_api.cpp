@@ -4,6 +4,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <algorithm>
 #include <string>
@@ -51,6 +52,23 @@ struct FfnArgsX3Host {
   const float* ln_w; const float* ln_b;
 };
 hipError_t launch_ffn_x3(const FfnArgsX3Host&, hipStream_t);
+struct TxLayerX3Host {  // vge_transformer_x3.hip
+  const _Float16* in_w;  const float* in_cs; const float* in_b;
+  const _Float16* out_w; const float* out_cs; const float* out_b;
+  const float* n1_w; const float* n1_b;
+  const _Float16* l1_w; const float* l1_cs; const float* l1_b;
+  const _Float16* l2_w; const float* l2_cs; const float* l2_b;
+  const float* n2_w; const float* n2_b;
+};
+struct TxArgsX3Host {
+  const float* pooled; int n_windows, n_layers;
+  const _Float16* ov_w; const float* ov_cs;
+  const float* cls; const float* pe;
+  const TxLayerX3Host* layers;  // host array [n_layers], n_layers <= 8 (passed as kernel arguments)
+  float* seq; float* frame; float* tc;
+};
+hipError_t transformer_x3_kernel_setup();
+hipError_t launch_transformer_x3(const TxArgsX3Host&, hipStream_t);
 hipError_t launch_conv_encoders(const float*, int, const void*, int, float*, hipStream_t);
 hipError_t launch_fuse(const float*, int, const FuseParamsHost&, float*, hipStream_t);
 hipError_t launch_gemm(int, const GemmArgsHost&, hipStream_t);
@@ -166,6 +184,8 @@ struct vge_encoder {
   float* wbuf = nullptr;
   _Float16* hbuf = nullptr;
   void* d_encs = nullptr;         // EncDescHost[10] or EncDescX3Host[10]
+  std::vector<vge::TxLayerX3Host> tx_layers;  // x3: the fused transformer kernel's layer table
+  bool tx_fused = true;           // x3: one fused transformer launch (VGE_X3_UNFUSED=1: per-layer kernels)
   vge::FuseParamsHost fuse{};
   const void* Wov = nullptr;      // packed (f32 chunks or fp16 chunks)
   const float* Wov_cs = nullptr;  // x3: its column scales
@@ -513,6 +533,21 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
                                         wb + o.l1_b, wb + o.l2_b, wb + o.n1_w, wb + o.n1_b, wb + o.n2_w, wb + o.n2_b,
                                         csp(o.in_w), csp(o.out_w), csp(o.l1_w), csp(o.l2_w)};
   }
+  if (x3) {
+    const char* uf = getenv("VGE_X3_UNFUSED");
+    enc->tx_fused = !(uf && uf[0] == '1');
+    if (L > 8) enc->tx_fused = false;  // the fused kernel takes up to 8 layers
+    std::vector<vge::TxLayerX3Host>& tl = enc->tx_layers;
+    tl.resize(L);
+    for (int l = 0; l < L; ++l) {
+      const vge_encoder::Layer& y = enc->layers[l];
+      tl[l] = vge::TxLayerX3Host{(const _Float16*)y.in_w, y.in_cs, y.in_b, (const _Float16*)y.out_w, y.out_cs, y.out_b,
+                                 y.n1_w, y.n1_b, (const _Float16*)y.l1_w, y.l1_cs, y.l1_b, (const _Float16*)y.l2_w,
+                                 y.l2_cs, y.l2_b, y.n2_w, y.n2_b};
+    }
+    he = vge::transformer_x3_kernel_setup();
+    if (he != hipSuccess) return hipfail(he);
+  }
   *out = enc;
   return VGE_OK;
 }
@@ -614,6 +649,15 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
   HIPCHK(mark(1));
   HIPCHK(vge::launch_fuse(enc->enc_out, frames, enc->fuse, enc->pooled, s));
   HIPCHK(mark(2));
+  if (x3 && enc->tx_fused) {  // tokens + all layers + outputs in one launch, one window per workgroup
+    HIPCHK(mark(3));
+    const vge::TxArgsX3Host ta{enc->pooled, B, enc->n_layers, (const _Float16*)enc->Wov, enc->Wov_cs, enc->cls, enc->pe,
+                               enc->tx_layers.data(), seq_embed, frame_embed, tc_window};
+    HIPCHK(vge::launch_transformer_x3(ta, s));
+    HIPCHK(mark(4));
+    HIPCHK(mark(5));
+    return VGE_OK;
+  }
   HIPCHK(gemm(vge::EPI_TOKENS, enc->pooled, 256, enc->Wov, enc->Wov_cs, enc->x, 256, frames, 256, 256, nullptr, nullptr,
               nullptr, nullptr));
   HIPCHK(mark(3));

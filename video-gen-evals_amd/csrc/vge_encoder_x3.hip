@@ -23,14 +23,10 @@
 // B[k = 8h + j][col i], j = 0..7; C/D: col = l&31, row = (r&3) + 8(r>>2) + 4(l>>5), r = 0..15.
 // A weight chunk = 16 K x 256 columns: [plane][h][n][8] fp16 = 16 KB, so a lane's B fragment of a chunk
 // is one 16-B load per plane and a wave's 32 columns are two contiguous 512-B runs per plane.
-#include "vge_common.h"
+#include "vge_x3.h"
 #include <algorithm>
 #include <cstring>
 
-#ifndef VGE_ABL
-#define VGE_ABL 0  // timing-only ablation builds (tools/ablate.sh), a bit mask: 1 no MFMA, 2 no B loads after the
-                   // prologue, 4 no A reads, 16 identity GELU; 0 = the product
-#endif
 
 #ifdef VGE_TRACE  // timing-only builds (tools/trace_encoder.py): s_memtime stamps of every wave of blocks 0..63
 __device__ long long g_vge_trace[64 * 8 * 32];
@@ -46,121 +42,6 @@ __device__ long long g_vge_trace[64 * 8 * 32];
 #endif
 
 namespace {
-
-typedef _Float16 half8 __attribute__((ext_vector_type(8)));
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-
-constexpr int XS = 264;              // fp16 per LDS activation row (256 + 8 pad: conflict-free b128 reads)
-constexpr int XSB = XS * 2;          // bytes per activation row
-constexpr int CHUNK_B = 16384;       // bytes per weight chunk
-constexpr int PLANE_B = 8192;        // bytes between the hi and lo planes of a chunk
-constexpr int STREAM_GROUP = 8;      // weight streams are packed as multiples of 8 chunks
-constexpr int CONV_PF = 4;           // weight chunks in flight per wave: conv (a quad wave holds 128 x 64 outputs)
-constexpr int GEMM_PF = 4;           // ... and GEMM waves (32 x 32 outputs, 4 waves per SIMD)
-
-__device__ __forceinline__ floatx16 mfma32(half8 a, half8 b, floatx16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
-}
-
-__device__ __forceinline__ void split_store(_Float16* hi, _Float16* lo, float v) {
-  const _Float16 h = (_Float16)v;
-  *hi = h;
-  *lo = (_Float16)(v - (float)h);
-}
-
-__device__ __forceinline__ int fp16_range_exp(float m) {  // 2^-e brings m into [2^8, 2^9); 2^+-e stays normal
-  return (m > 0.f && m <= 3.0e38f) ? max(ilogbf(m) - 8, -100) : 0;
-}
-
-// A wave's output tile: R row tiles x N column tiles of 32 x 32, one f32 accumulator each
-template <int R, int N>
-struct Acc {
-  floatx16 c[R][N];
-  __device__ __forceinline__ void zero() {
-#pragma unroll
-    for (int t = 0; t < R; ++t)
-#pragma unroll
-      for (int n = 0; n < N; ++n)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) c[t][n][r] = 0.f;
-  }
-};
-
-template <int R>
-struct AFrag {  // A fragments (hi, lo) of one 16-K chunk for R row tiles
-  half8 h[R], l[R];
-};
-
-template <int N>
-struct BFrag {  // B fragments (hi, lo) of one 16-K chunk for N column tiles
-  half8 h[N], l[N];
-};
-
-template <int R, int N>
-__device__ __forceinline__ void mma_chunk(Acc<R, N>& acc, const AFrag<R>& a, const BFrag<N>& b) {
-#if !(VGE_ABL & 1)
-#pragma unroll
-  for (int n = 0; n < N; ++n)
-#pragma unroll
-    for (int t = 0; t < R; ++t) {
-      acc.c[t][n] = mfma32(a.h[t], b.h[n], acc.c[t][n]);
-      acc.c[t][n] = mfma32(a.h[t], b.l[n], acc.c[t][n]);
-      acc.c[t][n] = mfma32(a.l[t], b.h[n], acc.c[t][n]);
-    }
-#else
-  asm volatile("" ::"v"(a.h[0]), "v"(a.l[R - 1]), "v"(b.h[0]), "v"(b.l[N - 1]));
-#endif
-}
-
-typedef const __attribute__((address_space(1))) char* gchar;  // global (not flat) loads: counted by vmcnt only
-typedef const __attribute__((address_space(1))) half8* ghalf8;
-
-// column tile n of this lane sits 32 columns (512 B) after tile n - 1
-template <int N>
-__device__ __forceinline__ void load_b(gchar g, int c, unsigned loff, BFrag<N>& b) {
-  gchar p = g + (size_t)c * CHUNK_B + loff;
-#pragma unroll
-  for (int n = 0; n < N; ++n) {
-    b.h[n] = *reinterpret_cast<ghalf8>(p + n * 512);
-    b.l[n] = *reinterpret_cast<ghalf8>(p + n * 512 + PLANE_B);
-  }
-}
-
-// Multiply a wave's output tile by a stream of n weight chunks (n a multiple of PF, >= PF, PF | 8).  afn(c, AFrag&)
-// reads the A fragments of chunk c from LDS (one chunk ahead).  B fragments are loaded PF - 1 chunks ahead
-// into a register ring; the loop is unrolled by PF so every ring index is static and the compiler's counted
-// vmcnt waits retire exactly the chunk being consumed.
-template <int PF, int R, int N, class AFn>
-__device__ __forceinline__ void run_stream(Acc<R, N>& acc, const void* gw, int n, unsigned loff, AFn afn) {
-  const gchar g = (gchar)gw;
-  BFrag<N> b[PF];
-#pragma unroll
-  for (int j = 0; j < PF - 1; ++j) load_b(g, j, loff, b[j]);
-  AFrag<R> a[2];
-  afn(0, a[0]);
-  for (int c0 = 0; c0 < n; c0 += PF) {
-#pragma unroll
-    for (int j = 0; j < PF; ++j) {
-      const int c = c0 + j;
-#if !(VGE_ABL & 2)
-      load_b(g, min(c + PF - 1, n - 1), loff, b[(j + PF - 1) % PF]);
-#endif
-#if !(VGE_ABL & 4)
-      afn(min(c + 1, n - 1), a[(j + 1) & 1]);
-#endif
-      mma_chunk(acc, a[j & 1], b[j]);
-      // pin this step's loads in place: without it the compiler hoists every A read of the unrolled group
-      // and sinks the B loads next to their use, which collapses the prefetch to vmcnt(0) waits
-      asm volatile("" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-    }
-#if !(VGE_ABL & 8)
-    // keep the two waves of each SIMD abreast (a raw s_barrier: LDS reads retired, loads stay in flight);
-    // a wave left alone at the end of a stream has too few loads in flight to keep the MFMA pipe busy
-    lds_barrier();
-#endif
-  }
-}
 
 // ------------------------------------------------------------------ conv encoder chain
 struct EncDescX3 {
