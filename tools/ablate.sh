@@ -1,6 +1,7 @@
 #!/bin/bash
 # Build timing-only variants of the 3xfp16 encoder + transformer kernels into video-gen-evals_amd/csrc/build/:
-#   ablN/libvge.so  for each VGE_ABL bit mask N given as an argument (see vge_encoder_x3.hip)
+#   ablN/libvge.so  for each VGE_ABL bit mask N given as an argument (see vge_x3.h; transformer: 32 L2-resident
+#                   weights, 64 no CLS dot products, 128 no stream barriers)
 #   trace/libvge.so with VGE_TRACE (s_memtime phase stamps, read by tools/trace_encoder.py)
 # Run them on the GPU box with VGE_LIB=<that path> python tools/time_encoder.py / trace_encoder.py.
 set -e

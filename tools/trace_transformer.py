@@ -52,5 +52,10 @@ epi = nxt - w0[:, 1:2 * nseg:2]
 out["stream_total"] = float(stream.sum(axis=1).mean())
 out["epi_total"] = float(epi.sum(axis=1).mean())
 out["segments"] = {n: [round(float(stream[:, k].mean())), round(float(epi[:, k].mean()))] for k, n in enumerate(names)}
+for base, nm in ((100, "L0_out"), (110, "L0_ffn2_3")):
+    st = w0[:, base + 1:base + 7]
+    prev = w0[:, 2 * names.index(nm) + 1]
+    marks = np.concatenate([prev[:, None], st], axis=1)
+    out[nm + "_fine"] = [round(float(x)) for x in np.diff(marks, axis=1).mean(axis=0)]
 out["start_skew"] = float((t[:, 0, 124].max() - t[:, 0, 124].min()))
 print(json.dumps(out))

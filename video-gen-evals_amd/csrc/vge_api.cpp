@@ -59,6 +59,7 @@ struct TxLayerX3Host {  // vge_transformer_x3.hip
   const _Float16* l1_w; const float* l1_cs; const float* l1_b;
   const _Float16* l2_w; const float* l2_cs; const float* l2_b;
   const float* n2_w; const float* n2_b;
+  int e_x1, e_x2, e_h, pad;  // static split exponents of LN1 / LN2 outputs and of the FFN hidden
 };
 struct TxArgsX3Host {
   const float* pooled; int n_windows, n_layers;
@@ -146,6 +147,12 @@ void pack_conv(const float* W, std::vector<float>& out) {
 // power-of-two column scale s_n bringing column n's largest |w| into [2^8, 2^9); plane 0 = hi = f16(w'),
 // plane 1 = lo = f16(w' - hi) (an fp16 residual, subnormals kept by the MFMA); chunk c covers
 // k = 16c + 8h + j (zero past K_real).  cs receives 2^-s_n per column (the kernels' epilogue factor).
+// host twin of fp16_range_exp (vge_x3.h): 2^-e brings m into [2^8, 2^9)
+int range_exp(double m) {
+  if (!(m > 0.0) || !(m <= 3.0e38)) return 0;
+  return std::max(std::ilogb(m) - 8, -100);
+}
+
 template <class Get>
 void pack_linear_x3(Get W, int N, int K_real, std::vector<_Float16>& out, std::vector<float>& cs, int chunk_mult = 1) {
   const int nch = ((K_real + 15) / 16 + chunk_mult - 1) / chunk_mult * chunk_mult;  // streams run in groups of chunk_mult
@@ -193,6 +200,7 @@ struct vge_encoder {
     const void *in_w, *out_w, *l1_w, *l2_w;  // packed matrices
     const float *in_b, *out_b, *l1_b, *l2_b, *n1_w, *n1_b, *n2_w, *n2_b;
     const float *in_cs, *out_cs, *l1_cs, *l2_cs;  // x3: per-column weight scales
+    int e_x1, e_x2, e_h;                          // x3: static split exponents (see LOff)
   };
   std::vector<Layer> layers;
   const float* cls = nullptr;
@@ -441,7 +449,7 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
   const size_t off_pe = pk.size();
   pk.insert(pk.end(), pe, pe + 33 * 256);
 
-  struct LOff { Mat in_w, out_w, l1_w, l2_w; size_t in_b, out_b, l1_b, l2_b, n1_w, n1_b, n2_w, n2_b; };
+  struct LOff { Mat in_w, out_w, l1_w, l2_w; size_t in_b, out_b, l1_b, l2_b, n1_w, n1_b, n2_w, n2_b; int e_x1, e_x2, e_h; };
   std::vector<LOff> loff(L);
   for (int l = 0; l < L; ++l) {
     const std::string p = "temporal.layers." + std::to_string(l);
@@ -471,6 +479,27 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
     o.n1_b = pk.size(); pk.insert(pk.end(), n1b, n1b + 256);
     o.n2_w = pk.size(); pk.insert(pk.end(), n2w, n2w + 256);
     o.n2_b = pk.size(); pk.insert(pk.end(), n2b, n2b + 256);
+    // static operand scales of the fused x3 transformer (vge_transformer_x3.hip): a LayerNorm output is
+    // bounded by 16 max|gamma| + max|beta| (sum_j z_j^2 <= 256), ReLU(X1 W1^T + b1) by
+    // max_n sum_k |W1[n][k]| * that + |b1[n]|
+    auto ln_bound = [](const float* g, const float* b) {
+      double mg = 0.0, mb = 0.0;
+      for (int j = 0; j < 256; ++j) {
+        mg = std::max(mg, (double)std::fabs(g[j]));
+        mb = std::max(mb, (double)std::fabs(b[j]));
+      }
+      return 16.0 * mg + mb;
+    };
+    const double b1 = ln_bound(n1w, n1b), b2 = ln_bound(n2w, n2b);
+    double bh = 0.0;
+    for (int n = 0; n < 1024; ++n) {
+      double a = 0.0;
+      for (int k = 0; k < 256; ++k) a += std::fabs((double)l1w[(size_t)n * 256 + k]);
+      bh = std::max(bh, a * b1 + std::fabs((double)l1b[n]));
+    }
+    o.e_x1 = range_exp(b1);
+    o.e_x2 = range_exp(b2);
+    o.e_h = range_exp(bh);
   }
 
   vge_encoder* enc = new vge_encoder();
@@ -531,7 +560,7 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
     auto csp = [&](const Mat& m) -> const float* { return x3 ? wb + m.cs : nullptr; };
     enc->layers[l] = vge_encoder::Layer{mat(o.in_w), mat(o.out_w), mat(o.l1_w), mat(o.l2_w), wb + o.in_b, wb + o.out_b,
                                         wb + o.l1_b, wb + o.l2_b, wb + o.n1_w, wb + o.n1_b, wb + o.n2_w, wb + o.n2_b,
-                                        csp(o.in_w), csp(o.out_w), csp(o.l1_w), csp(o.l2_w)};
+                                        csp(o.in_w), csp(o.out_w), csp(o.l1_w), csp(o.l2_w), o.e_x1, o.e_x2, o.e_h};
   }
   if (x3) {
     const char* uf = getenv("VGE_X3_UNFUSED");
@@ -543,7 +572,7 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
       const vge_encoder::Layer& y = enc->layers[l];
       tl[l] = vge::TxLayerX3Host{(const _Float16*)y.in_w, y.in_cs, y.in_b, (const _Float16*)y.out_w, y.out_cs, y.out_b,
                                  y.n1_w, y.n1_b, (const _Float16*)y.l1_w, y.l1_cs, y.l1_b, (const _Float16*)y.l2_w,
-                                 y.l2_cs, y.l2_b, y.n2_w, y.n2_b};
+                                 y.l2_cs, y.l2_b, y.n2_w, y.n2_b, y.e_x1, y.e_x2, y.e_h, 0};
     }
     he = vge::transformer_x3_kernel_setup();
     if (he != hipSuccess) return hipfail(he);

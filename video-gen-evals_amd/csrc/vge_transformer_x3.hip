@@ -40,6 +40,7 @@ struct TxLayerX3 {
   const _Float16* l1_w; const float* l1_cs; const float* l1_b;      // linear1 [1024][256]: 4 col blocks x 16
   const _Float16* l2_w; const float* l2_cs; const float* l2_b;      // linear2 [256][1024]: 4 K panels x 16
   const float* n2_w; const float* n2_b;
+  int e_x1, e_x2, e_h, pad;  // static split exponents: LN1 / LN2 outputs, FFN hidden (host: range bounds)
 };
 
 struct TxArgsX3 {  // by value: the layer table is kernel-argument memory (scalar loads, no vmcnt waits)
@@ -54,11 +55,14 @@ struct TxArgsX3 {  // by value: the layer table is kernel-argument memory (scala
 constexpr int TOK = 33;          // CLS + 32 frames
 constexpr int AROWS = TOK;       // rows of an A operand plane
 constexpr int QS = 260;          // f32 row stride of the Q / K / V / final-embedding staging (bank shift)
-constexpr int TX_PF = 4;
+#ifndef VGE_TX_PF
+#define VGE_TX_PF 4
+#endif
+constexpr int TX_PF = VGE_TX_PF;  // weight chunks in flight per wave (ring depth)
 constexpr int TX_NW = 4;         // waves
 constexpr int AP_BYTES = 2 * AROWS * XSB;            // hi / lo planes of the current A operand
 constexpr int U_BYTES = 3 * TOK * QS * 4;             // Q, K, V (f32) | FFN hidden planes | final embeddings
-constexpr int RED_FLOATS = TOK * TX_NW + 2 * TX_NW;
+constexpr int RED_FLOATS = 2 * TOK * TX_NW + 2 * TX_NW + TX_NW;  // row partials x2, maxima x2, tc
 constexpr int TX_LDS_BYTES = AP_BYTES + U_BYTES + RED_FLOATS * 4;
 static_assert(2 * AROWS * XSB <= U_BYTES, "hidden planes fit the union");
 static_assert(TX_LDS_BYTES <= 160 * 1024, "LDS");
@@ -68,6 +72,16 @@ typedef _Float16 half2v __attribute__((ext_vector_type(2)));
 struct AFragT {  // one chunk's A operand: the 32 frame rows (MFMA) and the CLS row (VALU dot products)
   half8 h, l, h0, l0;
 };
+
+// x of lane l combined with x of lane l ^ 32 (v_permlane32_swap: no LDS round trip)
+__device__ __forceinline__ float halves_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float halves_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
 
 // CLS row on the VALU: c += x . w over this lane's 8 k of the chunk, the same 3 products as the MFMAs
 __device__ __forceinline__ float cls_dot(float c, half8 xh, half8 xl, half8 wh, half8 wl) {
@@ -86,7 +100,16 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* Ap = lds;                                   // A planes: hi rows [0, AROWS), lo at + AROWS * XSB
   char* U = lds + AP_BYTES;                         // Q/K/V f32 [3][TOK][QS] | hidden planes | embeddings
-  float* red = reinterpret_cast<float*>(U + U_BYTES);  // [TOK][4] row partials, [2][4] maxima
+  float* red = reinterpret_cast<float*>(U + U_BYTES);  // [2][TOK][4] row partials, [2][4] maxima, [4] tc
+  // consecutive reductions alternate between two buffers, so none needs a trailing barrier: the writes of
+  // reduction k + 2 come after reduction k + 1's barrier, which every read of reduction k precedes
+  int rs_buf = 0, bm_buf = 0;
+  [[maybe_unused]] int tr_s = -1;  // VGE_TRACE: the current segment, for the fine stamps of layer 0's epilogues
+#ifdef VGE_TRACE
+#define TSTAMP_FINE(k) do { if (tr_s == 4) TSTAMP(100 + (k)); else if (tr_s == 12) TSTAMP(110 + (k)); } while (0)
+#else
+#define TSTAMP_FINE(k) do { } while (0)
+#endif
   const int w = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -98,34 +121,37 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
   const unsigned aoff = (unsigned)((1 + i) * XSB + h * 16), aoff0 = (unsigned)(h * 16);
 
   // ---- helpers -----------------------------------------------------------------------------------------
-  auto block_max = [&](float m, int slot) {  // over the workgroup, every thread gets it
+  auto block_max = [&](float m) {  // over the workgroup, every thread gets it
+    float* rb = red + 2 * TOK * TX_NW + bm_buf * TX_NW;
+    bm_buf ^= 1;
     m = wave_max_last(m);
-    if (lane == 63) red[TOK * TX_NW + slot * TX_NW + wave] = m;
+    if (lane == 63) rb[wave] = m;
     __syncthreads();
-    const floatx4 p = *reinterpret_cast<const floatx4*>(red + TOK * TX_NW + slot * TX_NW);
+    const floatx4 p = *reinterpret_cast<const floatx4*>(rb);
     return fmaxf(fmaxf(p[0], p[1]), fmaxf(p[2], p[3]));
-  };
-  auto sum4 = [&](int row) {
-    const floatx4 a = *reinterpret_cast<const floatx4*>(red + row * TX_NW);
-    return (a[0] + a[1]) + (a[2] + a[3]);
   };
   // row sums over the 256 columns, in place: x (token rows trow(r), both column tiles get the row sum),
   // x0 (CLS; the same value in both lane halves)
   auto row_sums = [&](float (&x)[2][16], float (&x0)[2]) {
+    float* rb = red + rs_buf * TOK * TX_NW;
+    rs_buf ^= 1;
+    auto sum4 = [&](int row) {
+      const floatx4 a = *reinterpret_cast<const floatx4*>(rb + row * TX_NW);
+      return (a[0] + a[1]) + (a[2] + a[3]);
+    };
     float y[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) y[r] = half_sum_last(x[0][r] + x[1][r]);  // valid in lanes 31 and 63
     const float y0 = half_sum_last(x0[0] + x0[1]);
     if (i == 31) {
 #pragma unroll
-      for (int r = 0; r < 16; ++r) red[trow(r) * TX_NW + wave] = y[r];
-      if (h == 0) red[wave] = y0;
+      for (int r = 0; r < 16; ++r) rb[trow(r) * TX_NW + wave] = y[r];
+      if (h == 0) rb[wave] = y0;
     }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < 16; ++r) x[0][r] = x[1][r] = sum4(trow(r));
     x0[0] = x0[1] = sum4(0);
-    __syncthreads();
   };
   // LayerNorm over 256 columns (in place), affine w, b [256], eps 1e-5
   auto layer_norm = [&](float (&v)[2][16], float (&v0)[2], const float (&lw)[2], const float (&lb)[2]) {
@@ -134,7 +160,9 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
     for (int n = 0; n < 2; ++n)
 #pragma unroll
       for (int r = 0; r < 16; ++r) s[n][r] = v[n][r];
+    TSTAMP_FINE(1);
     row_sums(s, s0);
+    TSTAMP_FINE(2);
     float q[2][16], q0[2];
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
@@ -148,35 +176,39 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
       q0[n] = (v0[n] - s0[n]) * (v0[n] - s0[n]);
     }
     row_sums(q, q0);
+    TSTAMP_FINE(3);
+    // 1 / sqrt(var + eps) once per row (v_rsq_f32, ~1 ulp; the IEEE sqrt + divide sequences cost ~50
+    // instructions per value)
+    float rstd[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) rstd[r] = __builtin_amdgcn_rsqf(q[0][r] * (1.0f / 256.0f) + 1e-5f);
+    const float rstd0 = __builtin_amdgcn_rsqf(q0[0] * (1.0f / 256.0f) + 1e-5f);
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
       const float gw = lw[n], gb = lb[n];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) v[n][r] = (v[n][r] - s[n][r]) * (1.0f / sqrtf(q[n][r] * (1.0f / 256.0f) + 1e-5f)) * gw + gb;
-      v0[n] = (v0[n] - s0[n]) * (1.0f / sqrtf(q0[n] * (1.0f / 256.0f) + 1e-5f)) * gw + gb;
+      for (int r = 0; r < 16; ++r) v[n][r] = (v[n][r] - s[n][r]) * rstd[r] * gw + gb;
+      v0[n] = (v0[n] - s0[n]) * rstd0 * gw + gb;
     }
   };
   // split rows into hi/lo planes at `plane` as v * 2^-e, e from the workgroup-wide max |v| (the barrier
   // inside also retires every read of the planes' previous content issued before it); returns e.  The
   // caller barriers before the planes are read.
-  auto split_rows = [&](char* plane, const float (&v)[2][16], const float (&v0)[2], int slot) {
-    float m = fmaxf(fabsf(v0[0]), fabsf(v0[1]));
-#pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) m = fmaxf(m, fabsf(v[n][r]));
-    const int e = fp16_range_exp(block_max(m, slot));
+  auto split_rows_e = [&](char* plane, const float (&v)[2][16], const float (&v0)[2], int e) {
     const float sc = ldexpf(1.0f, -e);
 #pragma unroll
     for (int n = 0; n < 2; ++n) {
       char* bh = plane + ((1 + 4 * h) * XS + col0 + 32 * n) * 2;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float y = v[n][r] * sc;
-        const _Float16 hi = (_Float16)y;
+      for (int r = 0; r < 16; r += 2) {  // two rows per packed conversion (v_cvt_pk_f16_f32)
+        const floatx2 y = floatx2{v[n][r], v[n][r + 1]} * sc;
+        const half2v hi = __builtin_convertvector(y, half2v);
+        const half2v lo = __builtin_convertvector(y - __builtin_convertvector(hi, floatx2), half2v);
         const int off = ((r & 3) + 8 * (r >> 2)) * XSB;
-        *reinterpret_cast<_Float16*>(bh + off) = hi;
-        *reinterpret_cast<_Float16*>(bh + off + AROWS * XSB) = (_Float16)(y - (float)hi);
+        *reinterpret_cast<_Float16*>(bh + off) = hi[0];
+        *reinterpret_cast<_Float16*>(bh + off + XSB) = hi[1];
+        *reinterpret_cast<_Float16*>(bh + off + AROWS * XSB) = lo[0];
+        *reinterpret_cast<_Float16*>(bh + off + XSB + AROWS * XSB) = lo[1];
       }
       if (h == 0) {
         const float y = v0[n] * sc;
@@ -187,7 +219,15 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
     }
     return e;
   };
-  auto both_halves = [&](float c) { return c + __shfl_xor(c, 32); };
+  auto split_rows = [&](char* plane, const float (&v)[2][16], const float (&v0)[2]) {
+    float m = fmaxf(fabsf(v0[0]), fabsf(v0[1]));
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) m = fmaxf(m, fabsf(v[n][r]));
+    return split_rows_e(plane, v, v0, fp16_range_exp(block_max(m)));
+  };
+  auto both_halves = [&](float c) { return halves_sum(c); };
 
   TSTAMP(124);
   // ---- token A operand: row 0 zero (the CLS token is not a product), rows 1..32 the window's pooled frames
@@ -203,7 +243,7 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
       a[j] = src[j * 256];
       m = fmaxf(m, fabsf(a[j]));
     }
-    ax = fp16_range_exp(block_max(m, 0));
+    ax = fp16_range_exp(block_max(m));
 #pragma unroll
     for (int j = 0; j < 32; ++j)
       split_store(reinterpret_cast<_Float16*>(Ap + (1 + j) * XSB) + tid,
@@ -321,15 +361,20 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
 #else
         asm volatile("" ::"v"(f.h), "v"(f.l), "v"(bb.h[n]), "v"(bb.l[n]));
 #endif
+#if !(VGE_ABL & 64)
         c0[n] = cls_dot(c0[n], f.h0, f.l0, bb.h[n], bb.l[n]);
+#endif
       }
       // the CLS dot products stay in their step (else they are sunk past the loop and the ring stays live)
       asm volatile("" : "+v"(c0[0]), "+v"(c0[1])::"memory");
       __builtin_amdgcn_sched_barrier(0);
-      if (c % TX_PF == TX_PF - 1) lds_barrier();  // keep the waves abreast (see run_stream)
+      // keep the waves abreast (see run_stream); the barrier after the last chunk also orders every
+      // epilogue's LDS writes after all waves' reads of the segment's A planes
+      if (c % TX_PF == TX_PF - 1 && (!(VGE_ABL & 128) || c == 15)) lds_barrier();
     }
 
     TSTAMP(2 * s + 1);
+    tr_s = s;
     // ---- segment epilogues ------------------------------------------------------------------------------
     const float xs = ldexpf(1.0f, ax);
     float cl[2];  // the CLS row of this segment's product (both k halves)
@@ -347,10 +392,11 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
         for (int r = 0; r < 16; ++r) X[n][r] += acc.c[0][n][r] * cs;  // X holds pe, x0 cls + pe_0
       }
       acc.zero();
-      ax = split_rows(Ap, X, x0, 1);
+      ax = split_rows(Ap, X, x0);
       __syncthreads();
       continue;
     }
+    const TxLayerX3& L = ta.layers[l];
     if (p < 3) {
       // q / k / v block p -> f32 staging U[p][row][col]
       float* dst = reinterpret_cast<float*>(U) + p * TOK * QS;
@@ -398,14 +444,14 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
             const floatx4 k0 = *reinterpret_cast<const floatx4*>(Kh + 16 * h + 4 * j);
             sc += qb[j][0] * k0[0] + qb[j][1] * k0[1] + qb[j][2] * k0[2] + qb[j][3] * k0[3];
           }
-          sc = (sc + __shfl_xor(sc, 32)) * kScale;
+          sc = halves_sum(sc) * kScale;
           float mx = sc;
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             st[r] *= kScale;
             mx = fmaxf(mx, st[r]);
           }
-          mx = fmaxf(mx, __shfl_xor(mx, 32));
+          mx = halves_max(mx);
           float den = 0.f;
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
@@ -413,7 +459,7 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
             den += st[r];
           }
           const float pc = expf(sc - mx);
-          den = den + __shfl_xor(den, 32) + pc;
+          den = halves_sum(den) + pc;
           // P V over the frame keys: A = V^T[d = i][key of register t of half h], B = P^T (register t)
           floatx16 o = {};
 #pragma unroll
@@ -447,14 +493,15 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
           }
           const float m0 = wave_max_all(s0);
           const float p0 = (lane < TOK) ? expf(s0 - m0) : 0.f;
-          const float d0 = __shfl(wave_sum_last(p0), 63);
-          float acc0 = 0.f;
+          const float d0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(wave_sum_last(p0)), 63));
+          float acc0[3] = {0.f, 0.f, 0.f};  // three chains (33 keys)
 #pragma unroll
-          for (int k = 0; k < TOK; ++k) acc0 += __shfl(p0, k) * Vh[k * QS + i];
-          oc[e] = acc0 / d0;
+          for (int k = 0; k < TOK; ++k)
+            acc0[k % 3] += __int_as_float(__builtin_amdgcn_readlane(__float_as_int(p0), k)) * Vh[k * QS + i];
+          oc[e] = ((acc0[0] + acc0[1]) + acc0[2]) / d0;
           if (h == 0) m = fmaxf(m, fabsf(oc[e]));
         }
-        ax = fp16_range_exp(block_max(m, 0));
+        ax = fp16_range_exp(block_max(m));
         {  // att -> the A planes of out_proj: frame rows 1 + i, CLS row 0
           const float scl = ldexpf(1.0f, -ax);
 #pragma unroll
@@ -496,8 +543,13 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
       }
       acc.zero();
       layer_norm(X, x0, eg, ebt);
-      ax = split_rows(Ap, X, x0, 1);
+      // a LayerNorm output's range is known statically; the barrier orders the writes after every wave's
+      // reads of the att planes (the out_proj stream) -- those all precede the LayerNorm's reductions
+      TSTAMP_FINE(4);
+      ax = split_rows_e(Ap, X, x0, L.e_x1);
+      TSTAMP_FINE(5);
       __syncthreads();
+      TSTAMP_FINE(6);
       continue;
     }
     const int hc = (p - 4) >> 1;
@@ -511,19 +563,15 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
         for (int r = 0; r < 16; ++r) hv[n][r] = fmaxf(acc.c[0][n][r] * cs + bb, 0.f);
         h0[n] = fmaxf(cl[n] * cs + bb, 0.f);
       }
-      const int e = split_rows(U, hv, h0, 0);  // its barrier retires the previous linear2 panel's reads
+      // one static exponent for all four hidden chunks: the running FFN2 sum needs no rescale
+      hexp = split_rows_e(U, hv, h0, L.e_h);
       if (hc == 0) {
         acc.zero();
       } else {
-        const float f = ldexpf(1.0f, hexp - e);
+        acc = acc2;
 #pragma unroll
-        for (int n = 0; n < 2; ++n) {
-#pragma unroll
-          for (int r = 0; r < 16; ++r) acc.c[0][n][r] = acc2.c[0][n][r] * f;
-          c0[n] = (h == 0) ? c02[n] * f : 0.f;  // c02 holds both k halves: carry it in one lane half
-        }
+        for (int n = 0; n < 2; ++n) c0[n] = (h == 0) ? c02[n] : 0.f;  // c02 holds both k halves: one half carries it
       }
-      hexp = e;
       __syncthreads();
       continue;
     }
@@ -545,9 +593,12 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
       }
       acc.zero();
       layer_norm(X, x0, eg, ebt);
-      if (l + 1 < ta.n_layers) {
-        ax = split_rows(Ap, X, x0, 1);
+      if (l + 1 < ta.n_layers) {  // (every wave's reads of the X1 planes precede the LayerNorm's barriers)
+        TSTAMP_FINE(4);
+        ax = split_rows_e(Ap, X, x0, L.e_x2);
+        TSTAMP_FINE(5);
         __syncthreads();
+        TSTAMP_FINE(6);
       }
     }
   }
@@ -562,18 +613,23 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
     ss0[n] = x0[n] * x0[n];
   }
   row_sums(ss, ss0);
+  // F.normalize: x / max(||x||, 1e-12), as x * (1 / max(...)) once per row
+  float inv_norm[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) inv_norm[r] = 1.0f / fmaxf(sqrtf(ss[0][r]), 1e-12f);
+  const float inv_norm0 = 1.0f / fmaxf(sqrtf(ss0[0]), 1e-12f);
   float* F = reinterpret_cast<float*>(U);  // [TOK][QS] normalised tokens
 #pragma unroll
   for (int n = 0; n < 2; ++n) {
     const int col = col0 + 32 * n;
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
-      const float f = X[n][r] / fmaxf(sqrtf(ss[n][r]), 1e-12f);
+      const float f = X[n][r] * inv_norm[r];
       F[trow(r) * QS + col] = f;
       if (ta.frame) ta.frame[((size_t)w * TOK + trow(r)) * 256 + col] = f;
     }
     if (h == 0) {
-      const float f0 = x0[n] / fmaxf(sqrtf(ss0[n]), 1e-12f);
+      const float f0 = x0[n] * inv_norm0;
       F[col] = f0;
       if (ta.frame) ta.frame[(size_t)w * TOK * 256 + col] = f0;
       ta.seq[(size_t)w * 256 + col] = f0;
@@ -592,9 +648,10 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
       }
       tsum += sqrtf(wave_sum(d2));
     }
-    if (lane == 0) red[wave] = tsum;
+    float* rt = red + 2 * TOK * TX_NW + 2 * TX_NW;
+    if (lane == 0) rt[wave] = tsum;
     __syncthreads();
-    if (tid == 0) ta.tc[w] = ((red[0] + red[1]) + (red[2] + red[3])) / (float)(TOK - 2);
+    if (tid == 0) ta.tc[w] = ((rt[0] + rt[1]) + (rt[2] + rt[3])) / (float)(TOK - 2);
   }
   TSTAMP(126);
 }
@@ -610,6 +667,7 @@ struct TxLayerX3Host {
   const _Float16* l1_w; const float* l1_cs; const float* l1_b;
   const _Float16* l2_w; const float* l2_cs; const float* l2_b;
   const float* n2_w; const float* n2_b;
+  int e_x1, e_x2, e_h, pad;
 };
 static_assert(sizeof(TxLayerX3Host) == sizeof(TxLayerX3), "TxLayerX3 layout");
 
