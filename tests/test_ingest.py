@@ -1,0 +1,109 @@
+"""Native on-disk ingest (include/vge_ingest.h, vge/ingest.py) against the
+reference's own reader, np.load (utils.py:383-424), as the checker: bit-identical frame stores on the
+golden dataset and on synthetic files covering savez / savez_compressed members, float64 arrays,
+keypoint files shorter than the mesh, absent and unreadable keypoint files, empty and truncated npz, and
+the packed sidecar round trip.  CPU only (host code in libvge.so)."""
+import os
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+from vge import ingest, synth
+from vge.data import VideoItem, create_dataset_from_generated_meshes, load_clip, pack_frame_store
+
+
+def numpy_store(items, kp_dir, require_kp):
+    clips = [load_clip(it, kp_dir, require_kp) for it in items]
+    return pack_frame_store(clips, [it.name for it in items], [it.cls for it in items])
+
+
+def assert_same(a, b):
+    assert a.names == b.names and a.classes == b.classes
+    assert np.array_equal(a.videos, b.videos)
+    for k in ("pose", "gori", "betas", "vit"):
+        assert getattr(a, k).shape == getattr(b, k).shape, k
+        assert np.array_equal(getattr(a, k), getattr(b, k)), k
+    nk = int(a.videos[:, 3].sum()) if len(a.videos) else 0
+    assert np.array_equal(a.kp[:nk], b.kp[:nk])
+
+
+def _write(root: Path, name, T, kp_len=None, compressed=True, f64=False, kp=True, vit_dim=64, seed=0):
+    c = synth.make_clip(synth.SEED_GEN, seed, max(T, 1), kp_len=kp_len, vit_dim=vit_dim)
+    arrs = dict(pose=c.pose[:T], global_orient=c.global_orient[:T], betas=c.betas[:T], vit=c.vit[:T])
+    if f64:
+        arrs = {k: v.astype(np.float64) for k, v in arrs.items()}
+    path = root / "gen" / f"{name}.npz"
+    path.parent.mkdir(parents=True, exist_ok=True)
+    (np.savez_compressed if compressed else np.savez)(path, **arrs, frame_idx=np.arange(T, dtype=np.int32))
+    if kp:
+        kp_path = root / "generated_kps" / name / "keypoints.npy"
+        kp_path.parent.mkdir(parents=True, exist_ok=True)
+        np.save(kp_path, c.keypoints.astype(np.float64) if f64 else c.keypoints)
+    return VideoItem(cls="Unknown", name=path.name, path=str(path), length=T, vit_dim=vit_dim)
+
+
+def test_golden_dataset_matches_numpy_reader(golden_dataset):
+    paths, _ = golden_dataset
+    gen = create_dataset_from_generated_meshes(paths["generated_meshes"]).items
+    a = ingest.load_frame_store_native(gen, paths["generated_kps"], require_kp=True, threads=4)
+    assert_same(a, numpy_store(gen, paths["generated_kps"], True))
+    from vge.data import NpzVideoDataset
+    real = NpzVideoDataset(paths["real"]).items
+    a = ingest.load_frame_store_native(real, paths["real_kp"], require_kp=False, threads=3)
+    assert_same(a, numpy_store(real, paths["real_kp"], False))
+
+
+def test_formats_and_edge_cases(tmp_path):
+    kp_dir = str(tmp_path / "generated_kps")
+    items = [_write(tmp_path, "a", 32), _write(tmp_path, "b", 64, kp_len=50, seed=1),
+             _write(tmp_path, "c", 5, compressed=False, seed=2), _write(tmp_path, "d", 40, f64=True, seed=3),
+             _write(tmp_path, "e", 0, kp_len=0, seed=4), _write(tmp_path, "f", 33, kp=False, seed=5)]
+    # without require_kp: "f" has no keypoints (kp_frames 0), like load_clip
+    a = ingest.load_frame_store_native(items, kp_dir, require_kp=False, threads=2)
+    assert_same(a, numpy_store(items, kp_dir, False))
+    assert a.videos[5, 3] == 0 and a.videos[1, 3] == 50 and a.videos[4, 1] == 0
+    # require_kp: the missing file raises like utils.py:416-417
+    with pytest.raises(FileNotFoundError):
+        ingest.load_frame_store_native(items, kp_dir, require_kp=True)
+    a = ingest.load_frame_store_native(items[:5], kp_dir, require_kp=True, threads=1)
+    assert_same(a, numpy_store(items[:5], kp_dir, True))
+    # no keypoint dir at all
+    a = ingest.load_frame_store_native(items, None, require_kp=False)
+    assert_same(a, numpy_store(items, None, False))
+
+
+def test_unreadable_files(tmp_path):
+    kp_dir = str(tmp_path / "generated_kps")
+    good = _write(tmp_path, "g", 32)
+    bad = _write(tmp_path, "t", 32, seed=7)
+    data = Path(bad.path).read_bytes()
+    Path(bad.path).write_bytes(data[: len(data) // 2])  # truncated: no central directory
+    with pytest.raises(RuntimeError):
+        ingest.load_frame_store_native([good, bad], kp_dir, require_kp=False)
+    junk = tmp_path / "junk.npz"
+    junk.write_bytes(b"PK\x03\x04 not really a zip")
+    with pytest.raises(RuntimeError):
+        ingest.load_frame_store_native([VideoItem("Unknown", "junk.npz", str(junk), 1, 64)], None, False)
+    # a keypoints.npy that is not [T', 120] float
+    k = _write(tmp_path, "k", 32, seed=8)
+    np.save(tmp_path / "generated_kps" / "k" / "keypoints.npy", np.zeros((32, 7), np.float32))
+    with pytest.raises(RuntimeError):
+        ingest.load_frame_store_native([k], kp_dir, require_kp=True)
+    a = ingest.load_frame_store_native([good, k], kp_dir, require_kp=False)
+    assert a.videos[1, 3] == 0 and a.videos[0, 3] == 32
+
+
+def test_sidecar_round_trip(tmp_path):
+    kp_dir = str(tmp_path / "generated_kps")
+    items = [_write(tmp_path, f"s{i}", 32 + 8 * i, kp_len=30 + i, seed=10 + i) for i in range(5)]
+    a = ingest.load_frame_store_native(items, kp_dir, require_kp=True)
+    p = str(tmp_path / "store.vgefs")
+    ingest.save_sidecar(a, p)
+    b = ingest.load_sidecar(p, pinned=False)
+    assert_same(a, b)
+    assert os.path.getsize(p) % 4096 != 1  # written
+    with open(p, "r+b") as f:
+        f.write(b"XXXX")
+    with pytest.raises(RuntimeError):
+        ingest.load_sidecar(p, pinned=False)

@@ -8,7 +8,7 @@ REPO = Path(__file__).resolve().parent.parent
 
 
 def declared():
-    txt = (REPO / "include" / "vge.h").read_text()
+    txt = "\n".join(h.read_text() for h in sorted((REPO / "include").glob("*.h")))
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
     return sorted(set(re.findall(r"\b(vge_[a-z0-9_]+)\s*\(", txt)))
 

@@ -10,7 +10,7 @@ make -s ARCH=gfx950
 HIPCC="/opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950"
 link() {
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$1/libvge.so" build/vge_featurize.o \
-    build/vge_encoder.o "$1/x3.o" "$1/tx.o" build/vge_score.o build/vge_api.o
+    build/vge_encoder.o "$1/x3.o" "$1/tx.o" build/vge_score.o build/vge_api.o build/vge_ingest.o -lz -lpthread
 }
 for v in "$@"; do
   mkdir -p build/abl$v
@@ -22,3 +22,7 @@ mkdir -p build/trace
 $HIPCC -DVGE_TRACE -c vge_encoder_x3.hip -o build/trace/x3.o
 $HIPCC -DVGE_TRACE -c vge_transformer_x3.hip -o build/trace/tx.o
 link build/trace
+mkdir -p build/trace2  # conv stamps of round 2 (the pair units at 256 windows)
+$HIPCC -DVGE_TRACE -DVGE_TRACE_ROUND=2 -c vge_encoder_x3.hip -o build/trace2/x3.o
+cp build/trace/tx.o build/trace2/tx.o
+link build/trace2

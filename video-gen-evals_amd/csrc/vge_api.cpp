@@ -37,6 +37,7 @@ struct EncDescX3Host {
   const _Float16* stem; const _Float16* conv; const _Float16* proj; const float* gn_w; const float* gn_b;
   const float* cs;
   int in_col, d_in, n_stem_panels, pad;
+  float gn_gmax[4], gn_bmax[4];  // max |gamma|, max |beta| per GroupNorm
 };
 struct GemmArgsX3Host {
   const float* A; int lda; const _Float16* W; float* out; int ldo; int M, K, N;
@@ -525,9 +526,20 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
   if (x3) {
     std::vector<vge::EncDescX3Host> descs(10);
     for (int e = 0; e < 10; ++e)
+    {
       descs[e] = vge::EncDescX3Host{hb + eoff[e].stem.off, hb + eoff[e].conv.off, hb + eoff[e].proj.off,
                                     wb + eoff[e].gnw, wb + eoff[e].gnb, wb + eoff[e].stem.cs,  // [10][256] scales
-                                    eoff[e].in_col, eoff[e].d_in, eoff[e].P, 0};
+                                    eoff[e].in_col, eoff[e].d_in, eoff[e].P, 0, {}, {}};
+      for (int b = 0; b < 4; ++b) {
+        float gm = 0.f, bm = 0.f;
+        for (int c = 0; c < 256; ++c) {
+          gm = std::max(gm, std::fabs(pk[eoff[e].gnw + b * 256 + c]));
+          bm = std::max(bm, std::fabs(pk[eoff[e].gnb + b * 256 + c]));
+        }
+        descs[e].gn_gmax[b] = gm;
+        descs[e].gn_bmax[b] = bm;
+      }
+    }
     he = hipMalloc(&enc->d_encs, sizeof(vge::EncDescX3Host) * 10);
     if (he == hipSuccess) he = hipMemcpy(enc->d_encs, descs.data(), sizeof(vge::EncDescX3Host) * 10, hipMemcpyHostToDevice);
   } else {

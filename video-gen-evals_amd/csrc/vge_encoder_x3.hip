@@ -28,11 +28,14 @@
 #include <cstring>
 
 
+#ifndef VGE_TRACE_ROUND
+#define VGE_TRACE_ROUND 0  // VGE_TRACE builds stamp the units of this round of the persistent schedule
+#endif
 #ifdef VGE_TRACE  // timing-only builds (tools/trace_encoder.py): s_memtime stamps of every wave of blocks 0..63
 __device__ long long g_vge_trace[64 * 8 * 32];
 #define STAMP(k)                                                                                        \
   do {                                                                                                  \
-    if (blockIdx.x < 64 && (threadIdx.x & 63) == 0)                                                     \
+    if (tr_on && blockIdx.x < 64 && (threadIdx.x & 63) == 0)                                            \
       g_vge_trace[(blockIdx.x * 8 + (threadIdx.x >> 6)) * 32 + (k)] = __builtin_amdgcn_s_memtime();     \
   } while (0)
 #else
@@ -52,6 +55,7 @@ struct EncDescX3 {
   const float* gn_b;     // [4][256]
   const float* cs;       // [10][256] weight column scales: stem, conv 0..7, proj
   int in_col, d_in, n_stem_panels, pad;
+  float gn_gmax[4], gn_bmax[4];  // max |gamma|, max |beta| of each GroupNorm (split-exponent bounds)
 };
 
 // One workgroup = one encoder x W windows (32 W rows), 8 waves (two per SIMD); wave w owns output columns
@@ -59,7 +63,7 @@ struct EncDescX3 {
 constexpr int CONV_WAVES = 8;
 template <int W>
 constexpr int conv_lds_bytes() {
-  return 2 * (32 * W + 1) * XSB + (4 * W * CONV_WAVES + 2 * 32 * W) * 4;
+  return 2 * (32 * W + 1) * XSB + (6 * W * CONV_WAVES + 2 * 32 * W) * 4;
 }
 
 // blocks [0, n_quad) take 4 windows, the rest 2: quads stream each weight byte for twice the rows, pairs
@@ -67,12 +71,12 @@ constexpr int conv_lds_bytes() {
 template <int W>
 __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feats, int n_windows, int win0,
                                                   const EncDescX3& ed, int e, float* __restrict__ enc_out,
-                                                  char* lds_raw) {
+                                                  char* lds_raw, [[maybe_unused]] bool tr_on) {
   constexpr int R = W, N = 1, ROWS = 32 * W, XROWS = ROWS + 1;
   _Float16* Xh = reinterpret_cast<_Float16*>(lds_raw);                   // [XROWS][XS]
   _Float16* Xl = Xh + XROWS * XS;                                        // [XROWS][XS]
-  float* red = reinterpret_cast<float*>(lds_raw + 2 * XROWS * XSB);      // [4 slots][W][waves] partials
-  int* rexp = reinterpret_cast<int*>(red + 4 * W * CONV_WAVES);          // [2][ROWS] stem row exponents
+  float* red = reinterpret_cast<float*>(lds_raw + 2 * XROWS * XSB);      // [6 slots][W][waves] partials
+  int* rexp = reinterpret_cast<int*>(red + 6 * W * CONV_WAVES);          // [2][ROWS] stem row exponents
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -108,19 +112,64 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
     }
   };
 
-  // Store the next conv's input as window * 2^-ex[t] (exact), the window's largest |value| in [2^8, 2^9);
-  // the consumer multiplies its accumulators back by 2^ex[t].  Caller guarantees X is no longer read.
-  auto store_x = [&](const floatx16 (&v)[R][N], int (&ex)[R]) {
-    float m[R], mm[R];
+  // sum of a, max of b and of c per window in one barrier (slots 0, 4, 5)
+  auto block_reduce3 = [&](const float (&a)[R], const float (&b)[R], const float (&c)[R], float (&oa)[R],
+                           float (&ob)[R], float (&oc)[R]) {
 #pragma unroll
     for (int t = 0; t < R; ++t) {
-      m[t] = 0.f;
-#pragma unroll
-      for (int n = 0; n < N; ++n)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) m[t] = fmaxf(m[t], fabsf(v[t][n][r]));
+      const float wa = wave_sum_last(a[t]), wb = wave_max_last(b[t]), wc = wave_max_last(c[t]);
+      if (lane == 63) {
+        red[(0 * R + t) * CONV_WAVES + wave] = wa;
+        red[(4 * R + t) * CONV_WAVES + wave] = wb;
+        red[(5 * R + t) * CONV_WAVES + wave] = wc;
+      }
     }
-    block_reduce(m, 3, true, mm);
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+      const float* pa = red + (0 * R + t) * CONV_WAVES;
+      const float* pb = red + (4 * R + t) * CONV_WAVES;
+      const float* pc = red + (5 * R + t) * CONV_WAVES;
+      float x = pa[0], y = pb[0], z = pc[0];
+#pragma unroll
+      for (int w = 1; w < CONV_WAVES; ++w) {
+        x += pa[w];
+        y = fmaxf(y, pb[w]);
+        z = fmaxf(z, pc[w]);
+      }
+      oa[t] = x;
+      ob[t] = y;
+      oc[t] = z;
+    }
+  };
+
+  // Store the next conv's input as window * 2^-ex[t] (exact), the window's largest |value| in [2^8, 2^9)
+  // -- from a block-wide max, or, when `bound` is given, from that per-window upper bound (a few times the
+  // max at most: the split stays exact to 2^-22 relative) -- the consumer multiplies its accumulators
+  // back by 2^ex[t].  The block-wide max's barrier orders the writes after every wave's reads of X; with
+  // a bound the caller has passed such a barrier since the last stream.
+  auto store_x = [&](const floatx16 (&v)[R][N], int (&ex)[R], const float* bound) {
+    float mm[R];
+    if (bound) {
+#pragma unroll
+      for (int t = 0; t < R; ++t) mm[t] = bound[t];
+    } else {
+      float m[R];
+#pragma unroll
+      for (int t = 0; t < R; ++t) {
+        m[t] = 0.f;
+#pragma unroll
+        for (int n = 0; n < N; ++n)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) m[t] = fmaxf(m[t], fabsf(v[t][n][r]));
+      }
+#if !(VGE_ABL & 512)
+      block_reduce(m, 3, true, mm);
+#else
+#pragma unroll
+      for (int t = 0; t < R; ++t) mm[t] = m[t];  // timing ablation: no block-wide max (wrong results)
+#endif
+    }
 #pragma unroll
     for (int t = 0; t < R; ++t) {
       ex[t] = fp16_range_exp(mm[t]);
@@ -132,15 +181,17 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
         char* bh = reinterpret_cast<char*>(Xh) + ((t * 32 + 4 * h) * XS + col0 + 32 * n) * 2;
         char* bl = bh + XROWS * XSB;
 #pragma unroll
-        for (int r = 0; r < 16; r += 2) {
+        for (int r = 0; r < 16; r += 2) {  // two rows per packed conversion (v_cvt_pk_f16_f32)
           const floatx2 y = (floatx2){v[t][n][r], v[t][n][r + 1]} * sc;
-          const _Float16 h0 = (_Float16)y.x, h1 = (_Float16)y.y;
-          const floatx2 lo = y - (floatx2){(float)h0, (float)h1};
+          const half2v hi = __builtin_convertvector(y, half2v);
+          const half2v lo = __builtin_convertvector(y - __builtin_convertvector(hi, floatx2), half2v);
           const int off = ((r & 3) + 8 * (r >> 2)) * XSB;  // rows r and r + 1 of the tile are adjacent
-          *reinterpret_cast<_Float16*>(bh + off) = h0;
-          *reinterpret_cast<_Float16*>(bh + off + XSB) = h1;
-          *reinterpret_cast<_Float16*>(bl + off) = (_Float16)lo.x;
-          *reinterpret_cast<_Float16*>(bl + off + XSB) = (_Float16)lo.y;
+          *reinterpret_cast<_Float16*>(bh + off) = hi[0];
+          *reinterpret_cast<_Float16*>(bh + off + XSB) = hi[1];
+#if !(VGE_ABL & 256)  // timing ablation: hi plane only (wrong results)
+          *reinterpret_cast<_Float16*>(bl + off) = lo[0];
+          *reinterpret_cast<_Float16*>(bl + off + XSB) = lo[1];
+#endif
         }
       }
     }
@@ -224,7 +275,7 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
   }
   STAMP(2);
   int xexp[R];
-  store_x(res, xexp);
+  store_x(res, xexp, nullptr);
   __syncthreads();
   STAMP(3);
 
@@ -277,12 +328,26 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
         }
       }
       STAMP(22 + blk * 2 + cv);
+      float gbound[R];  // cv == 1: a bound on each window's |GroupNorm output| for the split exponent
       if (cv == 1) {
-        // GroupNorm(1, 256) per window over its 32 x 256 values, spread over the 8 waves
-        float s[R], mean[R], q[R], var[R];
+        // GroupNorm(1, 256) per window over its 32 x 256 values, spread over the 8 waves; the window's max
+        // and min ride along with the sum (one barrier) and bound the normalised output
+        float s[R], mean[R], q[R], var[R], mx[R], mn[R], wmx[R], wmn[R];
 #pragma unroll
-        for (int t = 0; t < R; ++t) s[t] = s2[t].x + s2[t].y;
-        block_reduce(s, 0, false, mean);
+        for (int t = 0; t < R; ++t) {
+          s[t] = s2[t].x + s2[t].y;
+          float a = v[t][0][0], b = v[t][0][0];
+#pragma unroll
+          for (int n = 0; n < N; ++n)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              a = fmaxf(a, v[t][n][r]);
+              b = fminf(b, v[t][n][r]);
+            }
+          mx[t] = a;
+          mn[t] = -b;
+        }
+        block_reduce3(s, mx, mn, mean, wmx, wmn);
 #pragma unroll
         for (int t = 0; t < R; ++t) {
           mean[t] *= 1.0f / 8192.0f;
@@ -297,6 +362,12 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
           q[t] = q2.x + q2.y;
         }
         block_reduce(q, 1, false, var);
+#pragma unroll
+        for (int t = 0; t < R; ++t) {
+          const float rstd = 1.0f / sqrtf(var[t] * (1.0f / 8192.0f) + 1e-5f);
+          const float dev = fmaxf(wmx[t] - mean[t], mean[t] + wmn[t]);  // max |v - mean| over the window
+          gbound[t] = (dev * rstd * ed.gn_gmax[blk] + ed.gn_bmax[blk]) * 1.0001f;  // margin for rounding
+        }
 #pragma unroll
         for (int n = 0; n < N; ++n) {
           const float gw = ed.gn_w[blk * 256 + col0 + 32 * n], gb = ed.gn_b[blk * 256 + col0 + 32 * n];
@@ -314,8 +385,9 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
           }
         }
       }
-      __syncthreads();  // every wave is done reading X (this conv's A operand)
-      store_x(v, xexp);
+      // cv == 0: store_x's block-wide max is the barrier after every wave's reads of X (this conv's A
+      // operand); cv == 1: the GroupNorm reductions are
+      store_x(v, xexp, cv == 1 ? gbound : nullptr);
       __syncthreads();
       STAMP(5 + (blk * 2 + cv) * 2);
     }
@@ -340,7 +412,7 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
   }
   STAMP(21);
 #ifdef VGE_TRACE
-  if (blockIdx.x < 64 && threadIdx.x == 0) g_vge_trace[blockIdx.x * 8 * 32 + 31] = e;
+  if (tr_on && blockIdx.x < 64 && threadIdx.x == 0) g_vge_trace[blockIdx.x * 8 * 32 + 31] = e;
 #endif
 }
 
@@ -372,14 +444,14 @@ __global__ void __launch_bounds__(512, 1) conv_encoder_x3_kernel(const float* __
       const int big = cs.qr * (cs.qa + 1);
       const int e = u < big ? u / (cs.qa + 1) : cs.qr + (u - big) / cs.qa;
       const int j = u < big ? u % (cs.qa + 1) : (u - big) % cs.qa;
-      conv_encoder_body<4>(feats, n, 4 * j, encs[e], e, enc_out, lds_raw);
+      conv_encoder_body<4>(feats, n, 4 * j, encs[e], e, enc_out, lds_raw, round == VGE_TRACE_ROUND);
     } else {
       const int v = u - cs.Q;
       const int big = cs.qr * p_big;
       const int e = v < big ? v / p_big : cs.qr + (v - big) / p_small;
       const int j = v < big ? v % p_big : (v - big) % p_small;
       const int q_e = cs.qa + (e < cs.qr);
-      conv_encoder_body<2>(feats, n, 4 * q_e + 2 * j, encs[e], e, enc_out, lds_raw);
+      conv_encoder_body<2>(feats, n, 4 * q_e + 2 * j, encs[e], e, enc_out, lds_raw, round == VGE_TRACE_ROUND);
     }
   }
 }
@@ -719,6 +791,7 @@ struct EncDescX3Host {
   const _Float16* stem; const _Float16* conv; const _Float16* proj; const float* gn_w; const float* gn_b;
   const float* cs;
   int in_col, d_in, n_stem_panels, pad;
+  float gn_gmax[4], gn_bmax[4];
 };
 static_assert(sizeof(EncDescX3Host) == sizeof(EncDescX3), "EncDescX3 layout");
 

@@ -67,8 +67,6 @@ constexpr int TX_LDS_BYTES = AP_BYTES + U_BYTES + RED_FLOATS * 4;
 static_assert(2 * AROWS * XSB <= U_BYTES, "hidden planes fit the union");
 static_assert(TX_LDS_BYTES <= 160 * 1024, "LDS");
 
-typedef _Float16 half2v __attribute__((ext_vector_type(2)));
-
 struct AFragT {  // one chunk's A operand: the 32 frame rows (MFMA) and the CLS row (VALU dot products)
   half8 h, l, h0, l0;
 };

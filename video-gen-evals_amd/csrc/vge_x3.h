@@ -13,6 +13,7 @@ namespace {
 
 typedef _Float16 half8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
 
 constexpr int XS = 264;              // fp16 per LDS activation row (256 + 8 pad: conflict-free b128 reads)
 constexpr int XSB = XS * 2;          // bytes per activation row

@@ -213,8 +213,8 @@ def pack_frame_store(clips: Sequence[dict], names: Sequence[str], classes: Seque
     off = koff = 0
     for i, c in enumerate(clips):
         T = lens[i]
-        st.pose[off:off + T] = np.asarray(c["pose"], np.float32).reshape(T, -1)
-        st.gori[off:off + T] = np.asarray(c["global_orient"], np.float32).reshape(T, -1)
+        st.pose[off:off + T] = np.asarray(c["pose"], np.float32).reshape(T, 207)
+        st.gori[off:off + T] = np.asarray(c["global_orient"], np.float32).reshape(T, 9)
         st.betas[off:off + T] = np.asarray(c["betas"], np.float32)
         st.vit[off:off + T] = np.asarray(c["vit"], np.float32)
         if klens[i]:

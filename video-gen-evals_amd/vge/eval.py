@@ -11,8 +11,8 @@ Same function names, argument meaning and outputs as the reference:
   compute_temporal_coherence_scores   eval.py:209-226
   compute_spearman_correlation        eval.py:297-347
   run_eval                            eval.py:350-454 (writes video_scores.json)
-Per-frame features are decoded on the host (npz/zlib) into a frame store that lives in HBM; every
-numeric step after that runs in the HIP kernels of libvge.so.
+Per-frame features are decoded on the host (npz/zlib, libvge's native multithreaded decoder) into a
+frame store that lives in HBM; every numeric step after that runs in the HIP kernels of libvge.so.
 """
 from __future__ import annotations
 
@@ -35,8 +35,17 @@ from .data import (ACTION_CLASSES, FrameStore, NpzVideoDataset, VideoItem, _cano
 # ----------------------------------------------------------------------------- loading
 
 def load_frame_store(items: Sequence[VideoItem], keypoint_dir: Optional[str], require_kp: bool,
-                     workers: int = 8) -> FrameStore:
-    """Decode the npz + keypoints.npy of `items` (thread pool: zlib releases the GIL) and pack them."""
+                     workers: int = 0) -> FrameStore:
+    """Decode the npz + keypoints.npy of `items` into a frame store (pinned host memory when a GPU is
+    present): libvge's native multithreaded decoder (vge/ingest.py, include/vge_ingest.h)."""
+    from .ingest import load_frame_store_native
+    return load_frame_store_native(items, keypoint_dir, require_kp, threads=workers)
+
+
+def load_frame_store_numpy(items: Sequence[VideoItem], keypoint_dir: Optional[str], require_kp: bool,
+                           workers: int = 8) -> FrameStore:
+    """The np.load reader (the reference's own, utils.py:383-424) in a thread pool: kept as the ingest
+    baseline of tools/ingest_bench.py."""
     with ThreadPoolExecutor(max_workers=max(1, workers)) as ex:
         clips = list(ex.map(lambda it: load_clip(it, keypoint_dir, require_kp), items))
     return pack_frame_store(clips, [it.name for it in items], [it.cls for it in items])

@@ -16,7 +16,7 @@ STATUS = {0: "VGE_OK", 1: "VGE_ERR_ARG", 2: "VGE_ERR_HIP", 3: "VGE_ERR_MISSING_W
 EXPORTS = ["vge_featurize", "vge_stats_workspace_bytes", "vge_stats_accumulate", "vge_stats_finalize",
            "vge_encoder_create", "vge_encoder_reserve", "vge_encoder_destroy", "vge_encode", "vge_tc_windows",
            "vge_score_videos", "vge_centroid_accumulate", "vge_centroid_finalize", "vge_last_error", "vge_version",
-           "vge_encoder_profile_begin", "vge_encoder_profile_read"]
+           "vge_encoder_profile_begin", "vge_encoder_profile_read", "vge_ingest_probe", "vge_ingest_decode"]
 
 
 class VgeError(RuntimeError):
@@ -30,6 +30,13 @@ class Dims(C.Structure):
 
 class TensorView(C.Structure):
     _fields_ = [("name", C.c_char_p), ("data", C.c_void_p), ("ndim", C.c_int), ("shape", C.c_int64 * 4)]
+
+
+class ClipInfo(C.Structure):  # include/vge_ingest.h vge_clip_info
+    _fields_ = [("n_frames", C.c_int32), ("vit_dim", C.c_int32), ("kp_frames", C.c_int32), ("status", C.c_int32)]
+
+
+INGEST_STATUS = {0: "OK", 1: "ERR_ARG", 7: "ERR_IO", 8: "ERR_SHAPE", 9: "ERR_KP"}
 
 
 class FrameStoreC(C.Structure):
@@ -67,6 +74,9 @@ def load() -> C.CDLL:
         "vge_encoder_profile_read": [vp, C.POINTER(C.c_double), C.POINTER(C.c_int)],
         "vge_last_error": [],
         "vge_version": [],
+        "vge_ingest_probe": [C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), i32, i32, C.POINTER(ClipInfo)],
+        "vge_ingest_decode": [C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), i32, i32, vp, i32, vp, vp, vp, vp, vp,
+                              vp],
     }
     for name, args in sig.items():
         f = getattr(lib, name)
