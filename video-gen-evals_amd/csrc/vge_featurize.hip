@@ -206,6 +206,75 @@ __device__ __forceinline__ RowSrc row_src(int mode, int start, int L, int t) {
   return r;
 }
 
+// ---- (a) vit raw + cosine delta (utils.py:142-147): 8 rows per wave, 16 floats per lane; the next row's
+// loads are issued before the current row is finished, and each lane's z-norm divisors are inverted once
+// (x - mean) * (1 / (std + 1e-6)) -- within an ulp of the division)
+__device__ __forceinline__ void featurize_vit(const float* __restrict__ vit, int foff, int L, int mode, int mesh_start,
+                                              int mcount, const float* __restrict__ mean,
+                                              const float* __restrict__ stdv, float* __restrict__ out, int wave,
+                                              int lane) {
+  float mr[16], ir[16], md[16], id[16];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = k * 256 + lane * 4 + q;
+      mr[k * 4 + q] = mean ? mean[C_VIT_RAW + c] : 0.f;
+      ir[k * 4 + q] = mean ? 1.0f / (stdv[C_VIT_RAW + c] + 1e-6f) : 1.f;
+      md[k * 4 + q] = mean ? mean[C_VIT_DIFF + c] : 0.f;
+      id[k * 4 + q] = mean ? 1.0f / (stdv[C_VIT_DIFF + c] + 1e-6f) : 1.f;
+    }
+  auto issue = [&](int f, floatx4 (&x)[4]) {
+    const floatx4* p = reinterpret_cast<const floatx4*>(vit + (size_t)(foff + f) * 1024);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = p[k * 64 + lane];
+  };
+  auto finish = [&](const floatx4 (&x)[4], float (&v)[16], float (&raw)[16]) {
+    float ss = 0.f;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        raw[k * 4 + q] = x[k][q];
+        ss += x[k][q] * x[k][q];
+      }
+    const float n = fmaxf(sqrtf(wave_sum(ss)), 1e-12f);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = raw[i] / n;
+  };
+  const int t0 = wave * 8;
+  if (t0 >= mcount) return;
+  const int t1 = min(t0 + 8, mcount);
+  float vprev[16], raw[16], vcur[16];
+  floatx4 xa[4], xb[4];
+  issue(row_src(mode, mesh_start, L, t0).prv, xa);
+  issue(row_src(mode, mesh_start, L, t0).src, xb);
+  finish(xa, vprev, raw);
+  for (int t = t0; t < t1; ++t) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) xa[k] = xb[k];
+    if (t + 1 < t1) issue(row_src(mode, mesh_start, L, t + 1).src, xb);  // in flight during this row
+    finish(xa, vcur, raw);
+    float* orow = out + (size_t)t * VGE_FD;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      floatx4 o, d4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int i = k * 4 + q;
+        o[q] = (raw[i] - mr[i]) * ir[i];
+        d4[q] = ((vcur[i] - vprev[i]) - md[i]) * id[i];
+      }
+      const int c = k * 256 + lane * 4;
+      *reinterpret_cast<floatx4*>(orow + C_VIT_RAW + c) = o;
+      *reinterpret_cast<floatx2*>(orow + C_VIT_DIFF + c) = (floatx2){d4[0], d4[1]};
+      *reinterpret_cast<floatx2*>(orow + C_VIT_DIFF + c + 2) = (floatx2){d4[2], d4[3]};
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) vprev[i] = vcur[i];
+  }
+}
+
 // ---------------------------------------------------------------- the tile kernel
 __global__ void __launch_bounds__(256) featurize_tiles_kernel(
     const float* __restrict__ pose, const float* __restrict__ gori, const float* __restrict__ betas,
@@ -213,6 +282,7 @@ __global__ void __launch_bounds__(256) featurize_tiles_kernel(
     const TileDesc* __restrict__ tiles, const int* __restrict__ windows, const float* __restrict__ mean,
     const float* __restrict__ stdv, float* __restrict__ feats) {
   __shared__ float pn[33][120];  // normalised keypoints: slot 0 = prev of row 0, slot t+1 = row t
+  __shared__ float kR[32][4];    // per row: H = X_{t-1}^T X_t, then the Procrustes rotation R (row-major)
   TileDesc td;
   if (windows != nullptr) {  // window mode straight from the {video, start} list
     const int v = windows[2 * blockIdx.x], st = windows[2 * blockIdx.x + 1];
@@ -228,6 +298,10 @@ __global__ void __launch_bounds__(256) featurize_tiles_kernel(
   const int kcount = (mode == 0) ? (Lk > 0 ? 32 : 0) : td.kp_count;
   float* out = feats + (size_t)td.out_row * VGE_FD;
 
+  if (blockIdx.y == 0) {  // the vit columns (3/4 of the bytes) on one workgroup, the rest on another
+    featurize_vit(vit, foff, L, mode, td.mesh_start, mcount, mean, stdv, out, wave, lane);
+    return;
+  }
   // ---- (d1) keypoints: centre + Frobenius-normalise every needed frame (utils.py:191-196)
   for (int slot = wave; slot < 33; slot += 4) {
     int t = slot - 1;
@@ -248,67 +322,6 @@ __global__ void __launch_bounds__(256) featurize_tiles_kernel(
     if (lane < 60) {
       pn[slot][2 * lane] = cx / s;
       pn[slot][2 * lane + 1] = cy / s;
-    }
-  }
-
-  // ---- (a) vit raw + cosine delta (utils.py:142-147): 8 rows per wave, 16 floats per lane
-  {
-    float mr[16], sr[16], md[16], sd[16];
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        int c = k * 256 + lane * 4 + q;
-        mr[k * 4 + q] = mean ? mean[C_VIT_RAW + c] : 0.f;
-        sr[k * 4 + q] = mean ? stdv[C_VIT_RAW + c] : 0.f;
-        md[k * 4 + q] = mean ? mean[C_VIT_DIFF + c] : 0.f;
-        sd[k * 4 + q] = mean ? stdv[C_VIT_DIFF + c] : 0.f;
-      }
-    auto load_norm = [&](int f, float v[16], float raw[16]) {
-      const floatx4* p = reinterpret_cast<const floatx4*>(vit + (size_t)(foff + f) * 1024);
-      float ss = 0.f;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        floatx4 x = p[k * 64 + lane];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) { raw[k * 4 + q] = x[q]; ss += x[q] * x[q]; }
-      }
-      float n = fmaxf(sqrtf(wave_sum(ss)), 1e-12f);
-#pragma unroll
-      for (int i = 0; i < 16; ++i) v[i] = raw[i] / n;
-    };
-    float vprev[16], raw[16], vcur[16];
-    int t0 = wave * 8;
-    if (t0 < mcount) {
-      RowSrc r0 = row_src(mode, td.mesh_start, L, t0);
-      load_norm(r0.prv, vprev, raw);
-      for (int t = t0; t < t0 + 8 && t < mcount; ++t) {
-        RowSrc rs = row_src(mode, td.mesh_start, L, t);
-        load_norm(rs.src, vcur, raw);
-        float* orow = out + (size_t)t * VGE_FD;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          floatx4 o;
-          floatx2 d0, d1;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            int i = k * 4 + q;
-            float r = raw[i], d = vcur[i] - vprev[i];
-            if (mean) {
-              r = (r - mr[i]) / (sr[i] + 1e-6f);
-              d = (d - md[i]) / (sd[i] + 1e-6f);
-            }
-            o[q] = r;
-            if (q < 2) d0[q] = d; else d1[q - 2] = d;
-          }
-          int c = k * 256 + lane * 4;
-          *reinterpret_cast<floatx4*>(orow + C_VIT_RAW + c) = o;
-          *reinterpret_cast<floatx2*>(orow + C_VIT_DIFF + c) = d0;
-          *reinterpret_cast<floatx2*>(orow + C_VIT_DIFF + c + 2) = d1;
-        }
-#pragma unroll
-        for (int i = 0; i < 16; ++i) vprev[i] = vcur[i];
-      }
     }
   }
 
@@ -349,41 +362,59 @@ __global__ void __launch_bounds__(256) featurize_tiles_kernel(
 
   __syncthreads();  // pn[] complete
 
-  // ---- (d2) keypoints raw + Procrustes velocity (utils.py:177-217)
+  // ---- (d2) keypoints raw + Procrustes velocity (utils.py:177-217): H of every row by wave sums, then the
+  // 2x2 SVDs of all rows in parallel on the lanes of wave 0 (one dependent LAPACK chain instead of eight
+  // per wave), then the deltas
   for (int t = wave; t < kcount; t += 4) {
     RowSrc rs = row_src(mode, td.kp_start, Lk, t);
     float* orow = out + (size_t)t * VGE_FD;
-    // raw
     for (int c = lane; c < 120; c += 64)
       orow[C_KP_RAW + c] = znorm(kp[(size_t)(koff + rs.src) * 120 + c], mean, stdv, C_KP_RAW + c);
-    float dx = 0.f, dy = 0.f;
     if (!rs.first) {
       float x0 = 0.f, x1 = 0.f, y0 = 0.f, y1 = 0.f;
       if (lane < 60) {
         x0 = pn[t][2 * lane]; x1 = pn[t][2 * lane + 1];
         y0 = pn[t + 1][2 * lane]; y1 = pn[t + 1][2 * lane + 1];
       }
-      float h00 = wave_sum(x0 * y0), h01 = wave_sum(x0 * y1);
-      float h10 = wave_sum(x1 * y0), h11 = wave_sum(x1 * y1);
-      float U[2][2], Vh[2][2];
-      sgesdd_2x2(h00, h01, h10, h11, U, Vh);
-      // R = Vh @ U^T
-      float R[2][2];
+      const float h00 = wave_sum(x0 * y0), h01 = wave_sum(x0 * y1);
+      const float h10 = wave_sum(x1 * y0), h11 = wave_sum(x1 * y1);
+      if (lane == 0) {
+        kR[t][0] = h00; kR[t][1] = h01; kR[t][2] = h10; kR[t][3] = h11;
+      }
+    }
+  }
+  __syncthreads();
+  if (wave == 0 && lane < kcount && !row_src(mode, td.kp_start, Lk, lane).first) {
+    const int t = lane;
+    float U[2][2], Vh[2][2];
+    sgesdd_2x2(kR[t][0], kR[t][1], kR[t][2], kR[t][3], U, Vh);
+    // R = Vh @ U^T; det < 0: flip Vh's last column and recompute
+    float R[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) R[i][j] = Vh[i][0] * U[j][0] + Vh[i][1] * U[j][1];
+    const float det = R[0][0] * R[1][1] - R[0][1] * R[1][0];
+    if (det < 0.0f) {
+      Vh[0][1] = -Vh[0][1];
+      Vh[1][1] = -Vh[1][1];
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j) R[i][j] = Vh[i][0] * U[j][0] + Vh[i][1] * U[j][1];
-      float det = R[0][0] * R[1][1] - R[0][1] * R[1][0];
-      if (det < 0.0f) {
-        Vh[0][1] = -Vh[0][1];
-        Vh[1][1] = -Vh[1][1];
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) R[i][j] = Vh[i][0] * U[j][0] + Vh[i][1] * U[j][1];
-      }
-      dx = y0 - (x0 * R[0][0] + x1 * R[1][0]);
-      dy = y1 - (x0 * R[0][1] + x1 * R[1][1]);
+    }
+    kR[t][0] = R[0][0]; kR[t][1] = R[0][1]; kR[t][2] = R[1][0]; kR[t][3] = R[1][1];
+  }
+  __syncthreads();
+  for (int t = wave; t < kcount; t += 4) {
+    RowSrc rs = row_src(mode, td.kp_start, Lk, t);
+    float* orow = out + (size_t)t * VGE_FD;
+    float dx = 0.f, dy = 0.f;
+    if (!rs.first && lane < 60) {
+      const float x0 = pn[t][2 * lane], x1 = pn[t][2 * lane + 1];
+      const float y0 = pn[t + 1][2 * lane], y1 = pn[t + 1][2 * lane + 1];
+      dx = y0 - (x0 * kR[t][0] + x1 * kR[t][2]);
+      dy = y1 - (x0 * kR[t][1] + x1 * kR[t][3]);
     }
     if (lane < 60) {
       orow[C_KP_DIFF + 2 * lane] = znorm(dx, mean, stdv, C_KP_DIFF + 2 * lane);
@@ -451,7 +482,7 @@ hipError_t launch_featurize_tiles(const float* pose, const float* gori, const fl
                                   const float* kp, const int* videos, const void* tiles, const int* windows,
                                   int n_tiles, const float* mean, const float* stdv, float* feats, hipStream_t s) {
   if (n_tiles <= 0) return hipSuccess;
-  hipLaunchKernelGGL(featurize_tiles_kernel, dim3(n_tiles), dim3(256), 0, s, pose, gori, betas, vit, kp, videos,
+  hipLaunchKernelGGL(featurize_tiles_kernel, dim3(n_tiles, 2), dim3(256), 0, s, pose, gori, betas, vit, kp, videos,
                      reinterpret_cast<const TileDesc*>(tiles), windows, mean, stdv, feats);
   return hipGetLastError();
 }
