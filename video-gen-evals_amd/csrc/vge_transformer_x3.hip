@@ -71,16 +71,6 @@ struct AFragT {  // one chunk's A operand: the 32 frame rows (MFMA) and the CLS 
   half8 h, l, h0, l0;
 };
 
-// x of lane l combined with x of lane l ^ 32 (v_permlane32_swap: no LDS round trip)
-__device__ __forceinline__ float halves_sum(float x) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
-}
-__device__ __forceinline__ float halves_max(float x) {
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-}
-
 // CLS row on the VALU: c += x . w over this lane's 8 k of the chunk, the same 3 products as the MFMAs
 __device__ __forceinline__ float cls_dot(float c, half8 xh, half8 xl, half8 wh, half8 wl) {
 #pragma unroll

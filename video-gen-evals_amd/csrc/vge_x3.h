@@ -27,6 +27,16 @@ __device__ __forceinline__ floatx16 mfma32(half8 a, half8 b, floatx16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
+// x of lane l combined with x of lane l ^ 32 (v_permlane32_swap: no LDS round trip)
+__device__ __forceinline__ float halves_sum(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float halves_max(float x) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
 __device__ __forceinline__ void split_store(_Float16* hi, _Float16* lo, float v) {
   const _Float16 h = (_Float16)v;
   *hi = h;
