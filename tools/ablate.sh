@@ -9,14 +9,15 @@ cd "$(dirname "$0")/../video-gen-evals_amd/csrc"
 make -s ARCH=gfx950
 HIPCC="/opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950"
 link() {
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$1/libvge.so" build/vge_featurize.o \
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$1/libvge.so" "${FEAT:-build/vge_featurize.o}" \
     build/vge_encoder.o "$1/x3.o" "$1/tx.o" build/vge_score.o build/vge_api.o build/vge_ingest.o -lz -lpthread
 }
 for v in "$@"; do
   mkdir -p build/abl$v
   $HIPCC -DVGE_ABL=$v -c vge_encoder_x3.hip -o build/abl$v/x3.o
   $HIPCC -DVGE_ABL=$v -c vge_transformer_x3.hip -o build/abl$v/tx.o
-  link build/abl$v
+  $HIPCC -DVGE_ABL=$v -c vge_featurize.hip -o build/abl$v/feat.o
+  FEAT=build/abl$v/feat.o link build/abl$v
 done
 mkdir -p build/trace
 $HIPCC -DVGE_TRACE -c vge_encoder_x3.hip -o build/trace/x3.o

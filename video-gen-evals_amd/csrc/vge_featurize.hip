@@ -298,8 +298,52 @@ __global__ void __launch_bounds__(256) featurize_tiles_kernel(
   const int kcount = (mode == 0) ? (Lk > 0 ? 32 : 0) : td.kp_count;
   float* out = feats + (size_t)td.out_row * VGE_FD;
 
-  if (blockIdx.y == 0) {  // the vit columns (3/4 of the bytes) on one workgroup, the rest on another
+  // three workgroups per tile: vit columns (3/4 of the bytes), rotations + betas, keypoints
+  if (blockIdx.y == 0) {
+#if !(defined(VGE_ABL) && (VGE_ABL & 2048))
     featurize_vit(vit, foff, L, mode, td.mesh_start, mcount, mean, stdv, out, wave, lane);
+#endif
+    return;
+  }
+#if defined(VGE_ABL) && (VGE_ABL & 1024)
+  return;  // timing ablation: vit part only
+#endif
+  if (blockIdx.y == 1) {  // rotations + betas
+    // ---- (b) rotations: raw flattened rotmats + SO(3) log-map deltas (utils.py:165-174)
+    for (int it = tid; it < 32 * 24; it += 256) {
+      int t = it / 24, j = it % 24;
+      if (t >= mcount) continue;
+      RowSrc rs = row_src(mode, td.mesh_start, L, t);
+      const float* base = (j == 0) ? gori : pose;
+      int stride = (j == 0) ? 9 : 207, off = (j == 0) ? 0 : (j - 1) * 9;
+      const float* R = base + (size_t)(foff + rs.src) * stride + off;
+      const float* Rp = base + (size_t)(foff + rs.prv) * stride + off;
+      float Rl[9], Rpl[9];
+  #pragma unroll
+      for (int i = 0; i < 9; ++i) { Rl[i] = R[i]; Rpl[i] = Rp[i]; }
+      float w[3];
+      rot_delta(Rpl, Rl, w);
+      float* orow = out + (size_t)t * VGE_FD;
+      int craw = (j == 0) ? C_GORI_RAW : C_POSE_RAW + (j - 1) * 9;
+      int cdif = (j == 0) ? C_GORI_DIFF : C_POSE_DIFF + (j - 1) * 3;
+  #pragma unroll
+      for (int i = 0; i < 9; ++i) orow[craw + i] = znorm(Rl[i], mean, stdv, craw + i);
+  #pragma unroll
+      for (int i = 0; i < 3; ++i) orow[cdif + i] = znorm(w[i], mean, stdv, cdif + i);
+    }
+
+    // ---- (c) betas raw + first difference (utils.py:161-163)
+    for (int it = tid; it < 32 * 10; it += 256) {
+      int t = it / 10, i = it % 10;
+      if (t >= mcount) continue;
+      RowSrc rs = row_src(mode, td.mesh_start, L, t);
+      float b = betas[(size_t)(foff + rs.src) * 10 + i];
+      float bp = betas[(size_t)(foff + rs.prv) * 10 + i];
+      float* orow = out + (size_t)t * VGE_FD;
+      orow[C_BETA_RAW + i] = znorm(b, mean, stdv, C_BETA_RAW + i);
+      orow[C_BETA_DIFF + i] = znorm(b - bp, mean, stdv, C_BETA_DIFF + i);
+    }
+
     return;
   }
   // ---- (d1) keypoints: centre + Frobenius-normalise every needed frame (utils.py:191-196)
@@ -323,41 +367,6 @@ __global__ void __launch_bounds__(256) featurize_tiles_kernel(
       pn[slot][2 * lane] = cx / s;
       pn[slot][2 * lane + 1] = cy / s;
     }
-  }
-
-  // ---- (b) rotations: raw flattened rotmats + SO(3) log-map deltas (utils.py:165-174)
-  for (int it = tid; it < 32 * 24; it += 256) {
-    int t = it / 24, j = it % 24;
-    if (t >= mcount) continue;
-    RowSrc rs = row_src(mode, td.mesh_start, L, t);
-    const float* base = (j == 0) ? gori : pose;
-    int stride = (j == 0) ? 9 : 207, off = (j == 0) ? 0 : (j - 1) * 9;
-    const float* R = base + (size_t)(foff + rs.src) * stride + off;
-    const float* Rp = base + (size_t)(foff + rs.prv) * stride + off;
-    float Rl[9], Rpl[9];
-#pragma unroll
-    for (int i = 0; i < 9; ++i) { Rl[i] = R[i]; Rpl[i] = Rp[i]; }
-    float w[3];
-    rot_delta(Rpl, Rl, w);
-    float* orow = out + (size_t)t * VGE_FD;
-    int craw = (j == 0) ? C_GORI_RAW : C_POSE_RAW + (j - 1) * 9;
-    int cdif = (j == 0) ? C_GORI_DIFF : C_POSE_DIFF + (j - 1) * 3;
-#pragma unroll
-    for (int i = 0; i < 9; ++i) orow[craw + i] = znorm(Rl[i], mean, stdv, craw + i);
-#pragma unroll
-    for (int i = 0; i < 3; ++i) orow[cdif + i] = znorm(w[i], mean, stdv, cdif + i);
-  }
-
-  // ---- (c) betas raw + first difference (utils.py:161-163)
-  for (int it = tid; it < 32 * 10; it += 256) {
-    int t = it / 10, i = it % 10;
-    if (t >= mcount) continue;
-    RowSrc rs = row_src(mode, td.mesh_start, L, t);
-    float b = betas[(size_t)(foff + rs.src) * 10 + i];
-    float bp = betas[(size_t)(foff + rs.prv) * 10 + i];
-    float* orow = out + (size_t)t * VGE_FD;
-    orow[C_BETA_RAW + i] = znorm(b, mean, stdv, C_BETA_RAW + i);
-    orow[C_BETA_DIFF + i] = znorm(b - bp, mean, stdv, C_BETA_DIFF + i);
   }
 
   __syncthreads();  // pn[] complete
@@ -482,7 +491,7 @@ hipError_t launch_featurize_tiles(const float* pose, const float* gori, const fl
                                   const float* kp, const int* videos, const void* tiles, const int* windows,
                                   int n_tiles, const float* mean, const float* stdv, float* feats, hipStream_t s) {
   if (n_tiles <= 0) return hipSuccess;
-  hipLaunchKernelGGL(featurize_tiles_kernel, dim3(n_tiles, 2), dim3(256), 0, s, pose, gori, betas, vit, kp, videos,
+  hipLaunchKernelGGL(featurize_tiles_kernel, dim3(n_tiles, 3), dim3(256), 0, s, pose, gori, betas, vit, kp, videos,
                      reinterpret_cast<const TileDesc*>(tiles), windows, mean, stdv, feats);
   return hipGetLastError();
 }
