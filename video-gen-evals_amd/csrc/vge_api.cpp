@@ -216,6 +216,10 @@ struct vge_encoder {
         *h = nullptr;
 };
 
+namespace vge {
+void set_last_error(const std::string& msg) { g_err = msg; }  // vge_hmr.cpp
+}  // namespace vge
+
 extern "C" {
 
 const char* vge_last_error(void) { return g_err.c_str(); }

@@ -1,0 +1,637 @@
+// Per-frame mesh extractor (TokenHMR: ViT-H/16 backbone + SMPL token-decoder head) on gfx950.
+//
+// Reference: modifications/mesh_generator.py:119-171 runs TokenHMR on 256x256 person crops in batches of 8
+// and keeps pred_smpl_params {body_pose, global_orient, betas, token_out} (modifications/token_head.py:180-246);
+// extract_mesh.py:35-43 saves them as the npz arrays pose / global_orient / betas / vit that the scoring
+// path reads.  The backbone is HMR2's ViT-H/16 (256x192 input = columns 32..223 of the crop, patch 16,
+// padding 2, 16 x 12 tokens, embed 1280, 32 pre-norm blocks, 16 heads, MLP 5120, LayerNorm eps 1e-6).
+//
+// Kernels (all bf16 operands, f32 accumulation, residual stream kept in f32):
+//   gemm_bf16_kernel<EPI>  C = A W^T (+ epilogue) for every Linear / the patch-embed conv (as im2col GEMM):
+//                          256 x 256 x 64 tiles, 8 waves (2 M x 4 N, 128 x 64 per wave) on
+//                          v_mfma_f32_32x32x16_bf16, both operands staged HBM -> LDS by global_load_lds
+//                          (16 B per lane, double-buffered 128 KB), LDS image XOR-swizzled on the source
+//                          address so the fragment ds_read_b128 are conflict-free; XCD-grouped tile order.
+//   ln_bf16_kernel         LayerNorm f32 -> bf16 (one wave per row).
+//   patchify_kernel        uint8 RGB crop -> normalised, zero-padded im2col rows of the 16x16 patches.
+//   vit_attn_kernel        softmax(Q K^T / sqrt(hd)) V per (frame, head) on MFMA: S^T = K Q^T so a query's
+//                          192 scores are lane-local (+ the partner half via permlane32), P^T feeds the
+//                          PV MFMA straight from the accumulators.
+//   xattn1_kernel          the decoder's one-query cross-attention over the 192 context tokens.
+//   softmax_rows_kernel, readout_kernel (6D -> rotation matrix, mean-pose residuals), small helpers.
+#include "vge_common.h"
+
+namespace {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+// ------------------------------------------------------------------------------------------- GEMM
+constexpr int GB_M = 256, GB_N = 256, GB_K = 64;
+constexpr int GB_TILE = GB_M * GB_K * 2;  // 32 KB per operand tile
+constexpr int GB_LDS = 4 * GB_TILE;       // A0 B0 A1 B1
+
+enum GemmEpi { GE_BF16 = 0, GE_GELU_BF16 = 1, GE_RES_F32 = 2, GE_PE_F32 = 3, GE_F32 = 4 };
+
+struct GemmBf16Args {
+  const bf16* A;     // [M][lda]   rows of the activation
+  const bf16* W;     // [N][ldw]   nn.Linear weight (row n = output column n)
+  void* out;         // [M][ldo]   bf16 or f32
+  const float* bias; // [N] or null
+  const float* res;  // GE_RES_F32: [M][ldr] residual (may alias out)
+  const float* pos;  // GE_PE_F32: pos_embed [tokens + 1][N]
+  long lda, ldw, ldo, ldr;
+  int M, N, K, tokens;
+};
+
+// Stage a 256-row x 64-k operand tile: wave-instruction q (0..31) fills LDS bytes [1024 q, 1024 q + 1024) =
+// rows 8q .. 8q+7 (128 B each), lane L -> row 8q + L/8, physical 16-B chunk L%8.  The physical chunk p of row r
+// holds logical chunk p ^ ((r >> 1) & 7), so the source address is pre-swizzled and the LDS image stays
+// lane-linear (what global_load_lds requires).
+__device__ __forceinline__ void gb_stage(const bf16* __restrict__ X, long ld, int r0, int k0, char* tile, int wave,
+                                         int lane) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int q = wave * 4 + j;
+    const int row = 8 * q + (lane >> 3);
+    const int ch = (lane & 7) ^ ((row >> 1) & 7);
+    glds16(X + (size_t)(r0 + row) * ld + k0 + ch * 8, tile + q * 1024);
+  }
+}
+
+__device__ __forceinline__ int gb_xcd_remap(int b, int nblk) {  // bijective: each XCD takes a contiguous range
+  const int q8 = nblk >> 3, r8 = nblk & 7, x8 = b & 7;
+  return (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (b >> 3);
+}
+
+template <int EPI>
+__global__ void __launch_bounds__(512, 1) gemm_bf16_kernel(GemmBf16Args g) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int ntn = g.N / GB_N;
+  const int bid = gb_xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = bid / ntn, nt = bid % ntn;  // consecutive ids share the A row panel
+  const int m0 = mt * GB_M, n0 = nt * GB_N;
+  const int nk = g.K / GB_K;
+  const int h = lane >> 5;
+  const int swz = (lane >> 1) & 7;  // ((row >> 1) & 7) of every fragment row this lane reads
+  const int rowoff = (lane & 31) * 128;
+
+  floatx16 acc[4][2];
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
+
+  gb_stage(g.A, g.lda, m0, 0, lds, wave, lane);
+  gb_stage(g.W, g.ldw, n0, 0, lds + GB_TILE, wave, lane);
+  vmcnt0();
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    char* cur = lds + (kt & 1) * 2 * GB_TILE;
+    if (kt + 1 < nk) {
+      char* nxt = lds + ((kt + 1) & 1) * 2 * GB_TILE;
+      gb_stage(g.A, g.lda, m0, (kt + 1) * GB_K, nxt, wave, lane);
+      gb_stage(g.W, g.ldw, n0, (kt + 1) * GB_K, nxt + GB_TILE, wave, lane);
+    }
+    const char* As = cur + wm * 128 * 128 + rowoff;
+    const char* Bs = cur + GB_TILE + wn * 64 * 128 + rowoff;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int co = ((2 * s + h) ^ swz) * 16;
+      bf16x8 a[4], b[2];
+#pragma unroll
+      for (int t = 0; t < 4; ++t) a[t] = *reinterpret_cast<const bf16x8*>(As + t * 32 * 128 + co);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) b[u] = *reinterpret_cast<const bf16x8*>(Bs + u * 32 * 128 + co);
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[t], b[u], acc[t][u], 0, 0, 0);
+    }
+    vmcnt0();
+    __syncthreads();
+  }
+
+  // epilogue: lane holds column (lane & 31) of each 32 x 32 tile, rows (r&3) + 8(r>>2) + 4h.  One tile at a time
+  // (sched_barrier) so the residual / position loads of all 8 tiles are not hoisted together (register spills);
+  // 32-bit element offsets (the host checks M * ld < 2^31).
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int col = n0 + wn * 64 + u * 32 + (lane & 31);
+    const float bb = g.bias ? g.bias[col] : 0.f;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      const int rb = m0 + wm * 128 + t * 32 + 4 * h;
+      const int ob = rb * (int)g.ldo + col;
+      const int ostep = (int)g.ldo;
+      if constexpr (EPI == GE_BF16 || EPI == GE_GELU_BF16) {
+        bf16* o = reinterpret_cast<bf16*>(g.out);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float v = acc[t][u][r] + bb;
+          o[ob + ((r & 3) + 8 * (r >> 2)) * ostep] = (bf16)(EPI == GE_GELU_BF16 ? gelu_erf(v) : v);
+        }
+      } else if constexpr (EPI == GE_RES_F32) {
+        float* o = reinterpret_cast<float*>(g.out);
+        const int rstep = (int)g.ldr;
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {  // rows 8 g4 .. 8 g4 + 3 of the lane half: 4 loads in flight at a time
+          const float* rs = g.res + ((rb + 8 * g4) * rstep + col);
+          float rv[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) rv[j] = rs[j * rstep];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[ob + (8 * g4 + j) * ostep] = acc[t][u][4 * g4 + j] + bb + rv[j];
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else if constexpr (EPI == GE_PE_F32) {  // tokens per frame = AT_T (192), checked by the host
+        float* o = reinterpret_cast<float*>(g.out);
+        const float p0 = g.pos[col] + bb;
+#pragma unroll
+        for (int g4 = 0; g4 < 4; ++g4) {
+          const int row = rb + 8 * g4;  // rows row .. row + 3 lie in one frame (row % 4 == 0, 192 % 4 == 0)
+          const float* pp = g.pos + ((1 + row - (row / 192) * 192) * g.N + col);
+          float pv[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) pv[j] = pp[j * g.N];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[ob + (8 * g4 + j) * ostep] = acc[t][u][4 * g4 + j] + p0 + pv[j];
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      } else {
+        float* o = reinterpret_cast<float*>(g.out);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[ob + ((r & 3) + 8 * (r >> 2)) * ostep] = acc[t][u][r] + bb;
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------- LayerNorm
+// y = (x - mean) / sqrt(var + eps) * w + b over D = 256 NV columns, one wave per row (4 rows per block)
+template <int NV>
+__global__ void __launch_bounds__(256) ln_bf16_kernel(const float* __restrict__ x, long ldx, bf16* __restrict__ y,
+                                                      long ldy, const float* __restrict__ w,
+                                                      const float* __restrict__ b, int rows, float eps) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  constexpr int D = 256 * NV;
+  const float* xr = x + (size_t)row * ldx;
+  floatx4 v[NV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    v[i] = *reinterpret_cast<const floatx4*>(xr + 4 * (lane + 64 * i));
+    s += (v[i].x + v[i].y) + (v[i].z + v[i].w);
+  }
+  const float mean = wave_sum(s) * (1.0f / D);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const floatx4 d = v[i] - mean;
+    q += (d.x * d.x + d.y * d.y) + (d.z * d.z + d.w * d.w);
+  }
+  const float rstd = 1.0f / sqrtf(wave_sum(q) * (1.0f / D) + eps);
+  bf16* yr = y + (size_t)row * ldy;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = 4 * (lane + 64 * i);
+    const floatx4 ww = *reinterpret_cast<const floatx4*>(w + c);
+    const floatx4 bb = *reinterpret_cast<const floatx4*>(b + c);
+    const floatx4 o = (v[i] - mean) * rstd * ww + bb;
+    bf16x4 ob;
+    ob[0] = (bf16)o.x; ob[1] = (bf16)o.y; ob[2] = (bf16)o.z; ob[3] = (bf16)o.w;
+    *reinterpret_cast<bf16x4*>(yr + c) = ob;
+  }
+}
+
+// f32 -> bf16 copy of a [rows][D] block (D % 4 == 0)
+__global__ void cast_bf16_kernel(const float* __restrict__ x, long ldx, bf16* __restrict__ y, long ldy, int rows,
+                                 int D) {
+  const int q = D / 4;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= (long)rows * q) return;
+  const int r = (int)(i / q), c = (int)(i % q) * 4;
+  const floatx4 v = *reinterpret_cast<const floatx4*>(x + (size_t)r * ldx + c);
+  bf16x4 o;
+  o[0] = (bf16)v.x; o[1] = (bf16)v.y; o[2] = (bf16)v.z; o[3] = (bf16)v.w;
+  *reinterpret_cast<bf16x4*>(y + (size_t)r * ldy + c) = o;
+}
+
+// rows [0, rows) of a [rows][D] f32 block = vec[D] (the decoder's input token: to_token_embedding of the
+// zero token = its bias, plus pos_embedding)
+__global__ void bcast_rows_kernel(const float* __restrict__ vec, float* __restrict__ y, int rows, int D) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < (long)rows * D) y[i] = vec[i % D];
+}
+
+// ------------------------------------------------------------------------------------- patchify
+// Patch-embed input rows: A[f * gh * gw + py * gw + px][c * P * P + ky * P + kx] =
+//   (img[f][py P - pad + ky][x0 + px P - pad + kx][c] - mean[c]) / std[c], zero outside the img_h x img_w crop
+// (the conv's zero padding applies to the normalised image).  One thread per 8 consecutive kx.
+struct PatchArgs {
+  const uint8_t* frames;  // [F][in_h][in_w][3] RGB
+  bf16* out;              // [F * gh * gw][3 P P]
+  int F, in_h, in_w, x0, img_h, img_w, P, pad, gh, gw;
+  float mean[3], stdv[3];
+};
+
+__global__ void patchify_kernel(PatchArgs a) {
+  const int K = 3 * a.P * a.P, kc8 = K / 8, kxc = a.P / 8;
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long total = (long)a.F * a.gh * a.gw * kc8;
+  if (i >= total) return;
+  const int kc = (int)(i % kc8);
+  const long row = i / kc8;
+  const int f = (int)(row / (a.gh * a.gw)), p = (int)(row % (a.gh * a.gw));
+  const int py = p / a.gw, px = p % a.gw;
+  const int c = kc / (a.P * kxc), ky = (kc / kxc) % a.P, kx0 = (kc % kxc) * 8;
+  const int y = py * a.P - a.pad + ky;
+  bf16x8 o;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int x = px * a.P - a.pad + kx0 + j;
+    float v = 0.f;
+    if (y >= 0 && y < a.img_h && x >= 0 && x < a.img_w) {
+      const float u = (float)a.frames[(((size_t)f * a.in_h + y) * a.in_w + a.x0 + x) * 3 + c];
+      v = (u - a.mean[c]) / a.stdv[c];
+    }
+    o[j] = (bf16)v;
+  }
+  *reinterpret_cast<bf16x8*>(a.out + (size_t)row * K + kc * 8) = o;
+}
+
+// ------------------------------------------------------------------------------------- attention
+// softmax(Q K^T * scale) V for one (frame, head): qkv rows [tok0, tok0 + 192), q / k / v at column offsets
+// 0 / D / 2D + head * HD (timm's qkv.reshape(B, N, 3, heads, hd)).  6 waves, wave w = queries 32w..32w+31.
+constexpr int AT_T = 192;
+template <int HD>
+struct AttnCfg {
+  static constexpr int KS = HD + 8;                 // K row stride (bf16): conflict-free b128 fragment reads
+  static constexpr int DP = (HD + 31) / 32 * 32;    // V^T rows padded to whole 32-row MFMA tiles
+  static constexpr int VS = AT_T + 8;               // V^T row stride (bf16)
+  static constexpr int LDS = (AT_T * KS + DP * VS) * 2;
+};
+
+template <int HD>
+__global__ void __launch_bounds__(384) vit_attn_kernel(const bf16* __restrict__ qkv, long ldq, bf16* __restrict__ out,
+                                                       long ldo, int D, int heads, float scale_log2) {
+  using C = AttnCfg<HD>;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  bf16* Ks = reinterpret_cast<bf16*>(lds);
+  bf16* Vt = Ks + AT_T * C::KS;
+  const int f = blockIdx.x / heads, hd = blockIdx.x % heads;
+  const size_t tok0 = (size_t)f * AT_T;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int h = lane >> 5, i = lane & 31;
+  constexpr int CH = HD / 8;
+  const bf16* kbase = qkv + tok0 * ldq + D + hd * HD;
+  const bf16* vbase = kbase + D;
+  for (int c = tid; c < AT_T * CH; c += 384) {
+    const int row = c / CH, ch = c % CH;
+    *reinterpret_cast<bf16x8*>(Ks + row * C::KS + ch * 8) =
+        *reinterpret_cast<const bf16x8*>(kbase + (size_t)row * ldq + ch * 8);
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(vbase + (size_t)row * ldq + ch * 8);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) Vt[(ch * 8 + j) * C::VS + row] = v[j];
+  }
+  for (int c = tid; c < (C::DP - HD) * AT_T; c += 384) Vt[(HD + c / AT_T) * C::VS + c % AT_T] = (bf16)0.f;
+
+  // this lane's query row: B fragments of Q^T
+  const int q = wave * 32 + i;
+  bf16x8 qf[HD / 16];
+  const bf16* qrow = qkv + (tok0 + q) * ldq + hd * HD + 8 * h;
+#pragma unroll
+  for (int s = 0; s < HD / 16; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(qrow + 16 * s);
+  __syncthreads();
+
+  floatx16 st[AT_T / 32];  // S^T tiles: [key][query], lane = query
+#pragma unroll
+  for (int kt = 0; kt < AT_T / 32; ++kt) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) st[kt][r] = 0.f;
+    const bf16* krow = Ks + (kt * 32 + i) * C::KS + 8 * h;
+#pragma unroll
+    for (int s = 0; s < HD / 16; ++s)
+      st[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(*reinterpret_cast<const bf16x8*>(krow + 16 * s), qf[s], st[kt],
+                                                       0, 0, 0);
+  }
+  float m = -3.0e38f;
+#pragma unroll
+  for (int kt = 0; kt < AT_T / 32; ++kt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) m = fmaxf(m, st[kt][r]);
+  {
+    const auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(m), __float_as_uint(m), false, false);
+    m = fmaxf(__uint_as_float(r2[0]), __uint_as_float(r2[1]));
+  }
+  float sum = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < AT_T / 32; ++kt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = __builtin_amdgcn_exp2f((st[kt][r] - m) * scale_log2);
+      st[kt][r] = p;
+      sum += p;
+    }
+  {
+    const auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(sum), __float_as_uint(sum), false, false);
+    sum = __uint_as_float(r2[0]) + __uint_as_float(r2[1]);
+  }
+
+  // O^T[d][query] = V^T P^T: k-step (kt, sub) takes accumulator registers 8 sub .. 8 sub + 7 of S^T tile kt as
+  // the B fragment; its element j of lane half h is key kt*32 + 16 sub + 8 (j >> 2) + 4 h + (j & 3)
+  floatx16 o[C::DP / 32];
+#pragma unroll
+  for (int dt = 0; dt < C::DP / 32; ++dt)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[dt][r] = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < AT_T / 32; ++kt)
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      bf16x8 pb;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) pb[j] = (bf16)st[kt][8 * sub + j];
+      const int key = kt * 32 + 16 * sub + 4 * h;
+#pragma unroll
+      for (int dt = 0; dt < C::DP / 32; ++dt) {
+        const bf16* vr = Vt + (dt * 32 + i) * C::VS + key;
+        const bf16x4 lo = *reinterpret_cast<const bf16x4*>(vr);
+        const bf16x4 hi = *reinterpret_cast<const bf16x4*>(vr + 8);
+        const bf16x8 va = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(va, pb, o[dt], 0, 0, 0);
+      }
+    }
+  const float inv = 1.0f / sum;
+  bf16* orow = out + (tok0 + q) * ldo + hd * HD;
+#pragma unroll
+  for (int dt = 0; dt < C::DP / 32; ++dt)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const int d = dt * 32 + 8 * g4 + 4 * h;
+      if (d < HD) {
+        bf16x4 ob;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) ob[j] = (bf16)(o[dt][4 * g4 + j] * inv);
+        *reinterpret_cast<bf16x4*>(orow + d) = ob;
+      }
+    }
+}
+
+// One-query cross-attention of the decoder (HMR2 pose_transformer CrossAttention with a single token): per
+// (frame, head), scores over the frame's 192 context tokens, softmax, weighted sum of v.  One wave, dim_head 64.
+__global__ void __launch_bounds__(64) xattn1_kernel(const bf16* __restrict__ qv, long ldq, const bf16* __restrict__ kv,
+                                                    long ldkv, bf16* __restrict__ out, long ldo, int inner, int heads,
+                                                    int ctx, float scale) {
+  __shared__ float p[256];
+  const int f = blockIdx.x / heads, hd = blockIdx.x % heads, lane = threadIdx.x;
+  const bf16* qr = qv + (size_t)f * ldq + hd * 64;
+  float qreg[64];
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    const bf16x8 t = *reinterpret_cast<const bf16x8*>(qr + 8 * c);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) qreg[8 * c + j] = (float)t[j];
+  }
+  float m = -3.0e38f;
+  for (int k = lane; k < ctx; k += 64) {
+    const bf16* kr = kv + ((size_t)f * ctx + k) * ldkv + hd * 64;
+    float s = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const bf16x8 t = *reinterpret_cast<const bf16x8*>(kr + 8 * c);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += qreg[8 * c + j] * (float)t[j];
+    }
+    s *= scale;
+    p[k] = s;
+    m = fmaxf(m, s);
+  }
+  m = wave_max(m);
+  float sum = 0.f;
+  for (int k = lane; k < ctx; k += 64) {
+    const float e = __expf(p[k] - m);
+    p[k] = e;
+    sum += e;
+  }
+  sum = wave_sum(sum);
+  __syncthreads();
+  float acc = 0.f;
+  const bf16* vb = kv + (size_t)f * ctx * ldkv + inner + hd * 64 + lane;
+  for (int k = 0; k < ctx; ++k) acc += p[k] * (float)vb[(size_t)k * ldkv];
+  out[(size_t)f * ldo + hd * 64 + lane] = (bf16)(acc / sum);
+}
+
+// softmax over each row of C logits (f32 in, bf16 out), one wave per row
+__global__ void __launch_bounds__(256) softmax_rows_kernel(const float* __restrict__ x, bf16* __restrict__ y, int rows,
+                                                           int C) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* xr = x + (size_t)row * C;
+  float m = -3.0e38f;
+  for (int c = lane; c < C; c += 64) m = fmaxf(m, xr[c]);
+  m = wave_max(m);
+  float s = 0.f;
+  for (int c = lane; c < C; c += 64) s += __expf(xr[c] - m);
+  const float inv = 1.0f / wave_sum(s);
+  for (int c = lane; c < C; c += 64) y[(size_t)row * C + c] = (bf16)(__expf(xr[c] - m) * inv);
+}
+
+// Readout (token_head.py:207-246): body 6D = [grot | decoded body pose | hands] + init_body_pose, HMR2
+// rot6d_to_rotmat (Gram-Schmidt, F.normalize eps 1e-12), global_orient = joint 0, body_pose = joints 1..23;
+// betas = decshape + init_betas; vit = token_out.  One thread per (frame, joint); joint 0 also writes betas.
+struct ReadoutArgs {
+  const float* rd;        // [Fp][ldrd]: grot 0..5 | hands 6..17 | shape 18..27 | cam 28..30
+  const float* bp;        // [Fp][ldbp]: decoded body pose 6D, 21 joints
+  const float* init_pose; // [24 * 6]
+  const float* init_betas;// [10]
+  float* pose;            // [F][207]
+  float* gori;            // [F][9]
+  float* betas;           // [F][10]
+  int F, ldrd, ldbp;
+};
+
+__global__ void readout_kernel(ReadoutArgs a) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.F * 24) return;
+  const int f = i / 24, j = i % 24;
+  const float* src = j == 0 ? a.rd + (size_t)f * a.ldrd : j <= 21 ? a.bp + (size_t)f * a.ldbp + (j - 1) * 6
+                                                                   : a.rd + (size_t)f * a.ldrd + 6 + (j - 22) * 6;
+  float x[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) x[k] = src[k] + a.init_pose[j * 6 + k];
+  // x.reshape(2, 3).T: a1 = (x0, x1, x2), a2 = (x3, x4, x5)
+  float n1 = fmaxf(sqrtf(x[0] * x[0] + x[1] * x[1] + x[2] * x[2]), 1e-12f);
+  const float b1[3] = {x[0] / n1, x[1] / n1, x[2] / n1};
+  const float d = b1[0] * x[3] + b1[1] * x[4] + b1[2] * x[5];
+  float u[3] = {x[3] - d * b1[0], x[4] - d * b1[1], x[5] - d * b1[2]};
+  const float n2 = fmaxf(sqrtf(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]), 1e-12f);
+  const float b2[3] = {u[0] / n2, u[1] / n2, u[2] / n2};
+  const float b3[3] = {b1[1] * b2[2] - b1[2] * b2[1], b1[2] * b2[0] - b1[0] * b2[2], b1[0] * b2[1] - b1[1] * b2[0]};
+  float* o = j == 0 ? a.gori + (size_t)f * 9 : a.pose + (size_t)f * 207 + (j - 1) * 9;
+#pragma unroll
+  for (int r = 0; r < 3; ++r) {  // R[r][c] = b_c[r]
+    o[r * 3 + 0] = b1[r];
+    o[r * 3 + 1] = b2[r];
+    o[r * 3 + 2] = b3[r];
+  }
+  if (j == 0)
+    for (int k = 0; k < 10; ++k) a.betas[(size_t)f * 10 + k] = a.rd[(size_t)f * a.ldrd + 18 + k] + a.init_betas[k];
+}
+
+// token_out (the decoder's f32 residual stream) -> vit rows of the frame store
+__global__ void copy_rows_kernel(const float* __restrict__ x, long ldx, float* __restrict__ y, long ldy, int rows,
+                                 int D) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < (long)rows * D) y[(i / D) * ldy + i % D] = x[(i / D) * ldx + i % D];
+}
+
+}  // namespace
+
+// ================================================================================== host launchers
+namespace vge {
+
+struct GemmBf16 {
+  const void* A; long lda;
+  const void* W; long ldw;
+  void* out; long ldo;
+  const float* bias;
+  const float* res; long ldr;
+  const float* pos; int tokens;
+  int M, N, K;
+};
+
+hipError_t vit_kernels_setup() {
+  const void* ks[5] = {(const void*)gemm_bf16_kernel<GE_BF16>, (const void*)gemm_bf16_kernel<GE_GELU_BF16>,
+                       (const void*)gemm_bf16_kernel<GE_RES_F32>, (const void*)gemm_bf16_kernel<GE_PE_F32>,
+                       (const void*)gemm_bf16_kernel<GE_F32>};
+  for (auto k : ks) {
+    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, GB_LDS);
+    if (e != hipSuccess) return e;
+  }
+  hipError_t e = hipFuncSetAttribute((const void*)vit_attn_kernel<80>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     AttnCfg<80>::LDS);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute((const void*)vit_attn_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             AttnCfg<64>::LDS);
+}
+
+// shapes are validated by the caller (vge_hmr.cpp): M % 256 == N % 256 == K % 64 == 0, 16-B aligned rows
+hipError_t launch_gemm_bf16(int epi, const GemmBf16& a, hipStream_t s) {
+  GemmBf16Args g;
+  g.A = reinterpret_cast<const bf16*>(a.A);
+  g.W = reinterpret_cast<const bf16*>(a.W);
+  g.out = a.out;
+  g.bias = a.bias;
+  g.res = a.res;
+  g.pos = a.pos;
+  g.lda = a.lda; g.ldw = a.ldw; g.ldo = a.ldo; g.ldr = a.ldr;
+  g.M = a.M; g.N = a.N; g.K = a.K; g.tokens = a.tokens;
+  if ((long)a.M * a.ldo >= (1L << 31) || (a.res && (long)a.M * a.ldr >= (1L << 31)) || (epi == GE_PE_F32 && a.tokens != AT_T))
+    return hipErrorInvalidValue;
+  const dim3 grid((a.M / GB_M) * (a.N / GB_N));
+  switch (epi) {
+    case GE_BF16: hipLaunchKernelGGL(gemm_bf16_kernel<GE_BF16>, grid, dim3(512), GB_LDS, s, g); break;
+    case GE_GELU_BF16: hipLaunchKernelGGL(gemm_bf16_kernel<GE_GELU_BF16>, grid, dim3(512), GB_LDS, s, g); break;
+    case GE_RES_F32: hipLaunchKernelGGL(gemm_bf16_kernel<GE_RES_F32>, grid, dim3(512), GB_LDS, s, g); break;
+    case GE_PE_F32: hipLaunchKernelGGL(gemm_bf16_kernel<GE_PE_F32>, grid, dim3(512), GB_LDS, s, g); break;
+    default: hipLaunchKernelGGL(gemm_bf16_kernel<GE_F32>, grid, dim3(512), GB_LDS, s, g); break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_ln_bf16(const float* x, long ldx, void* y, long ldy, const float* w, const float* b, int rows, int D,
+                          float eps, hipStream_t s) {
+  const dim3 grid((rows + 3) / 4);
+  bf16* yy = reinterpret_cast<bf16*>(y);
+  switch (D) {
+    case 256: hipLaunchKernelGGL(ln_bf16_kernel<1>, grid, dim3(256), 0, s, x, ldx, yy, ldy, w, b, rows, eps); break;
+    case 512: hipLaunchKernelGGL(ln_bf16_kernel<2>, grid, dim3(256), 0, s, x, ldx, yy, ldy, w, b, rows, eps); break;
+    case 768: hipLaunchKernelGGL(ln_bf16_kernel<3>, grid, dim3(256), 0, s, x, ldx, yy, ldy, w, b, rows, eps); break;
+    case 1024: hipLaunchKernelGGL(ln_bf16_kernel<4>, grid, dim3(256), 0, s, x, ldx, yy, ldy, w, b, rows, eps); break;
+    case 1280: hipLaunchKernelGGL(ln_bf16_kernel<5>, grid, dim3(256), 0, s, x, ldx, yy, ldy, w, b, rows, eps); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_cast_bf16(const float* x, long ldx, void* y, long ldy, int rows, int D, hipStream_t s) {
+  const long n = (long)rows * (D / 4);
+  hipLaunchKernelGGL(cast_bf16_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, ldx,
+                     reinterpret_cast<bf16*>(y), ldy, rows, D);
+  return hipGetLastError();
+}
+
+hipError_t launch_bcast_rows(const float* vec, float* y, int rows, int D, hipStream_t s) {
+  const long n = (long)rows * D;
+  hipLaunchKernelGGL(bcast_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, vec, y, rows, D);
+  return hipGetLastError();
+}
+
+hipError_t launch_patchify(const uint8_t* frames, int F, int in_h, int in_w, int x0, int img_h, int img_w, int P,
+                           int pad, int gh, int gw, const float* mean, const float* stdv, void* out, hipStream_t s) {
+  PatchArgs a;
+  a.frames = frames; a.out = reinterpret_cast<bf16*>(out);
+  a.F = F; a.in_h = in_h; a.in_w = in_w; a.x0 = x0; a.img_h = img_h; a.img_w = img_w; a.P = P; a.pad = pad;
+  a.gh = gh; a.gw = gw;
+  for (int c = 0; c < 3; ++c) { a.mean[c] = mean[c]; a.stdv[c] = stdv[c]; }
+  const long n = (long)F * gh * gw * (3 * P * P / 8);
+  hipLaunchKernelGGL(patchify_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_vit_attn(const void* qkv, long ldq, void* out, long ldo, int F, int D, int heads, int hd,
+                           hipStream_t s) {
+  const float scale_log2 = 1.4426950408889634f / sqrtf((float)hd);
+  const bf16* q = reinterpret_cast<const bf16*>(qkv);
+  bf16* o = reinterpret_cast<bf16*>(out);
+  if (hd == 80)
+    hipLaunchKernelGGL(vit_attn_kernel<80>, dim3(F * heads), dim3(384), AttnCfg<80>::LDS, s, q, ldq, o, ldo, D, heads,
+                       scale_log2);
+  else if (hd == 64)
+    hipLaunchKernelGGL(vit_attn_kernel<64>, dim3(F * heads), dim3(384), AttnCfg<64>::LDS, s, q, ldq, o, ldo, D, heads,
+                       scale_log2);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_xattn1(const void* q, long ldq, const void* kv, long ldkv, void* out, long ldo, int F, int inner,
+                         int heads, int ctx, hipStream_t s) {
+  hipLaunchKernelGGL(xattn1_kernel, dim3(F * heads), dim3(64), 0, s, reinterpret_cast<const bf16*>(q), ldq,
+                     reinterpret_cast<const bf16*>(kv), ldkv, reinterpret_cast<bf16*>(out), ldo, inner, heads, ctx,
+                     0.125f);
+  return hipGetLastError();
+}
+
+hipError_t launch_softmax_rows(const float* x, void* y, int rows, int C, hipStream_t s) {
+  hipLaunchKernelGGL(softmax_rows_kernel, dim3((rows + 3) / 4), dim3(256), 0, s, x, reinterpret_cast<bf16*>(y), rows,
+                     C);
+  return hipGetLastError();
+}
+
+hipError_t launch_readout(const float* rd, int ldrd, const float* bp, int ldbp, const float* init_pose,
+                          const float* init_betas, float* pose, float* gori, float* betas, int F, hipStream_t s) {
+  ReadoutArgs a{rd, bp, init_pose, init_betas, pose, gori, betas, F, ldrd, ldbp};
+  hipLaunchKernelGGL(readout_kernel, dim3((F * 24 + 255) / 256), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_copy_rows(const float* x, long ldx, float* y, long ldy, int rows, int D, hipStream_t s) {
+  const long n = (long)rows * D;
+  hipLaunchKernelGGL(copy_rows_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, ldx, y, ldy, rows, D);
+  return hipGetLastError();
+}
+
+}  // namespace vge

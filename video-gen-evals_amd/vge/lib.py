@@ -16,7 +16,9 @@ STATUS = {0: "VGE_OK", 1: "VGE_ERR_ARG", 2: "VGE_ERR_HIP", 3: "VGE_ERR_MISSING_W
 EXPORTS = ["vge_featurize", "vge_stats_workspace_bytes", "vge_stats_accumulate", "vge_stats_finalize",
            "vge_encoder_create", "vge_encoder_reserve", "vge_encoder_destroy", "vge_encode", "vge_tc_windows",
            "vge_score_videos", "vge_centroid_accumulate", "vge_centroid_finalize", "vge_last_error", "vge_version",
-           "vge_encoder_profile_begin", "vge_encoder_profile_read", "vge_ingest_probe", "vge_ingest_decode"]
+           "vge_encoder_profile_begin", "vge_encoder_profile_read", "vge_ingest_probe", "vge_ingest_decode",
+           "vge_hmr_create", "vge_hmr_reserve", "vge_hmr_destroy", "vge_hmr_extract", "vge_hmr_profile_begin",
+           "vge_hmr_profile_read", "vge_op_gemm_bf16", "vge_op_vit_attention", "vge_op_layernorm_bf16"]
 
 
 class VgeError(RuntimeError):

@@ -238,3 +238,87 @@ def save_checkpoint(path: str, sd: Dict[str, np.ndarray], d_model: int = 256, ti
     torch.save({"model_state_dict": {k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in sd.items()},
                 "d_model": d_model, "latent_dim": 128, "time_layers": time_layers,
                 "time_heads": time_heads, "dropout": 0.1}, path)
+
+
+def make_hmr_state_dict(cfg, seed: int = SEED_WEIGHTS + 10) -> Dict[str, np.ndarray]:
+    """Deterministic random weights for the TokenHMR extractor (vge.hmr.HmrConfig shapes, the upstream
+    state_dict key names of include/vge_hmr.h).  No trained weights exist offline, so the extractor is
+    measured and parity-checked on these (parity vs upstream TokenHMR unpinned).  Linear weights
+    U(-1/sqrt(fan_in), 1/sqrt(fan_in)) (torch's default), biases N(0, 0.02), LayerNorm affines 1 + N(0, 0.1) /
+    N(0, 0.1), ViT pos_embed N(0, 0.02) (trunc-normal init), decoder pos_embedding N(0, 1), mean pose = identity
+    6D + N(0, 0.1)."""
+    rng = np.random.default_rng(seed)
+    sd: Dict[str, np.ndarray] = {}
+
+    def U(shape, fan_in):
+        b = np.float32(1.0 / np.sqrt(fan_in))
+        return (rng.random(size=shape, dtype=np.float32) * (2 * b) - b).astype(np.float32)
+
+    def N(shape, s):
+        return (rng.standard_normal(size=shape, dtype=np.float32) * np.float32(s)).astype(np.float32)
+
+    def linear(prefix, n, k, bias=True):
+        sd[prefix + ".weight"] = U((n, k), k)
+        if bias:
+            sd[prefix + ".bias"] = N((n,), 0.02)
+
+    def norm(prefix, n):
+        sd[prefix + ".weight"] = (1.0 + N((n,), 0.1)).astype(np.float32)
+        sd[prefix + ".bias"] = N((n,), 0.1)
+
+    E, P = cfg.embed_dim, cfg.patch
+    sd["backbone.patch_embed.proj.weight"] = U((E, 3, P, P), 3 * P * P)
+    sd["backbone.patch_embed.proj.bias"] = N((E,), 0.02)
+    sd["backbone.pos_embed"] = N((1, 193, E), 0.02)
+    for i in range(cfg.depth):
+        b = f"backbone.blocks.{i}."
+        norm(b + "norm1", E)
+        linear(b + "attn.qkv", 3 * E, E)
+        linear(b + "attn.proj", E, E)
+        norm(b + "norm2", E)
+        linear(b + "mlp.fc1", cfg.mlp_dim, E)
+        linear(b + "mlp.fc2", E, cfg.mlp_dim)
+    norm("backbone.last_norm", E)
+    D, inner = cfg.dec_dim, cfg.dec_heads * cfg.dec_dim_head
+    t = "smpl_head.transformer."
+    linear(t + "to_token_embedding", D, 1)
+    sd[t + "pos_embedding"] = N((1, 1, D), 1.0)
+    for l in range(cfg.dec_depth):
+        p = f"{t}transformer.layers.{l}."
+        norm(p + "0.norm", D)
+        linear(p + "0.fn.to_qkv", 3 * inner, D, bias=False)
+        linear(p + "0.fn.to_out.0", D, inner)
+        norm(p + "1.norm", D)
+        linear(p + "1.fn.to_q", inner, D, bias=False)
+        linear(p + "1.fn.to_kv", 2 * inner, E, bias=False)
+        linear(p + "1.fn.to_out.0", D, inner)
+        norm(p + "2.norm", D)
+        linear(p + "2.fn.net.0", cfg.dec_mlp, D)
+        linear(p + "2.fn.net.3", D, cfg.dec_mlp)
+    s = "smpl_head."
+    linear(s + "decpose_grot", 6, D)
+    linear(s + "decpose_hands", 12, D)
+    linear(s + "decshape", 10, D)
+    linear(s + "deccam", 3, D)
+    linear(s + "decpose.cls", cfg.tok_num * cfg.tok_classes, D)
+    sd[s + "decpose.codebook"] = N((cfg.tok_classes, cfg.tok_code_dim), 1.0)
+    linear(s + "decpose.dec", 21 * 6, cfg.tok_num * cfg.tok_code_dim)
+    ident = np.tile(np.array([1, 0, 0, 0, 1, 0], np.float32), 24)
+    sd[s + "init_body_pose"] = (ident + N((144,), 0.1))[None]
+    sd[s + "init_betas"] = N((1, 10), 0.5)
+    sd[s + "init_cam"] = np.array([[0.9, 0.0, 0.0]], np.float32)
+    return sd
+
+
+def make_frames(seed: int, n_frames: int, h: int = 256, w: int = 256) -> np.ndarray:
+    """uint8 RGB person-crop frames [F, h, w, 3]: a per-clip random low-frequency image drifting by a few
+    pixels per frame plus pixel noise (shape of ViTDetDataset's 256x256 crops)."""
+    rng = np.random.default_rng(seed)
+    base = rng.integers(0, 256, size=(h // 8 + 8, w // 8 + 8, 3), dtype=np.uint8)
+    big = np.kron(base, np.ones((8, 8, 1), np.uint8))
+    out = np.empty((n_frames, h, w, 3), np.uint8)
+    for f in range(n_frames):
+        dy, dx = f % 8, (2 * f) % 8
+        noise = rng.integers(-12, 13, size=(h, w, 3))
+        out[f] = np.clip(big[dy:dy + h, dx:dx + w].astype(np.int32) + noise, 0, 255).astype(np.uint8)
+    return out
