@@ -1,0 +1,18 @@
+"""Summarise tools/prof_gemm.sh passes: per-dispatch averages of every counter for the gemm_bf16 kernel."""
+import collections, csv, glob, json, sys
+tag = sys.argv[1]
+res = {}
+for d in sorted(glob.glob(f"gpurun_out/pg_{tag}_*/")):
+    for f in glob.glob(d + "*counter_collection.csv"):
+        acc = collections.defaultdict(list)
+        for r in csv.DictReader(open(f)):
+            if "gemm_bf16_kernel" not in r["Kernel_Name"]:
+                continue
+            acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
+        for k, v in acc.items():
+            res[k] = sum(v) / len(v) * (1 if True else 1)
+    for f in glob.glob(d + "*kernel_stats.csv"):
+        for r in csv.DictReader(open(f)):
+            if "gemm_bf16_kernel" in r["Name"]:
+                res["avg_ns"] = float(r["AverageNs"])
+print(json.dumps(res, indent=1))

@@ -174,3 +174,17 @@ __device__ __forceinline__ void vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"
 // retired first (WAR safety for the ring slot being refilled), then s_barrier.  The "memory" clobber
 // keeps the compiler from moving loads/stores across it.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// The same waits as builtins (gfx9 s_waitcnt simm16: vmcnt[3:0] | expcnt[6:4] | lgkmcnt[11:8] | vmcnt_hi[15:14]):
+// unlike an asm statement, hipcc's waitcnt insertion sees them and knows what they retired, so it does not add a
+// conservative lgkmcnt(0) before later uses of registers loaded earlier.
+template <int N>
+__device__ __forceinline__ void vmcnt_b() {
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | ((N >> 4) << 14) | 0x70 | 0xF00);
+}
+__device__ __forceinline__ void lds_barrier_b() {
+  asm volatile("" ::: "memory");  // the builtins are IntrNoMem: keep LDS / global_load_lds ops on their side
+  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}

@@ -8,9 +8,9 @@
 //
 // Kernels (all bf16 operands, f32 accumulation, residual stream kept in f32):
 //   gemm_bf16_kernel<EPI>  C = A W^T (+ epilogue) for every Linear / the patch-embed conv (as im2col GEMM):
-//                          256 x 256 x 64 tiles, 8 waves (2 M x 4 N, 128 x 64 per wave) on
+//                          256 x 256 tiles, 8 waves (2 M x 4 N, 128 x 64 per wave) on
 //                          v_mfma_f32_32x32x16_bf16, both operands staged HBM -> LDS by global_load_lds
-//                          (16 B per lane, double-buffered 128 KB), LDS image XOR-swizzled on the source
+//                          (16 B per lane) through a 5-stage x 32-k ring (160 KB, counted vmcnt), LDS image XOR-swizzled on the source
 //                          address so the fragment ds_read_b128 are conflict-free; XCD-grouped tile order.
 //   ln_bf16_kernel         LayerNorm f32 -> bf16 (one wave per row).
 //   patchify_kernel        uint8 RGB crop -> normalised, zero-padded im2col rows of the 16x16 patches.
@@ -20,6 +20,12 @@
 //   xattn1_kernel          the decoder's one-query cross-attention over the 192 context tokens.
 //   softmax_rows_kernel, readout_kernel (6D -> rotation matrix, mean-pose residuals), small helpers.
 #include "vge_common.h"
+#include <cstdlib>
+
+#ifndef VGE_GABL
+#define VGE_GABL 0  // timing-only GEMM ablations (tools/ablate_gemm.sh): 1 no global_load_lds after the prologue,
+                    // 2 no LDS fragment reads after the first, 4 no per-stage wait + barrier; 0 = the product
+#endif
 
 namespace {
 
@@ -29,9 +35,13 @@ typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 // ------------------------------------------------------------------------------------------- GEMM
-constexpr int GB_M = 256, GB_N = 256, GB_K = 64;
-constexpr int GB_TILE = GB_M * GB_K * 2;  // 32 KB per operand tile
-constexpr int GB_LDS = 4 * GB_TILE;       // A0 B0 A1 B1
+// 256 x 256 output tile per 512-thread workgroup; K in 32-deep stages through a 5-slot LDS ring (A 16 KB + B 16 KB
+// per slot = 160 KB).  Step kt MFMAs stage kt from registers while the wave reads stage kt + 1's fragments from
+// LDS (register double buffer, so no ds_read latency restarts at the per-stage barrier) and global_load_lds
+// fills stage kt + 4; the per-stage wait is a counted vmcnt (stages kt + 2, kt + 3 stay in flight), never a drain.
+constexpr int GB_M = 256, GB_N = 256, GB_K = 32, GB_ST = 5, GB_GM = 8;
+constexpr int GB_TILE = GB_M * GB_K * 2;      // 16 KB per operand per stage
+constexpr int GB_LDS = GB_ST * 2 * GB_TILE;   // 160 KB
 
 enum GemmEpi { GE_BF16 = 0, GE_GELU_BF16 = 1, GE_RES_F32 = 2, GE_PE_F32 = 3, GE_F32 = 4 };
 
@@ -46,17 +56,18 @@ struct GemmBf16Args {
   int M, N, K, tokens;
 };
 
-// Stage a 256-row x 64-k operand tile: wave-instruction q (0..31) fills LDS bytes [1024 q, 1024 q + 1024) =
-// rows 8q .. 8q+7 (128 B each), lane L -> row 8q + L/8, physical 16-B chunk L%8.  The physical chunk p of row r
-// holds logical chunk p ^ ((r >> 1) & 7), so the source address is pre-swizzled and the LDS image stays
-// lane-linear (what global_load_lds requires).
+// Stage a 256-row x 32-k operand tile (64-B rows) with NW waves: wave-instruction q (0..15) fills LDS bytes
+// [1024 q, 1024 q + 1024) = rows 16q .. 16q+15, lane L -> row 16q + L/4, physical 16-B chunk L%4.  Physical chunk
+// p of row r holds logical chunk p ^ ((r >> 2) & 3): the source address is pre-swizzled, the LDS image stays
+// lane-linear (global_load_lds), and the 16 rows a ds_read_b128 lane group reads land on 16 distinct 16-B slots.
+template <int NW>
 __device__ __forceinline__ void gb_stage(const bf16* __restrict__ X, long ld, int r0, int k0, char* tile, int wave,
                                          int lane) {
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int q = wave * 4 + j;
-    const int row = 8 * q + (lane >> 3);
-    const int ch = (lane & 7) ^ ((row >> 1) & 7);
+  for (int j = 0; j < 16 / NW; ++j) {
+    const int q = wave * (16 / NW) + j;
+    const int row = 16 * q + (lane >> 2);
+    const int ch = (lane & 3) ^ ((row >> 2) & 3);
     glds16(X + (size_t)(r0 + row) * ld + k0 + ch * 8, tile + q * 1024);
   }
 }
@@ -66,65 +77,114 @@ __device__ __forceinline__ int gb_xcd_remap(int b, int nblk) {  // bijective: ea
   return (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (b >> 3);
 }
 
-template <int EPI>
-__global__ void __launch_bounds__(512, 1) gemm_bf16_kernel(GemmBf16Args g) {
+// NW = 8: waves 2 (M) x 4 (N), 128 x 64 per wave (2 waves per SIMD); NW = 4: waves 2 x 2, 128 x 128 per wave
+// (one wave per SIMD, 256 accumulator registers): 25 % fewer LDS fragment bytes per MFMA.
+template <int EPI, int NW>
+__global__ void __launch_bounds__(64 * NW, 1) gemm_bf16_kernel(GemmBf16Args g) {
+  constexpr int TN = NW == 8 ? 2 : 4;  // 32-column tiles per wave
+  constexpr int LPS = 2 * (16 / NW);   // global_load_lds per thread per stage
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int ntn = g.N / GB_N;
+  const int wm = wave / (NW / 2), wn = wave % (NW / 2);
+  // tile order: each XCD takes a contiguous range of ids (gb_xcd_remap); inside it, groups of GB_GM row panels
+  // walk the column panels with the row panel fastest, so the ~32 blocks an XCD runs at once cover ~8 A panels x
+  // ~4 W panels and read the same K slices at about the same time (L2 hits instead of fabric re-fetches)
+  const int ntn = g.N / GB_N, mtn = g.M / GB_M;
   const int bid = gb_xcd_remap(blockIdx.x, gridDim.x);
-  const int mt = bid / ntn, nt = bid % ntn;  // consecutive ids share the A row panel
+  const int grp = bid / (GB_GM * ntn), rem = bid % (GB_GM * ntn);
+  const int gm = min(GB_GM, mtn - grp * GB_GM);
+  const int mt = grp * GB_GM + rem % gm, nt = rem / gm;
   const int m0 = mt * GB_M, n0 = nt * GB_N;
-  const int nk = g.K / GB_K;
+  const int nk = g.K / GB_K;                 // >= 2 (K % 64 == 0)
   const int h = lane >> 5;
-  const int swz = (lane >> 1) & 7;  // ((row >> 1) & 7) of every fragment row this lane reads
-  const int rowoff = (lane & 31) * 128;
+  const int swz = (lane >> 2) & 3;           // ((row >> 2) & 3) of every fragment row this lane reads
+  const int rowoff = (lane & 31) * 64;
 
-  floatx16 acc[4][2];
+  floatx16 acc[4][TN];
 #pragma unroll
   for (int t = 0; t < 4; ++t)
 #pragma unroll
-    for (int u = 0; u < 2; ++u)
+    for (int u = 0; u < TN; ++u)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
 
-  gb_stage(g.A, g.lda, m0, 0, lds, wave, lane);
-  gb_stage(g.W, g.ldw, n0, 0, lds + GB_TILE, wave, lane);
-  vmcnt0();
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    char* cur = lds + (kt & 1) * 2 * GB_TILE;
-    if (kt + 1 < nk) {
-      char* nxt = lds + ((kt + 1) & 1) * 2 * GB_TILE;
-      gb_stage(g.A, g.lda, m0, (kt + 1) * GB_K, nxt, wave, lane);
-      gb_stage(g.W, g.ldw, n0, (kt + 1) * GB_K, nxt + GB_TILE, wave, lane);
-    }
-    const char* As = cur + wm * 128 * 128 + rowoff;
-    const char* Bs = cur + GB_TILE + wn * 64 * 128 + rowoff;
+  auto issue = [&](int st) {
+    char* slot = lds + (st % GB_ST) * 2 * GB_TILE;
+    gb_stage<NW>(g.A, g.lda, m0, st * GB_K, slot, wave, lane);
+    gb_stage<NW>(g.W, g.ldw, n0, st * GB_K, slot + GB_TILE, wave, lane);
+  };
+  struct Frag {
+    bf16x8 a[2][4], b[2][TN];
+  };
+  auto read = [&](int st, Frag& f) {  // this wave's fragments of stage st (both 16-k steps)
+    const char* cur = lds + (st % GB_ST) * 2 * GB_TILE;
+    const char* As = cur + wm * 128 * 64 + rowoff;
+    const char* Bs = cur + GB_TILE + wn * (32 * TN) * 64 + rowoff;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
+    for (int s = 0; s < 2; ++s) {
       const int co = ((2 * s + h) ^ swz) * 16;
-      bf16x8 a[4], b[2];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) a[t] = *reinterpret_cast<const bf16x8*>(As + t * 32 * 128 + co);
+      for (int t = 0; t < 4; ++t) f.a[s][t] = *reinterpret_cast<const bf16x8*>(As + t * 32 * 64 + co);
 #pragma unroll
-      for (int u = 0; u < 2; ++u) b[u] = *reinterpret_cast<const bf16x8*>(Bs + u * 32 * 128 + co);
-#pragma unroll
-      for (int t = 0; t < 4; ++t)
-#pragma unroll
-        for (int u = 0; u < 2; ++u) acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[t], b[u], acc[t][u], 0, 0, 0);
+      for (int u = 0; u < TN; ++u) f.b[s][u] = *reinterpret_cast<const bf16x8*>(Bs + u * 32 * 64 + co);
     }
-    vmcnt0();
-    __syncthreads();
+  };
+  auto mma = [&](const Frag& f, int s) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int u = 0; u < TN; ++u)
+        acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[s][t], f.b[s][u], acc[t][u], 0, 0, 0);
+  };
+  // Step kt: stage kt's fragments are already in registers (read during step kt - 1).  Wait for stage kt + 1 and
+  // barrier (it also retires every wave's reads of stage kt - 1's slot); then one straight-line block: stage
+  // kt + 4's global_load_lds into that slot interleaved with the first 16-k MFMAs, stage kt + 1's fragment reads
+  // interleaved with the second (sched_group_barrier), so loads and LDS reads issue between MFMAs instead of in a
+  // burst in front of them.  Branch-free: past the last stage the loads re-fetch stage nk - 1 into its own slot
+  // (identical bytes) and the reads re-read it, so the wait is always vmcnt(2 LPS) (3 stages = 96 KB in flight).
+  auto step = [&](int kt, Frag& cur, Frag& nxt) {
+#if !(VGE_GABL & 4)
+    vmcnt_b<2 * LPS>();  // outstanding: the loads of steps kt - 3 .. kt - 1 -> retire step kt - 3's (stage kt + 1)
+    lds_barrier_b();
+#endif
+#if !(VGE_GABL & 1)
+    issue(min(kt + 4, nk - 1));
+#endif
+#if !(VGE_GABL & 2)
+    read(min(kt + 1, nk - 1), nxt);
+#else
+    nxt = cur;
+#endif
+    mma(cur, 0);
+    mma(cur, 1);
+#pragma unroll
+    for (int j = 0; j < LPS; ++j) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 8 / LPS, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);        // VMEM read (global_load_lds)
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                   // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, (8 + 2 * TN) / 4, 0);    // DS read
+    }
+  };
+  for (int st = 0; st < GB_ST - 1; ++st) issue(min(st, nk - 1));
+  vmcnt_b<3 * LPS>();  // retire stage 0
+  lds_barrier_b();
+  Frag f0, f1;
+  read(0, f0);
+  for (int kt = 0; kt < nk; kt += 2) {  // nk is even (K % 64 == 0)
+    step(kt, f0, f1);
+    step(kt + 1, f1, f0);
   }
 
   // epilogue: lane holds column (lane & 31) of each 32 x 32 tile, rows (r&3) + 8(r>>2) + 4h.  One tile at a time
-  // (sched_barrier) so the residual / position loads of all 8 tiles are not hoisted together (register spills);
+  // (sched_barrier) so the residual / position loads of all tiles are not hoisted together (register spills);
   // 32-bit element offsets (the host checks M * ld < 2^31).
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
-    const int col = n0 + wn * 64 + u * 32 + (lane & 31);
+  for (int u = 0; u < TN; ++u) {
+    const int col = n0 + wn * (32 * TN) + u * 32 + (lane & 31);
     const float bb = g.bias ? g.bias[col] : 0.f;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -151,7 +211,7 @@ __global__ void __launch_bounds__(512, 1) gemm_bf16_kernel(GemmBf16Args g) {
           for (int j = 0; j < 4; ++j) o[ob + (8 * g4 + j) * ostep] = acc[t][u][4 * g4 + j] + bb + rv[j];
           __builtin_amdgcn_sched_barrier(0);
         }
-      } else if constexpr (EPI == GE_PE_F32) {  // tokens per frame = AT_T (192), checked by the host
+      } else if constexpr (EPI == GE_PE_F32) {  // tokens per frame = 192, checked by the host
         float* o = reinterpret_cast<float*>(g.out);
         const float p0 = g.pos[col] + bb;
 #pragma unroll
@@ -512,19 +572,41 @@ struct GemmBf16 {
   int M, N, K;
 };
 
-hipError_t vit_kernels_setup() {
-  const void* ks[5] = {(const void*)gemm_bf16_kernel<GE_BF16>, (const void*)gemm_bf16_kernel<GE_GELU_BF16>,
-                       (const void*)gemm_bf16_kernel<GE_RES_F32>, (const void*)gemm_bf16_kernel<GE_PE_F32>,
-                       (const void*)gemm_bf16_kernel<GE_F32>};
+template <int NW>
+hipError_t gemm_setup_nw() {
+  const void* ks[5] = {(const void*)gemm_bf16_kernel<GE_BF16, NW>, (const void*)gemm_bf16_kernel<GE_GELU_BF16, NW>,
+                       (const void*)gemm_bf16_kernel<GE_RES_F32, NW>, (const void*)gemm_bf16_kernel<GE_PE_F32, NW>,
+                       (const void*)gemm_bf16_kernel<GE_F32, NW>};
   for (auto k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, GB_LDS);
     if (e != hipSuccess) return e;
   }
-  hipError_t e = hipFuncSetAttribute((const void*)vit_attn_kernel<80>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     AttnCfg<80>::LDS);
+  return hipSuccess;
+}
+
+hipError_t vit_kernels_setup() {
+  hipError_t e = gemm_setup_nw<8>();
+  if (e == hipSuccess) e = gemm_setup_nw<4>();
+  if (e != hipSuccess) return e;
+  e = hipFuncSetAttribute((const void*)vit_attn_kernel<80>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          AttnCfg<80>::LDS);
   if (e != hipSuccess) return e;
   return hipFuncSetAttribute((const void*)vit_attn_kernel<64>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              AttnCfg<64>::LDS);
+}
+
+static int g_gemm_waves = 0;  // 8 or 4 (VGE_GEMM_WAVES), chosen once
+
+template <int NW>
+void launch_gemm_nw(int epi, dim3 grid, const GemmBf16Args& g, hipStream_t s) {
+  const dim3 blk(64 * NW);
+  switch (epi) {
+    case GE_BF16: hipLaunchKernelGGL((gemm_bf16_kernel<GE_BF16, NW>), grid, blk, GB_LDS, s, g); break;
+    case GE_GELU_BF16: hipLaunchKernelGGL((gemm_bf16_kernel<GE_GELU_BF16, NW>), grid, blk, GB_LDS, s, g); break;
+    case GE_RES_F32: hipLaunchKernelGGL((gemm_bf16_kernel<GE_RES_F32, NW>), grid, blk, GB_LDS, s, g); break;
+    case GE_PE_F32: hipLaunchKernelGGL((gemm_bf16_kernel<GE_PE_F32, NW>), grid, blk, GB_LDS, s, g); break;
+    default: hipLaunchKernelGGL((gemm_bf16_kernel<GE_F32, NW>), grid, blk, GB_LDS, s, g); break;
+  }
 }
 
 // shapes are validated by the caller (vge_hmr.cpp): M % 256 == N % 256 == K % 64 == 0, 16-B aligned rows
@@ -540,15 +622,21 @@ hipError_t launch_gemm_bf16(int epi, const GemmBf16& a, hipStream_t s) {
   g.M = a.M; g.N = a.N; g.K = a.K; g.tokens = a.tokens;
   if ((long)a.M * a.ldo >= (1L << 31) || (a.res && (long)a.M * a.ldr >= (1L << 31)) || (epi == GE_PE_F32 && a.tokens != AT_T))
     return hipErrorInvalidValue;
-  const dim3 grid((a.M / GB_M) * (a.N / GB_N));
-  switch (epi) {
-    case GE_BF16: hipLaunchKernelGGL(gemm_bf16_kernel<GE_BF16>, grid, dim3(512), GB_LDS, s, g); break;
-    case GE_GELU_BF16: hipLaunchKernelGGL(gemm_bf16_kernel<GE_GELU_BF16>, grid, dim3(512), GB_LDS, s, g); break;
-    case GE_RES_F32: hipLaunchKernelGGL(gemm_bf16_kernel<GE_RES_F32>, grid, dim3(512), GB_LDS, s, g); break;
-    case GE_PE_F32: hipLaunchKernelGGL(gemm_bf16_kernel<GE_PE_F32>, grid, dim3(512), GB_LDS, s, g); break;
-    default: hipLaunchKernelGGL(gemm_bf16_kernel<GE_F32>, grid, dim3(512), GB_LDS, s, g); break;
+  if (g_gemm_waves == 0) {
+    const char* e = getenv("VGE_GEMM_WAVES");
+    g_gemm_waves = (e && atoi(e) == 4) ? 4 : 8;
   }
+  const dim3 grid((a.M / GB_M) * (a.N / GB_N));
+  if (g_gemm_waves == 4)
+    launch_gemm_nw<4>(epi, grid, g, s);
+  else
+    launch_gemm_nw<8>(epi, grid, g, s);
   return hipGetLastError();
+}
+
+extern "C" int vge_debug_set_gemm_waves(int nw) {  // A/B timing (tools/gemm_bench.py)
+  g_gemm_waves = (nw == 4) ? 4 : 8;
+  return 0;
 }
 
 hipError_t launch_ln_bf16(const float* x, long ldx, void* y, long ldy, const float* w, const float* b, int rows, int D,
