@@ -137,9 +137,23 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--compute", default="f32x3", choices=["f32x3", "f32"],
                     help="f32x3: 3xfp16 split-precision MFMA (f32-class, default); f32: exact f32 MFMA")
+    ap.add_argument("--workload", default="score", choices=["score", "e2e"],
+                    help="score: config 2 (default, the bench line); e2e: config 3, frames -> TokenHMR extractor -> "
+                         "scores (bench_e2e.py; --clips defaults to 8 there)")
     args = ap.parse_args()
 
     world, rank, dev = setup_dist()
+    if args.workload == "e2e":
+        import bench_e2e
+        if args.clips == 256:
+            args.clips = 8
+        out = bench_e2e.run(args, world, rank, dev, METRIC, allreduce_sum, make_clips)
+        if rank == 0:
+            print(json.dumps(out))
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     from vge import eval as VE
     from vge import ops, synth
     from vge.data import ACTION_CLASSES, pack_frame_store

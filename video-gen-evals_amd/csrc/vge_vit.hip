@@ -179,58 +179,50 @@ __global__ void __launch_bounds__(64 * NW, 1) gemm_bf16_kernel(GemmBf16Args g) {
     step(kt + 1, f1, f0);
   }
 
-  // epilogue: lane holds column (lane & 31) of each 32 x 32 tile, rows (r&3) + 8(r>>2) + 4h.  One tile at a time
-  // (sched_barrier) so the residual / position loads of all tiles are not hoisted together (register spills);
-  // 32-bit element offsets (the host checks M * ld < 2^31).
+  // Epilogue through LDS (free once every wave's tail loads and reads have retired): each wave writes half of its
+  // 128 x (32 TN) accumulator tile (C layout, wave-private region, in-order LDS so no barrier) and reads it back
+  // row-major, 16 B per lane, so bias / residual / position loads and the output stores are whole-row vector
+  // accesses (256-B f32 rows, 128-B bf16 rows) instead of 2-4-byte column scatters.
+  constexpr int WC = 32 * TN;            // wave tile columns
+  constexpr int RPI = 64 / (WC / 4);     // rows per read instruction (16 B per lane)
+  vmcnt_b<0>();
+  lds_barrier_b();
+  float* my = reinterpret_cast<float*>(lds) + wave * (64 * WC);
+  const int lr = lane / (WC / 4), c4 = (lane % (WC / 4)) * 4;
+  const int gcol = n0 + wn * WC + c4;
+  floatx4 bb = {0.f, 0.f, 0.f, 0.f};
+  if (g.bias) bb = *reinterpret_cast<const floatx4*>(g.bias + gcol);
+  if constexpr (EPI == GE_PE_F32) bb += *reinterpret_cast<const floatx4*>(g.pos + gcol);  // pos_embed[:, :1]
 #pragma unroll
-  for (int u = 0; u < TN; ++u) {
-    const int col = n0 + wn * (32 * TN) + u * 32 + (lane & 31);
-    const float bb = g.bias ? g.bias[col] : 0.f;
+  for (int half = 0; half < 2; ++half) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const int rb = m0 + wm * 128 + t * 32 + 4 * h;
-      const int ob = rb * (int)g.ldo + col;
-      const int ostep = (int)g.ldo;
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int u = 0; u < TN; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          my[(tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * WC + u * 32 + (lane & 31)] = acc[2 * half + tt][u][r];
+#pragma unroll 4
+    for (int it = 0; it < 64 / RPI; ++it) {
+      const int rl = it * RPI + lr;
+      const int grow = m0 + wm * 128 + half * 64 + rl;
+      floatx4 v = *reinterpret_cast<const floatx4*>(my + rl * WC + c4) + bb;
+      const int o = grow * (int)g.ldo + gcol;
       if constexpr (EPI == GE_BF16 || EPI == GE_GELU_BF16) {
-        bf16* o = reinterpret_cast<bf16*>(g.out);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float v = acc[t][u][r] + bb;
-          o[ob + ((r & 3) + 8 * (r >> 2)) * ostep] = (bf16)(EPI == GE_GELU_BF16 ? gelu_erf(v) : v);
+        if constexpr (EPI == GE_GELU_BF16) {
+          floatx2 y[2] = {{v.x, v.y}, {v.z, v.w}};
+          gelu2_many(y);
+          v = {y[0].x, y[0].y, y[1].x, y[1].y};
         }
-      } else if constexpr (EPI == GE_RES_F32) {
-        float* o = reinterpret_cast<float*>(g.out);
-        const int rstep = (int)g.ldr;
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {  // rows 8 g4 .. 8 g4 + 3 of the lane half: 4 loads in flight at a time
-          const float* rs = g.res + ((rb + 8 * g4) * rstep + col);
-          float rv[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) rv[j] = rs[j * rstep];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) o[ob + (8 * g4 + j) * ostep] = acc[t][u][4 * g4 + j] + bb + rv[j];
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      } else if constexpr (EPI == GE_PE_F32) {  // tokens per frame = 192, checked by the host
-        float* o = reinterpret_cast<float*>(g.out);
-        const float p0 = g.pos[col] + bb;
-#pragma unroll
-        for (int g4 = 0; g4 < 4; ++g4) {
-          const int row = rb + 8 * g4;  // rows row .. row + 3 lie in one frame (row % 4 == 0, 192 % 4 == 0)
-          const float* pp = g.pos + ((1 + row - (row / 192) * 192) * g.N + col);
-          float pv[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) pv[j] = pp[j * g.N];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) o[ob + (8 * g4 + j) * ostep] = acc[t][u][4 * g4 + j] + p0 + pv[j];
-          __builtin_amdgcn_sched_barrier(0);
-        }
+        bf16x4 ob;
+        ob[0] = (bf16)v.x; ob[1] = (bf16)v.y; ob[2] = (bf16)v.z; ob[3] = (bf16)v.w;
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(g.out) + o) = ob;
       } else {
-        float* o = reinterpret_cast<float*>(g.out);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) o[ob + ((r & 3) + 8 * (r >> 2)) * ostep] = acc[t][u][r] + bb;
+        if constexpr (EPI == GE_RES_F32) v += *reinterpret_cast<const floatx4*>(g.res + (grow * (int)g.ldr + gcol));
+        if constexpr (EPI == GE_PE_F32)  // tokens per frame = 192 (checked by the host)
+          v += *reinterpret_cast<const floatx4*>(g.pos + ((1 + grow - (grow / 192) * 192) * g.N + gcol));
+        *reinterpret_cast<floatx4*>(reinterpret_cast<float*>(g.out) + o) = v;
       }
-      __builtin_amdgcn_sched_barrier(0);
     }
   }
 }
