@@ -1,0 +1,579 @@
+// Convolutional-network kernels of the per-frame keypoint extractor (DWPose: RTMPose-l whole-body and the
+// YOLOX-L person detector) on gfx950.  Activations are NHWC bf16 with an explicit pixel stride, so a
+// torch.cat along channels is just an output written at a channel offset of a wider buffer.
+//
+//   conv_bf16_kernel<TN,ACT,OUT,RES>  implicit-GEMM convolution on v_mfma_f32_32x32x16_bf16: C[pixel][cout] =
+//       sum_k A[pixel][k] W[cout][k], k = tap * Cin + ci (tap-major, Cin a power of two >= 8).  A rows are
+//       gathered straight from the NHWC input by global_load_lds (16 B = 8 channels per lane); taps that fall
+//       in the zero padding (and K / M padding) read a zero page instead of being masked, so the LDS ring is
+//       filled exactly like a dense GEMM's.  128 x TN output tile per 256-thread workgroup, 32-deep K stages in
+//       a 3-slot ring, LDS image XOR-swizzled on the source address (conflict-free ds_read_b128 fragments),
+//       XCD-contiguous tile ranges.  Epilogue through LDS, row-major: + bias (folded BatchNorm), SiLU /
+//       sigmoid, + residual (bf16 identity of CSPNeXtBlock, or f32 x per-column scale for RTMCCBlock's
+//       res_scale), bf16 or f32 store.  Every nn.Linear of the head runs here too (1x1 "image").
+//   dwconv_kernel        depthwise KxK conv + folded BN + SiLU (one thread = 8 channels of one pixel).
+//   spp_pool_kernel      SPPBottleneck's stride-1 max pools (5, 9, 13) written beside their input.
+//   chan_mean_kernel / chan_attn_fc_kernel / chan_scale_kernel   ChannelAttention: avgpool -> 1x1 conv ->
+//                        hardsigmoid -> x * a.
+//   warp_prep_kernel     onnxpose.preprocess: per-instance affine crop (bilinear, border 0, uint8 round) of the
+//                        RGB frame, BGR mean/std normalisation -> NHWC bf16 with 8 channels (3 used).
+//   letterbox_focus_kernel  onnxdet.preprocess (resize by r, pad 114) + YOLOX Focus space-to-depth -> 16 ch.
+#include "vge_common.h"
+#include "vge_cnn.h"
+
+namespace {
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+constexpr int CV_M = 128, CV_K = 32, CV_ST = 3;
+
+enum { ACT_NONE = 0, ACT_SILU = 1, ACT_SIGMOID = 2 };
+enum { OUT_BF16 = 0, OUT_F32 = 1 };
+enum { RES_NONE = 0, RES_BF16 = 1, RES_F32S = 2 };
+
+struct ConvArgs {
+  const bf16* x;       // NHWC input, pixel stride ldx elements (channel offset folded into the pointer)
+  const bf16* w;       // [Npad][Kp] bf16, k = tap * Cin + ci, zero padded
+  const float* bias;   // [Npad]
+  void* out;           // NHWC output, pixel stride ldo
+  const void* res;     // residual [M][ldr] (bf16 or f32)
+  const float* rscale; // RES_F32S: per-column scale [Npad]
+  const bf16* zero;    // >= 16 B of zeros (the source of padding taps)
+  long ldx, ldo, ldr;
+  int H, W, cin_log2, Ho, Wo, KW, kw_magic, stride, pad, taps, Kp, Cout, M;
+};
+
+__device__ __forceinline__ int xcd_remap(int b, int nblk) {  // bijective: each XCD takes a contiguous range
+  const int q8 = nblk >> 3, r8 = nblk & 7, x8 = b & 7;
+  return (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (b >> 3);
+}
+
+__device__ __forceinline__ float silu(float v) { return v / (1.0f + __expf(-v)); }
+__device__ __forceinline__ float sigm(float v) { return 1.0f / (1.0f + __expf(-v)); }
+
+// 256 threads = 4 waves (2 along M x 2 along N), wave tile 64 x TN/2 on 32x32x16 MFMAs.
+template <int TN, int ACT, int OUT, int RES>
+__global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
+  constexpr int TA = CV_M * CV_K * 2;         // 8 KB A stage
+  constexpr int TB = TN * CV_K * 2;           // B stage
+  constexpr int SLOT = TA + TB;
+  constexpr int NB = TN / 64;                 // 32-col MFMA tiles per wave
+  constexpr int BQ = TN / 16 / 4;             // B wave-instructions per wave per stage
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int ntn = (a.Cout + TN - 1) / TN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = bid / ntn, nt = bid - mt * ntn;
+  const int m0 = mt * CV_M, n0 = nt * TN;
+  const int nk = a.Kp / CV_K;
+  const int cmask = (1 << a.cin_log2) - 1;
+
+  // per-lane gather state of this lane's two A rows (row = 16 q + lane / 4, q = 2 wave + j)
+  const int lc = (lane & 3) ^ ((lane >> 4) & 3);  // logical 16-B chunk this lane fetches (pre-swizzled)
+  int img_hw[2], ih0[2], iw0[2];
+  bool mval[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = 16 * (2 * wave + j) + (lane >> 2);
+    const int m = m0 + row;
+    mval[j] = m < a.M;
+    const int hw = a.Ho * a.Wo;
+    const int img = m / hw, rem = m - img * hw;
+    const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
+    img_hw[j] = img * a.H;
+    ih0[j] = oh * a.stride - a.pad;
+    iw0[j] = ow * a.stride - a.pad;
+  }
+  const bf16* wrow[BQ];
+#pragma unroll
+  for (int j = 0; j < BQ; ++j) wrow[j] = a.w + (size_t)(n0 + 16 * (BQ * wave + j) + (lane >> 2)) * a.Kp + lc * 8;
+
+  auto issue = [&](int st) {
+    char* slot = lds + (st % CV_ST) * SLOT;
+    const int k = st * CV_K + lc * 8;
+    const int tap = k >> a.cin_log2, ci = k & cmask;
+    const int kh = (tap * a.kw_magic) >> 16, kw = tap - kh * a.KW;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ih = ih0[j] + kh, iw = iw0[j] + kw;
+      const bool ok = mval[j] && tap < a.taps && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      const bf16* src = ok ? a.x + ((size_t)(img_hw[j] + ih) * a.W + iw) * a.ldx + ci : a.zero;
+      glds16(src, slot + (2 * wave + j) * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < BQ; ++j) glds16(wrow[j] + st * CV_K, slot + TA + (BQ * wave + j) * 1024);
+  };
+
+  floatx16 acc[2][NB];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < NB; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
+
+  const int h = lane >> 5;
+  const int swz = (lane >> 2) & 3;
+  const int rowoff = (lane & 31) * 64;
+  constexpr int LPS = 2 + BQ;  // global_load_lds per thread per stage
+  for (int st = 0; st < CV_ST - 1; ++st) issue(min(st, nk - 1));
+  for (int kt = 0; kt < nk; ++kt) {
+    vmcnt_b<LPS>();     // stage kt landed (stage kt + 1 may still be in flight)
+    lds_barrier_b();    // ... for every wave; every wave is done reading stage kt - 1's slot
+    issue(min(kt + CV_ST - 1, nk - 1));  // past the end: re-fetch the last stage into its own slot (same bytes)
+    const char* cur = lds + (kt % CV_ST) * SLOT;
+    const char* As = cur + wm * 64 * 64 + rowoff;
+    const char* Bs = cur + TA + wn * (TN / 2) * 64 + rowoff;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int co = ((2 * s + h) ^ swz) * 16;
+      bf16x8 fa[2], fb[NB];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) fa[t] = *reinterpret_cast<const bf16x8*>(As + t * 32 * 64 + co);
+#pragma unroll
+      for (int u = 0; u < NB; ++u) fb[u] = *reinterpret_cast<const bf16x8*>(Bs + u * 32 * 64 + co);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int u = 0; u < NB; ++u)
+          acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[t], fb[u], acc[t][u], 0, 0, 0);
+    }
+  }
+
+  // epilogue through LDS in two 64-row halves (32 KB of f32 each), row-major re-read: 8 columns per thread
+  vmcnt_b<0>();
+  lds_barrier_b();
+  constexpr int LDC = TN + 4;
+  float* cs = reinterpret_cast<float*>(lds);
+  constexpr int TPR = TN / 8;       // threads per row
+  constexpr int RPP = 256 / TPR;    // rows per pass
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    if (wm == half) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int u = 0; u < NB; ++u)
+#pragma unroll
+          for (int r = 0; r < 16; ++r)
+            cs[(t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * LDC + wn * (TN / 2) + u * 32 + (lane & 31)] = acc[t][u][r];
+    }
+    __syncthreads();
+    const int c8 = (tid % TPR) * 8;
+    const int col = n0 + c8;
+    floatx4 b0 = *reinterpret_cast<const floatx4*>(a.bias + col);
+    floatx4 b1 = *reinterpret_cast<const floatx4*>(a.bias + col + 4);
+#pragma unroll
+    for (int p = 0; p < 64 / RPP; ++p) {
+      const int rl = p * RPP + tid / TPR;
+      const int m = m0 + half * 64 + rl;
+      if (m >= a.M || col >= a.Cout) continue;
+      float v[8];
+      const floatx4 x0 = *reinterpret_cast<const floatx4*>(cs + rl * LDC + c8) + b0;
+      const floatx4 x1 = *reinterpret_cast<const floatx4*>(cs + rl * LDC + c8 + 4) + b1;
+      v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        if constexpr (ACT == ACT_SILU) v[i] = silu(v[i]);
+        if constexpr (ACT == ACT_SIGMOID) v[i] = sigm(v[i]);
+      }
+      if constexpr (RES == RES_BF16) {
+        const bf16x8 r8 = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(a.res) + (size_t)m * a.ldr + col);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] += (float)r8[i];
+      }
+      if constexpr (RES == RES_F32S) {
+        const float* rr = reinterpret_cast<const float*>(a.res) + (size_t)m * a.ldr + col;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = fmaf(a.rscale[col + i], rr[i], v[i]);
+      }
+      if constexpr (OUT == OUT_BF16) {  // Cout % 8 == 0 (host-checked)
+        bf16x8 o;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) o[i] = (bf16)v[i];
+        *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(a.out) + (size_t)m * a.ldo + col) = o;
+      } else {
+        float* o = reinterpret_cast<float*>(a.out) + (size_t)m * a.ldo + col;
+        if (col + 8 <= a.Cout && (a.ldo & 3) == 0) {
+          *reinterpret_cast<floatx4*>(o) = floatx4{v[0], v[1], v[2], v[3]};
+          *reinterpret_cast<floatx4*>(o + 4) = floatx4{v[4], v[5], v[6], v[7]};
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+            if (col + i < a.Cout) o[i] = v[i];
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------ depthwise
+// y[p][c] = SiLU(b[c] + sum_{kh,kw} w[kh*K+kw][c] x[p + (kh - pad, kw - pad)][c]), stride 1, f32 weights.
+template <int K>
+__global__ void __launch_bounds__(256) dwconv_kernel(const bf16* __restrict__ x, long ldx, const float* __restrict__ w,
+                                                     const float* __restrict__ b, bf16* __restrict__ y, long ldy,
+                                                     int n_img, int H, int W, int C) {
+  const int cg = C >> 3;
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (long)n_img * H * W * cg) return;
+  const int c8 = (int)(gid % cg) * 8;
+  const long pix = gid / cg;
+  const int ow = (int)(pix % W), oh = (int)((pix / W) % H);
+  const long img = pix / ((long)W * H);
+  float acc[8];
+  {
+    const floatx4 b0 = *reinterpret_cast<const floatx4*>(b + c8), b1 = *reinterpret_cast<const floatx4*>(b + c8 + 4);
+    acc[0] = b0.x; acc[1] = b0.y; acc[2] = b0.z; acc[3] = b0.w; acc[4] = b1.x; acc[5] = b1.y; acc[6] = b1.z; acc[7] = b1.w;
+  }
+  constexpr int P = K / 2;
+#pragma unroll
+  for (int kh = 0; kh < K; ++kh) {
+    const int ih = oh + kh - P;
+    if ((unsigned)ih >= (unsigned)H) continue;
+#pragma unroll
+    for (int kw = 0; kw < K; ++kw) {
+      const int iw = ow + kw - P;
+      if ((unsigned)iw >= (unsigned)W) continue;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + ((img * H + ih) * W + iw) * ldx + c8);
+      const float* wt = w + (kh * K + kw) * C + c8;
+      const floatx4 w0 = *reinterpret_cast<const floatx4*>(wt), w1 = *reinterpret_cast<const floatx4*>(wt + 4);
+      acc[0] = fmaf(w0.x, (float)v[0], acc[0]);
+      acc[1] = fmaf(w0.y, (float)v[1], acc[1]);
+      acc[2] = fmaf(w0.z, (float)v[2], acc[2]);
+      acc[3] = fmaf(w0.w, (float)v[3], acc[3]);
+      acc[4] = fmaf(w1.x, (float)v[4], acc[4]);
+      acc[5] = fmaf(w1.y, (float)v[5], acc[5]);
+      acc[6] = fmaf(w1.z, (float)v[6], acc[6]);
+      acc[7] = fmaf(w1.w, (float)v[7], acc[7]);
+    }
+  }
+  bf16x8 o;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = (bf16)silu(acc[i]);
+  *reinterpret_cast<bf16x8*>(y + pix * ldy + c8) = o;
+}
+
+// ------------------------------------------------------------------------------------ SPP max pools
+// buf[p][0:C] is the input; writes max_pool(k)(input) for k = k0, k1, k2 at channel offsets C, 2C, 3C.
+__global__ void __launch_bounds__(256) spp_pool_kernel(bf16* __restrict__ buf, long ld, int n_img, int H, int W, int C,
+                                                       int k0, int k1, int k2) {
+  const int cg = C >> 3;
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (long)n_img * H * W * cg) return;
+  const int c8 = (int)(gid % cg) * 8;
+  const long pix = gid / cg;
+  const int ow = (int)(pix % W), oh = (int)((pix / W) % H);
+  const long img = pix / ((long)W * H);
+  const int r2 = k2 / 2, r1 = k1 / 2, r0 = k0 / 2;
+  float m0[8], m1[8], m2[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) m0[i] = m1[i] = m2[i] = -INFINITY;
+  for (int dy = -r2; dy <= r2; ++dy) {
+    const int ih = oh + dy;
+    if ((unsigned)ih >= (unsigned)H) continue;
+    for (int dx = -r2; dx <= r2; ++dx) {
+      const int iw = ow + dx;
+      if ((unsigned)iw >= (unsigned)W) continue;
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(buf + ((img * H + ih) * W + iw) * ld + c8);
+      const bool in1 = dy >= -r1 && dy <= r1 && dx >= -r1 && dx <= r1;
+      const bool in0 = dy >= -r0 && dy <= r0 && dx >= -r0 && dx <= r0;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float f = (float)v[i];
+        m2[i] = fmaxf(m2[i], f);
+        if (in1) m1[i] = fmaxf(m1[i], f);
+        if (in0) m0[i] = fmaxf(m0[i], f);
+      }
+    }
+  }
+  bf16x8 o0, o1, o2;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    o0[i] = (bf16)m0[i];
+    o1[i] = (bf16)m1[i];
+    o2[i] = (bf16)m2[i];
+  }
+  bf16* d = buf + pix * ld + c8;
+  *reinterpret_cast<bf16x8*>(d + C) = o0;
+  *reinterpret_cast<bf16x8*>(d + 2 * C) = o1;
+  *reinterpret_cast<bf16x8*>(d + 3 * C) = o2;
+}
+
+// ------------------------------------------------------------------------------------ ChannelAttention
+// mean over the H*W pixels of each (image, channel): one workgroup per (image, 256-channel slab)
+__global__ void __launch_bounds__(256) chan_mean_kernel(const bf16* __restrict__ x, long ld, int HW, int C,
+                                                        float* __restrict__ mean) {
+  __shared__ float part[8][256];
+  const int img = blockIdx.x, slab = blockIdx.y * 256;
+  const int cw = min(256, C - slab);         // channels in this slab (multiple of 8)
+  const int g = threadIdx.x % (cw / 8), lanes_per_pix = cw / 8;
+  const int pr = threadIdx.x / lanes_per_pix, npr = 256 / lanes_per_pix;  // pixel rows in flight
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (pr < npr)
+    for (int p = pr; p < HW; p += npr) {
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + ((long)img * HW + p) * ld + slab + g * 8);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) acc[i] += (float)v[i];
+    }
+  // reduce over the npr pixel rows: stage by row groups of 8
+  __shared__ float red[256][9];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) red[threadIdx.x][i] = acc[i];
+  __syncthreads();
+  (void)part;
+  if (threadIdx.x < cw) {
+    const int c = threadIdx.x, gg = c / 8, ii = c % 8;
+    float s = 0.f;
+    for (int r = 0; r < npr; ++r) s += red[r * lanes_per_pix + gg][ii];
+    mean[(long)img * C + slab + c] = s / (float)HW;
+  }
+}
+
+// a[img][c] = hardsigmoid(b[c] + sum_k Wt[k][c] mean[img][k])  (Wt = fc.weight transposed, f32)
+__global__ void __launch_bounds__(256) chan_attn_fc_kernel(const float* __restrict__ mean, const float* __restrict__ Wt,
+                                                           const float* __restrict__ b, float* __restrict__ att, int C) {
+  extern __shared__ float mrow[];
+  const int img = blockIdx.y;
+  for (int k = threadIdx.x; k < C; k += blockDim.x) mrow[k] = mean[(long)img * C + k];
+  __syncthreads();
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s = b[c];
+  for (int k = 0; k < C; ++k) s = fmaf(Wt[(long)k * C + c], mrow[k], s);
+  att[(long)img * C + c] = fminf(fmaxf(s + 3.0f, 0.0f), 6.0f) / 6.0f;  // nn.Hardsigmoid: relu6(x + 3) / 6
+}
+
+__global__ void __launch_bounds__(256) chan_scale_kernel(bf16* __restrict__ x, long ld, int HW, int C,
+                                                         const float* __restrict__ att, long n_pix) {
+  const int cg = C >> 3;
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= n_pix * cg) return;
+  const int c8 = (int)(gid % cg) * 8;
+  const long pix = gid / cg;
+  const long img = pix / HW;
+  bf16x8* p = reinterpret_cast<bf16x8*>(x + pix * ld + c8);
+  bf16x8 v = *p;
+  const float* a = att + img * C + c8;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (bf16)((float)v[i] * a[i]);
+  *p = v;
+}
+
+// ------------------------------------------------------------------------------------ input preparation
+using vge::WarpInst;
+
+// onnxpose.preprocess restated in float (no contraction, so the host oracle reproduces every uint8)
+__global__ void __launch_bounds__(256) warp_prep_kernel(const uint8_t* __restrict__ frames, int H, int W,
+                                                        const WarpInst* __restrict__ inst, int n_inst, int oh, int ow,
+                                                        bf16* __restrict__ out) {
+#pragma clang fp contract(off)
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (long)n_inst * oh * ow) return;
+  const int u = (int)(gid % ow), v = (int)((gid / ow) % oh);
+  const int i = (int)(gid / ((long)ow * oh));
+  const WarpInst in = inst[i];
+  const float sx = in.cx + ((float)u - 0.5f * (float)ow) * in.k;
+  const float sy = in.cy + ((float)v - 0.5f * (float)oh) * in.k;
+  const float x0f = floorf(sx), y0f = floorf(sy);
+  const float fx = sx - x0f, fy = sy - y0f;
+  const int x0 = (int)x0f, y0 = (int)y0f;
+  const uint8_t* fr = frames + (long)in.frame * H * W * 3;
+  const float mean[3] = {123.675f, 116.28f, 103.53f}, stdv[3] = {58.395f, 57.12f, 57.375f};
+  bf16x8 o;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {  // model channel c = BGR[c] = RGB[2 - c]
+    auto px = [&](int yy, int xx) -> float {
+      return ((unsigned)yy < (unsigned)H && (unsigned)xx < (unsigned)W) ? (float)fr[((long)yy * W + xx) * 3 + 2 - c] : 0.f;
+    };
+    const float top = (1.0f - fx) * px(y0, x0) + fx * px(y0, x0 + 1);
+    const float bot = (1.0f - fx) * px(y0 + 1, x0) + fx * px(y0 + 1, x0 + 1);
+    const float val = (1.0f - fy) * top + fy * bot;
+    const float q = rintf(fminf(fmaxf(val, 0.f), 255.f));
+    o[c] = (bf16)((q - mean[c]) / stdv[c]);
+  }
+#pragma unroll
+  for (int c = 3; c < 8; ++c) o[c] = (bf16)0.f;
+  *reinterpret_cast<bf16x8*>(out + gid * 8) = o;
+}
+
+// onnxdet.preprocess (cv2.resize INTER_LINEAR by r into the top-left of a 114-filled S x S canvas, BGR,
+// uint8 values) + YOLOX Focus (channels: [::2, ::2], [1::2, ::2], [::2, 1::2], [1::2, 1::2], 3 each) ->
+// NHWC bf16 [F][S/2][S/2][16] (12 used).  cv2.resize maps dst x to src (x + 0.5) / r - 0.5, clamped.
+__global__ void __launch_bounds__(256) letterbox_focus_kernel(const uint8_t* __restrict__ frames, int n, int H, int W,
+                                                              int S, int rh, int rw, float inv_r, bf16* __restrict__ out) {
+#pragma clang fp contract(off)
+  const int S2 = S / 2;
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (long)n * S2 * S2) return;
+  const int u = (int)(gid % S2), v = (int)((gid / S2) % S2);
+  const int f = (int)(gid / ((long)S2 * S2));
+  const uint8_t* fr = frames + (long)f * H * W * 3;
+  bf16 o[16];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int dy = q & 1, dx = q >> 1;  // Focus order: (0,0), (1,0), (0,1), (1,1) as (row, col) parity
+    const int yy = 2 * v + dy, xx = 2 * u + dx;
+    float val[3] = {114.f, 114.f, 114.f};
+    if (yy < rh && xx < rw) {
+      float sx = ((float)xx + 0.5f) * inv_r - 0.5f, sy = ((float)yy + 0.5f) * inv_r - 0.5f;
+      sx = fmaxf(sx, 0.f);
+      sy = fmaxf(sy, 0.f);
+      int x0 = (int)floorf(sx), y0 = (int)floorf(sy);
+      float fx = sx - (float)x0, fy = sy - (float)y0;
+      if (x0 >= W - 1) { x0 = W - 1; fx = 0.f; }
+      if (y0 >= H - 1) { y0 = H - 1; fy = 0.f; }
+      const int x1 = min(x0 + 1, W - 1), y1 = min(y0 + 1, H - 1);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float p00 = fr[((long)y0 * W + x0) * 3 + 2 - c], p01 = fr[((long)y0 * W + x1) * 3 + 2 - c];
+        const float p10 = fr[((long)y1 * W + x0) * 3 + 2 - c], p11 = fr[((long)y1 * W + x1) * 3 + 2 - c];
+        const float top = (1.0f - fx) * p00 + fx * p01, bot = (1.0f - fx) * p10 + fx * p11;
+        val[c] = rintf(fminf(fmaxf((1.0f - fy) * top + fy * bot, 0.f), 255.f));
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) o[q * 3 + c] = (bf16)val[c];
+  }
+#pragma unroll
+  for (int c = 12; c < 16; ++c) o[c] = (bf16)0.f;
+  bf16x8* d = reinterpret_cast<bf16x8*>(out + gid * 16);
+  bf16x8 lo, hi;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    lo[i] = o[i];
+    hi[i] = o[8 + i];
+  }
+  d[0] = lo;
+  d[1] = hi;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------ launchers
+namespace vge {
+
+static int ilog2(int v) {
+  int l = 0;
+  while ((1 << l) < v) ++l;
+  return l;
+}
+
+template <int TN, int ACT, int OUT, int RES>
+static hipError_t conv_go(const ConvArgs& a, int grid, hipStream_t s) {
+  constexpr int LDS = CV_ST * (CV_M * CV_K * 2 + TN * CV_K * 2);
+  constexpr int EPI = 64 * (TN + 4) * 4;
+  constexpr int BYTES = LDS > EPI ? LDS : EPI;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_bf16_kernel<TN, ACT, OUT, RES>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, BYTES);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL((conv_bf16_kernel<TN, ACT, OUT, RES>), dim3(grid), dim3(256), BYTES, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_conv_bf16(const ConvLaunch& c, hipStream_t s) {
+  ConvArgs a;
+  a.x = static_cast<const bf16*>(c.x);
+  a.w = static_cast<const bf16*>(c.w);
+  a.bias = c.bias;
+  a.out = c.out;
+  a.res = c.res;
+  a.rscale = c.rscale;
+  a.zero = static_cast<const bf16*>(c.zero);
+  a.ldx = c.ldx;
+  a.ldo = c.ldo;
+  a.ldr = c.ldr;
+  a.H = c.H;
+  a.W = c.W;
+  a.cin_log2 = ilog2(c.Cin);
+  a.Ho = (c.H + 2 * c.pad - c.KH) / c.stride + 1;
+  a.Wo = (c.W + 2 * c.pad - c.KW) / c.stride + 1;
+  a.KW = c.KW;
+  a.kw_magic = (65536 + c.KW - 1) / c.KW;
+  a.stride = c.stride;
+  a.pad = c.pad;
+  a.taps = c.KH * c.KW;
+  a.Kp = c.Kp;
+  a.Cout = c.Cout;
+  a.M = c.n_img * a.Ho * a.Wo;
+  const int grid = ((a.M + CV_M - 1) / CV_M) * ((c.Cout + c.tn - 1) / c.tn);
+  if (a.M <= 0) return hipSuccess;
+#define VGE_CONV_CASE(ACT, OUT, RES)                                                              \
+  if (c.act == ACT && c.out_f32 == OUT && c.res_mode == RES)                                      \
+    return c.tn == 64 ? conv_go<64, ACT, OUT, RES>(a, grid, s) : conv_go<128, ACT, OUT, RES>(a, grid, s);
+  if (c.tn != 64 && c.tn != 128) return hipErrorInvalidValue;
+  VGE_CONV_CASE(ACT_SILU, OUT_BF16, RES_NONE)
+  VGE_CONV_CASE(ACT_SILU, OUT_BF16, RES_BF16)
+  VGE_CONV_CASE(ACT_NONE, OUT_BF16, RES_NONE)
+  VGE_CONV_CASE(ACT_NONE, OUT_BF16, RES_F32S)
+  VGE_CONV_CASE(ACT_NONE, OUT_F32, RES_NONE)
+  VGE_CONV_CASE(ACT_SILU, OUT_F32, RES_NONE)
+  VGE_CONV_CASE(ACT_SIGMOID, OUT_F32, RES_NONE)
+#undef VGE_CONV_CASE
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_dwconv(const void* x, long ldx, const float* w, const float* b, void* y, long ldy, int n_img, int H,
+                         int W, int C, int K, hipStream_t s) {
+  const long n = (long)n_img * H * W * (C / 8);
+  if (n == 0) return hipSuccess;
+  const int grid = (int)((n + 255) / 256);
+  if (K == 5)
+    hipLaunchKernelGGL(dwconv_kernel<5>, dim3(grid), dim3(256), 0, s, static_cast<const bf16*>(x), ldx, w, b,
+                       static_cast<bf16*>(y), ldy, n_img, H, W, C);
+  else if (K == 3)
+    hipLaunchKernelGGL(dwconv_kernel<3>, dim3(grid), dim3(256), 0, s, static_cast<const bf16*>(x), ldx, w, b,
+                       static_cast<bf16*>(y), ldy, n_img, H, W, C);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_spp_pool(void* buf, long ld, int n_img, int H, int W, int C, int k0, int k1, int k2, hipStream_t s) {
+  const long n = (long)n_img * H * W * (C / 8);
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(spp_pool_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, static_cast<bf16*>(buf), ld,
+                     n_img, H, W, C, k0, k1, k2);
+  return hipGetLastError();
+}
+
+hipError_t launch_chan_attn(void* x, long ld, int n_img, int HW, int C, const float* Wt, const float* b, float* mean,
+                            float* att, hipStream_t s) {
+  if (n_img == 0) return hipSuccess;
+  hipLaunchKernelGGL(chan_mean_kernel, dim3(n_img, (C + 255) / 256), dim3(256), 0, s, static_cast<const bf16*>(x), ld,
+                     HW, C, mean);
+  hipLaunchKernelGGL(chan_attn_fc_kernel, dim3((C + 255) / 256, n_img), dim3(256), C * sizeof(float), s, mean, Wt, b,
+                     att, C);
+  const long n = (long)n_img * HW * (C / 8);
+  hipLaunchKernelGGL(chan_scale_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, static_cast<bf16*>(x), ld,
+                     HW, C, att, (long)n_img * HW);
+  return hipGetLastError();
+}
+
+hipError_t launch_warp_prep(const uint8_t* frames, int H, int W, const void* inst, int n_inst, int oh, int ow, void* out,
+                            hipStream_t s) {
+  const long n = (long)n_inst * oh * ow;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(warp_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, frames, H, W,
+                     static_cast<const WarpInst*>(inst), n_inst, oh, ow, static_cast<bf16*>(out));
+  return hipGetLastError();
+}
+
+hipError_t launch_letterbox_focus(const uint8_t* frames, int n, int H, int W, int S, int rh, int rw, float inv_r,
+                                  void* out, hipStream_t s) {
+  const long tot = (long)n * (S / 2) * (S / 2);
+  if (tot == 0) return hipSuccess;
+  hipLaunchKernelGGL(letterbox_focus_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, frames, n, H, W, S,
+                     rh, rw, inv_r, static_cast<bf16*>(out));
+  return hipGetLastError();
+}
+
+}  // namespace vge

@@ -1,0 +1,260 @@
+// RTMPose whole-body head + DWPose output composition on gfx950 (the dense layers run on conv_bf16_kernel,
+// vge_cnn.hip).
+//
+//   head_sn_t_kernel     RTMCCHead: flatten(final_layer(x), 2) -> ScaleNorm over the h*w positions of each
+//                        keypoint channel -> bf16 rows [inst * K + k][hw (zero padded)]
+//   scalenorm_rows_kernel RTMCCBlock.ln: ScaleNorm over the hidden dim -> bf16
+//   gau_attn_kernel      RTMCCBlock token mixing of one instance: q / k = base * gamma + beta, kernel =
+//                        relu(q k^T / sqrt(s))^2, out = u * (kernel @ v) (f32 on the VALU, K x K kernel in LDS)
+//   simcc_decode_kernel  get_simcc_maximum: first-index argmax over the x / y bins, vals = min of the maxima,
+//                        locs = -1 where vals <= 0, / split ratio
+//   kp120_kernel         onnxpose.postprocess (float64) + wholebody neck / OpenPose reorder + dwpose_init's
+//                        normalisation (/ W, / H; hand points with score < 0.3 -> -1, body points unmasked) +
+//                        flatten_first_person_no_padding
+#include "vge_common.h"
+#include "vge_cnn.h"
+
+#include <cmath>
+
+namespace {
+
+typedef __bf16 bf16;
+
+__global__ void __launch_bounds__(256) head_sn_t_kernel(const float* __restrict__ y, long ldy, int hw, int K, int Kp,
+                                                        float g, float inv_sqrt_hw, long n_rows, bf16* __restrict__ out) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);  // row = inst * K + k
+  const int lane = threadIdx.x & 63;
+  if (row >= n_rows) return;
+  const long inst = row / K;
+  const int k = (int)(row - inst * K);
+  float v[4];
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int p = lane + 64 * j;
+    v[j] = p < hw ? y[(inst * hw + p) * ldy + k] : 0.f;
+    ss = fmaf(v[j], v[j], ss);
+  }
+  ss = wave_sum(ss);
+  const float norm = fmaxf(sqrtf(ss) * inv_sqrt_hw, 1e-5f);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int p = lane + 64 * j;
+    if (p < Kp) out[row * Kp + p] = (bf16)(p < hw ? v[j] / norm * g : 0.f);
+  }
+}
+
+// D = 256 per row (RTMPose hidden dims), one wave per row, 4 values per lane
+__global__ void __launch_bounds__(256) scalenorm_rows_kernel(const float* __restrict__ x, int D, float g,
+                                                             float inv_sqrt_d, long rows, bf16* __restrict__ y) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  float v[8];
+  float ss = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = lane + 64 * j;
+    v[j] = c < D ? x[row * D + c] : 0.f;
+    ss = fmaf(v[j], v[j], ss);
+  }
+  ss = wave_sum(ss);
+  const float norm = fmaxf(sqrtf(ss) * inv_sqrt_d, 1e-5f);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = lane + 64 * j;
+    if (c < D) y[row * D + c] = (bf16)(v[j] / norm * g);
+  }
+}
+
+// One workgroup (4 waves) per instance.  uv [inst * K + t][2E + S] f32 (SiLU already applied): u = cols
+// [0, E), v = [E, 2E), base = [2E, 2E + S).  LDS: k-matrix [K][S + 1], kernel [K][KP], one q row per wave.
+template <int KMAX>
+__global__ void __launch_bounds__(256) gau_attn_kernel(const float* __restrict__ uv, int K, int E, int S,
+                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                       float sqrt_s, bf16* __restrict__ out) {
+  extern __shared__ float sm[];
+  constexpr int KP = KMAX + 1;
+  const int SP = S + 1;
+  float* kk = sm;                       // [K][SP]
+  float* A = kk + KMAX * SP;            // [K][KP]
+  float* qrow = A + KMAX * KP;          // [4][S]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const long base_row = (long)blockIdx.x * K;
+  const int ld = 2 * E + S;
+  for (int idx = tid; idx < K * S; idx += 256) {
+    const int j = idx / S, s = idx - j * S;
+    kk[j * SP + s] = uv[(base_row + j) * ld + 2 * E + s] * gamma[S + s] + beta[S + s];
+  }
+  __syncthreads();
+  for (int i = wave; i < K; i += 4) {
+    for (int s = lane; s < S; s += 64) qrow[wave * S + s] = uv[(base_row + i) * ld + 2 * E + s] * gamma[s] + beta[s];
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    for (int j = lane; j < K; j += 64) {
+      float d = 0.f;
+      for (int s = 0; s < S; ++s) d = fmaf(qrow[wave * S + s], kk[j * SP + s], d);
+      const float r = fmaxf(d / sqrt_s, 0.f);
+      A[i * KP + j] = r * r;
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  // out[i][e] = u[i][e] * sum_j A[i][j] v[j][e]: 128-column chunks of v staged in LDS over the (dead) k-matrix;
+  // thread = one column e (coalesced v / u / out) x 4-row groups, the two thread halves take alternate groups
+  float* vs = kk;  // [K][128]
+  const int el = tid & 127, half = tid >> 7;
+  for (int e0 = 0; e0 < E; e0 += 128) {
+    __syncthreads();
+    for (int j = half; j < K; j += 2) vs[j * 128 + el] = uv[(base_row + j) * ld + E + e0 + el];
+    __syncthreads();
+    for (int i0 = 4 * half; i0 < K; i0 += 8) {
+      float acc[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < K; ++j) {
+        const float v = vs[j * 128 + el];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[r] = fmaf(A[(i0 + r) * KP + j], v, acc[r]);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        if (i0 + r < K)
+          out[(base_row + i0 + r) * E + e0 + el] = (bf16)(uv[(base_row + i0 + r) * ld + e0 + el] * acc[r]);
+    }
+  }
+}
+
+// one wave per (inst, k): logits row [x bins | y bins] (f32, row stride ld)
+__global__ void __launch_bounds__(256) simcc_decode_kernel(const float* __restrict__ logits, long ld, int WX, int WY,
+                                                           float split, long rows, float* __restrict__ lv) {
+  const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (row >= rows) return;
+  const float* p = logits + row * ld;
+  float mx[2];
+  int ix[2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const int n = a ? WY : WX, off = a ? WX : 0;
+    float best = -INFINITY;
+    int bi = 0x7fffffff;
+    for (int c = lane; c < n; c += 64) {
+      const float v = p[off + c];
+      if (v > best) { best = v; bi = c; }  // strictly greater: the first index per lane
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const float ob = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+    }
+    mx[a] = best;
+    ix[a] = bi;
+  }
+  if (lane == 0) {
+    const float val = fminf(mx[0], mx[1]);  // max_val_x[mask] = max_val_y[mask] where x > y
+    float lx = (float)ix[0], ly = (float)ix[1];
+    if (val <= 0.f) { lx = -1.f; ly = -1.f; }
+    lv[row * 3 + 0] = lx / split;
+    lv[row * 3 + 1] = ly / split;
+    lv[row * 3 + 2] = val;
+  }
+}
+
+using vge::PoseInst;
+
+__constant__ int c_body18[18] = {0, 17, 6, 8, 10, 5, 7, 9, 12, 14, 16, 11, 13, 15, 2, 1, 4, 3};
+
+// inst_of_frame [F][2]: pose instance of person 0 and of person 1 (-1 when the frame has < 2 persons)
+__global__ void __launch_bounds__(128) kp120_kernel(const float* __restrict__ lv, const PoseInst* __restrict__ inst,
+                                                    const int* __restrict__ inst_of_frame, int F, int K, int in_w,
+                                                    int in_h, int H, int W, float* __restrict__ out) {
+  const int f = blockIdx.x, e = threadIdx.x;
+  if (f >= F || e >= 120) return;
+  const int j = e >> 1, xy = e & 1;
+  int person = 0, wb;
+  if (j < 18) {
+    wb = c_body18[j];
+  } else if (j < 39) {
+    wb = 91 + (j - 18);
+  } else if (inst_of_frame[2 * f + 1] >= 0) {
+    person = 1;
+    wb = 91 + (j - 39);
+  } else {
+    wb = 112 + (j - 39);
+  }
+  const int ii = inst_of_frame[2 * f + person];
+  const PoseInst P = inst[ii];
+  const double in = xy ? (double)in_h : (double)in_w, sc = xy ? (double)P.sh : (double)P.sw;
+  const double ce = xy ? (double)P.cy : (double)P.cx;
+  auto coord = [&](int k) -> double { return (double)lv[((long)ii * K + k) * 3 + xy] / in * sc + ce - sc / 2.0; };
+  double c, s;
+  if (wb == 17) {  // neck: mean of the shoulders; score 1 if both > 0.3 else 0
+    c = (coord(5) + coord(6)) / 2.0;
+    const double s5 = lv[((long)ii * K + 5) * 3 + 2], s6 = lv[((long)ii * K + 6) * 3 + 2];
+    s = (s5 > 0.3 && s6 > 0.3) ? 1.0 : 0.0;
+  } else {
+    c = coord(wb);
+    s = lv[((long)ii * K + wb) * 3 + 2];
+  }
+  c /= xy ? (double)H : (double)W;
+  // dwpose_init.py:45-59: the body rows are copied before `candidate[subset < 0.3] = -1`, so only hand points
+  // are masked
+  out[(long)f * 120 + e] = (j >= 18 && s < 0.3) ? -1.0f : (float)c;
+}
+
+}  // namespace
+
+namespace vge {
+
+hipError_t launch_head_sn_t(const float* y, long ldy, int hw, int K, int Kp, float g, long n_rows, void* out,
+                            hipStream_t s) {
+  if (n_rows == 0) return hipSuccess;
+  hipLaunchKernelGGL(head_sn_t_kernel, dim3((unsigned)((n_rows + 3) / 4)), dim3(256), 0, s, y, ldy, hw, K, Kp, g,
+                     (float)(1.0 / std::sqrt((double)hw)), n_rows, static_cast<bf16*>(out));
+  return hipGetLastError();
+}
+
+hipError_t launch_scalenorm_rows(const float* x, int D, float g, long rows, void* y, hipStream_t s) {
+  if (rows == 0) return hipSuccess;
+  hipLaunchKernelGGL(scalenorm_rows_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, x, D, g,
+                     (float)(1.0 / std::sqrt((double)D)), rows, static_cast<bf16*>(y));
+  return hipGetLastError();
+}
+
+constexpr int GAU_KMAX = 136;
+
+size_t gau_lds_bytes(int S) { return sizeof(float) * ((size_t)GAU_KMAX * (S + 1) + GAU_KMAX * (GAU_KMAX + 1) + 4 * S); }
+
+hipError_t launch_gau_attn(const float* uv, int n_inst, int K, int E, int S, const float* gamma, const float* beta,
+                           void* out, hipStream_t s) {
+  if (n_inst == 0) return hipSuccess;
+  const size_t bytes = gau_lds_bytes(S);
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gau_attn_kernel<GAU_KMAX>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(gau_attn_kernel<GAU_KMAX>, dim3(n_inst), dim3(256), bytes, s, uv, K, E, S, gamma, beta,
+                     (float)std::sqrt((double)S), static_cast<bf16*>(out));
+  return hipGetLastError();
+}
+
+hipError_t launch_simcc_decode(const float* logits, long ld, int WX, int WY, float split, long rows, float* lv,
+                               hipStream_t s) {
+  if (rows == 0) return hipSuccess;
+  hipLaunchKernelGGL(simcc_decode_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, logits, ld, WX, WY, split,
+                     rows, lv);
+  return hipGetLastError();
+}
+
+hipError_t launch_kp120(const float* lv, const void* inst, const int* inst_of_frame, int F, int K, int in_w, int in_h,
+                        int H, int W, float* out, hipStream_t s) {
+  if (F == 0) return hipSuccess;
+  hipLaunchKernelGGL(kp120_kernel, dim3(F), dim3(128), 0, s, lv, static_cast<const PoseInst*>(inst), inst_of_frame, F,
+                     K, in_w, in_h, H, W, out);
+  return hipGetLastError();
+}
+
+}  // namespace vge

@@ -18,7 +18,9 @@ EXPORTS = ["vge_featurize", "vge_stats_workspace_bytes", "vge_stats_accumulate",
            "vge_score_videos", "vge_centroid_accumulate", "vge_centroid_finalize", "vge_last_error", "vge_version",
            "vge_encoder_profile_begin", "vge_encoder_profile_read", "vge_ingest_probe", "vge_ingest_decode",
            "vge_hmr_create", "vge_hmr_reserve", "vge_hmr_destroy", "vge_hmr_extract", "vge_hmr_profile_begin",
-           "vge_hmr_profile_read", "vge_op_gemm_bf16", "vge_op_vit_attention", "vge_op_layernorm_bf16"]
+           "vge_hmr_profile_read", "vge_op_gemm_bf16", "vge_op_vit_attention", "vge_op_layernorm_bf16",
+           "vge_dwpose_create", "vge_dwpose_reserve", "vge_dwpose_destroy", "vge_dwpose_keypoints",
+           "vge_dwpose_profile_begin", "vge_dwpose_profile_read", "vge_op_conv_bf16"]
 
 
 class VgeError(RuntimeError):

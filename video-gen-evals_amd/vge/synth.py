@@ -322,3 +322,75 @@ def make_frames(seed: int, n_frames: int, h: int = 256, w: int = 256) -> np.ndar
         noise = rng.integers(-12, 13, size=(h, w, 3))
         out[f] = np.clip(big[dy:dy + h, dx:dx + w].astype(np.int32) + noise, 0, 255).astype(np.uint8)
     return out
+
+
+def make_rtmpose_state_dict(cfg, seed: int = SEED_WEIGHTS + 20, gain: float = 1.0) -> Dict[str, np.ndarray]:
+    """Deterministic random weights for the DWPose whole-body pose model (vge.dwpose.RtmposeConfig shapes;
+    mmpose RTMPose state_dict keys: CSPNeXt backbone.stem / backbone.stage<i>, RTMCCHead head.*).  No trained
+    weights exist offline (DWPose ships dw-ll_ucoco_384.onnx by download), so the model is measured and
+    parity-checked on these (parity vs the upstream ONNX unpinned).  Conv weights N(0, 2/fan_in) (He init, so
+    SiLU activations stay O(1) through the 40-odd layers), BatchNorm gamma 1 + N(0, 0.1), beta / running mean
+    N(0, 0.1), running var U(0.5, 1.5); head Linears U(-1/sqrt(fan_in), 1/sqrt(fan_in)); GAU gamma/beta
+    N(0, 1) / N(0, 0.1) scaled to keep the squared-ReLU kernel O(1)."""
+    rng = np.random.default_rng(seed)
+    sd: Dict[str, np.ndarray] = {}
+
+    def N(shape, s):
+        return (rng.standard_normal(size=shape, dtype=np.float32) * np.float32(s)).astype(np.float32)
+
+    def U(shape, fan_in):
+        b = np.float32(1.0 / np.sqrt(fan_in))
+        return (rng.random(size=shape, dtype=np.float32) * (2 * b) - b).astype(np.float32)
+
+    def convmod(prefix, cin, cout, k, groups=1):
+        fan = (cin // groups) * k * k
+        sd[prefix + ".conv.weight"] = N((cout, cin // groups, k, k), np.sqrt(gain / fan))
+        sd[prefix + ".bn.weight"] = (1.0 + N((cout,), 0.1)).astype(np.float32)
+        sd[prefix + ".bn.bias"] = N((cout,), 0.1)
+        sd[prefix + ".bn.running_mean"] = N((cout,), 0.1)
+        sd[prefix + ".bn.running_var"] = (0.5 + rng.random(size=(cout,), dtype=np.float32)).astype(np.float32)
+
+    def csp(prefix, cin, cout, n, add_identity):
+        mid = cout // 2
+        convmod(prefix + ".main_conv", cin, mid, 1)
+        convmod(prefix + ".short_conv", cin, mid, 1)
+        convmod(prefix + ".final_conv", 2 * mid, cout, 1)
+        for b in range(n):
+            p = f"{prefix}.blocks.{b}"
+            convmod(p + ".conv1", mid, mid, 3)
+            convmod(p + ".conv2.depthwise_conv", mid, mid, 5, groups=mid)
+            convmod(p + ".conv2.pointwise_conv", mid, mid, 1)
+        sd[prefix + ".attention.fc.weight"] = N((2 * mid, 2 * mid, 1, 1), np.sqrt(1.0 / (2 * mid)))
+        sd[prefix + ".attention.fc.bias"] = N((2 * mid,), 0.1)
+
+    s0 = cfg.stem_ch
+    convmod("backbone.stem.0", 3, s0 // 2, 3)
+    convmod("backbone.stem.1", s0 // 2, s0 // 2, 3)
+    convmod("backbone.stem.2", s0 // 2, s0, 3)
+    cin = s0
+    for i, (cout, n) in enumerate(zip(cfg.stage_ch, cfg.stage_blocks)):
+        st = f"backbone.stage{i + 1}"
+        convmod(st + ".0", cin, cout, 3)
+        j = 1
+        if i == 3:  # SPPBottleneck(5, 9, 13) on the last stage
+            convmod(st + ".1.conv1", cout, cout // 2, 1)
+            convmod(st + ".1.conv2", (cout // 2) * 4, cout, 1)
+            j = 2
+        csp(f"{st}.{j}", cout, cout, n, add_identity=(i < 3))
+        cin = cout
+    K, hw = cfg.keypoints, (cfg.in_h // 32) * (cfg.in_w // 32)
+    fk = cfg.final_k
+    sd["head.final_layer.weight"] = N((K, cin, fk, fk), np.sqrt(1.0 / (cin * fk * fk)))
+    sd["head.final_layer.bias"] = N((K,), 0.1)
+    sd["head.mlp.0.g"] = np.ones((1,), np.float32)
+    sd["head.mlp.1.weight"] = U((cfg.gau_hidden, hw), hw)
+    H, S, E = cfg.gau_hidden, cfg.gau_s, cfg.gau_e
+    sd["head.gau.uv.weight"] = U((2 * E + S, H), H)
+    sd["head.gau.gamma"] = N((2, S), 1.0)
+    sd["head.gau.beta"] = N((2, S), 0.1)
+    sd["head.gau.o.weight"] = U((H, E), E)
+    sd["head.gau.ln.g"] = np.ones((1,), np.float32)
+    sd["head.gau.res_scale.scale"] = (1.0 + N((H,), 0.1)).astype(np.float32)
+    sd["head.cls_x.weight"] = U((cfg.in_w * cfg.split, H), H)
+    sd["head.cls_y.weight"] = U((cfg.in_h * cfg.split, H), H)
+    return sd
