@@ -1,11 +1,13 @@
 """End-to-end workload of bench.py (`--workload e2e`, BASELINE.json configs[2]): 256x256 RGB frames resident in HBM
--> TokenHMR extractor (ViT-H/16 backbone + SMPL token-decoder head, bf16 MFMA; vge_hmr.h) writing the frame store
--> featurise -> fusion encoder (f32x3) -> AC/TC, per step `--clips` 32-frame clips per GPU.
+-> TokenHMR extractor (ViT-H/16 backbone + SMPL token-decoder head, bf16 MFMA; vge_hmr.h) and DWPose keypoints
+(RTMPose-l whole-body, bf16 MFMA implicit-GEMM convs; vge_dwpose.h) writing the frame store -> featurise ->
+fusion encoder (f32x3) -> AC/TC, per step `--clips` 32-frame clips per GPU.
 
 The reference pipeline is extract_mesh.py (TokenHMR per frame, modifications/mesh_generator.py:119-171) + DWPose
-(modifications/process_video.py) -> npz on disk -> eval.py.  Here the frames-to-scores path stays in HBM.  Out of
-this workload: the person detector / crop warp (upstream of the extractor boundary) and DWPose (keypoints are
-synthetic, resident like the frames; parity for both upstream models is unpinned).
+(modifications/process_video.py) -> npz / keypoints.npy on disk -> eval.py.  Here the frames-to-scores path stays
+in HBM.  Person boxes: every synthetic frame takes the no-detection path of onnxpose.preprocess (the whole frame
+is the pose box) and TokenHMR's frames are already person crops, so neither detector runs in this workload
+(parity for the upstream models is unpinned).
 
 Roofline: the backbone GEMM kernel (gemm_bf16_kernel, MFMA bound): achieved = algorithmic FLOPs of every backbone
 GEMM launch / their summed durations (hipEvents recorded around each launch on the extract stream inside the timed
@@ -26,25 +28,32 @@ BF16_MFMA_PEAK_TFLOPS = 2516.6
 
 
 def cpu_baseline_e2e(seconds: float):
+    from oracle.dwpose import OracleRtmpose
     from oracle.hmr import OracleHmr
     from vge import synth
+    from vge.dwpose import RTMPOSE_L
     from vge.hmr import TOKENHMR
     threads = max(1, min(16, len(os.sched_getaffinity(0))))
     torch.set_num_threads(threads)
-    sd = synth.make_hmr_state_dict(TOKENHMR)
-    o = OracleHmr(sd, TOKENHMR, bf16=False)
+    o = OracleHmr(synth.make_hmr_state_dict(TOKENHMR), TOKENHMR, bf16=False)
+    p = OracleRtmpose(synth.make_rtmpose_state_dict(RTMPOSE_L), RTMPOSE_L, bf16=False)
     frames = synth.make_frames(99, 4)
-    n, used = 0, 0.0
-    while used < seconds or n == 0:
+    full = [[0.0, 0.0, 256.0, 256.0]] * frames.shape[0]
+    n, used_h, used_p = 0, 0.0, 0.0
+    while used_h + used_p < seconds or n == 0:
         t0 = time.perf_counter()
         o.forward(frames)
-        used += time.perf_counter() - t0
+        t1 = time.perf_counter()
+        p.simcc(frames, list(range(frames.shape[0])), full)
+        used_p += time.perf_counter() - t1
+        used_h += t1 - t0
         n += frames.shape[0]
-    fps = n / used
+    fps = n / (used_h + used_p)
     return {"value": fps / 32.0, "unit": "videos/s", "cores": threads, "kind": "port",
-            "sample": f"{n} frames through oracle/hmr.py (fp32 torch ViT-H/16 + decoder head, {threads} threads) in "
-                      f"{used:.1f} s = {fps:.3f} frames/s, / 32 frames per clip (the scoring stages, ~450 clips/s on "
-                      f"the same host in the config-2 baseline, are <0.1% of this and not added)"}
+            "sample": f"{n} frames through oracle/hmr.py (fp32 torch ViT-H/16 + decoder head) and oracle/dwpose.py "
+                      f"(fp32 torch RTMPose-l whole-body), {threads} threads, {used_h:.1f} + {used_p:.1f} s = "
+                      f"{fps:.3f} frames/s, / 32 frames per clip (the scoring stages, ~450 clips/s on the same host in "
+                      f"the config-2 baseline, are <0.1% of this and not added)"}
 
 
 def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
@@ -52,6 +61,7 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
     from vge import ops, synth
     from vge.data import ACTION_CLASSES, pack_frame_store
     from vge.dist import shard
+    from vge.dwpose import RTMPOSE_L, DwposeExtractor
     from vge.hmr import TOKENHMR, HmrExtractor
 
     C, T = args.clips, 32
@@ -82,11 +92,13 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
     ops.centroid_accumulate(rseq, y, csum, ccnt)
     centroids = ops.centroid_finalize(allreduce_sum(csum, world), allreduce_sum(ccnt, world))
 
-    # extractor + generated clips: frames and (synthetic, DWPose out of scope) keypoints resident in HBM; the frame
-    # store's SMPL / token arrays are written by the extractor every step
+    # extractors + generated clips: frames resident in HBM; the frame store's SMPL / token arrays (TokenHMR) and
+    # keypoint rows (DWPose, whole-frame boxes) are written by the extractors every step
     hsd = synth.make_hmr_state_dict(TOKENHMR)
     ex = HmrExtractor(hsd, TOKENHMR, device=dev, max_frames=F)
     del hsd
+    dw = DwposeExtractor(synth.make_rtmpose_state_dict(RTMPOSE_L), RTMPOSE_L, device=dev, max_instances=F)
+    no_box = np.zeros(F, np.int32)
     frames = torch.from_numpy(synth.make_frames(1000 + rank, F)).to(dev)
     gen_clips = make_clips(synth.SEED_GEN, rank * C, C, T)
     names = [synth.generated_name(rank * C + i) for i in range(C)]
@@ -102,8 +114,11 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t_setup
 
+    assert tuple(gstore.kp.shape) == (F, 120)
+
     def step():
         ex.extract(frames, out=outs)
+        dw.keypoints(frames, None, no_box, out=gstore.kp)
         ops.featurize(gstore, windows, stats.mean, stats.std, out=feats)
         seq, _, tcw = enc.encode(feats, frame_embed=False, tc=True)
         ac, tc = ops.score_videos(seq, tcw, first, vcls, centroids)
@@ -114,6 +129,7 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
         step()
     torch.cuda.synchronize()
     ex.profile_begin(args.steps)
+    dw.profile_begin(args.steps)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -130,6 +146,7 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
     dt = float(dt_t.item())
     st, ncalls, gemm_flops_per_frame = ex.profile_read()
+    dst, dcalls, dw_flops = dw.profile_read()
     assert np.isfinite(host_ac.numpy()).all() and np.isfinite(host_tc.numpy()).all()
     if rank != 0:
         return None
@@ -148,18 +165,20 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16 (extractor: bf16 operands, f32 accumulate / residual stream) + f32x3 (scorer)",
-        "data": "synthetic 256x256 RGB frames (vge.synth.make_frames) and keypoints; random-init weights of the "
-                "TokenHMR (ViT-H/16 + decoder) and scorer architectures",
-        "config": {"workload": "BASELINE config 3: TokenHMR extract -> featurise -> encoder -> AC/TC, 32-frame 256x256 "
-                               "clips, frames resident in HBM (person detector and DWPose out of scope: keypoints "
-                               "synthetic)", "clips_per_gpu": C, "frames_per_step_per_gpu": F,
+        "data": "synthetic 256x256 RGB frames (vge.synth.make_frames); random-init weights of the TokenHMR "
+                "(ViT-H/16 + decoder), RTMPose-l whole-body and scorer architectures",
+        "config": {"workload": "BASELINE config 3: TokenHMR + DWPose extract -> featurise -> encoder -> AC/TC, "
+                               "32-frame 256x256 clips, frames resident in HBM (no person detector: crops for "
+                               "TokenHMR, whole-frame boxes for DWPose)", "clips_per_gpu": C, "frames_per_step_per_gpu": F,
                    "parallelism": f"video-sharded x{world}"},
         "roofline": {"bound": "mfma", "kernel": "gemm_bf16_kernel (ViT-H/16 backbone: patch-embed, qkv, proj, fc1, "
                                                 "fc2; dense bf16 MFMA peak)",
                      "achieved": achieved, "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / BF16_MFMA_PEAK_TFLOPS, "traffic": None,
                      "flop_per_call": gemm_flops_per_frame * F, "gemm_ms_per_call": gemm_ms},
-        "stage_ms": {k: v / n for k, v in st.items()},
+        "stage_ms": {**{f"hmr_{k}": v / n for k, v in st.items()},
+                     **{f"dwpose_{k}": v / max(dcalls, 1) for k, v in dst.items()}},
+        "dwpose_gemm_tflops": dw_flops / (dst["gemm"] / max(dcalls, 1) * 1e-3) / 1e12,
         "frames_per_s": world * F * args.steps / dt,
         "setup_s": setup_s,
     }
