@@ -70,6 +70,38 @@ int vge_dwpose_keypoints(vge_dwpose* m, const uint8_t* frames, int n_frames, int
 int vge_dwpose_profile_begin(vge_dwpose* m, int max_calls);
 int vge_dwpose_profile_read(vge_dwpose* m, double* stage_ms, int* n_calls, double* gemm_flops_per_call);
 
+/* ---- YOLOX person detector (onnxdet.inference_detector: yolox_l.onnx, 640x640 letterbox) ---------------------
+ * The published YOLOX-L (CSPDarknet + YOLOPAFPN + YOLOXHead, BaseConv = conv + BN(eps 1e-3) + SiLU) restated; only
+ * class 0 (person) is computed, because multiclass_nms is class-aware and inference_detector keeps class 0 with
+ * score > 0.3 only.  Output = what reaches DWPose: the first two persons of the greedy NMS in score order and
+ * min(person count, 2) (0 -> the pose model falls back to the whole frame). */
+typedef struct {
+  int in_size;       /* 640 */
+  int width;         /* base channels: 64 (YOLOX-L, wid_mul 1.0) */
+  int depth;         /* base depth: 3 (dep_mul 1.0; CSP blocks 3, 9, 9, 3) */
+  int head_ch;       /* 256 */
+  int num_classes;   /* 80 (the cls_preds weight shape; only row 0 is used) */
+} vge_yolox_config;
+
+typedef struct vge_yolox vge_yolox;
+
+/* Weights: float32 host views with the YOLOX state_dict keys: backbone.backbone.{stem.conv, dark2..dark5}.*,
+ * backbone.{lateral_conv0, C3_p4, reduce_conv1, C3_p3, bu_conv2, C3_n3, bu_conv1, C3_n4}.*, head.{stems,
+ * cls_convs, reg_convs}.<k>.*, head.{cls_preds, reg_preds, obj_preds}.<k>.{weight,bias}; BaseConv = .conv.weight
+ * + .bn.{weight,bias,running_mean,running_var}. */
+int vge_yolox_create(const vge_yolox_config* cfg, const vge_tensor_view* weights, int n_weights, vge_yolox** out);
+/* frames processed per internal chunk (workspace ~90 MB per frame at 640) */
+int vge_yolox_reserve(vge_yolox* m, int chunk_frames);
+int vge_yolox_destroy(vge_yolox* m);
+/* frames: device uint8 [F][H][W][3] RGB.  boxes: device float [F][2][4] xyxy frame pixels of persons 0 and 1
+ * (zeros where absent); n_persons: device int [F] = min(count, 2).  cand (optional): device float [F][A][5] =
+ * every anchor's decoded box and score (A = 3 * 16^2 * (in_size / 128)^2 ... = 8400 at 640), for tests. */
+int vge_yolox_detect(vge_yolox* m, const uint8_t* frames, int n_frames, int H, int W, float* boxes, int* n_persons,
+                     float* cand, vge_stream_t stream);
+/* stage_ms[0] = convolutions (implicit GEMMs), [1] = letterbox / upsample / pooling / decode + NMS */
+int vge_yolox_profile_begin(vge_yolox* m, int max_calls);
+int vge_yolox_profile_read(vge_yolox* m, double* stage_ms, int* n_calls, double* gemm_flops_per_call);
+
 /* Op-level entry point (parity tests; the kernel every dense layer uses): NHWC bf16 convolution as an implicit
  * GEMM.  x [n_img][H][W][ldx] bf16 (channels 0..Cin-1 used, Cin a power of two >= 8), w [Npad][Kp] bf16 packed
  * k = (kh * KW + kw) * Cin + ci (Kp = KH*KW*Cin rounded up to 32, Npad = Cout rounded up to 128, zero padded),

@@ -31,8 +31,15 @@ hipError_t launch_chan_attn(void* x, long ld, int n_img, int HW, int C, const fl
                             float* att, hipStream_t s);
 hipError_t launch_warp_prep(const uint8_t* frames, int H, int W, const void* inst, int n_inst, int oh, int ow, void* out,
                             hipStream_t s);
-hipError_t launch_letterbox_focus(const uint8_t* frames, int n, int H, int W, int S, int rh, int rw, float inv_r,
-                                  void* out, hipStream_t s);
+hipError_t launch_letterbox_focus(const uint8_t* frames, int n, int H, int W, int S, int rh, int rw, float inv_rx,
+                                  float inv_ry, void* out, hipStream_t s);
+hipError_t launch_upsample2x(const void* x, long ldx, void* y, long ldy, int n_img, int H, int W, int C, hipStream_t s);
+struct DetLevel {      // one YOLOX head level: f32 [n][g*g][8] = reg xywh, obj logit, cls-0 logit
+  const float* out;
+  int grid, stride;
+};
+hipError_t launch_yolox_decode_nms(DetLevel l0, DetLevel l1, DetLevel l2, int F, float ratio, float* boxes, int* n_out,
+                                   float* cand, hipStream_t s);
 hipError_t launch_head_sn_t(const float* y, long ldy, int hw, int K, int Kp, float g, long n_rows, void* out,
                             hipStream_t s);
 hipError_t launch_scalenorm_rows(const float* x, int D, float g, long rows, void* y, hipStream_t s);

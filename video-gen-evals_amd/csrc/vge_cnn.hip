@@ -405,7 +405,8 @@ __global__ void __launch_bounds__(256) warp_prep_kernel(const uint8_t* __restric
 // uint8 values) + YOLOX Focus (channels: [::2, ::2], [1::2, ::2], [::2, 1::2], [1::2, 1::2], 3 each) ->
 // NHWC bf16 [F][S/2][S/2][16] (12 used).  cv2.resize maps dst x to src (x + 0.5) / r - 0.5, clamped.
 __global__ void __launch_bounds__(256) letterbox_focus_kernel(const uint8_t* __restrict__ frames, int n, int H, int W,
-                                                              int S, int rh, int rw, float inv_r, bf16* __restrict__ out) {
+                                                              int S, int rh, int rw, float inv_rx, float inv_ry,
+                                                              bf16* __restrict__ out) {
 #pragma clang fp contract(off)
   const int S2 = S / 2;
   const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -420,7 +421,7 @@ __global__ void __launch_bounds__(256) letterbox_focus_kernel(const uint8_t* __r
     const int yy = 2 * v + dy, xx = 2 * u + dx;
     float val[3] = {114.f, 114.f, 114.f};
     if (yy < rh && xx < rw) {
-      float sx = ((float)xx + 0.5f) * inv_r - 0.5f, sy = ((float)yy + 0.5f) * inv_r - 0.5f;
+      float sx = ((float)xx + 0.5f) * inv_rx - 0.5f, sy = ((float)yy + 0.5f) * inv_ry - 0.5f;
       sx = fmaxf(sx, 0.f);
       sy = fmaxf(sy, 0.f);
       int x0 = (int)floorf(sx), y0 = (int)floorf(sy);
@@ -450,6 +451,20 @@ __global__ void __launch_bounds__(256) letterbox_focus_kernel(const uint8_t* __r
   }
   d[0] = lo;
   d[1] = hi;
+}
+
+// nearest 2x upsample (F.interpolate(scale_factor=2, mode="nearest")) of an NHWC slice into a wider buffer
+__global__ void __launch_bounds__(256) upsample2x_kernel(const bf16* __restrict__ x, long ldx, bf16* __restrict__ y,
+                                                         long ldy, int n_img, int H, int W, int C) {
+  const int cg = C >> 3;
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (long)n_img * 4 * H * W * cg) return;
+  const int c8 = (int)(gid % cg) * 8;
+  const long pix = gid / cg;  // output pixel
+  const int ow = (int)(pix % (2 * W)), oh = (int)((pix / (2 * W)) % (2 * H));
+  const long img = pix / (4L * W * H);
+  *reinterpret_cast<bf16x8*>(y + pix * ldy + c8) =
+      *reinterpret_cast<const bf16x8*>(x + ((img * H + (oh >> 1)) * W + (ow >> 1)) * ldx + c8);
 }
 
 }  // namespace
@@ -567,12 +582,20 @@ hipError_t launch_warp_prep(const uint8_t* frames, int H, int W, const void* ins
   return hipGetLastError();
 }
 
-hipError_t launch_letterbox_focus(const uint8_t* frames, int n, int H, int W, int S, int rh, int rw, float inv_r,
-                                  void* out, hipStream_t s) {
+hipError_t launch_letterbox_focus(const uint8_t* frames, int n, int H, int W, int S, int rh, int rw, float inv_rx,
+                                  float inv_ry, void* out, hipStream_t s) {
   const long tot = (long)n * (S / 2) * (S / 2);
   if (tot == 0) return hipSuccess;
   hipLaunchKernelGGL(letterbox_focus_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, frames, n, H, W, S,
-                     rh, rw, inv_r, static_cast<bf16*>(out));
+                     rh, rw, inv_rx, inv_ry, static_cast<bf16*>(out));
+  return hipGetLastError();
+}
+
+hipError_t launch_upsample2x(const void* x, long ldx, void* y, long ldy, int n_img, int H, int W, int C, hipStream_t s) {
+  const long tot = (long)n_img * 4 * H * W * (C / 8);
+  if (tot == 0) return hipSuccess;
+  hipLaunchKernelGGL(upsample2x_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, static_cast<const bf16*>(x),
+                     ldx, static_cast<bf16*>(y), ldy, n_img, H, W, C);
   return hipGetLastError();
 }
 

@@ -12,48 +12,15 @@
 
 #include "../../include/vge_dwpose.h"
 #include "vge_cnn.h"
+#include "vge_cnn_host.h"
 
-namespace vge {
-void set_last_error(const std::string& msg);  // vge_api.cpp (vge_last_error)
-}
+using namespace vge::cnnh;
+#define HIPCHK VGE_HIPCHK
 
 namespace {
 
 constexpr float BN_EPS = 1e-5f;  // mmpose RTMPose configs: SyncBN, default eps
 
-int fail(int code, const std::string& msg) {
-  vge::set_last_error(msg);
-  return code;
-}
-
-#define HIPCHK(expr)                                                                                    \
-  do {                                                                                                  \
-    hipError_t _e = (expr);                                                                             \
-    if (_e != hipSuccess) return fail(VGE_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e)); \
-  } while (0)
-
-hipStream_t S(vge_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
-int rup(int x, int a) { return (x + a - 1) / a * a; }
-bool pow2(int v) { return v > 0 && (v & (v - 1)) == 0; }
-int pow2_at_least(int v, int lo) {
-  int p = lo;
-  while (p < v) p <<= 1;
-  return p;
-}
-
-uint16_t to_bf16(float f) {  // round to nearest even (torch .to(bfloat16))
-  uint32_t u;
-  memcpy(&u, &f, 4);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0;
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
-}
-
-struct ConvW {  // packed dense conv / Linear: bf16 [Npad][Kp], k = tap * Cinp + ci; bias f32 [Npad]
-  void* w = nullptr;
-  float* b = nullptr;
-  int Cin = 0, Cinp = 0, Cout = 0, KH = 1, KW = 1, Kp = 0, Npad = 0;
-};
 struct DwW {  // depthwise: f32 [K*K][C] + bias
   float* w = nullptr;
   float* b = nullptr;
@@ -81,7 +48,7 @@ struct StageW {
 
 struct vge_dwpose {
   vge_rtmpose_config c{};
-  std::vector<void*> allocs;
+  DevAllocs dev;
   ConvW stem[3];
   StageW st[4];
   ConvW fin, mlp, uv, o, cls;
@@ -114,82 +81,12 @@ struct vge_dwpose {
     if (staged) (void)hipEventSynchronize(staged), (void)hipEventDestroy(staged);
     for (void* p : {pin_w, pin_p, pin_iof})
       if (p) (void)hipHostFree(p);
-    for (void* p : allocs) (void)hipFree(p);
   }
-  void* dmalloc(size_t bytes) {
-    void* p = nullptr;
-    if (hipMalloc(&p, std::max<size_t>(bytes, 256)) != hipSuccess) return nullptr;
-    allocs.push_back(p);
-    return p;
-  }
+  void* dmalloc(size_t bytes) { return dev.dmalloc(bytes); }
+  ConvCtx cx() { return ConvCtx{zero, &gemm_flops}; }
 };
 
 namespace {
-
-struct WeightMap {
-  std::unordered_map<std::string, const vge_tensor_view*> m;
-  std::string missing, badshape;
-  const vge_tensor_view* get(const std::string& k, std::initializer_list<int64_t> shape) {
-    auto it = m.find(k);
-    if (it == m.end()) {
-      if (missing.empty()) missing = k;
-      return nullptr;
-    }
-    const vge_tensor_view* v = it->second;
-    bool ok = v->ndim == (int)shape.size() && v->data;
-    int i = 0;
-    for (int64_t s : shape) ok = ok && v->shape[i++] == s;
-    if (!ok && badshape.empty()) badshape = k;
-    return ok ? v : nullptr;
-  }
-};
-
-template <class T>
-bool upload(vge_dwpose* m, const std::vector<T>& h, T** out) {
-  *out = static_cast<T*>(m->dmalloc(h.size() * sizeof(T)));
-  return *out && hipMemcpy(*out, h.data(), h.size() * sizeof(T), hipMemcpyHostToDevice) == hipSuccess;
-}
-
-// W [Cout][Cin][KH][KW] (f32, already folded) -> bf16 [Npad][Kp] tap-major with Cin padded to Cinp
-bool pack_conv(vge_dwpose* m, const float* W, const float* bias, int Cout, int Cin, int Cinp, int KH, int KW, ConvW& L) {
-  L.Cin = Cin;
-  L.Cinp = Cinp;
-  L.Cout = Cout;
-  L.KH = KH;
-  L.KW = KW;
-  L.Kp = rup(KH * KW * Cinp, 32);
-  L.Npad = rup(Cout, 128);
-  std::vector<uint16_t> h((size_t)L.Npad * L.Kp, 0);
-  for (int n = 0; n < Cout; ++n)
-    for (int ci = 0; ci < Cin; ++ci)
-      for (int t = 0; t < KH * KW; ++t)
-        h[(size_t)n * L.Kp + (size_t)t * Cinp + ci] = to_bf16(W[((size_t)n * Cin + ci) * KH * KW + t]);
-  std::vector<float> b(L.Npad, 0.f);
-  if (bias) memcpy(b.data(), bias, Cout * 4);
-  uint16_t* dw = nullptr;
-  return upload(m, h, &dw) && (L.w = dw) && upload(m, b, &L.b);
-}
-
-// ConvModule: conv.weight + bn.{weight,bias,running_mean,running_var} -> folded (w * s, beta - mean * s)
-#pragma clang fp contract(off)
-bool fold(WeightMap& wm, const std::string& p, int Cout, int Cin_g, int K, std::vector<float>& W, std::vector<float>& b) {
-  const vge_tensor_view* w = wm.get(p + ".conv.weight", {Cout, Cin_g, K, K});
-  const vge_tensor_view* g = wm.get(p + ".bn.weight", {Cout});
-  const vge_tensor_view* be = wm.get(p + ".bn.bias", {Cout});
-  const vge_tensor_view* mu = wm.get(p + ".bn.running_mean", {Cout});
-  const vge_tensor_view* var = wm.get(p + ".bn.running_var", {Cout});
-  if (!w || !g || !be || !mu || !var) return false;
-  const size_t per = (size_t)Cin_g * K * K;
-  W.resize((size_t)Cout * per);
-  b.resize(Cout);
-  for (int n = 0; n < Cout; ++n) {
-    const float s = g->data[n] / std::sqrt(var->data[n] + BN_EPS);
-    for (size_t i = 0; i < per; ++i) W[n * per + i] = w->data[n * per + i] * s;
-    b[n] = be->data[n] - mu->data[n] * s;
-  }
-  return true;
-}
-#pragma clang fp contract(on)
 
 // Two passes over the same load sequence: dry (key / shape checks only, no device work) then real (upload).
 struct Loader {
@@ -199,20 +96,20 @@ struct Loader {
   bool ok = true;
   void convmod(const std::string& p, int Cin, int Cout, int K, ConvW& L, int Cinp = 0) {
     std::vector<float> W, b;
-    if (!ok || !fold(wm, p, Cout, Cin, K, W, b)) return (void)(ok = false);
+    if (!ok || !fold(wm, p, Cout, Cin, K, BN_EPS, W, b)) return (void)(ok = false);
     if (dry) return;
-    ok = pack_conv(m, W.data(), b.data(), Cout, Cin, Cinp ? Cinp : Cin, K, K, L);
+    ok = pack_conv(m->dev, W.data(), b.data(), Cout, Cin, Cinp ? Cinp : Cin, K, K, L);
   }
   void dwmod(const std::string& p, int C, int K, DwW& L) {
     std::vector<float> W, b;
-    if (!ok || !fold(wm, p, C, 1, K, W, b)) return (void)(ok = false);
+    if (!ok || !fold(wm, p, C, 1, K, BN_EPS, W, b)) return (void)(ok = false);
     if (dry) return;
     std::vector<float> t((size_t)K * K * C);
     for (int c = 0; c < C; ++c)
       for (int i = 0; i < K * K; ++i) t[(size_t)i * C + c] = W[(size_t)c * K * K + i];
     L.C = C;
     L.K = K;
-    ok = upload(m, t, &L.w) && upload(m, b, &L.b);
+    ok = upload(m->dev, t, &L.w) && upload(m->dev, b, &L.b);
   }
   void attn(const std::string& p, int C, AttW& L) {
     const vge_tensor_view* w = wm.get(p + ".fc.weight", {C, C, 1, 1});
@@ -223,13 +120,13 @@ struct Loader {
     for (int c = 0; c < C; ++c)
       for (int k = 0; k < C; ++k) t[(size_t)k * C + c] = w->data[(size_t)c * C + k];
     L.C = C;
-    ok = upload(m, t, &L.Wt) && upload(m, bb, &L.b);
+    ok = upload(m->dev, t, &L.Wt) && upload(m->dev, bb, &L.b);
   }
   void linear(const std::string& k, int N, int K, int Kpow2, ConvW& L) {  // no bias, as a 1x1 conv
     const vge_tensor_view* w = wm.get(k, {N, K});
     if (!ok || !w) return (void)(ok = false);
     if (dry) return;
-    ok = pack_conv(m, w->data, nullptr, N, K, Kpow2, 1, 1, L);
+    ok = pack_conv(m->dev, w->data, nullptr, N, K, Kpow2, 1, 1, L);
   }
   void vec(const std::string& k, std::initializer_list<int64_t> shape, size_t npad, float** out) {
     const vge_tensor_view* t = wm.get(k, shape);
@@ -239,7 +136,7 @@ struct Loader {
     for (int64_t s : shape) n *= (size_t)s;
     std::vector<float> h(std::max(n, npad), 0.f);
     memcpy(h.data(), t->data, n * 4);
-    ok = upload(m, h, out);
+    ok = upload(m->dev, h, out);
   }
   float scalar(const std::string& k) {
     const vge_tensor_view* t = wm.get(k, {1});
@@ -266,41 +163,6 @@ bool cfg_ok(const vge_rtmpose_config& c, std::string& why) {
   const int hw = (c.in_h / 32) * (c.in_w / 32);
   if (hw > 256) return why = "head feature map must have <= 256 positions", false;
   return true;
-}
-
-int conv(vge_dwpose* m, const ConvW& L, const void* x, long ldx, int n, int H, int W, int stride, void* out, long ldo,
-         hipStream_t s, int act = 1, int out_f32 = 0, int res_mode = 0, const void* res = nullptr, long ldr = 0,
-         const float* rscale = nullptr) {
-  vge::ConvLaunch c{};
-  c.x = x;
-  c.ldx = ldx;
-  c.w = L.w;
-  c.bias = L.b;
-  c.out = out;
-  c.ldo = ldo;
-  c.res = res;
-  c.ldr = ldr;
-  c.rscale = rscale;
-  c.zero = m->zero;
-  c.n_img = n;
-  c.H = H;
-  c.W = W;
-  c.Cin = L.Cinp;
-  c.KH = L.KH;
-  c.KW = L.KW;
-  c.stride = stride;
-  c.pad = L.KH / 2;
-  c.Kp = L.Kp;
-  c.Cout = L.Cout;
-  c.Npad = L.Npad;
-  c.act = act;
-  c.out_f32 = out_f32;
-  c.res_mode = res_mode;
-  c.tn = L.Cout <= 64 ? 64 : 128;
-  HIPCHK(vge::launch_conv_bf16(c, s));
-  const int Ho = (H + 2 * c.pad - L.KH) / stride + 1, Wo = (W + 2 * c.pad - L.KW) / stride + 1;
-  m->gemm_flops += 2.0 * n * Ho * Wo * (double)L.Cout * L.KH * L.KW * L.Cin;
-  return VGE_OK;
 }
 
 }  // namespace
@@ -355,7 +217,7 @@ void load_all(Loader& ld, const vge_rtmpose_config& c) {
   if (ld.ok) {
     const vge_tensor_view* w = wm.get("head.final_layer.weight", {K, cin, fk, fk});
     const vge_tensor_view* b = wm.get("head.final_layer.bias", {K});
-    ld.ok = w && b && (ld.dry || pack_conv(m, w->data, b->data, K, cin, cin, fk, fk, m->fin));
+    ld.ok = w && b && (ld.dry || pack_conv(m->dev, w->data, b->data, K, cin, cin, fk, fk, m->fin));
   }
   m->mlp_g = ld.scalar("head.mlp.0.g");
   ld.linear("head.mlp.1.weight", H, m->hw, m->hwp, m->mlp);
@@ -373,7 +235,7 @@ void load_all(Loader& ld, const vge_rtmpose_config& c) {
       std::vector<float> Wc((size_t)(WX + WY) * H);
       memcpy(Wc.data(), wx->data, (size_t)WX * H * 4);
       memcpy(Wc.data() + (size_t)WX * H, wy->data, (size_t)WY * H * 4);
-      ld.ok = pack_conv(m, Wc.data(), nullptr, WX + WY, H, H, 1, 1, m->cls);
+      ld.ok = pack_conv(m->dev, Wc.data(), nullptr, WX + WY, H, H, 1, 1, m->cls);
     } else if (!wx || !wy) {
       ld.ok = false;
     }
@@ -381,7 +243,7 @@ void load_all(Loader& ld, const vge_rtmpose_config& c) {
   if (ld.ok && !ld.dry) {
     std::vector<uint16_t> z(128, 0);
     uint16_t* zp = nullptr;
-    ld.ok = upload(m, z, &zp);
+    ld.ok = upload(m->dev, z, &zp);
     m->zero = zp;
   }
 }
@@ -396,9 +258,7 @@ int vge_dwpose_create(const vge_rtmpose_config* cfg, const vge_tensor_view* weig
   std::string why;
   if (!cfg_ok(*cfg, why)) return fail(VGE_ERR_ARG, "vge_dwpose_create: unsupported config: " + why);
   const vge_rtmpose_config c = *cfg;
-  WeightMap wm;
-  for (int i = 0; i < n_weights; ++i)
-    if (weights[i].name) wm.m[weights[i].name] = &weights[i];
+  WeightMap wm(weights, n_weights);
   auto* m = new vge_dwpose();
   m->c = c;
   bool ok_all = true;
@@ -408,11 +268,8 @@ int vge_dwpose_create(const vge_rtmpose_config* cfg, const vge_tensor_view* weig
     ok_all = ld.ok;
   }
   if (!ok_all) {
-    const std::string miss = wm.missing, bad = wm.badshape;
     delete m;
-    if (!miss.empty()) return fail(VGE_ERR_MISSING_WEIGHT, "vge_dwpose_create: missing weight " + miss);
-    if (!bad.empty()) return fail(VGE_ERR_WEIGHT_SHAPE, "vge_dwpose_create: wrong shape for " + bad);
-    return fail(VGE_ERR_HIP, "vge_dwpose_create: device allocation / upload failed");
+    return wm.status("vge_dwpose_create");
   }
   *out = m;
   return VGE_OK;
@@ -577,7 +434,7 @@ int vge_dwpose_keypoints(vge_dwpose* m, const uint8_t* frames, int F, int H, int
 #define CONV(...)            \
   do {                       \
     RC(beg(0));              \
-    RC(conv(m, __VA_ARGS__)); \
+    RC(conv(m->cx(), __VA_ARGS__)); \
     RC(end());               \
   } while (0)
 #define OTHER(kind, expr) \

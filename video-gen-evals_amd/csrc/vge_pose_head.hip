@@ -202,6 +202,121 @@ __global__ void __launch_bounds__(128) kp120_kernel(const float* __restrict__ lv
   out[(long)f * 120 + e] = (j >= 18 && s < 0.3) ? -1.0f : (float)c;
 }
 
+// ------------------------------------------------------------------------------------ YOLOX decode + NMS
+// onnxdet.demo_postprocess + xyxy / ratio + score = sigmoid(obj) * sigmoid(cls0), then the part of the class-aware
+// greedy NMS (+1-pixel IoU, keep if ovr <= 0.45) and the score > 0.3 person filter that can reach DWPose: person 0
+// = the best-scoring anchor above 0.3, person 1 = the best one above 0.3 that person 0 does not suppress.  Ties ->
+// lowest anchor index.  One workgroup per frame.
+struct DetBox {
+  float x0, y0, x1, y1, score;
+};
+
+__device__ __forceinline__ DetBox det_anchor(const vge::DetLevel& L0, const vge::DetLevel& L1, const vge::DetLevel& L2,
+                                             int f, int a, float ratio) {
+#pragma clang fp contract(off)
+  const vge::DetLevel* L = &L0;
+  int i = a;
+  const int a0 = L0.grid * L0.grid, a1 = L1.grid * L1.grid;
+  if (i >= a0) {
+    i -= a0;
+    L = &L1;
+    if (i >= a1) {
+      i -= a1;
+      L = &L2;
+    }
+  }
+  const int g = L->grid;
+  const float* o = L->out + ((long)f * g * g + i) * 8;
+  const int gy = i / g, gx = i - gy * g;
+  const double st = (double)L->stride;
+  const float cx = (float)(((double)o[0] + gx) * st), cy = (float)(((double)o[1] + gy) * st);
+  const float w = (float)((double)expf(o[2]) * st), h = (float)((double)expf(o[3]) * st);
+  DetBox b;
+  b.x0 = (cx - w / 2.0f) / ratio;
+  b.y0 = (cy - h / 2.0f) / ratio;
+  b.x1 = (cx + w / 2.0f) / ratio;
+  b.y1 = (cy + h / 2.0f) / ratio;
+  const float so = 1.0f / (1.0f + expf(-o[4])), sc = 1.0f / (1.0f + expf(-o[5]));
+  b.score = so * sc;
+  return b;
+}
+
+__device__ __forceinline__ float iou_plus1(const DetBox& a, const DetBox& b) {
+#pragma clang fp contract(off)
+  const float area_a = (a.x1 - a.x0 + 1.0f) * (a.y1 - a.y0 + 1.0f);
+  const float area_b = (b.x1 - b.x0 + 1.0f) * (b.y1 - b.y0 + 1.0f);
+  const float w = fmaxf(0.0f, fminf(a.x1, b.x1) - fmaxf(a.x0, b.x0) + 1.0f);
+  const float h = fmaxf(0.0f, fminf(a.y1, b.y1) - fmaxf(a.y0, b.y0) + 1.0f);
+  const float inter = w * h;
+  return inter / (area_a + area_b - inter);
+}
+
+// block argmax of (score, -index) over anchors passing `ok`; 256 threads
+template <class OK>
+__device__ int block_argmax(const vge::DetLevel& L0, const vge::DetLevel& L1, const vge::DetLevel& L2, int f, int A,
+                            float ratio, OK ok, float* s_best, int* s_idx) {
+  float best = -INFINITY;
+  int bi = 0x7fffffff;
+  for (int a = threadIdx.x; a < A; a += blockDim.x) {
+    const DetBox b = det_anchor(L0, L1, L2, f, a, ratio);
+    if (b.score > 0.3f && ok(b, a) && (b.score > best)) {
+      best = b.score;
+      bi = a;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    const float ob = __shfl_xor(best, o, 64);
+    const int oi = __shfl_xor(bi, o, 64);
+    if (ob > best || (ob == best && oi < bi)) { best = ob; bi = oi; }
+  }
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    s_best[wave] = best;
+    s_idx[wave] = bi;
+  }
+  __syncthreads();
+  float b = s_best[0];
+  int idx = s_idx[0];
+  for (int w = 1; w < (int)(blockDim.x >> 6); ++w)
+    if (s_best[w] > b || (s_best[w] == b && s_idx[w] < idx)) { b = s_best[w]; idx = s_idx[w]; }
+  __syncthreads();
+  return b > 0.3f ? idx : -1;
+}
+
+__global__ void __launch_bounds__(256) yolox_decode_nms_kernel(vge::DetLevel L0, vge::DetLevel L1, vge::DetLevel L2,
+                                                               float ratio, float* __restrict__ boxes,
+                                                               int* __restrict__ n_out, float* __restrict__ cand) {
+  __shared__ float s_best[4];
+  __shared__ int s_idx[4];
+  const int f = blockIdx.x;
+  const int A = L0.grid * L0.grid + L1.grid * L1.grid + L2.grid * L2.grid;
+  if (cand)
+    for (int a = threadIdx.x; a < A; a += blockDim.x) {
+      const DetBox b = det_anchor(L0, L1, L2, f, a, ratio);
+      float* c = cand + ((long)f * A + a) * 5;
+      c[0] = b.x0; c[1] = b.y0; c[2] = b.x1; c[3] = b.y1; c[4] = b.score;
+    }
+  const int i0 = block_argmax(L0, L1, L2, f, A, ratio, [](const DetBox&, int) { return true; }, s_best, s_idx);
+  int i1 = -1;
+  if (i0 >= 0) {
+    const DetBox k0 = det_anchor(L0, L1, L2, f, i0, ratio);
+    i1 = block_argmax(L0, L1, L2, f, A, ratio,
+                      [&](const DetBox& b, int a) { return a != i0 && iou_plus1(k0, b) <= 0.45f; }, s_best, s_idx);
+  }
+  if (threadIdx.x < 8) {
+    const int p = threadIdx.x >> 2, c = threadIdx.x & 3;
+    const int ii = p ? i1 : i0;
+    float v = 0.f;
+    if (ii >= 0) {
+      const DetBox b = det_anchor(L0, L1, L2, f, ii, ratio);
+      v = c == 0 ? b.x0 : c == 1 ? b.y0 : c == 2 ? b.x1 : b.y1;
+    }
+    boxes[(long)f * 8 + threadIdx.x] = v;
+  }
+  if (threadIdx.x == 0) n_out[f] = i0 < 0 ? 0 : (i1 < 0 ? 1 : 2);
+}
+
 }  // namespace
 
 namespace vge {
@@ -246,6 +361,13 @@ hipError_t launch_simcc_decode(const float* logits, long ld, int WX, int WY, flo
   if (rows == 0) return hipSuccess;
   hipLaunchKernelGGL(simcc_decode_kernel, dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, s, logits, ld, WX, WY, split,
                      rows, lv);
+  return hipGetLastError();
+}
+
+hipError_t launch_yolox_decode_nms(DetLevel l0, DetLevel l1, DetLevel l2, int F, float ratio, float* boxes, int* n_out,
+                                   float* cand, hipStream_t s) {
+  if (F == 0) return hipSuccess;
+  hipLaunchKernelGGL(yolox_decode_nms_kernel, dim3(F), dim3(256), 0, s, l0, l1, l2, ratio, boxes, n_out, cand);
   return hipGetLastError();
 }
 

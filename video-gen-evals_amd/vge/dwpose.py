@@ -41,6 +41,52 @@ class RtmposeConfig:
 
 RTMPOSE_L = RtmposeConfig()
 
+
+@dataclass(frozen=True)
+class YoloxConfig:
+    in_size: int = 640      # onnxdet.inference_detector input_shape (640, 640)
+    width: int = 64         # YOLOX-L: wid_mul 1.0 -> base channels 64 (dark2..dark5: 128, 256, 512, 1024)
+    depth: int = 3          # YOLOX-L: dep_mul 1.0 -> base depth 3 (CSP blocks 3, 9, 9, 3; PAFPN CSP 3)
+    head_ch: int = 256      # int(256 * width)
+    num_classes: int = 80   # COCO; only class 0 (person) can reach DWPose (class-aware NMS, cls_ind == 0 filter)
+
+
+YOLOX_L = YoloxConfig()
+NMS_THR, SCORE_THR_DET, PERSON_THR = 0.45, 0.1, 0.3   # onnxdet.inference_detector
+
+
+def yolox_flops(cfg: YoloxConfig = YOLOX_L) -> float:
+    """Algorithmic 2 x MACs of every convolution of the detector as libvge runs it (class-0 cls_pred only)."""
+    S, w0, d, hc = cfg.in_size, cfg.width, cfg.depth, cfg.head_ch
+    fl = 0.0
+
+    def cv(hw, cin, cout, k):
+        nonlocal fl
+        fl += 2.0 * hw * cin * cout * k * k
+
+    def csp(hw, cin, cout, n):
+        hid = cout // 2
+        cv(hw, cin, hid, 1); cv(hw, cin, hid, 1); cv(hw, 2 * hid, cout, 1)
+        for _ in range(n):
+            cv(hw, hid, hid, 1); cv(hw, hid, hid, 3)
+
+    s2, s4, s8, s16, s32 = (S // 2) ** 2, (S // 4) ** 2, (S // 8) ** 2, (S // 16) ** 2, (S // 32) ** 2
+    cv(s2, 12, w0, 3)
+    cv(s4, w0, 2 * w0, 3); csp(s4, 2 * w0, 2 * w0, d)
+    cv(s8, 2 * w0, 4 * w0, 3); csp(s8, 4 * w0, 4 * w0, 3 * d)
+    cv(s16, 4 * w0, 8 * w0, 3); csp(s16, 8 * w0, 8 * w0, 3 * d)
+    cv(s32, 8 * w0, 16 * w0, 3); cv(s32, 16 * w0, 8 * w0, 1); cv(s32, 32 * w0, 16 * w0, 1); csp(s32, 16 * w0, 16 * w0, d)
+    c3, c4, c5 = 4 * w0, 8 * w0, 16 * w0
+    cv(s32, c5, c4, 1); csp(s16, 2 * c4, c4, d); cv(s16, c4, c3, 1); csp(s8, 2 * c3, c3, d)
+    cv(s16, c3, c3, 3)  # bu_conv2 (stride 2: output positions at /16)
+    csp(s16, 2 * c3, c4, d); cv(s32, c4, c4, 3); csp(s32, 2 * c4, c5, d)
+    for hw, cin in ((s8, c3), (s16, c4), (s32, c5)):
+        cv(hw, cin, hc, 1)
+        for _ in range(4):
+            cv(hw, hc, hc, 3)
+        cv(hw, hc, 1 + 4 + 1, 1)
+    return fl
+
 MEAN_BGR = (123.675, 116.28, 103.53)   # onnxpose.preprocess normalises the cv2 BGR frame with these, in order
 STD_BGR = (58.395, 57.12, 57.375)
 BBOX_PADDING = 1.25
@@ -93,6 +139,14 @@ class RtmposeConfigC(C.Structure):
                 ("gau_e", C.c_int), ("final_k", C.c_int), ("split", C.c_int)]
 
 
+class YoloxConfigC(C.Structure):
+    _fields_ = [(k, C.c_int) for k in ("in_size", "width", "depth", "head_ch", "num_classes")]
+
+
+def _ycfg_c(cfg: YoloxConfig) -> YoloxConfigC:
+    return YoloxConfigC(cfg.in_size, cfg.width, cfg.depth, cfg.head_ch, cfg.num_classes)
+
+
 def _cfg_c(cfg: RtmposeConfig) -> RtmposeConfigC:
     return RtmposeConfigC(cfg.in_h, cfg.in_w, cfg.stem_ch, (C.c_int * 4)(*cfg.stage_ch),
                           (C.c_int * 4)(*cfg.stage_blocks), cfg.keypoints, cfg.gau_hidden, cfg.gau_s, cfg.gau_e,
@@ -112,6 +166,12 @@ def _sig(lib):
         "vge_dwpose_profile_read": [vp, C.POINTER(C.c_double), C.POINTER(C.c_int), C.POINTER(C.c_double)],
         "vge_op_conv_bf16": [vp, i64, vp, vp, vp, i64, vp, i64, vp, i32, i32, i32, i32, i32, i32, i32, i32, i32, i32,
                              i32, i32, vp],
+        "vge_yolox_create": [C.POINTER(YoloxConfigC), C.POINTER(L.TensorView), i32, C.POINTER(vp)],
+        "vge_yolox_reserve": [vp, i32],
+        "vge_yolox_destroy": [vp],
+        "vge_yolox_detect": [vp, vp, i32, i32, i32, vp, vp, vp, vp],
+        "vge_yolox_profile_begin": [vp, i32],
+        "vge_yolox_profile_read": [vp, C.POINTER(C.c_double), C.POINTER(C.c_int), C.POINTER(C.c_double)],
     }
     for name, args in sig.items():
         f = getattr(lib, name)
@@ -214,6 +274,84 @@ class DwposeExtractor:
             self.close()
         except Exception:
             pass
+
+
+class YoloxDetector:
+    """DWPose's YOLOX person detector resident in HBM (onnxdet.inference_detector restated; person class only)."""
+
+    def __init__(self, state_dict: Dict[str, np.ndarray], cfg: YoloxConfig = YOLOX_L, device="cuda", chunk: int = 32):
+        self.lib = _sig(L.load())
+        self.cfg = cfg
+        self.device = torch.device(device)
+        keep, arr, n = _views(state_dict)
+        h = C.c_void_p()
+        cc = _ycfg_c(cfg)
+        with torch.cuda.device(self.device):
+            L.check(self.lib.vge_yolox_create(C.byref(cc), arr, n, C.byref(h)), "vge_yolox_create")
+            del keep
+            self.h = h
+            L.check(self.lib.vge_yolox_reserve(self.h, int(chunk)), "vge_yolox_reserve")
+
+    @property
+    def anchors(self) -> int:
+        S = self.cfg.in_size
+        return (S // 8) ** 2 + (S // 16) ** 2 + (S // 32) ** 2
+
+    def detect(self, frames: torch.Tensor, cand: Optional[torch.Tensor] = None):
+        """frames uint8 [F, H, W, 3] RGB on the device -> (boxes float [F, 2, 4] xyxy frame pixels of persons 0 and 1,
+        n_persons int32 [F] = min(count, 2)), both on the device (inference_detector's final_boxes, first two)."""
+        if frames.dtype != torch.uint8 or frames.dim() != 4 or frames.shape[3] != 3:
+            raise L.VgeError("frames must be uint8 [F,H,W,3]")
+        F_, H_, W_ = (int(v) for v in frames.shape[:3])
+        boxes = torch.empty((F_, 2, 4), device=frames.device, dtype=torch.float32)
+        npers = torch.empty((F_,), device=frames.device, dtype=torch.int32)
+        L.check(self.lib.vge_yolox_detect(self.h, _ptr(frames), F_, H_, W_, _ptr(boxes), _ptr(npers),
+                                          _ptr(cand) if cand is not None else None, _stream(frames.device)),
+                "vge_yolox_detect")
+        return boxes, npers
+
+    def profile_begin(self, max_calls: int) -> None:
+        L.check(self.lib.vge_yolox_profile_begin(self.h, int(max_calls)), "vge_yolox_profile_begin")
+
+    def profile_read(self):
+        ms = (C.c_double * 2)()
+        n = C.c_int()
+        fl = C.c_double()
+        L.check(self.lib.vge_yolox_profile_read(self.h, ms, C.byref(n), C.byref(fl)), "vge_yolox_profile_read")
+        return {"gemm": ms[0], "other": ms[1]}, n.value, fl.value
+
+    def close(self) -> None:
+        if self.h:
+            self.lib.vge_yolox_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Wholebody:
+    """DWposeDetector's per-frame path (dwpose_init.py:37-69 -> process_video.py:23-57): YOLOX persons -> RTMPose on
+    persons 0 / 1 (whole frame when none) -> keypoints.npy rows [F, 120].  The person counts and boxes cross to the
+    host once per call (the instance table of the pose model), as the reference's numpy NMS output does."""
+
+    def __init__(self, det: YoloxDetector, pose: DwposeExtractor):
+        self.det, self.pose = det, pose
+        self._pin_b = self._pin_n = None
+
+    def __call__(self, frames: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        boxes, npers = self.det.detect(frames)
+        F_ = int(frames.shape[0])
+        if self._pin_b is None or self._pin_b.shape[0] < F_:
+            self._pin_b = torch.empty((F_, 2, 4), dtype=torch.float32, pin_memory=True)
+            self._pin_n = torch.empty((F_,), dtype=torch.int32, pin_memory=True)
+        hb, hn = self._pin_b[:F_], self._pin_n[:F_]
+        hb.copy_(boxes, non_blocking=True)
+        hn.copy_(npers, non_blocking=True)
+        torch.cuda.current_stream(frames.device).synchronize()
+        return self.pose.keypoints(frames, hb.numpy(), hn.numpy(), out=out)
 
 
 # ---- op-level entry point (parity tests) ----------------------------------------------------------

@@ -394,3 +394,70 @@ def make_rtmpose_state_dict(cfg, seed: int = SEED_WEIGHTS + 20, gain: float = 1.
     sd["head.cls_x.weight"] = U((cfg.in_w * cfg.split, H), H)
     sd["head.cls_y.weight"] = U((cfg.in_h * cfg.split, H), H)
     return sd
+
+
+def make_yolox_state_dict(cfg, seed: int = SEED_WEIGHTS + 30, gain: float = 1.0) -> Dict[str, np.ndarray]:
+    """Deterministic random weights for DWPose's YOLOX person detector (vge.dwpose.YoloxConfig shapes; the
+    official YOLOX state_dict keys: backbone.backbone.{stem,dark2..dark5}, backbone.{lateral_conv0, C3_p4,
+    reduce_conv1, C3_p3, bu_conv2, C3_n3, bu_conv1, C3_n4}, head.{stems, cls_convs, reg_convs, cls_preds,
+    reg_preds, obj_preds}).  yolox_l.onnx is a download (no weights offline): parity vs upstream unpinned.
+    BaseConv weights N(0, gain/fan_in) (residual-branch 3x3 convs 0.1 gain/fan_in, so the 9-block CSP stages
+    stay O(1)), BatchNorm as in make_rtmpose_state_dict; prediction convs small, so sigmoid scores spread
+    around the 0.1 / 0.3 thresholds."""
+    rng = np.random.default_rng(seed)
+    sd: Dict[str, np.ndarray] = {}
+
+    def N(shape, s):
+        return (rng.standard_normal(size=shape, dtype=np.float32) * np.float32(s)).astype(np.float32)
+
+    def base(prefix, cin, cout, k, g=1.0):
+        sd[prefix + ".conv.weight"] = N((cout, cin, k, k), np.sqrt(g * gain / (cin * k * k)))
+        sd[prefix + ".bn.weight"] = (1.0 + N((cout,), 0.1)).astype(np.float32)
+        sd[prefix + ".bn.bias"] = N((cout,), 0.1)
+        sd[prefix + ".bn.running_mean"] = N((cout,), 0.1)
+        sd[prefix + ".bn.running_var"] = (0.5 + rng.random(size=(cout,), dtype=np.float32)).astype(np.float32)
+
+    def csp(prefix, cin, cout, n, shortcut):
+        hid = cout // 2
+        base(prefix + ".conv1", cin, hid, 1)
+        base(prefix + ".conv2", cin, hid, 1)
+        base(prefix + ".conv3", 2 * hid, cout, 1)
+        for i in range(n):
+            base(f"{prefix}.m.{i}.conv1", hid, hid, 1)
+            base(f"{prefix}.m.{i}.conv2", hid, hid, 3, 0.1 if shortcut else 1.0)  # small residual branches
+
+    w0, d = cfg.width, cfg.depth
+    bb = "backbone.backbone."
+    base(bb + "stem.conv", 12, w0, 3)
+    base(bb + "dark2.0", w0, 2 * w0, 3)
+    csp(bb + "dark2.1", 2 * w0, 2 * w0, d, True)
+    base(bb + "dark3.0", 2 * w0, 4 * w0, 3)
+    csp(bb + "dark3.1", 4 * w0, 4 * w0, 3 * d, True)
+    base(bb + "dark4.0", 4 * w0, 8 * w0, 3)
+    csp(bb + "dark4.1", 8 * w0, 8 * w0, 3 * d, True)
+    base(bb + "dark5.0", 8 * w0, 16 * w0, 3)
+    base(bb + "dark5.1.conv1", 16 * w0, 8 * w0, 1)
+    base(bb + "dark5.1.conv2", 32 * w0, 16 * w0, 1)
+    csp(bb + "dark5.2", 16 * w0, 16 * w0, d, False)
+    c3, c4, c5 = 4 * w0, 8 * w0, 16 * w0
+    base("backbone.lateral_conv0", c5, c4, 1)
+    csp("backbone.C3_p4", 2 * c4, c4, d, False)
+    base("backbone.reduce_conv1", c4, c3, 1)
+    csp("backbone.C3_p3", 2 * c3, c3, d, False)
+    base("backbone.bu_conv2", c3, c3, 3)
+    csp("backbone.C3_n3", 2 * c3, c4, d, False)
+    base("backbone.bu_conv1", c4, c4, 3)
+    csp("backbone.C3_n4", 2 * c4, c5, d, False)
+    hc = cfg.head_ch
+    for k, cin in enumerate((c3, c4, c5)):
+        base(f"head.stems.{k}", cin, hc, 1)
+        for br in ("cls_convs", "reg_convs"):
+            base(f"head.{br}.{k}.0", hc, hc, 3)
+            base(f"head.{br}.{k}.1", hc, hc, 3)
+        sd[f"head.cls_preds.{k}.weight"] = N((cfg.num_classes, hc, 1, 1), 0.01 * np.sqrt(hc))
+        sd[f"head.cls_preds.{k}.bias"] = N((cfg.num_classes,), 0.5)
+        sd[f"head.reg_preds.{k}.weight"] = N((4, hc, 1, 1), 0.3 / np.sqrt(hc))
+        sd[f"head.reg_preds.{k}.bias"] = N((4,), 0.2)
+        sd[f"head.obj_preds.{k}.weight"] = N((1, hc, 1, 1), 0.01 * np.sqrt(hc))
+        sd[f"head.obj_preds.{k}.bias"] = N((1,), 0.5)
+    return sd
