@@ -5,9 +5,10 @@ fusion encoder (f32x3) -> AC/TC, per step `--clips` 32-frame clips per GPU.
 
 The reference pipeline is extract_mesh.py (TokenHMR per frame, modifications/mesh_generator.py:119-171) + DWPose
 (modifications/process_video.py) -> npz / keypoints.npy on disk -> eval.py.  Here the frames-to-scores path stays
-in HBM.  Person boxes: every synthetic frame takes the no-detection path of onnxpose.preprocess (the whole frame
-is the pose box) and TokenHMR's frames are already person crops, so neither detector runs in this workload
-(parity for the upstream models is unpinned).
+in HBM.  DWPose runs as the reference's Wholebody does: YOLOX-L person detector (640x640 letterbox) -> RTMPose-l on
+persons 0 / 1 (the whole frame when nobody is found) -> keypoints.npy rows; `--no-detector` takes the no-detection
+path for every frame instead.  TokenHMR's frames are already person crops (its detectron2 ViTDet gate is upstream
+of the extractor boundary).  Parity for the upstream models is unpinned.
 
 Roofline: the backbone GEMM kernel (gemm_bf16_kernel, MFMA bound): achieved = algorithmic FLOPs of every backbone
 GEMM launch / their summed durations (hipEvents recorded around each launch on the extract stream inside the timed
@@ -27,16 +28,18 @@ import torch.distributed as dist
 BF16_MFMA_PEAK_TFLOPS = 2516.6
 
 
-def cpu_baseline_e2e(seconds: float):
+def cpu_baseline_e2e(seconds: float, detector: bool = True):
     from oracle.dwpose import OracleRtmpose
     from oracle.hmr import OracleHmr
+    from oracle.yolox import OracleYolox
     from vge import synth
-    from vge.dwpose import RTMPOSE_L
+    from vge.dwpose import RTMPOSE_L, YOLOX_L
     from vge.hmr import TOKENHMR
     threads = max(1, min(16, len(os.sched_getaffinity(0))))
     torch.set_num_threads(threads)
     o = OracleHmr(synth.make_hmr_state_dict(TOKENHMR), TOKENHMR, bf16=False)
     p = OracleRtmpose(synth.make_rtmpose_state_dict(RTMPOSE_L), RTMPOSE_L, bf16=False)
+    y = OracleYolox(synth.make_yolox_state_dict(YOLOX_L), YOLOX_L, bf16=False) if detector else None
     frames = synth.make_frames(99, 4)
     full = [[0.0, 0.0, 256.0, 256.0]] * frames.shape[0]
     n, used_h, used_p = 0, 0.0, 0.0
@@ -44,6 +47,8 @@ def cpu_baseline_e2e(seconds: float):
         t0 = time.perf_counter()
         o.forward(frames)
         t1 = time.perf_counter()
+        if y is not None:
+            y.forward(frames)
         p.simcc(frames, list(range(frames.shape[0])), full)
         used_p += time.perf_counter() - t1
         used_h += t1 - t0
@@ -51,7 +56,8 @@ def cpu_baseline_e2e(seconds: float):
     fps = n / (used_h + used_p)
     return {"value": fps / 32.0, "unit": "videos/s", "cores": threads, "kind": "port",
             "sample": f"{n} frames through oracle/hmr.py (fp32 torch ViT-H/16 + decoder head) and oracle/dwpose.py "
-                      f"(fp32 torch RTMPose-l whole-body), {threads} threads, {used_h:.1f} + {used_p:.1f} s = "
+                      f"({'fp32 torch YOLOX-L + ' if y is not None else ''}RTMPose-l whole-body), {threads} threads, "
+                      f"{used_h:.1f} + {used_p:.1f} s = "
                       f"{fps:.3f} frames/s, / 32 frames per clip (the scoring stages, ~450 clips/s on the same host in "
                       f"the config-2 baseline, are <0.1% of this and not added)"}
 
@@ -61,7 +67,7 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
     from vge import ops, synth
     from vge.data import ACTION_CLASSES, pack_frame_store
     from vge.dist import shard
-    from vge.dwpose import RTMPOSE_L, DwposeExtractor
+    from vge.dwpose import RTMPOSE_L, YOLOX_L, DwposeExtractor, Wholebody, YoloxDetector
     from vge.hmr import TOKENHMR, HmrExtractor
 
     C, T = args.clips, 32
@@ -97,7 +103,10 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
     hsd = synth.make_hmr_state_dict(TOKENHMR)
     ex = HmrExtractor(hsd, TOKENHMR, device=dev, max_frames=F)
     del hsd
-    dw = DwposeExtractor(synth.make_rtmpose_state_dict(RTMPOSE_L), RTMPOSE_L, device=dev, max_instances=F)
+    dw = DwposeExtractor(synth.make_rtmpose_state_dict(RTMPOSE_L), RTMPOSE_L, device=dev, max_instances=2 * F)
+    det = None if args.no_detector else YoloxDetector(synth.make_yolox_state_dict(YOLOX_L), YOLOX_L, device=dev,
+                                                      chunk=min(F, 64))
+    wholebody = Wholebody(det, dw) if det is not None else None
     no_box = np.zeros(F, np.int32)
     frames = torch.from_numpy(synth.make_frames(1000 + rank, F)).to(dev)
     gen_clips = make_clips(synth.SEED_GEN, rank * C, C, T)
@@ -118,7 +127,10 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
 
     def step():
         ex.extract(frames, out=outs)
-        dw.keypoints(frames, None, no_box, out=gstore.kp)
+        if wholebody is not None:
+            wholebody(frames, out=gstore.kp)
+        else:
+            dw.keypoints(frames, None, no_box, out=gstore.kp)
         ops.featurize(gstore, windows, stats.mean, stats.std, out=feats)
         seq, _, tcw = enc.encode(feats, frame_embed=False, tc=True)
         ac, tc = ops.score_videos(seq, tcw, first, vcls, centroids)
@@ -130,6 +142,8 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
     torch.cuda.synchronize()
     ex.profile_begin(args.steps)
     dw.profile_begin(args.steps)
+    if det is not None:
+        det.profile_begin(args.steps)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -147,6 +161,7 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
     dt = float(dt_t.item())
     st, ncalls, gemm_flops_per_frame = ex.profile_read()
     dst, dcalls, dw_flops = dw.profile_read()
+    yst, ycalls, y_flops = det.profile_read() if det is not None else ({}, 0, 0.0)
     assert np.isfinite(host_ac.numpy()).all() and np.isfinite(host_tc.numpy()).all()
     if rank != 0:
         return None
@@ -166,10 +181,11 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
         "vs_baseline": None,
         "dtype": "bf16 (extractor: bf16 operands, f32 accumulate / residual stream) + f32x3 (scorer)",
         "data": "synthetic 256x256 RGB frames (vge.synth.make_frames); random-init weights of the TokenHMR "
-                "(ViT-H/16 + decoder), RTMPose-l whole-body and scorer architectures",
-        "config": {"workload": "BASELINE config 3: TokenHMR + DWPose extract -> featurise -> encoder -> AC/TC, "
-                               "32-frame 256x256 clips, frames resident in HBM (no person detector: crops for "
-                               "TokenHMR, whole-frame boxes for DWPose)", "clips_per_gpu": C, "frames_per_step_per_gpu": F,
+                "(ViT-H/16 + decoder), YOLOX-L, RTMPose-l whole-body and scorer architectures",
+        "config": {"workload": "BASELINE config 3: TokenHMR + DWPose (YOLOX-L + RTMPose-l) extract -> featurise -> "
+                               "encoder -> AC/TC, 32-frame 256x256 clips, frames resident in HBM (TokenHMR frames are "
+                               "person crops)" + (" [--no-detector: whole-frame pose boxes]" if det is None else ""),
+                   "clips_per_gpu": C, "frames_per_step_per_gpu": F,
                    "parallelism": f"video-sharded x{world}"},
         "roofline": {"bound": "mfma", "kernel": "gemm_bf16_kernel (ViT-H/16 backbone: patch-embed, qkv, proj, fc1, "
                                                 "fc2; dense bf16 MFMA peak)",
@@ -177,10 +193,12 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
                      "frac": achieved / BF16_MFMA_PEAK_TFLOPS, "traffic": None,
                      "flop_per_call": gemm_flops_per_frame * F, "gemm_ms_per_call": gemm_ms},
         "stage_ms": {**{f"hmr_{k}": v / n for k, v in st.items()},
-                     **{f"dwpose_{k}": v / max(dcalls, 1) for k, v in dst.items()}},
+                     **{f"dwpose_{k}": v / max(dcalls, 1) for k, v in dst.items()},
+                     **{f"yolox_{k}": v / max(ycalls, 1) for k, v in yst.items()}},
+        "yolox_gemm_tflops": (y_flops / (yst["gemm"] / ycalls * 1e-3) / 1e12) if ycalls else None,
         "dwpose_gemm_tflops": dw_flops / (dst["gemm"] / max(dcalls, 1) * 1e-3) / 1e12,
         "frames_per_s": world * F * args.steps / dt,
         "setup_s": setup_s,
     }
-    out["cpu_baseline"] = None if (world > 1 or args.no_cpu_baseline) else cpu_baseline_e2e(args.cpu_seconds)
+    out["cpu_baseline"] = None if (world > 1 or args.no_cpu_baseline) else cpu_baseline_e2e(args.cpu_seconds, det is not None)
     return out

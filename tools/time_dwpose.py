@@ -18,6 +18,8 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--frames", type=int, default=256)
 ap.add_argument("--iters", type=int, default=5)
 ap.add_argument("--persons", type=int, default=0, help="persons per frame (0 = whole-frame box)")
+ap.add_argument("--detector", action="store_true", help="also time the YOLOX-L detector on the same frames")
+ap.add_argument("--chunk", type=int, default=64)
 a = ap.parse_args()
 cfg = D.RTMPOSE_L
 t0 = time.time()
@@ -41,3 +43,18 @@ print(json.dumps({"frames": a.frames, "instances": inst, "ms_per_call": dt * 1e3
                   "stage_ms": {k: v / n for k, v in st.items()},
                   "gemm_tflops": fl / (st["gemm"] / n * 1e-3) / 1e12, "gflop_per_instance": fl / inst / 1e9,
                   "setup_s": setup, "finite": bool(torch.isfinite(out).all())}))
+if a.detector:
+    det = D.YoloxDetector(synth.make_yolox_state_dict(D.YOLOX_L), D.YOLOX_L, device="cuda:0", chunk=a.chunk)
+    det.detect(frames)
+    torch.cuda.synchronize()
+    det.profile_begin(a.iters)
+    t = time.perf_counter()
+    for _ in range(a.iters):
+        b, n = det.detect(frames)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t) / a.iters
+    st, nc, fl = det.profile_read()
+    print(json.dumps({"detector": "yolox_l", "frames": a.frames, "chunk": a.chunk, "ms_per_call": dt * 1e3,
+                      "frames_per_s": a.frames / dt, "stage_ms": {k: v / nc for k, v in st.items()},
+                      "gemm_tflops": fl / (st["gemm"] / nc * 1e-3) / 1e12, "gflop_per_frame": fl / a.frames / 1e9,
+                      "persons": np.bincount(n.cpu().numpy(), minlength=3).tolist()}))
