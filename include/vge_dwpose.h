@@ -104,7 +104,7 @@ int vge_yolox_profile_read(vge_yolox* m, double* stage_ms, int* n_calls, double*
 
 /* Op-level entry point (parity tests; the kernel every dense layer uses): NHWC bf16 convolution as an implicit
  * GEMM.  x [n_img][H][W][ldx] bf16 (channels 0..Cin-1 used, Cin a power of two >= 8), w [Npad][Kp] bf16 packed
- * k = (kh * KW + kw) * Cin + ci (Kp = KH*KW*Cin rounded up to 32, Npad = Cout rounded up to 128, zero padded),
+ * k = (kh * KW + kw) * Cin + ci (Kp = KH*KW*Cin rounded up to 32, Npad = Cout rounded up to 256, zero padded),
  * bias [Npad] f32, out [n_img][Ho][Wo][ldo].  act: 0 none, 1 SiLU, 2 sigmoid; out_f32: 0 bf16 (Cout % 8 == 0),
  * 1 f32; res_mode: 0 none, 1 bf16 residual [M][ldr] added after the activation, 2 f32 residual x rscale[col]. */
 int vge_op_conv_bf16(const void* x, long ldx, const void* w, const float* bias, void* out, long ldo, const void* res,

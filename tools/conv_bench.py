@@ -1,0 +1,63 @@
+"""Time conv_bf16 (the DWPose / YOLOX implicit-GEMM conv) on representative layer shapes: v2 (256-row tiles, default
+for Cout > 64) vs v1 (128-row tiles) vs torch/MIOpen conv2d (bf16, channels_last).  python tools/conv_bench.py"""
+import ctypes as C
+import json
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "video-gen-evals_amd"))
+import torch  # noqa: E402
+
+from vge import dwpose as D, lib as L  # noqa: E402
+
+SHAPES = [  # name, n, H, W, Cin, Cout, k, stride
+    ("yolox_head0_fused_3x3", 64, 80, 80, 256, 512, 3, 1),
+    ("yolox_dark3_bneck_3x3", 64, 80, 80, 128, 128, 3, 1),
+    ("yolox_dark4_bneck_3x3", 64, 40, 40, 256, 256, 3, 1),
+    ("yolox_dark3_down_3x3s2", 64, 160, 160, 128, 256, 3, 2),
+    ("yolox_1x1_256_128", 64, 80, 80, 256, 128, 1, 1),
+    ("rtm_stage1_3x3_64", 256, 96, 72, 64, 64, 3, 1),
+    ("rtm_stem2_3x3_32_64", 256, 192, 144, 32, 64, 3, 1),
+    ("rtm_final_7x7", 256, 12, 9, 1024, 133, 7, 1),
+]
+
+
+def timeit(fn, iters=10):
+    fn()
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(iters):
+        fn()
+    b.record()
+    torch.cuda.synchronize()
+    return a.elapsed_time(b) / iters
+
+
+lib = L.load()
+lib.vge_debug_set_conv_v1.argtypes = [C.c_int]
+res = []
+for name, n, H, W, Cin, Cout, k, st in SHAPES:
+    x = torch.randn(n, H, W, Cin, device="cuda").to(torch.bfloat16)
+    w = (torch.randn(Cout, Cin, k, k, device="cuda") * (2.0 / (Cin * k * k)) ** 0.5)
+    b = torch.zeros(Cout, device="cuda")
+    Ho, Wo = (H + 2 * (k // 2) - k) // st + 1, (W + 2 * (k // 2) - k) // st + 1
+    out_f32 = Cout % 8 != 0
+    out = torch.empty(n, Ho, Wo, Cout, device="cuda", dtype=torch.float32 if out_f32 else torch.bfloat16)
+    fl = 2.0 * n * Ho * Wo * Cout * Cin * k * k
+    r = {"shape": name, "gflop": fl / 1e9}
+    for v1 in (0, 1):
+        lib.vge_debug_set_conv_v1(v1)
+        ms = timeit(lambda: D.conv_bf16(x, w, b, stride=st, pad=k // 2, act="none" if out_f32 else "silu",
+                                        out_f32=out_f32, out=out))
+        r["v1" if v1 else "v2"] = {"ms": ms, "tflops": fl / ms / 1e9}
+    lib.vge_debug_set_conv_v1(0)
+    xc = x.permute(0, 3, 1, 2)  # NCHW view of NHWC memory = channels_last
+    wc = w.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    try:
+        ms = timeit(lambda: torch.nn.functional.conv2d(xc, wc, None, st, k // 2))
+        r["miopen"] = {"ms": ms, "tflops": fl / ms / 1e9}
+    except Exception as e:  # noqa: BLE001
+        r["miopen"] = str(e)[:80]
+    print(json.dumps(r), flush=True)

@@ -21,6 +21,8 @@
 #include "vge_common.h"
 #include "vge_cnn.h"
 
+#include <cstdlib>
+
 namespace {
 
 typedef __bf16 bf16;
@@ -209,6 +211,199 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
       }
     }
     __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------------------------ conv v2 (wide tiles)
+// The same implicit GEMM on 256 x BN tiles with 8 waves and gemm_bf16_kernel's schedule (vge_vit.hip): 32-deep
+// stages in a 5-slot ring with three stages in flight (counted vmcnt, one barrier per stage), the next stage's
+// fragments read into a second register set while the current one's MFMAs run, loads and LDS reads interleaved
+// between the MFMAs (sched_group_barrier).  BN 256: waves 2 (M) x 4 (N) of 128 x 64; BN 128: 4 x 2 of 64 x 64.
+// Epilogue through LDS (wave-private 64-row chunks re-read row-major, 4 columns per lane).
+constexpr int C2_M = 256, C2_ST = 5;
+
+template <int BN>
+struct C2Cfg {
+  static constexpr int WM = BN == 256 ? 2 : 4, WN = 8 / WM;
+  static constexpr int WR = C2_M / WM, WC = BN / WN;          // wave tile
+  static constexpr int TM = WR / 32, TN = WC / 32;            // 32x32 MFMA tiles per wave
+  static constexpr int TA = C2_M * CV_K * 2, TB = BN * CV_K * 2, SLOT = TA + TB;
+  static constexpr int BQ = BN / 128;                         // B wave-instructions per wave per stage
+  static constexpr int LPS = 2 + BQ;                          // global_load_lds per thread per stage
+  static constexpr int RING = C2_ST * SLOT, EPI = 8 * 64 * WC * 4;
+  static constexpr int LDS = RING > EPI ? RING : EPI;
+};
+
+template <int BN, int ACT, int OUT, int RES>
+__global__ void __launch_bounds__(512, 1) conv2_bf16_kernel(ConvArgs a) {
+  using Cf = C2Cfg<BN>;
+  constexpr int TM = Cf::TM, TN = Cf::TN, LPS = Cf::LPS, BQ = Cf::BQ;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / Cf::WN, wn = wave % Cf::WN;
+  const int ntn = (a.Cout + BN - 1) / BN;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int mt = bid / ntn, nt = bid - mt * ntn;
+  const int m0 = mt * C2_M, n0 = nt * BN;
+  const int nk = a.Kp / CV_K;
+  const int cmask = (1 << a.cin_log2) - 1;
+  const int lc = (lane & 3) ^ ((lane >> 4) & 3);
+  int img_hw[2], ih0[2], iw0[2];
+  bool mval[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int m = m0 + 16 * (2 * wave + j) + (lane >> 2);
+    mval[j] = m < a.M;
+    const int hw = a.Ho * a.Wo;
+    const int img = m / hw, rem = m - img * hw;
+    const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
+    img_hw[j] = img * a.H;
+    ih0[j] = oh * a.stride - a.pad;
+    iw0[j] = ow * a.stride - a.pad;
+  }
+  const bf16* wrow[BQ];
+#pragma unroll
+  for (int j = 0; j < BQ; ++j) wrow[j] = a.w + (size_t)(n0 + 16 * (BQ * wave + j) + (lane >> 2)) * a.Kp + lc * 8;
+
+  auto issue = [&](int st) {
+    char* slot = lds + (st % C2_ST) * Cf::SLOT;
+    const int k = st * CV_K + lc * 8;
+    const int tap = k >> a.cin_log2, ci = k & cmask;
+    const int kh = (tap * a.kw_magic) >> 16, kw = tap - kh * a.KW;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ih = ih0[j] + kh, iw = iw0[j] + kw;
+      const bool ok = mval[j] && tap < a.taps && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      glds16(ok ? a.x + ((size_t)(img_hw[j] + ih) * a.W + iw) * a.ldx + ci : a.zero, slot + (2 * wave + j) * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < BQ; ++j) glds16(wrow[j] + st * CV_K, slot + Cf::TA + (BQ * wave + j) * 1024);
+  };
+  const int h = lane >> 5, swz = (lane >> 2) & 3, rowoff = (lane & 31) * 64;
+  struct Frag {
+    bf16x8 a[2][TM], b[2][TN];
+  };
+  auto read = [&](int st, Frag& f) {
+    const char* cur = lds + (st % C2_ST) * Cf::SLOT;
+    const char* As = cur + wm * Cf::WR * 64 + rowoff;
+    const char* Bs = cur + Cf::TA + wn * Cf::WC * 64 + rowoff;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int co = ((2 * s + h) ^ swz) * 16;
+#pragma unroll
+      for (int t = 0; t < TM; ++t) f.a[s][t] = *reinterpret_cast<const bf16x8*>(As + t * 32 * 64 + co);
+#pragma unroll
+      for (int u = 0; u < TN; ++u) f.b[s][u] = *reinterpret_cast<const bf16x8*>(Bs + u * 32 * 64 + co);
+    }
+  };
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int t = 0; t < TM; ++t)
+#pragma unroll
+    for (int u = 0; u < TN; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
+  auto mma = [&](const Frag& f, int s) {
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int u = 0; u < TN; ++u)
+        acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[s][t], f.b[s][u], acc[t][u], 0, 0, 0);
+  };
+  constexpr int NM = TM * TN;  // MFMAs per 16-k half-stage
+  auto step = [&](int kt, Frag& cur, Frag& nxt) {
+    vmcnt_b<2 * LPS>();  // stage kt + 1 landed (kt + 2, kt + 3 in flight)
+    lds_barrier_b();
+    issue(min(kt + 4, nk - 1));  // past the end: the last stage again, into its own slot (same bytes)
+    read(min(kt + 1, nk - 1), nxt);
+    mma(cur, 0);
+    mma(cur, 1);
+#pragma unroll
+    for (int j = 0; j < LPS; ++j) {
+      __builtin_amdgcn_sched_group_barrier(0x008, NM / LPS > 0 ? NM / LPS : 1, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                            // VMEM (global_load_lds)
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      __builtin_amdgcn_sched_group_barrier(0x008, NM / 4 > 0 ? NM / 4 : 1, 0);      // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, (2 * (TM + TN) + 3) / 4, 0);     // DS read
+    }
+  };
+  for (int st = 0; st < C2_ST - 1; ++st) issue(min(st, nk - 1));
+  vmcnt_b<3 * LPS>();  // stage 0 landed
+  lds_barrier_b();
+  Frag f0, f1;
+  read(0, f0);
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    step(kt, f0, f1);
+    step(kt + 1, f1, f0);
+  }
+  if (kt < nk) step(kt, f0, f1);
+
+  // epilogue: each wave stages 64-row chunks of its tile (C layout) in its private LDS region and re-reads them
+  // row-major, 4 columns per lane (in-order LDS: no barrier between a wave's own stores and loads)
+  vmcnt_b<0>();
+  lds_barrier_b();
+  constexpr int WC = Cf::WC, RPI = 256 / WC;  // rows per read instruction
+  float* my = reinterpret_cast<float*>(lds) + wave * (64 * WC);
+  const int lr = lane / (WC / 4), c4 = (lane % (WC / 4)) * 4;
+  const int gcol = n0 + wn * WC + c4;
+  const floatx4 bb = *reinterpret_cast<const floatx4*>(a.bias + gcol);
+  floatx4 rsc = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (RES == RES_F32S) rsc = *reinterpret_cast<const floatx4*>(a.rscale + gcol);
+#pragma unroll
+  for (int half = 0; half < TM / 2; ++half) {
+#pragma unroll
+    for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+      for (int u = 0; u < TN; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          my[(tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * WC + u * 32 + (lane & 31)] = acc[2 * half + tt][u][r];
+#pragma unroll 4
+    for (int it = 0; it < 64 / RPI; ++it) {
+      const int rl = it * RPI + lr;
+      const int m = m0 + wm * Cf::WR + half * 64 + rl;
+      floatx4 v = *reinterpret_cast<const floatx4*>(my + rl * WC + c4) + bb;
+      if (m >= a.M || gcol >= a.Cout) continue;
+      float e[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if constexpr (ACT == ACT_SILU) e[i] = silu(e[i]);
+        if constexpr (ACT == ACT_SIGMOID) e[i] = sigm(e[i]);
+      }
+      if constexpr (RES == RES_BF16) {
+        typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+        const bf16x4_t r4 = *reinterpret_cast<const bf16x4_t*>(reinterpret_cast<const bf16*>(a.res) + (size_t)m * a.ldr + gcol);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) e[i] += (float)r4[i];
+      }
+      if constexpr (RES == RES_F32S) {
+        const floatx4 r4 = *reinterpret_cast<const floatx4*>(reinterpret_cast<const float*>(a.res) + (size_t)m * a.ldr + gcol);
+        e[0] = fmaf(rsc.x, r4.x, e[0]);
+        e[1] = fmaf(rsc.y, r4.y, e[1]);
+        e[2] = fmaf(rsc.z, r4.z, e[2]);
+        e[3] = fmaf(rsc.w, r4.w, e[3]);
+      }
+      if constexpr (OUT == OUT_BF16) {
+        typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+        bf16x4_t o;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) o[i] = (bf16)e[i];
+        *reinterpret_cast<bf16x4_t*>(reinterpret_cast<bf16*>(a.out) + (size_t)m * a.ldo + gcol) = o;
+      } else {
+        float* o = reinterpret_cast<float*>(a.out) + (size_t)m * a.ldo + gcol;
+        if (gcol + 4 <= a.Cout && (a.ldo & 3) == 0) {
+          *reinterpret_cast<floatx4*>(o) = floatx4{e[0], e[1], e[2], e[3]};
+        } else {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (gcol + i < a.Cout) o[i] = e[i];
+        }
+      }
+    }
   }
 }
 
@@ -478,8 +673,32 @@ static int ilog2(int v) {
   return l;
 }
 
+template <int BN, int ACT, int OUT, int RES>
+static hipError_t conv2_go(const ConvArgs& a, hipStream_t s) {
+  constexpr int BYTES = C2Cfg<BN>::LDS;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv2_bf16_kernel<BN, ACT, OUT, RES>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, BYTES);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int grid = ((a.M + C2_M - 1) / C2_M) * ((a.Cout + BN - 1) / BN);
+  hipLaunchKernelGGL((conv2_bf16_kernel<BN, ACT, OUT, RES>), dim3(grid), dim3(512), BYTES, s, a);
+  return hipGetLastError();
+}
+
+static int g_conv_v1 = -1;  // VGE_CONV_V1=1: every layer on the 128-row kernel (A/B timing)
+
 template <int TN, int ACT, int OUT, int RES>
 static hipError_t conv_go(const ConvArgs& a, int grid, hipStream_t s) {
+  if (g_conv_v1 < 0) {
+    const char* e = getenv("VGE_CONV_V1");
+    g_conv_v1 = (e && atoi(e) == 1) ? 1 : 0;
+  }
+  if constexpr (TN == 256) {
+    return g_conv_v1 ? conv_go<128, ACT, OUT, RES>(a, grid, s) : conv2_go<256, ACT, OUT, RES>(a, s);
+  } else {
   constexpr int LDS = CV_ST * (CV_M * CV_K * 2 + TN * CV_K * 2);
   constexpr int EPI = 64 * (TN + 4) * 4;
   constexpr int BYTES = LDS > EPI ? LDS : EPI;
@@ -492,6 +711,7 @@ static hipError_t conv_go(const ConvArgs& a, int grid, hipStream_t s) {
   }
   hipLaunchKernelGGL((conv_bf16_kernel<TN, ACT, OUT, RES>), dim3(grid), dim3(256), BYTES, s, a);
   return hipGetLastError();
+  }
 }
 
 hipError_t launch_conv_bf16(const ConvLaunch& c, hipStream_t s) {
@@ -519,12 +739,14 @@ hipError_t launch_conv_bf16(const ConvLaunch& c, hipStream_t s) {
   a.Kp = c.Kp;
   a.Cout = c.Cout;
   a.M = c.n_img * a.Ho * a.Wo;
-  const int grid = ((a.M + CV_M - 1) / CV_M) * ((c.Cout + c.tn - 1) / c.tn);
+  const int tn1 = c.tn > 128 ? 128 : c.tn;  // v1 grid (the tn 256 case runs conv2 with its own grid)
+  const int grid = ((a.M + CV_M - 1) / CV_M) * ((c.Cout + tn1 - 1) / tn1);
   if (a.M <= 0) return hipSuccess;
 #define VGE_CONV_CASE(ACT, OUT, RES)                                                              \
   if (c.act == ACT && c.out_f32 == OUT && c.res_mode == RES)                                      \
-    return c.tn == 64 ? conv_go<64, ACT, OUT, RES>(a, grid, s) : conv_go<128, ACT, OUT, RES>(a, grid, s);
-  if (c.tn != 64 && c.tn != 128) return hipErrorInvalidValue;
+    return c.tn == 64 ? conv_go<64, ACT, OUT, RES>(a, grid, s)                                    \
+                      : c.tn == 128 ? conv_go<128, ACT, OUT, RES>(a, grid, s) : conv_go<256, ACT, OUT, RES>(a, grid, s);
+  if (c.tn != 64 && c.tn != 128 && c.tn != 256) return hipErrorInvalidValue;
   VGE_CONV_CASE(ACT_SILU, OUT_BF16, RES_NONE)
   VGE_CONV_CASE(ACT_SILU, OUT_BF16, RES_BF16)
   VGE_CONV_CASE(ACT_NONE, OUT_BF16, RES_NONE)
@@ -600,3 +822,8 @@ hipError_t launch_upsample2x(const void* x, long ldx, void* y, long ldy, int n_i
 }
 
 }  // namespace vge
+
+extern "C" int vge_debug_set_conv_v1(int on) {  // A/B timing (tools/conv_bench.py)
+  vge::g_conv_v1 = on ? 1 : 0;
+  return 0;
+}

@@ -110,7 +110,7 @@ inline bool pack_conv(DevAllocs& d, const float* W, const float* bias, int Cout,
   L.KH = KH;
   L.KW = KW;
   L.Kp = rup(KH * KW * Cinp, 32);
-  L.Npad = rup(Cout, 128);
+  L.Npad = rup(Cout, 256);  // conv2_bf16_kernel reads 256-row weight tiles
   std::vector<uint16_t> h((size_t)L.Npad * L.Kp, 0);
   for (int n = 0; n < Cout; ++n)
     for (int ci = 0; ci < Cin; ++ci)
@@ -147,10 +147,28 @@ inline bool fold(WeightMap& wm, const std::string& p, int Cout, int Cin_g, int K
 }
 #pragma clang fp contract(on)
 
+// two ConvModules / BaseConvs over the same input (CSP main + short 1x1s) as ONE conv with both weight sets along
+// Cout: output channels [first | second] = the CSP concat order, written straight into the concat buffer
+inline bool fold_pair(WeightMap& wm, const std::string& p0, const std::string& p1, int Cout, int Cin, int K, float eps,
+                      std::vector<float>& W, std::vector<float>& b) {
+  std::vector<float> W1, b1;
+  if (!fold(wm, p0, Cout, Cin, K, eps, W, b) || !fold(wm, p1, Cout, Cin, K, eps, W1, b1)) return false;
+  W.insert(W.end(), W1.begin(), W1.end());
+  b.insert(b.end(), b1.begin(), b1.end());
+  return true;
+}
+
 struct ConvCtx {
   const void* zero;      // >= 16 B of device zeros (padding taps)
   double* flops;         // accumulates algorithmic 2 x MACs of every launch
 };
+
+// output-channel tile: 256-wide tiles (conv2_bf16_kernel, 8 waves) when Cout fills them, else the 128-row kernel
+// with whichever of 64 / 128 pads Cout least (tools/conv_bench.py: conv2 wins at Cout 256 / 512, loses at 128)
+inline int conv_tile_n(int Cout) {
+  if (Cout % 256 == 0) return 256;
+  return rup(Cout, 64) < rup(Cout, 128) ? 64 : 128;
+}
 
 // act 0 none / 1 SiLU / 2 sigmoid; res_mode 0 / 1 bf16 (after act) / 2 f32 x rscale
 inline int conv(const ConvCtx& cx, const ConvW& L, const void* x, long ldx, int n, int H, int W, int stride, void* out,
@@ -181,7 +199,7 @@ inline int conv(const ConvCtx& cx, const ConvW& L, const void* x, long ldx, int 
   c.act = act;
   c.out_f32 = out_f32;
   c.res_mode = res_mode;
-  c.tn = L.Cout <= 64 ? 64 : 128;
+  c.tn = conv_tile_n(L.Cout);
   VGE_HIPCHK(launch_conv_bf16(c, s));
   const int Ho = (H + 2 * c.pad - L.KH) / stride + 1, Wo = (W + 2 * c.pad - L.KW) / stride + 1;
   if (cx.flops) *cx.flops += 2.0 * n * Ho * Wo * (double)L.Cout * L.KH * L.KW * L.Cin;

@@ -32,7 +32,7 @@ struct AttW {  // ChannelAttention fc: f32 W^T [C][C] + bias
   int C = 0;
 };
 struct CspW {
-  ConvW main, shortc, fin;
+  ConvW ms, fin;  // ms = main_conv | short_conv fused along Cout (cat order)
   std::vector<ConvW> c1, pw;
   std::vector<DwW> dw;
   AttW att;
@@ -99,6 +99,12 @@ struct Loader {
     if (!ok || !fold(wm, p, Cout, Cin, K, BN_EPS, W, b)) return (void)(ok = false);
     if (dry) return;
     ok = pack_conv(m->dev, W.data(), b.data(), Cout, Cin, Cinp ? Cinp : Cin, K, K, L);
+  }
+  void convpair(const std::string& p0, const std::string& p1, int Cin, int Cout, ConvW& L) {  // 1x1 pair
+    std::vector<float> W, b;
+    if (!ok || !fold_pair(wm, p0, p1, Cout, Cin, 1, BN_EPS, W, b)) return (void)(ok = false);
+    if (dry) return;
+    ok = pack_conv(m->dev, W.data(), b.data(), 2 * Cout, Cin, Cin, 1, 1, L);
   }
   void dwmod(const std::string& p, int C, int K, DwW& L) {
     std::vector<float> W, b;
@@ -195,8 +201,7 @@ void load_all(Loader& ld, const vge_rtmpose_config& c) {
     const std::string q = p + "." + I(j);
     CspW& L = S.csp;
     L.add = i < 3;
-    ld.convmod(q + ".main_conv", C, mid, 1, L.main);
-    ld.convmod(q + ".short_conv", C, mid, 1, L.shortc);
+    ld.convpair(q + ".main_conv", q + ".short_conv", C, mid, L.ms);
     ld.convmod(q + ".final_conv", 2 * mid, C, 1, L.fin);
     L.c1.resize(c.stage_blocks[i]);
     L.pw.resize(c.stage_blocks[i]);
@@ -465,18 +470,20 @@ int vge_dwpose_keypoints(vge_dwpose* m, const uint8_t* frames, int F, int H, int
     }
     const CspW& L = St.csp;
     uint16_t* cat = static_cast<uint16_t*>(m->CAT);  // bf16 NHWC, (main | short) channel halves
-    CONV(L.shortc, src, C, N, h, w, 1, cat + mid, C, s);
+    CONV(L.ms, src, C, N, h, w, 1, cat, C, s);  // [main | short] straight into the concat buffer
     const int nb = (int)L.c1.size();
-    void* Ma = m->Ma;
-    void* Mb = m->Mb;
-    CONV(L.main, src, C, N, h, w, 1, nb ? Ma : (void*)cat, nb ? mid : C, s);
+    const void* Ma = cat;  // current main branch and its pixel stride
+    long lda = C;
+    void* scratch[2] = {m->Ma, m->Mb};
     for (int b = 0; b < nb; ++b) {
-      CONV(L.c1[b], Ma, mid, N, h, w, 1, m->T1, mid, s);
+      CONV(L.c1[b], Ma, lda, N, h, w, 1, m->T1, mid, s);
       OTHER(1, vge::launch_dwconv(m->T1, mid, L.dw[b].w, L.dw[b].b, m->T2, mid, N, h, w, mid, 5, s));
       const bool last = b == nb - 1;
-      CONV(L.pw[b], m->T2, mid, N, h, w, 1, last ? (void*)cat : Mb, last ? C : mid, s, 1, 0, L.add ? 1 : 0,
-           L.add ? Ma : nullptr, mid);
-      std::swap(Ma, Mb);
+      void* out = last ? (void*)cat : scratch[b & 1];
+      const long ldo = last ? C : mid;
+      CONV(L.pw[b], m->T2, mid, N, h, w, 1, out, ldo, s, 1, 0, L.add ? 1 : 0, L.add ? Ma : nullptr, lda);
+      Ma = out;
+      lda = ldo;
     }
     OTHER(1, vge::launch_chan_attn(cat, C, N, h * w, C, L.att.Wt, L.att.b, m->mean, m->att, s));
     CONV(L.fin, cat, C, N, h, w, 1, m->X, C, s);
@@ -524,8 +531,8 @@ int vge_op_conv_bf16(const void* x, long ldx, const void* w, const float* bias, 
   vge::ConvLaunch c{};
   c.x = x; c.ldx = ldx; c.w = w; c.bias = bias; c.out = out; c.ldo = ldo; c.res = res; c.ldr = ldr; c.rscale = rscale;
   c.zero = zero; c.n_img = n_img; c.H = H; c.W = W; c.Cin = Cin; c.KH = KH; c.KW = KW; c.stride = stride; c.pad = pad;
-  c.Kp = rup(KH * KW * Cin, 32); c.Cout = Cout; c.Npad = rup(Cout, 128); c.act = act; c.out_f32 = out_f32;
-  c.res_mode = res_mode; c.tn = Cout <= 64 ? 64 : 128;
+  c.Kp = rup(KH * KW * Cin, 32); c.Cout = Cout; c.Npad = rup(Cout, 256); c.act = act; c.out_f32 = out_f32;
+  c.res_mode = res_mode; c.tn = conv_tile_n(Cout);
   HIPCHK(vge::launch_conv_bf16(c, S(stream)));
   return VGE_OK;
 }

@@ -15,8 +15,8 @@ namespace {
 
 constexpr float BN_EPS = 1e-3f;  // YOLOX init_yolo: BatchNorm eps 1e-3
 
-struct YCsp {  // YOLOX CSPLayer: conv1 / conv2 1x1 -> hid, n Bottlenecks (1x1, 3x3 [+x]), conv3 1x1 on cat
-  ConvW c1, c2, c3;
+struct YCsp {  // YOLOX CSPLayer: conv1 | conv2 (one fused 1x1 -> [x_1 | x_2]), n Bottlenecks (1x1, 3x3 [+x]), conv3
+  ConvW c12, c3;
   std::vector<ConvW> m1, m2;
   bool shortcut = false;
   int hid = 0;
@@ -63,8 +63,11 @@ struct YLoader {
     const int hid = Cout / 2;
     L.hid = hid;
     L.shortcut = shortcut;
-    base(p + ".conv1", Cin, hid, 1, L.c1);
-    base(p + ".conv2", Cin, hid, 1, L.c2);
+    {
+      std::vector<float> W, b;
+      if (!ok || !fold_pair(wm, p + ".conv1", p + ".conv2", hid, Cin, 1, BN_EPS, W, b)) return (void)(ok = false);
+      if (!dry) ok = pack_conv(m->dev, W.data(), b.data(), 2 * hid, Cin, Cin, 1, 1, L.c12);
+    }
     base(p + ".conv3", 2 * hid, Cout, 1, L.c3);
     L.m1.resize(n);
     L.m2.resize(n);
@@ -154,24 +157,28 @@ bool cfg_ok(const vge_yolox_config& c, std::string& why) {
   return true;
 }
 
-// CSPLayer: out = conv3(cat(m(conv1(x)), conv2(x)))
+// CSPLayer: out = conv3(cat(m(conv1(x)), conv2(x))); conv1 | conv2 write [x_1 | x_2] into the concat buffer and the
+// last Bottleneck overwrites x_1 in place (its identity read and its store touch the same element)
 int ycsp(vge_yolox* m, const YCsp& L, const void* x, long ldx, int n, int h, int w, void* out, long ldo, hipStream_t s,
          int& rc_kind) {
   (void)rc_kind;
   const int hid = L.hid, nb = (int)L.m1.size();
   uint16_t* cat = static_cast<uint16_t*>(m->CAT);
   int rc;
-  if ((rc = conv(m->cx(), L.c2, x, ldx, n, h, w, 1, cat + hid, 2 * hid, s)) != VGE_OK) return rc;
-  void* Ma = m->Ma;
-  void* Mb = m->Mb;
-  if ((rc = conv(m->cx(), L.c1, x, ldx, n, h, w, 1, nb ? Ma : (void*)cat, nb ? hid : 2 * hid, s)) != VGE_OK) return rc;
+  if ((rc = conv(m->cx(), L.c12, x, ldx, n, h, w, 1, cat, 2 * hid, s)) != VGE_OK) return rc;
+  const void* Ma = cat;
+  long lda = 2 * hid;
+  void* scratch[2] = {m->Ma, m->Mb};
   for (int b = 0; b < nb; ++b) {
     const bool last = b == nb - 1;
-    if ((rc = conv(m->cx(), L.m1[b], Ma, hid, n, h, w, 1, m->T, hid, s)) != VGE_OK) return rc;
-    if ((rc = conv(m->cx(), L.m2[b], m->T, hid, n, h, w, 1, last ? (void*)cat : Mb, last ? 2 * hid : hid, s, 1, 0,
-                   L.shortcut ? 1 : 0, L.shortcut ? Ma : nullptr, hid)) != VGE_OK)
+    void* o = last ? (void*)cat : scratch[b & 1];
+    const long ldb = last ? 2 * hid : hid;
+    if ((rc = conv(m->cx(), L.m1[b], Ma, lda, n, h, w, 1, m->T, hid, s)) != VGE_OK) return rc;
+    if ((rc = conv(m->cx(), L.m2[b], m->T, hid, n, h, w, 1, o, ldb, s, 1, 0, L.shortcut ? 1 : 0,
+                   L.shortcut ? Ma : nullptr, lda)) != VGE_OK)
       return rc;
-    std::swap(Ma, Mb);
+    Ma = o;
+    lda = ldb;
   }
   return conv(m->cx(), L.c3, cat, 2 * hid, n, h, w, 1, out, ldo, s);
 }

@@ -359,7 +359,7 @@ def pack_conv_weight(w: torch.Tensor) -> torch.Tensor:
     """[Cout, Cin, KH, KW] -> the kernel's bf16 [Npad, Kp] layout (k = (kh * KW + kw) * Cin + ci)."""
     Cout, Cin, KH, KW = w.shape
     Kp = -(-KH * KW * Cin // 32) * 32
-    Np = -(-Cout // 128) * 128
+    Np = -(-Cout // 256) * 256
     p = torch.zeros((Np, Kp), dtype=torch.bfloat16, device=w.device)
     p[:Cout, :KH * KW * Cin] = w.permute(0, 2, 3, 1).reshape(Cout, -1).to(torch.bfloat16)
     return p
