@@ -453,6 +453,66 @@ __global__ void __launch_bounds__(256) dwconv_kernel(const bf16* __restrict__ x,
   *reinterpret_cast<bf16x8*>(y + pix * ldy + c8) = o;
 }
 
+// Sliding-window form: one thread = 4 channels of RB consecutive output rows of one column.  A 5 x 5 window of raw
+// bf16x4 pixels slides down the column in registers, so each output row loads one new input row (5 pixels, 8 B
+// each): 1/5 of the loads of the form above, weights for the 4 channels held in registers.  Per output the taps
+// are summed in (kh, kw) order with out-of-range taps adding 0 -- the same sums as dwconv_kernel.
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+template <int RB>
+__global__ void __launch_bounds__(256) dwconv5_rb_kernel(const bf16* __restrict__ x, long ldx, const float* __restrict__ w,
+                                                         const float* __restrict__ b, bf16* __restrict__ y, long ldy,
+                                                         int n_img, int H, int W, int C) {
+  const int cg = C >> 2, nstrip = (H + RB - 1) / RB;
+  const long gid = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (gid >= (long)n_img * nstrip * W * cg) return;
+  const int c4 = (int)(gid % cg) * 4;
+  long t = gid / cg;
+  const int ow = (int)(t % W);
+  t /= W;
+  const int oh0 = (int)(t % nstrip) * RB;
+  const long img = t / nstrip;
+  float wr[25][4];
+#pragma unroll
+  for (int k = 0; k < 25; ++k) {
+    const floatx4 v = *reinterpret_cast<const floatx4*>(w + k * C + c4);
+    wr[k][0] = v.x; wr[k][1] = v.y; wr[k][2] = v.z; wr[k][3] = v.w;
+  }
+  const floatx4 bb = *reinterpret_cast<const floatx4*>(b + c4);
+  const bf16* colp = x + img * H * W * ldx + c4;
+  auto load_row = [&](int ih, bf16x4_t (&raw)[5]) {
+#pragma unroll
+    for (int kw = 0; kw < 5; ++kw) {
+      const int iw = ow - 2 + kw;
+      raw[kw] = bf16x4_t{(bf16)0.f, (bf16)0.f, (bf16)0.f, (bf16)0.f};
+      if ((unsigned)ih < (unsigned)H && (unsigned)iw < (unsigned)W)
+        raw[kw] = *reinterpret_cast<const bf16x4_t*>(colp + ((long)ih * W + iw) * ldx);
+    }
+  };
+  bf16x4_t win[5][5];
+#pragma unroll
+  for (int kh = 0; kh < 4; ++kh) load_row(oh0 - 2 + kh, win[kh + 1]);
+  const int rows = min(RB, H - oh0);
+#pragma unroll 1
+  for (int r = 0; r < rows; ++r) {
+#pragma unroll
+    for (int kh = 0; kh < 4; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 5; ++kw) win[kh][kw] = win[kh + 1][kw];
+    load_row(oh0 + r + 2, win[4]);
+    float acc[4] = {bb.x, bb.y, bb.z, bb.w};
+#pragma unroll
+    for (int kh = 0; kh < 5; ++kh)
+#pragma unroll
+      for (int kw = 0; kw < 5; ++kw)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[c] = fmaf(wr[kh * 5 + kw][c], (float)win[kh][kw][c], acc[c]);
+    bf16x4_t o;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) o[c] = (bf16)silu(acc[c]);
+    *reinterpret_cast<bf16x4_t*>(y + ((img * H + oh0 + r) * W + ow) * ldy + c4) = o;
+  }
+}
+
 // ------------------------------------------------------------------------------------ SPP max pools
 // buf[p][0:C] is the input; writes max_pool(k)(input) for k = k0, k1, k2 at channel offsets C, 2C, 3C.
 __global__ void __launch_bounds__(256) spp_pool_kernel(bf16* __restrict__ buf, long ld, int n_img, int H, int W, int C,
@@ -497,6 +557,60 @@ __global__ void __launch_bounds__(256) spp_pool_kernel(bf16* __restrict__ buf, l
   *reinterpret_cast<bf16x8*>(d + C) = o0;
   *reinterpret_cast<bf16x8*>(d + 2 * C) = o1;
   *reinterpret_cast<bf16x8*>(d + 3 * C) = o2;
+}
+
+// The same three pools from LDS: one workgroup per (image, 64-channel slab) holds the whole map, and
+// max_pool(9) = max_pool(5) o max_pool(5), max_pool(13) = max_pool(5)^3 (stride 1, -inf padding: SPPF's identity),
+// each pool5 done as a row pass and a column pass.  Maps of up to 400 positions (3 x 50 KB of LDS).
+constexpr int SPP_LDS_MAX_HW = 400;
+__device__ __forceinline__ bf16x8 max8(bf16x8 a, bf16x8 b) {
+  bf16x8 r;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) r[i] = (bf16)fmaxf((float)a[i], (float)b[i]);
+  return r;
+}
+__global__ void __launch_bounds__(256) spp_lds_kernel(bf16* __restrict__ buf, long ld, int H, int W, int C) {
+  extern __shared__ __attribute__((aligned(16))) char sm[];
+  const int HW = H * W;
+  bf16x8* P = reinterpret_cast<bf16x8*>(sm);          // [HW][8 groups]
+  bf16x8* T = P + SPP_LDS_MAX_HW * 8;
+  bf16x8* Q = T + SPP_LDS_MAX_HW * 8;
+  const long img = blockIdx.x;
+  const int c0 = blockIdx.y * 64;
+  const int groups = min(8, (C - c0) / 8);
+  const int items = HW * 8;
+  bf16* base = buf + img * HW * ld + c0;
+  for (int it = threadIdx.x; it < items; it += 256) {
+    const int px = it >> 3, g = it & 7;
+    if (g < groups) P[it] = *reinterpret_cast<const bf16x8*>(base + px * ld + g * 8);
+  }
+  __syncthreads();
+  bf16x8* src = P;
+  bf16x8* dst = Q;
+  for (int k = 1; k <= 3; ++k) {
+    for (int it = threadIdx.x; it < items; it += 256) {  // row pass src -> T
+      const int px = it >> 3, g = it & 7, y = px / W, x = px - y * W;
+      bf16x8 m = src[it];
+#pragma unroll
+      for (int d = -2; d <= 2; ++d)
+        if (d && (unsigned)(x + d) < (unsigned)W) m = max8(m, src[((y * W) + x + d) * 8 + g]);
+      T[it] = m;
+    }
+    __syncthreads();
+    for (int it = threadIdx.x; it < items; it += 256) {  // column pass T -> dst, and out to channel slice k
+      const int px = it >> 3, g = it & 7, y = px / W, x = px - y * W;
+      bf16x8 m = T[it];
+#pragma unroll
+      for (int d = -2; d <= 2; ++d)
+        if (d && (unsigned)(y + d) < (unsigned)H) m = max8(m, T[(((y + d) * W) + x) * 8 + g]);
+      dst[it] = m;
+      if (g < groups) *reinterpret_cast<bf16x8*>(base + px * ld + k * C + g * 8) = m;
+    }
+    __syncthreads();
+    bf16x8* t = src;  // the next pool reads this pool's output; the old input buffer is free
+    src = dst;
+    dst = t;
+  }
 }
 
 // ------------------------------------------------------------------------------------ ChannelAttention
@@ -763,7 +877,12 @@ hipError_t launch_dwconv(const void* x, long ldx, const float* w, const float* b
   const long n = (long)n_img * H * W * (C / 8);
   if (n == 0) return hipSuccess;
   const int grid = (int)((n + 255) / 256);
-  if (K == 5)
+  if (K == 5) {
+    constexpr int RB = 8;
+    const long nt = (long)n_img * ((H + RB - 1) / RB) * W * (C / 4);
+    hipLaunchKernelGGL(dwconv5_rb_kernel<RB>, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s,
+                       static_cast<const bf16*>(x), ldx, w, b, static_cast<bf16*>(y), ldy, n_img, H, W, C);
+  } else if (K == 55)  // the one-thread-per-output form (kept for A/B timing)
     hipLaunchKernelGGL(dwconv_kernel<5>, dim3(grid), dim3(256), 0, s, static_cast<const bf16*>(x), ldx, w, b,
                        static_cast<bf16*>(y), ldy, n_img, H, W, C);
   else if (K == 3)
@@ -777,6 +896,19 @@ hipError_t launch_dwconv(const void* x, long ldx, const float* w, const float* b
 hipError_t launch_spp_pool(void* buf, long ld, int n_img, int H, int W, int C, int k0, int k1, int k2, hipStream_t s) {
   const long n = (long)n_img * H * W * (C / 8);
   if (n == 0) return hipSuccess;
+  if (k0 == 5 && k1 == 9 && k2 == 13 && H * W <= SPP_LDS_MAX_HW) {
+    static bool attr = false;
+    const int bytes = 3 * SPP_LDS_MAX_HW * 8 * 16;
+    if (!attr) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&spp_lds_kernel),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+      if (e != hipSuccess) return e;
+      attr = true;
+    }
+    hipLaunchKernelGGL(spp_lds_kernel, dim3(n_img, (C + 63) / 64), dim3(256), bytes, s, static_cast<bf16*>(buf), ld, H,
+                       W, C);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(spp_pool_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, static_cast<bf16*>(buf), ld,
                      n_img, H, W, C, k0, k1, k2);
   return hipGetLastError();
