@@ -139,12 +139,22 @@ def main():
                     help="f32x3: 3xfp16 split-precision MFMA (f32-class, default); f32: exact f32 MFMA")
     ap.add_argument("--no-detector", action="store_true",
                     help="e2e: skip DWPose's YOLOX person detector (every frame takes the whole-frame pose box)")
-    ap.add_argument("--workload", default="score", choices=["score", "e2e"],
+    ap.add_argument("--workload", default="score", choices=["score", "e2e", "tag"],
                     help="score: config 2 (default, the bench line); e2e: config 3, frames -> TokenHMR + DWPose -> "
-                         "scores (bench_e2e.py; --clips defaults to 8 there)")
+                         "scores (bench_e2e.py; --clips defaults to 8 there); tag: config 4 on pre-extracted "
+                         "features, the full sharded eval flow over 300 videos (bench_tag.py)")
     args = ap.parse_args()
 
     world, rank, dev = setup_dist()
+    if args.workload == "tag":
+        import bench_tag
+        out = bench_tag.run(args, world, rank, dev, METRIC)
+        if rank == 0:
+            print(json.dumps(out))
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
     if args.workload == "e2e":
         import bench_e2e
         if args.clips == 256:

@@ -74,14 +74,17 @@ class NpzVideoDataset:
             if self.filter_classes and cls not in self.filter_classes:
                 continue
             cls_dir = os.path.join(root, cls)
-            for f in sorted(os.listdir(cls_dir)):
-                if not f.endswith(".npz"):
-                    continue
+            names = [f for f in sorted(os.listdir(cls_dir)) if f.endswith(".npz")]
+            shapes = _probe_shapes([os.path.join(cls_dir, f) for f in names])
+            for f, shape in zip(names, shapes):
                 path = os.path.join(cls_dir, f)
                 try:
-                    with np.load(path) as npz:
-                        T = int(npz["pose"].shape[0])
-                        Dv = int(npz["vit"].shape[1])
+                    if shape is not None:
+                        T, Dv = shape
+                    else:
+                        with np.load(path) as npz:
+                            T = int(npz["pose"].shape[0])
+                            Dv = int(npz["vit"].shape[1])
                     items.append(VideoItem(cls=cls, name=f, path=path, length=T, vit_dim=Dv))
                 except Exception:
                     print(f"Failed for {f}")
@@ -109,9 +112,30 @@ def train_test_split(dataset: NpzVideoDataset, train_ratio: float = 0.8, seed: i
             NpzVideoDataset(dataset.root_dir, items=test_items))
 
 
+def _probe_shapes(paths: Sequence[str]) -> List[Optional[Tuple[int, int]]]:
+    """(T, vit_dim) of each npz from its npy headers (libvge's native multithreaded probe: no payload inflate),
+    None where the probe cannot read a file -- the caller then takes the reference's np.load path for that file,
+    so unreadable / partial files keep the reference's behaviour exactly."""
+    if not paths:
+        return []
+    try:
+        import ctypes as C
+        from . import lib as L
+        lib = L.load()
+    except Exception:  # the scan works without libvge (np.load for every file)
+        return [None] * len(paths)
+    arr = (C.c_char_p * len(paths))(*[str(p).encode() for p in paths])
+    kps = (C.c_char_p * len(paths))(*([None] * len(paths)))
+    info = (L.ClipInfo * len(paths))()
+    lib.vge_ingest_probe(arr, kps, len(paths), 0, info)
+    return [(int(info[i].n_frames), int(info[i].vit_dim)) if info[i].status == 0 else None for i in range(len(paths))]
+
+
 def create_dataset_from_generated_meshes(generated_meshes_dir: str) -> NpzVideoDataset:
     items = []
-    for npz_file in sorted(Path(generated_meshes_dir).glob("*.npz")):
+    files = sorted(Path(generated_meshes_dir).glob("*.npz"))
+    shapes = _probe_shapes([str(f) for f in files])
+    for npz_file, shape in zip(files, shapes):
         try:
             stem = npz_file.stem
             parts = stem.split("_")
@@ -129,13 +153,16 @@ def create_dataset_from_generated_meshes(generated_meshes_dir: str) -> NpzVideoD
                         break
             if cls_name is None:
                 cls_name = "Unknown"
-            with np.load(npz_file) as npz:
-                T = int(npz["pose"].shape[0]) if "pose" in npz else 0
-                if "vit" in npz:
-                    vshape = npz["vit"].shape
-                    Dv = int(vshape[1]) if len(vshape) > 1 else 0
-                else:
-                    Dv = 0
+            if shape is not None:
+                T, Dv = shape
+            else:
+                with np.load(npz_file) as npz:
+                    T = int(npz["pose"].shape[0]) if "pose" in npz else 0
+                    if "vit" in npz:
+                        vshape = npz["vit"].shape
+                        Dv = int(vshape[1]) if len(vshape) > 1 else 0
+                    else:
+                        Dv = 0
             items.append(VideoItem(cls=cls_name, name=npz_file.name, path=str(npz_file), length=T, vit_dim=Dv))
         except Exception as e:
             print(f"Failed to load {npz_file}: {e}")
