@@ -10,6 +10,8 @@
 #include <string>
 #include <unordered_map>
 #include <vector>
+#include <thread>
+#include <atomic>
 
 #include "../../include/vge.h"
 
@@ -154,21 +156,39 @@ int range_exp(double m) {
   return std::max(std::ilogb(m) - 8, -100);
 }
 
+// run f(i) for i in [0, n) on up to hardware_concurrency host threads (weight packing at load time)
+template <class F>
+void parallel_for(int n, F f) {
+  const int nt = std::max(1, std::min<int>(n, (int)std::thread::hardware_concurrency()));
+  if (nt <= 1 || n < 4) {
+    for (int i = 0; i < n; ++i) f(i);
+    return;
+  }
+  std::vector<std::thread> th;
+  std::atomic<int> next{0};
+  for (int t = 0; t < std::min(nt, 32); ++t)
+    th.emplace_back([&] {
+      for (int i = next++; i < n; i = next++) f(i);
+    });
+  for (auto& x : th) x.join();
+}
+
 template <class Get>
 void pack_linear_x3(Get W, int N, int K_real, std::vector<_Float16>& out, std::vector<float>& cs, int chunk_mult = 1) {
   const int nch = ((K_real + 15) / 16 + chunk_mult - 1) / chunk_mult * chunk_mult;  // streams run in groups of chunk_mult
   std::vector<int> sh(N);
-  for (int n = 0; n < N; ++n) {
+  parallel_for(N, [&](int n) {
     float m = 0.f;
     for (int k = 0; k < K_real; ++k) m = std::max(m, std::fabs(W(n, k)));
     sh[n] = (m > 0.f) ? std::min(8 - std::ilogb(m), 100) : 0;
-    cs.push_back(std::ldexp(1.0f, -sh[n]));
-  }
+  });
+  for (int n = 0; n < N; ++n) cs.push_back(std::ldexp(1.0f, -sh[n]));
   const size_t base = out.size();
   out.resize(base + (size_t)(N / 256) * nch * 8192, (_Float16)0.0f);
   _Float16* o = out.data() + base;
-  for (int nb = 0; nb < N / 256; ++nb)
-    for (int c = 0; c < nch; ++c) {
+  parallel_for((N / 256) * nch, [&](int idx) {
+    const int nb = idx / nch, c = idx % nch;
+    {
       _Float16* ch = o + ((size_t)nb * nch + c) * 8192;
       for (int h = 0; h < 2; ++h)
         for (int n = 0; n < 256; ++n)
@@ -181,6 +201,7 @@ void pack_linear_x3(Get W, int N, int K_real, std::vector<_Float16>& out, std::v
             ch[((1 * 2 + h) * 256 + n) * 8 + j] = lo;
           }
     }
+  });
 }
 
 }  // namespace
