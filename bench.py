@@ -137,6 +137,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--compute", default="f32x3", choices=["f32x3", "f32"],
                     help="f32x3: 3xfp16 split-precision MFMA (f32-class, default); f32: exact f32 MFMA")
+    ap.add_argument("--serial-extract", action="store_true",
+                    help="e2e: run TokenHMR and DWPose one after the other on one stream (default: two streams)")
     ap.add_argument("--no-detector", action="store_true",
                     help="e2e: skip DWPose's YOLOX person detector (every frame takes the whole-frame pose box)")
     ap.add_argument("--workload", default="score", choices=["score", "e2e", "tag"],
