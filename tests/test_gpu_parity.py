@@ -148,6 +148,28 @@ def test_video_scores_match_reference(vg, golden_dataset, golden_meta, tmp_path,
     assert json.loads(out.read_text()) == combined
 
 
+def test_cli_with_saved_features(vg, golden_dataset, golden_flow, golden_meta, tmp_path):
+    """python -m vge.eval (eval.py's __main__ with arguments): video_scores.json + window_features.pt in the
+    reference's format (eval.py:197-204: CPU tensors seq_embeds [Nw,256], frame_embeds [Nw,33,256], names)."""
+    VE, ops = vg
+    paths, ckpt = golden_dataset
+    out, feats = tmp_path / "video_scores.json", tmp_path / "window_features.pt"
+    assert VE.main(["--generated-meshes", paths["generated_meshes"], "--real-meshes", paths["real"], "--model", ckpt,
+                    "--keypoints", paths["generated_kps"], "--real-keypoints", paths["real_kp"], "--out", str(out),
+                    "--save-features", str(feats)]) == 0
+    import json
+    scores = json.loads(out.read_text())
+    ref = golden_meta["video_scores"]
+    assert sorted(scores) == sorted(ref)
+    assert max(abs(ref[v][k] - scores[v][k]) for v in ref for k in ref[v]) < 1e-4
+    f = torch.load(str(feats), weights_only=True)
+    assert set(f) == {"seq_embeds", "frame_embeds", "cls_names", "vid_names"}
+    assert f["seq_embeds"].device.type == "cpu" and tuple(f["frame_embeds"].shape[1:]) == (33, 256)
+    assert np.abs(f["seq_embeds"].numpy() - golden_flow["seq_embeds"]).max() < 2e-5
+    assert np.abs(f["frame_embeds"][:4].numpy() - golden_flow["frame_embeds_first4"]).max() < 2e-5
+    assert len(f["vid_names"]) == f["seq_embeds"].shape[0]
+
+
 def test_featurize_edge_cases_vs_oracle(vg):
     """Static / all-invisible / partly invisible keypoints, start past the end, single-frame clip."""
     VE, ops = vg

@@ -164,16 +164,23 @@ def build_real_centroids(model: ops.Encoder, real_meshes_dir: str, real_kp_dir: 
 
 def extract_window_features(model: ops.Encoder, dataset: NpzVideoDataset, keypoint_dir: str, stats: ModalityStatsGPU,
                             clip_len: int = 32, stride: int = 8, device="cuda", frame_embed: bool = False,
-                            store: Optional[ops.DeviceFrameStore] = None):
-    """eval.py:168-206 over all windows of `dataset` (sample_all_windows_npz order)."""
+                            store: Optional[ops.DeviceFrameStore] = None, save_path: Optional[str] = None):
+    """eval.py:168-206 over all windows of `dataset` (sample_all_windows_npz order).  save_path: torch.save of
+    {seq_embeds [Nw,256], frame_embeds [Nw,33,256], cls_names, vid_names} on the CPU like eval.py:197-204
+    (frame embeddings are then produced too)."""
     samples = sample_all_windows_npz(dataset, clip_len, stride)
     if store is None:
         store = ops.DeviceFrameStore.from_host(load_frame_store(dataset.items, keypoint_dir, require_kp=True), device)
     idx = {it.path: i for i, it in enumerate(dataset.items)}
     win = _window_tensor(samples, idx, device)
-    seq, fe, tcw = encode_windows(model, store, win, stats, frame_embed=frame_embed)
-    return {"seq_embeds": seq, "frame_embeds": fe, "tc_window": tcw,
-            "cls_names": [it.cls for it, _ in samples], "vid_names": [it.name for it, _ in samples]}
+    seq, fe, tcw = encode_windows(model, store, win, stats, frame_embed=frame_embed or bool(save_path))
+    out = {"seq_embeds": seq, "frame_embeds": fe, "tc_window": tcw,
+           "cls_names": [it.cls for it, _ in samples], "vid_names": [it.name for it, _ in samples]}
+    if save_path:
+        torch.save({"seq_embeds": seq.cpu(), "frame_embeds": fe.cpu(), "cls_names": list(out["cls_names"]),
+                    "vid_names": list(out["vid_names"])}, save_path)
+        print(f"Saved features to {save_path}")
+    return out
 
 
 # ----------------------------------------------------------------------------- metrics
@@ -276,8 +283,9 @@ def compute_spearman_correlation(model_scores: dict, human_scores_path: str, hum
 def run_eval(generated_meshes_dir: str, real_meshes_dir: str, model_path, keypoint_dir: str, real_kp_dir: str,
              human_scores_path: Optional[str] = None, clip_len: int = 32, stride: int = 8,
              out_json: Optional[str] = "video_scores.json", device="cuda", timings: Optional[dict] = None,
-             compute: str = "f32x3"):
-    """eval.py __main__ (350-466) on one GPU; returns the combined {video: {ac, tc}} dict."""
+             compute: str = "f32x3", save_features: Optional[str] = None):
+    """eval.py __main__ (350-466) on one GPU; returns the combined {video: {ac, tc}} dict.  save_features: the
+    window_features.pt of eval.py:439-443 (off by default: it copies every frame embedding to the host)."""
     t0 = time.perf_counter()
     real_ds = NpzVideoDataset(real_meshes_dir, filter_classes=ACTION_CLASSES)
     train_ds, _ = train_test_split(real_ds, train_ratio=0.8, seed=1337)
@@ -295,7 +303,8 @@ def run_eval(generated_meshes_dir: str, real_meshes_dir: str, model_path, keypoi
                                                     train_items=train_ds.items, label_dict=label_dict, store=real_store)
     t2 = time.perf_counter()
     dataset = create_dataset_from_generated_meshes(generated_meshes_dir)
-    feats = extract_window_features(model, dataset, keypoint_dir, stats, clip_len, stride, device)
+    feats = extract_window_features(model, dataset, keypoint_dir, stats, clip_len, stride, device,
+                                    save_path=save_features)
     ac = compute_action_consistency_scores(feats, centroids, label_dict)
     tc = compute_temporal_coherence_scores(feats, centroids, label_dict)
     combined = combine_scores(ac, tc)
@@ -312,3 +321,45 @@ def run_eval(generated_meshes_dir: str, real_meshes_dir: str, model_path, keypoi
     if timings is not None:
         timings.update(stats_s=t1 - t0, centroids_s=t2 - t1, gen_s=t3 - t2, n_windows=len(feats["vid_names"]))
     return combined
+
+
+def main(argv=None):
+    """Command line of eval.py (its __main__ hard-codes the paths; here they are arguments).  Under torchrun
+    (WORLD_SIZE > 1) the flow is sharded over the ranks (vge.dist.run_eval_distributed, RCCL)."""
+    import argparse
+    ap = argparse.ArgumentParser(description="AC / TC scores of generated videos (MI355X)")
+    ap.add_argument("--generated-meshes", required=True)
+    ap.add_argument("--real-meshes", required=True)
+    ap.add_argument("--model", required=True, help="checkpoint with model_state_dict (eval.py:136-165)")
+    ap.add_argument("--keypoints", required=True, help="generated keypoint dir (<stem>/keypoints.npy)")
+    ap.add_argument("--real-keypoints", required=True)
+    ap.add_argument("--human-scores", default=None)
+    ap.add_argument("--out", default="video_scores.json")
+    ap.add_argument("--save-features", default=None, help="e.g. window_features.pt")
+    ap.add_argument("--clip-len", type=int, default=32)
+    ap.add_argument("--stride", type=int, default=8)
+    ap.add_argument("--compute", default="f32x3", choices=["f32x3", "f32"])
+    a = ap.parse_args(argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1:
+        import torch.distributed as dist
+        from .dist import run_eval_distributed
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        try:
+            res = run_eval_distributed(a.generated_meshes, a.real_meshes, a.model, a.keypoints, a.real_keypoints,
+                                       a.clip_len, a.stride, out_json=a.out, device=f"cuda:{local}",
+                                       compute=a.compute)
+        finally:
+            dist.destroy_process_group()
+    else:
+        res = run_eval(a.generated_meshes, a.real_meshes, a.model, a.keypoints, a.real_keypoints, a.human_scores,
+                       a.clip_len, a.stride, out_json=a.out, compute=a.compute, save_features=a.save_features)
+    if res is not None:
+        print(f"Saved AC/TC scores for {len(res)} videos to {a.out}")
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
