@@ -22,6 +22,7 @@
 #include "vge_cnn.h"
 
 #include <cstdlib>
+#include <algorithm>
 
 namespace {
 
@@ -453,7 +454,7 @@ __global__ void __launch_bounds__(256) dwconv_kernel(const bf16* __restrict__ x,
   *reinterpret_cast<bf16x8*>(y + pix * ldy + c8) = o;
 }
 
-// Sliding-window form: one thread = 4 channels of RB consecutive output rows of one column.  A 5 x 5 window of raw
+// Sliding-window form: one thread = 4 channels of RB (32) consecutive output rows of one column.  A 5 x 5 window of raw
 // bf16x4 pixels slides down the column in registers, so each output row loads one new input row (5 pixels, 8 B
 // each): 1/5 of the loads of the form above, weights for the 4 channels held in registers.  Per output the taps
 // are summed in (kh, kw) order with out-of-range taps adding 0 -- the same sums as dwconv_kernel.
@@ -488,28 +489,42 @@ __global__ void __launch_bounds__(256) dwconv5_rb_kernel(const bf16* __restrict_
         raw[kw] = *reinterpret_cast<const bf16x4_t*>(colp + ((long)ih * W + iw) * ldx);
     }
   };
-  bf16x4_t win[5][5];
+  // the window lives in f32, input row ih in slot (ih - oh0 + 2) % 5; the output loop is unrolled by 5 so every
+  // slot index is static (no register moves); the next input row is loaded one output ahead
+  float wf[5][5][4];
+  bf16x4_t nxt[5];
+  auto to_slot = [&](const bf16x4_t (&raw)[5], float (&slot)[5][4]) {
 #pragma unroll
-  for (int kh = 0; kh < 4; ++kh) load_row(oh0 - 2 + kh, win[kh + 1]);
+    for (int kw = 0; kw < 5; ++kw)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) slot[kw][c] = (float)raw[kw][c];
+  };
+#pragma unroll
+  for (int kh = 0; kh < 4; ++kh) {
+    load_row(oh0 - 2 + kh, nxt);
+    to_slot(nxt, wf[kh]);
+  }
+  load_row(oh0 + 2, nxt);
   const int rows = min(RB, H - oh0);
 #pragma unroll 1
-  for (int r = 0; r < rows; ++r) {
+  for (int r = 0; r < rows; r += 5) {
 #pragma unroll
-    for (int kh = 0; kh < 4; ++kh)
+    for (int j = 0; j < 5; ++j) {
+      if (r + j >= rows) break;
+      to_slot(nxt, wf[(j + 4) % 5]);
+      load_row(oh0 + r + j + 3, nxt);  // in flight while this output's 100 FMAs run
+      float acc[4] = {bb.x, bb.y, bb.z, bb.w};
 #pragma unroll
-      for (int kw = 0; kw < 5; ++kw) win[kh][kw] = win[kh + 1][kw];
-    load_row(oh0 + r + 2, win[4]);
-    float acc[4] = {bb.x, bb.y, bb.z, bb.w};
+      for (int kh = 0; kh < 5; ++kh)
 #pragma unroll
-    for (int kh = 0; kh < 5; ++kh)
+        for (int kw = 0; kw < 5; ++kw)
 #pragma unroll
-      for (int kw = 0; kw < 5; ++kw)
+          for (int c = 0; c < 4; ++c) acc[c] = fmaf(wr[kh * 5 + kw][c], wf[(j + kh) % 5][kw][c], acc[c]);
+      bf16x4_t o;
 #pragma unroll
-        for (int c = 0; c < 4; ++c) acc[c] = fmaf(wr[kh * 5 + kw][c], (float)win[kh][kw][c], acc[c]);
-    bf16x4_t o;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) o[c] = (bf16)silu(acc[c]);
-    *reinterpret_cast<bf16x4_t*>(y + ((img * H + oh0 + r) * W + ow) * ldy + c4) = o;
+      for (int c = 0; c < 4; ++c) o[c] = (bf16)silu(acc[c]);
+      *reinterpret_cast<bf16x4_t*>(y + ((img * H + oh0 + r + j) * W + ow) * ldy + c4) = o;
+    }
   }
 }
 
@@ -614,41 +629,47 @@ __global__ void __launch_bounds__(256) spp_lds_kernel(bf16* __restrict__ buf, lo
 }
 
 // ------------------------------------------------------------------------------------ ChannelAttention
-// mean over the H*W pixels of each (image, channel): one workgroup per (image, 256-channel slab)
-__global__ void __launch_bounds__(256) chan_mean_kernel(const bf16* __restrict__ x, long ld, int HW, int C,
-                                                        float* __restrict__ mean) {
-  __shared__ float part[8][256];
-  const int img = blockIdx.x, slab = blockIdx.y * 256;
+// per-(image, channel) sums over the H*W pixels, split over `chunks` pixel ranges so a whole map is read by many
+// workgroups: grid (image, 256-channel slab, chunk) -> part[image][chunk][C] (summed in a fixed order by the fc
+// kernel: deterministic)
+__global__ void __launch_bounds__(256) chan_mean_kernel(const bf16* __restrict__ x, long ld, int HW, int C, int chunks,
+                                                        float* __restrict__ part) {
+  __shared__ float red[256][9];
+  const int img = blockIdx.x, slab = blockIdx.y * 256, chunk = blockIdx.z;
+  const int per = (HW + chunks - 1) / chunks, p0 = chunk * per, p1 = min(HW, p0 + per);
   const int cw = min(256, C - slab);         // channels in this slab (multiple of 8)
-  const int g = threadIdx.x % (cw / 8), lanes_per_pix = cw / 8;
+  const int lanes_per_pix = cw / 8, g = threadIdx.x % lanes_per_pix;
   const int pr = threadIdx.x / lanes_per_pix, npr = 256 / lanes_per_pix;  // pixel rows in flight
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   if (pr < npr)
-    for (int p = pr; p < HW; p += npr) {
+    for (int p = p0 + pr; p < p1; p += npr) {
       const bf16x8 v = *reinterpret_cast<const bf16x8*>(x + ((long)img * HW + p) * ld + slab + g * 8);
 #pragma unroll
       for (int i = 0; i < 8; ++i) acc[i] += (float)v[i];
     }
-  // reduce over the npr pixel rows: stage by row groups of 8
-  __shared__ float red[256][9];
 #pragma unroll
   for (int i = 0; i < 8; ++i) red[threadIdx.x][i] = acc[i];
   __syncthreads();
-  (void)part;
   if (threadIdx.x < cw) {
     const int c = threadIdx.x, gg = c / 8, ii = c % 8;
     float s = 0.f;
     for (int r = 0; r < npr; ++r) s += red[r * lanes_per_pix + gg][ii];
-    mean[(long)img * C + slab + c] = s / (float)HW;
+    part[((long)img * chunks + chunk) * C + slab + c] = s;
   }
 }
 
-// a[img][c] = hardsigmoid(b[c] + sum_k Wt[k][c] mean[img][k])  (Wt = fc.weight transposed, f32)
-__global__ void __launch_bounds__(256) chan_attn_fc_kernel(const float* __restrict__ mean, const float* __restrict__ Wt,
-                                                           const float* __restrict__ b, float* __restrict__ att, int C) {
+// a[img][c] = hardsigmoid(b[c] + sum_k Wt[k][c] mean[img][k])  (Wt = fc.weight transposed, f32); mean from the
+// chunk partial sums
+__global__ void __launch_bounds__(256) chan_attn_fc_kernel(const float* __restrict__ part, int chunks, int HW,
+                                                           const float* __restrict__ Wt, const float* __restrict__ b,
+                                                           float* __restrict__ att, int C) {
   extern __shared__ float mrow[];
   const int img = blockIdx.y;
-  for (int k = threadIdx.x; k < C; k += blockDim.x) mrow[k] = mean[(long)img * C + k];
+  for (int k = threadIdx.x; k < C; k += blockDim.x) {
+    float s = 0.f;
+    for (int q = 0; q < chunks; ++q) s += part[((long)img * chunks + q) * C + k];
+    mrow[k] = s / (float)HW;
+  }
   __syncthreads();
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
@@ -878,7 +899,7 @@ hipError_t launch_dwconv(const void* x, long ldx, const float* w, const float* b
   if (n == 0) return hipSuccess;
   const int grid = (int)((n + 255) / 256);
   if (K == 5) {
-    constexpr int RB = 8;
+    constexpr int RB = 32;  // output rows per thread: the 25 weight vectors a thread loads serve 32 outputs
     const long nt = (long)n_img * ((H + RB - 1) / RB) * W * (C / 4);
     hipLaunchKernelGGL(dwconv5_rb_kernel<RB>, dim3((unsigned)((nt + 255) / 256)), dim3(256), 0, s,
                        static_cast<const bf16*>(x), ldx, w, b, static_cast<bf16*>(y), ldy, n_img, H, W, C);
@@ -917,10 +938,12 @@ hipError_t launch_spp_pool(void* buf, long ld, int n_img, int H, int W, int C, i
 hipError_t launch_chan_attn(void* x, long ld, int n_img, int HW, int C, const float* Wt, const float* b, float* mean,
                             float* att, hipStream_t s) {
   if (n_img == 0) return hipSuccess;
-  hipLaunchKernelGGL(chan_mean_kernel, dim3(n_img, (C + 255) / 256), dim3(256), 0, s, static_cast<const bf16*>(x), ld,
-                     HW, C, mean);
-  hipLaunchKernelGGL(chan_attn_fc_kernel, dim3((C + 255) / 256, n_img), dim3(256), C * sizeof(float), s, mean, Wt, b,
-                     att, C);
+  // `mean` holds n_img x 2048 floats (vge_dwpose_reserve): pixel chunks of >= 512 within that budget
+  const int chunks = std::max(1, std::min((HW + 511) / 512, 2048 / C));
+  hipLaunchKernelGGL(chan_mean_kernel, dim3(n_img, (C + 255) / 256, chunks), dim3(256), 0, s,
+                     static_cast<const bf16*>(x), ld, HW, C, chunks, mean);
+  hipLaunchKernelGGL(chan_attn_fc_kernel, dim3((C + 255) / 256, n_img), dim3(256), C * sizeof(float), s, mean, chunks,
+                     HW, Wt, b, att, C);
   const long n = (long)n_img * HW * (C / 8);
   hipLaunchKernelGGL(chan_scale_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, static_cast<bf16*>(x), ld,
                      HW, C, att, (long)n_img * HW);

@@ -14,11 +14,14 @@
 #include "vge_common.h"
 #include "vge_cnn.h"
 
+#include <algorithm>
 #include <cmath>
+#include <cstdlib>
 
 namespace {
 
 typedef __bf16 bf16;
+typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 __global__ void __launch_bounds__(256) head_sn_t_kernel(const float* __restrict__ y, long ldy, int hw, int K, int Kp,
                                                         float g, float inv_sqrt_hw, long n_rows, bf16* __restrict__ out) {
@@ -120,6 +123,85 @@ __global__ void __launch_bounds__(256) gau_attn_kernel(const float* __restrict__
         if (i0 + r < K)
           out[(base_row + i0 + r) * E + e0 + el] = (bf16)(uv[(base_row + i0 + r) * ld + e0 + el] * acc[r]);
     }
+  }
+}
+
+// The same token mixing on exact-f32 MFMAs (v_mfma_f32_32x32x2_f32): lane l supplies A[m = l % 32][k = l / 32] and
+// B[k = l / 32][n = l % 32], register r of D is row (r & 3) + 8 (r >> 2) + 4 (l / 32), column l % 32.  One
+// workgroup (4 waves) per instance; tokens padded to 160 rows (5 tiles), pad rows / keys read as 0.
+//   phase 1  base = uv[:, 2E : 2E + S] -> LDS [K][S + 1] (conflict-free column reads)
+//   phase 2  kernel tile (ti, tj) = sum_k q[m][k] k[n][k], q = base * gamma0 + beta0, k = base * gamma1 + beta1
+//            formed per element as torch does (a product, then a sum), relu(x / sqrt(s))^2 -> LDS [K][K | 1]
+//   phase 3  u * (kernel @ v): v staged 128 columns at a time in LDS over the dead base rows (row stride 160:
+//            the two k rows of a step land in opposite bank halves), 5 x 4 tiles per round
+constexpr int GAU_M_TILES = 5;  // 160 padded tokens
+__device__ __forceinline__ floatx16 mfma_f32x2(float a, float b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+__global__ void __launch_bounds__(256) gau_mfma_kernel(const float* __restrict__ uv, int K, int E, int S,
+                                                       const float* __restrict__ gamma, const float* __restrict__ beta,
+                                                       float sqrt_s, bf16* __restrict__ out) {
+#pragma clang fp contract(off)
+  extern __shared__ float sm[];
+  const int SP = S + 1, AP = K | 1, VS = 160;
+  const int KP2 = (K + 1) & ~1;
+  float* base = sm;                                            // [K][SP], later V [KP2][VS]
+  float* A = sm + max(K * SP, KP2 * VS);                       // [K][AP]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int li = lane & 31, lh = lane >> 5;
+  const long row0 = (long)blockIdx.x * K;
+  const int ld = 2 * E + S;
+  for (int idx = tid; idx < K * S; idx += 256) {
+    const int j = idx / S, c = idx - j * S;
+    base[j * SP + c] = uv[(row0 + j) * ld + 2 * E + c];
+  }
+  __syncthreads();
+  // phase 2: 25 tiles over the 4 waves
+  for (int tile = wave; tile < GAU_M_TILES * GAU_M_TILES; tile += 4) {
+    const int ti = tile / GAU_M_TILES, tj = tile - ti * GAU_M_TILES;
+    const int m = ti * 32 + li, n = tj * 32 + li;
+    floatx16 acc = {};
+    for (int ks = 0; ks < S; ks += 2) {
+      const int kk = ks + lh;
+      const float qa = m < K ? __fadd_rn(__fmul_rn(base[m * SP + kk], gamma[kk]), beta[kk]) : 0.f;
+      const float kb = n < K ? __fadd_rn(__fmul_rn(base[n * SP + kk], gamma[S + kk]), beta[S + kk]) : 0.f;
+      acc = mfma_f32x2(qa, kb, acc);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int mm = ti * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      if (mm < K && n < K) {
+        const float x = fmaxf(acc[r] / sqrt_s, 0.f);
+        A[mm * AP + n] = x * x;
+      }
+    }
+  }
+  __syncthreads();
+  // phase 3: rounds of 128 v columns
+  float* V = base;
+  for (int e0 = 0; e0 < E; e0 += 128) {
+    for (int idx = tid; idx < KP2 * 128; idx += 256) {
+      const int j = idx >> 7, c = idx & 127;
+      V[j * VS + c] = j < K ? uv[(row0 + j) * ld + E + e0 + c] : 0.f;
+    }
+    __syncthreads();
+    for (int tile = wave; tile < GAU_M_TILES * 4; tile += 4) {
+      const int ti = tile >> 2, tn = tile & 3;
+      const int m = ti * 32 + li;
+      floatx16 acc = {};
+      for (int ks = 0; ks < KP2; ks += 2) {
+        const int kk = ks + lh;
+        const float a = (m < K && kk < K) ? A[m * AP + kk] : 0.f;
+        acc = mfma_f32x2(a, V[kk * VS + tn * 32 + li], acc);
+      }
+      const int col = e0 + tn * 32 + li;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int mm = ti * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+        if (mm < K) out[(row0 + mm) * E + col] = (bf16)(uv[(row0 + mm) * ld + col] * acc[r]);
+      }
+    }
+    __syncthreads();
   }
 }
 
@@ -340,9 +422,32 @@ constexpr int GAU_KMAX = 136;
 
 size_t gau_lds_bytes(int S) { return sizeof(float) * ((size_t)GAU_KMAX * (S + 1) + GAU_KMAX * (GAU_KMAX + 1) + 4 * S); }
 
+size_t gau_mfma_lds_bytes(int K, int S) {
+  const int KP2 = (K + 1) & ~1;
+  return sizeof(float) * ((size_t)std::max(K * (S + 1), KP2 * 160) + (size_t)K * (K | 1));
+}
+
 hipError_t launch_gau_attn(const float* uv, int n_inst, int K, int E, int S, const float* gamma, const float* beta,
                            void* out, hipStream_t s) {
   if (n_inst == 0) return hipSuccess;
+  static int use_valu = -1;  // VGE_GAU_VALU=1: the VALU kernel (A/B timing)
+  if (use_valu < 0) {
+    const char* e = getenv("VGE_GAU_VALU");
+    use_valu = (e && atoi(e) == 1) ? 1 : 0;
+  }
+  const size_t mb = gau_mfma_lds_bytes(K, S);
+  if (!use_valu && K <= GAU_M_TILES * 32 && S % 2 == 0 && E % 128 == 0 && mb <= 160 * 1024) {
+    static bool mattr = false;
+    if (!mattr) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gau_mfma_kernel),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      if (e != hipSuccess) return e;
+      mattr = true;
+    }
+    hipLaunchKernelGGL(gau_mfma_kernel, dim3(n_inst), dim3(256), mb, s, uv, K, E, S, gamma, beta,
+                       (float)std::sqrt((double)S), static_cast<bf16*>(out));
+    return hipGetLastError();
+  }
   const size_t bytes = gau_lds_bytes(S);
   static bool attr = false;
   if (!attr) {
