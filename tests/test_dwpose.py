@@ -125,6 +125,9 @@ def _bf(shape, scale=1.0, seed=0):
     (266, 1, 1, 512, 256, 1, 1, "none", False, "f32"),
     (2, 20, 20, 256, 85, 1, 1, "sigmoid", True, None),
     (1, 40, 40, 1024, 512, 3, 2, "silu", False, None),
+    (9, 97, 97, 64, 256, 1, 1, "silu", False, None),      # persistent grid: 331 tiles (ragged) on <= 256 workgroups
+    (7, 100, 100, 32, 256, 3, 1, "silu", False, None),    # 274 tiles, odd K stage count (9 -> 10 with a zero stage)
+    (9, 90, 90, 64, 256, 1, 1, "sigmoid", True, None),    # persistent f32 epilogue
 ])
 def test_conv_bf16_vs_torch(D, n, H, W, Cin, Cout, k, stride, act, outf32, res):
     x = _bf((n, H, W, Cin), seed=1)
@@ -150,6 +153,38 @@ def test_conv_bf16_vs_torch(D, n, H, W, Cin, Cout, k, stride, act, outf32, res):
     err = (out - ref).abs()
     tol = 2e-5 * scale + (0 if outf32 else 2.0 ** -8 * ref.abs())
     assert bool((err <= tol + 1e-6).all()), (float(err.max()), scale)
+
+
+@gpu
+@pytest.mark.parametrize("n,H,W,Cin,Cout,k,stride,act,outf32", [
+    (64, 80, 80, 256, 256, 1, 1, "silu", False),
+    (33, 41, 37, 128, 512, 3, 1, "silu", False),
+    (64, 40, 40, 512, 256, 3, 2, "none", True),
+    (300, 1, 1, 512, 768, 1, 1, "silu", False),
+])
+def test_conv_persistent_matches_one_tile_per_workgroup(D, n, H, W, Cin, Cout, k, stride, act, outf32):
+    """conv2p_bf16_kernel (persistent grid, register epilogue) and conv_bf16_kernel (128-row tiles) against
+    conv2_bf16_kernel (one tile per workgroup, LDS epilogue): same per-element MFMA order over K and the same epilogue
+    arithmetic -> bit-identical outputs, so the per-layer tuner (vge_cnn_host.h ConvTuner) cannot change results."""
+    import ctypes as C
+    from vge import lib as Lb
+    lib = Lb.load()
+    lib.vge_debug_set_conv_persist.argtypes = [C.c_int]
+    lib.vge_debug_set_conv_v1.argtypes = [C.c_int]
+    x = _bf((n, H, W, Cin), seed=7).to(DEV)
+    w = _bf((Cout, Cin, k, k), (2.0 / (Cin * k * k)) ** 0.5, seed=8).to(DEV)
+    b = (torch.randn(Cout, generator=torch.Generator().manual_seed(9)) * 0.1).to(DEV)
+    outs = []
+    try:
+        for v1, p in ((0, 0), (0, 1), (1, 1)):  # the 128-row kernel too: every conv variant the tuner picks from
+            lib.vge_debug_set_conv_v1(v1)
+            lib.vge_debug_set_conv_persist(p)
+            outs.append(D.conv_bf16(x, w, b, stride=stride, pad=k // 2, act=act, out_f32=outf32))
+            torch.cuda.synchronize()
+    finally:
+        lib.vge_debug_set_conv_persist(1)
+        lib.vge_debug_set_conv_v1(0)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
 
 
 @gpu

@@ -1,5 +1,6 @@
 """Time conv_bf16 (the DWPose / YOLOX implicit-GEMM conv) on representative layer shapes: v2 (256-row tiles, default
-for Cout > 64) vs v1 (128-row tiles) vs torch/MIOpen conv2d (bf16, channels_last).  python tools/conv_bench.py"""
+for Cout % 256 == 0; persistent grid) vs v2_one_tile (VGE_CONV_PERSIST=0) vs v1 (128-row tiles) vs torch/MIOpen
+conv2d (bf16, channels_last).  python tools/conv_bench.py"""
 import ctypes as C
 import json
 import sys
@@ -17,6 +18,10 @@ SHAPES = [  # name, n, H, W, Cin, Cout, k, stride
     ("yolox_dark4_bneck_3x3", 64, 40, 40, 256, 256, 3, 1),
     ("yolox_dark3_down_3x3s2", 64, 160, 160, 128, 256, 3, 2),
     ("yolox_1x1_256_128", 64, 80, 80, 256, 128, 1, 1),
+    ("yolox_1x1_256_256", 64, 80, 80, 256, 256, 1, 1),
+    ("yolox_1x1_512_256", 64, 40, 40, 512, 256, 1, 1),
+    ("yolox_1x1_1024_512", 64, 20, 20, 1024, 512, 1, 1),
+    ("yolox_head_1x1_256", 64, 80, 80, 256, 256, 1, 1),
     ("rtm_stage1_3x3_64", 256, 96, 72, 64, 64, 3, 1),
     ("rtm_stem2_3x3_32_64", 256, 192, 144, 32, 64, 3, 1),
     ("rtm_final_7x7", 256, 12, 9, 1024, 133, 7, 1),
@@ -37,6 +42,7 @@ def timeit(fn, iters=10):
 
 lib = L.load()
 lib.vge_debug_set_conv_v1.argtypes = [C.c_int]
+lib.vge_debug_set_conv_persist.argtypes = [C.c_int]
 res = []
 for name, n, H, W, Cin, Cout, k, st in SHAPES:
     x = torch.randn(n, H, W, Cin, device="cuda").to(torch.bfloat16)
@@ -47,12 +53,14 @@ for name, n, H, W, Cin, Cout, k, st in SHAPES:
     out = torch.empty(n, Ho, Wo, Cout, device="cuda", dtype=torch.float32 if out_f32 else torch.bfloat16)
     fl = 2.0 * n * Ho * Wo * Cout * Cin * k * k
     r = {"shape": name, "gflop": fl / 1e9}
-    for v1 in (0, 1):
+    for name_v, v1, pers in (("v2", 0, 1), ("v2p_grid_ntiles", 0, 2), ("v2_one_tile", 0, 0), ("v1", 1, 1)):
         lib.vge_debug_set_conv_v1(v1)
+        lib.vge_debug_set_conv_persist(pers)
         ms = timeit(lambda: D.conv_bf16(x, w, b, stride=st, pad=k // 2, act="none" if out_f32 else "silu",
                                         out_f32=out_f32, out=out))
-        r["v1" if v1 else "v2"] = {"ms": ms, "tflops": fl / ms / 1e9}
+        r[name_v] = {"ms": ms, "tflops": fl / ms / 1e9}
     lib.vge_debug_set_conv_v1(0)
+    lib.vge_debug_set_conv_persist(1)
     xc = x.permute(0, 3, 1, 2)  # NCHW view of NHWC memory = channels_last
     wc = w.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     try:

@@ -23,12 +23,15 @@
 
 #include <cstdlib>
 #include <algorithm>
+#include <type_traits>
 
 namespace {
 
 typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef unsigned uintx2_t __attribute__((ext_vector_type(2)));
+typedef unsigned uintx4_t __attribute__((ext_vector_type(4)));
 
 constexpr int CV_M = 128, CV_K = 32, CV_ST = 3;
 
@@ -406,6 +409,302 @@ __global__ void __launch_bounds__(512, 1) conv2_bf16_kernel(ConvArgs a) {
       }
     }
   }
+}
+
+// ------------------------------------------------------------------------- conv v2, persistent (default)
+// conv2_bf16_kernel's tiles and schedule on a persistent grid (one workgroup per CU, tiles b, b + G, b + 2G, ...
+// with G a multiple of 8, so a workgroup stays on its XCD's contiguous tile range) with ONE stage stream across
+// its tiles: the ring issues stage g + 4 of the global sequence (tile g / nk, k-stage g % nk), so the next tile's
+// first four stages are in flight while this tile's epilogue runs, and the next tile's first fragments are read
+// during this tile's last MFMAs.  The epilogue leaves the LDS (ring) alone: the C-layout accumulators are turned
+// row-major inside each 4-lane quad (two DPP quad_perm exchange rounds: lane i of a quad then holds row i, four
+// consecutive columns) and stored straight to global memory, 8 B (bf16) / 16 B (f32) per lane.  vmcnt counts the
+// epilogue's stores in issue order between the ring stages, so the three steps after an epilogue allow NST more
+// outstanding operations.
+template <int CTRL>
+__device__ __forceinline__ float dppq(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+// 4x4 transpose inside each quad: on entry lane i holds column i of rows 0..3 (v0..v3), on exit row i, columns 0..3
+__device__ __forceinline__ void quad_t4(float& v0, float& v1, float& v2, float& v3, bool o1, bool o2) {
+  float x = o1 ? v0 : v1, y = dppq<0xB1>(x);  // quad_perm [1,0,3,2]
+  v0 = o1 ? y : v0;
+  v1 = o1 ? v1 : y;
+  x = o1 ? v2 : v3;
+  y = dppq<0xB1>(x);
+  v2 = o1 ? y : v2;
+  v3 = o1 ? v3 : y;
+  x = o2 ? v0 : v2;
+  y = dppq<0x4E>(x);  // quad_perm [2,3,0,1]
+  v0 = o2 ? y : v0;
+  v2 = o2 ? v2 : y;
+  x = o2 ? v1 : v3;
+  y = dppq<0x4E>(x);
+  v1 = o2 ? y : v1;
+  v3 = o2 ? v3 : y;
+}
+
+template <int BN, int ACT, int OUT, int RES>
+__global__ void __launch_bounds__(512, 1) conv2p_bf16_kernel(ConvArgs a) {
+  using Cf = C2Cfg<BN>;
+  constexpr int TM = Cf::TM, TN = Cf::TN, LPS = Cf::LPS, BQ = Cf::BQ;
+  constexpr int NST = TM * TN * 4;  // epilogue stores per thread
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / Cf::WN, wn = wave % Cf::WN;
+  const int ntn = (a.Cout + BN - 1) / BN, ntiles = ((a.M + C2_M - 1) / C2_M) * ntn;
+  const int G = gridDim.x, b = blockIdx.x;
+  const int T = (ntiles - b + G - 1) / G;  // host: G <= ntiles, G % 8 == 0 unless G == ntiles
+  const int nk = (a.Kp / CV_K + 1) & ~1, total = T * nk;  // even: an odd K gets one all-zero stage (zero page)
+  const int cmask = (1 << a.cin_log2) - 1;
+  const int lc = (lane & 3) ^ ((lane >> 4) & 3);
+
+  // ---- issue side: gather state of the tile whose stages are being issued
+  int img_hw[2], ih0[2], iw0[2];
+  bool mval[2];
+  const bf16* wrow[BQ];
+  auto setup = [&](int i) {
+    const int bid = xcd_remap(b + i * G, ntiles);
+    const int mt = bid / ntn, m0 = mt * C2_M, n0 = (bid - mt * ntn) * BN;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int m = m0 + 16 * (2 * wave + j) + (lane >> 2);
+      mval[j] = m < a.M;
+      const int hw = a.Ho * a.Wo;
+      const int img = m / hw, rem = m - img * hw;
+      const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
+      img_hw[j] = img * a.H;
+      ih0[j] = oh * a.stride - a.pad;
+      iw0[j] = ow * a.stride - a.pad;
+    }
+#pragma unroll
+    for (int j = 0; j < BQ; ++j) wrow[j] = a.w + (size_t)(n0 + 16 * (BQ * wave + j) + (lane >> 2)) * a.Kp + lc * 8;
+  };
+  int is_t = 0, is_k = -1, is_g = -1;  // last issued stage (tile, k-stage, global index)
+  setup(0);
+  auto issue = [&](int g) {  // g == is_g + 1, or past the end: re-fetch the last stage into its own slot (same bytes)
+    if (g < total) {
+      is_g = g;
+      if (++is_k == nk) {
+        is_k = 0;
+        setup(++is_t);
+      }
+    }
+    char* slot = lds + (is_g % C2_ST) * Cf::SLOT;
+    const int k = is_k * CV_K + lc * 8;
+    const int tap = k >> a.cin_log2, ci = k & cmask;
+    const int kh = (tap * a.kw_magic) >> 16, kw = tap - kh * a.KW;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int ih = ih0[j] + kh, iw = iw0[j] + kw;
+      const bool ok = mval[j] && tap < a.taps && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      glds16(ok ? a.x + ((size_t)(img_hw[j] + ih) * a.W + iw) * a.ldx + ci : a.zero, slot + (2 * wave + j) * 1024);
+    }
+    const bool kin = is_k * CV_K < a.Kp;
+#pragma unroll
+    for (int j = 0; j < BQ; ++j) glds16(kin ? wrow[j] + is_k * CV_K : a.zero, slot + Cf::TA + (BQ * wave + j) * 1024);
+  };
+
+  // ---- compute side
+  const int h = lane >> 5, swz = (lane >> 2) & 3, rowoff = (lane & 31) * 64;
+  struct Frag {
+    bf16x8 a[2][TM], b[2][TN];
+  };
+  auto read = [&](int g, Frag& f) {
+    const char* cur = lds + (g % C2_ST) * Cf::SLOT;
+    const char* As = cur + wm * Cf::WR * 64 + rowoff;
+    const char* Bs = cur + Cf::TA + wn * Cf::WC * 64 + rowoff;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int co = ((2 * s + h) ^ swz) * 16;
+#pragma unroll
+      for (int t = 0; t < TM; ++t) f.a[s][t] = *reinterpret_cast<const bf16x8*>(As + t * 32 * 64 + co);
+#pragma unroll
+      for (int u = 0; u < TN; ++u) f.b[s][u] = *reinterpret_cast<const bf16x8*>(Bs + u * 32 * 64 + co);
+    }
+  };
+  floatx16 acc[TM][TN];
+  auto zero = [&]() {
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int u = 0; u < TN; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
+  };
+  zero();
+  auto mma = [&](const Frag& f, int s) {
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int u = 0; u < TN; ++u)
+        acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[s][t], f.b[s][u], acc[t][u], 0, 0, 0);
+  };
+
+  // epilogue: quad i of lanes holds (after quad_t4) row 8 q + 4 h + i of each 32-row block, columns 4 (lane % 32 / 4)
+  // .. + 3.  Residual loads and output stores are raw buffer accesses on per-tile descriptors (rows past M and columns
+  // past Cout get an out-of-range offset: loads return 0, stores are dropped), so the epilogue is one branch-free block
+  // and the compiler's in-order vmcnt accounting stays exact.  The tile's bias / rscale are loaded at the top of its
+  // last step (before that step's ring loads); residual rows are loaded one 32-row block ahead of their use.
+  const bool o1 = lane & 1, o2 = lane & 2;
+  const int qrow = 4 * h + (lane & 3), qcol = 4 * ((lane & 31) >> 2);
+  constexpr int OE = OUT == OUT_BF16 ? 2 : 4;  // output element bytes
+  constexpr int RE = RES == RES_F32S ? 4 : 2;  // residual element bytes
+  typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+  typedef typename std::conditional<RES == RES_F32S, uintx4_t, uintx2_t>::type RV;
+  floatx4 bb[TN], rs[TN];
+  auto tile_mn = [&](int i, int& m0, int& n0) {
+    const int bid = xcd_remap(b + i * G, ntiles);
+    const int mt = bid / ntn;
+    m0 = mt * C2_M;
+    n0 = (bid - mt * ntn) * BN;
+  };
+  // bias / rscale: asm loads, invisible to hipcc's waitcnt pass (which answers any load issued among LDS-DMA ring
+  // loads and stores with vmcnt(0)); consts_wait retires them by count, naming the registers so nothing reads them
+  // earlier (cdna_hip_programming.md 5.7 item 1 form ii)
+  constexpr int NCL = RES == RES_F32S ? 2 * TN : TN;  // asm loads per load_consts
+  auto load_consts = [&](int i) {
+    int m0, n0;
+    tile_mn(i, m0, n0);
+    const int cw = n0 + wn * Cf::WC + qcol;
+#pragma unroll
+    for (int u = 0; u < TN; ++u) {
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(bb[u]) : "v"(a.bias + cw + 32 * u) : "memory");
+      if constexpr (RES == RES_F32S)
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(rs[u]) : "v"(a.rscale + cw + 32 * u) : "memory");
+    }
+  };
+  auto consts_wait = [&]() {  // issued after them: two steps' ring loads (the last step's vmcnt(LPS) retired them)
+    static_assert(TN == 2, "consts_wait names two registers");
+    __builtin_amdgcn_sched_barrier(0);
+    if constexpr (RES == RES_F32S)
+      asm volatile("s_waitcnt vmcnt(%4)" : "+v"(bb[0]), "+v"(bb[1]), "+v"(rs[0]), "+v"(rs[1]) : "i"(2 * LPS) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(%2)" : "+v"(bb[0]), "+v"(bb[1]) : "i"(2 * LPS) : "memory");
+    (void)NCL;
+  };
+  auto epilogue = [&](int i) {
+    consts_wait();
+    int m0, n0;
+    tile_mn(i, m0, n0);
+    const int rows = min(C2_M, a.M - m0);
+    const __amdgpu_buffer_rsrc_t ob = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<char*>(a.out) + (size_t)m0 * a.ldo * OE, (short)0, (int)((size_t)rows * a.ldo * OE), 0x00020000);
+    __amdgpu_buffer_rsrc_t rb = ob;
+    if constexpr (RES != RES_NONE)
+      rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(reinterpret_cast<const char*>(a.res)) + (size_t)m0 * a.ldr * RE,
+                                             (short)0, (int)((size_t)rows * a.ldr * RE), 0x00020000);
+    const int rw = wm * Cf::WR + qrow, cw = n0 + wn * Cf::WC + qcol;
+    auto offs = [&](int t, int u, int q, long ld, int eb) {
+      const int r = rw + 32 * t + 8 * q, col = cw + 32 * u;
+      return (r < rows && col + 4 <= a.Cout) ? (r * (int)ld + col) * eb : 0x7FFFFFF0;  // host: Cout % 4 == 0
+    };
+    RV rv[2][4];  // residual of one 32 x 32 block, loaded one block ahead
+    auto rload = [&](int blk, RV (&d)[4]) {
+      const int t = blk / TN, u = blk % TN;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        if constexpr (RES == RES_BF16) d[q] = __builtin_amdgcn_raw_buffer_load_b64(rb, offs(t, u, q, a.ldr, RE), 0, 0);
+        if constexpr (RES == RES_F32S) d[q] = __builtin_amdgcn_raw_buffer_load_b128(rb, offs(t, u, q, a.ldr, RE), 0, 0);
+      }
+    };
+    if constexpr (RES != RES_NONE) rload(0, rv[0]);
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+#pragma unroll
+      for (int u = 0; u < TN; ++u) {
+        const int blk = t * TN + u;
+        if constexpr (RES != RES_NONE)
+          if (blk + 1 < TM * TN) rload(blk + 1, rv[(blk + 1) & 1]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          float e[4] = {acc[t][u][4 * q], acc[t][u][4 * q + 1], acc[t][u][4 * q + 2], acc[t][u][4 * q + 3]};
+          quad_t4(e[0], e[1], e[2], e[3], o1, o2);
+          e[0] += bb[u].x;
+          e[1] += bb[u].y;
+          e[2] += bb[u].z;
+          e[3] += bb[u].w;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            if constexpr (ACT == ACT_SILU) e[c] = silu(e[c]);
+            if constexpr (ACT == ACT_SIGMOID) e[c] = sigm(e[c]);
+          }
+          if constexpr (RES == RES_BF16) {
+            const bf16x4_t r4 = __builtin_bit_cast(bf16x4_t, rv[blk & 1][q]);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) e[c] += (float)r4[c];
+          }
+          if constexpr (RES == RES_F32S) {
+            const floatx4 r4 = __builtin_bit_cast(floatx4, rv[blk & 1][q]);
+            e[0] = fmaf(rs[u].x, r4.x, e[0]);
+            e[1] = fmaf(rs[u].y, r4.y, e[1]);
+            e[2] = fmaf(rs[u].z, r4.z, e[2]);
+            e[3] = fmaf(rs[u].w, r4.w, e[3]);
+          }
+          const int oo = offs(t, u, q, a.ldo, OE);
+          if constexpr (OUT == OUT_BF16) {
+            bf16x4_t o;
+#pragma unroll
+            for (int c = 0; c < 4; ++c) o[c] = (bf16)e[c];
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uintx2_t, o), ob, oo, 0, 0);
+          } else {
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(uintx4_t, floatx4{e[0], e[1], e[2], e[3]}), ob, oo, 0, 0);
+          }
+        }
+    }
+  };
+
+  constexpr int NM = TM * TN;
+  // one 32-deep stage; kk = its index in the tile; after an epilogue (tile i > 0) its NST stores sit between the
+  // ring stages for three steps
+  // mode 0: plain step; 1: the tile's second-to-last step, which loads its bias / rscale ahead of its ring loads;
+  // 2: the last step, whose wait also retires them (and every store of the previous epilogue)
+  auto body = [&](int g, int kk, int i, Frag& cur, Frag& nxt, int mode) {
+    if (mode == 2)
+      vmcnt_b<LPS>();
+    else if (i > 0 && kk < 3)
+      vmcnt_b<2 * LPS + NST>();
+    else
+      vmcnt_b<2 * LPS>();
+    lds_barrier_b();
+    if (mode == 1) load_consts(i);
+    issue(g + 4);
+    read(min(g + 1, total - 1), nxt);
+    mma(cur, 0);
+    mma(cur, 1);
+#pragma unroll
+    for (int j = 0; j < LPS; ++j) {
+      __builtin_amdgcn_sched_group_barrier(0x008, NM / LPS > 0 ? NM / LPS : 1, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);                            // VMEM (global_load_lds)
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      __builtin_amdgcn_sched_group_barrier(0x008, NM / 4 > 0 ? NM / 4 : 1, 0);      // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, (2 * (TM + TN) + 3) / 4, 0);     // DS read
+    }
+  };
+  auto last = [&](int g, int kk, int i, Frag& cur, Frag& nxt) {  // the tile's last stage + its epilogue
+    body(g, kk, i, cur, nxt, 2);
+    epilogue(i);
+    zero();
+  };
+  for (int st = 0; st < C2_ST - 1; ++st) issue(st);
+  vmcnt_b<3 * LPS>();  // stage 0 landed
+  lds_barrier_b();
+  Frag f0, f1;
+  read(0, f0);
+  int g = 0;
+  for (int i = 0; i < T; ++i) {  // every tile starts with its first fragments in f0
+    for (int kk = 0; kk < nk - 2; kk += 2, g += 2) {
+      body(g, kk, i, f0, f1, 0);
+      body(g + 1, kk + 1, i, f1, f0, 0);
+    }
+    body(g, nk - 2, i, f0, f1, 1);
+    last(g + 1, nk - 1, i, f1, f0);
+    g += 2;
+  }
+  vmcnt_b<0>();
 }
 
 // ------------------------------------------------------------------------------------ depthwise
@@ -808,8 +1107,44 @@ static int ilog2(int v) {
   return l;
 }
 
+static int g_conv_persist = -1;  // VGE_CONV_PERSIST=0: one tile per workgroup (conv2_bf16_kernel, A/B timing)
+
+static int persistent_grid(int ntiles) {  // one workgroup per CU, a multiple of 8 (whole XCDs)
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      n = 256;
+    cus = std::max(8, n / 8 * 8);
+  }
+  return ntiles <= cus ? ntiles : cus;
+}
+
 template <int BN, int ACT, int OUT, int RES>
-static hipError_t conv2_go(const ConvArgs& a, hipStream_t s) {
+static hipError_t conv2p_go(const ConvArgs& a, hipStream_t s) {
+  constexpr int BYTES = C2Cfg<BN>::RING;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv2p_bf16_kernel<BN, ACT, OUT, RES>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, BYTES);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int ntiles = ((a.M + C2_M - 1) / C2_M) * ((a.Cout + BN - 1) / BN);
+  const int grid = g_conv_persist == 2 ? ntiles : persistent_grid(ntiles);  // 2: A/B of the schedule alone
+  hipLaunchKernelGGL((conv2p_bf16_kernel<BN, ACT, OUT, RES>), dim3(grid), dim3(512), BYTES, s, a);
+  return hipGetLastError();
+}
+
+// pmode: -1 = VGE_CONV_PERSIST (default on), 0 = one tile per workgroup, 1 = persistent
+template <int BN, int ACT, int OUT, int RES>
+static hipError_t conv2_go(const ConvArgs& a, hipStream_t s, int pmode) {
+  if (g_conv_persist < 0) {
+    const char* e = getenv("VGE_CONV_PERSIST");
+    g_conv_persist = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  if constexpr (RES == RES_NONE)  // residual epilogues stay on conv2_bf16_kernel (their loads need vmcnt drains)
+    if (pmode < 0 ? g_conv_persist : pmode) return conv2p_go<BN, ACT, OUT, RES>(a, s);
   constexpr int BYTES = C2Cfg<BN>::LDS;
   static bool attr = false;
   if (!attr) {
@@ -826,13 +1161,13 @@ static hipError_t conv2_go(const ConvArgs& a, hipStream_t s) {
 static int g_conv_v1 = -1;  // VGE_CONV_V1=1: every layer on the 128-row kernel (A/B timing)
 
 template <int TN, int ACT, int OUT, int RES>
-static hipError_t conv_go(const ConvArgs& a, int grid, hipStream_t s) {
+static hipError_t conv_go(const ConvArgs& a, int grid, hipStream_t s, int pmode) {
   if (g_conv_v1 < 0) {
     const char* e = getenv("VGE_CONV_V1");
     g_conv_v1 = (e && atoi(e) == 1) ? 1 : 0;
   }
   if constexpr (TN == 256) {
-    return g_conv_v1 ? conv_go<128, ACT, OUT, RES>(a, grid, s) : conv2_go<256, ACT, OUT, RES>(a, s);
+    return g_conv_v1 && pmode < 0 ? conv_go<128, ACT, OUT, RES>(a, grid, s, pmode) : conv2_go<256, ACT, OUT, RES>(a, s, pmode);
   } else {
   constexpr int LDS = CV_ST * (CV_M * CV_K * 2 + TN * CV_K * 2);
   constexpr int EPI = 64 * (TN + 4) * 4;
@@ -874,14 +1209,22 @@ hipError_t launch_conv_bf16(const ConvLaunch& c, hipStream_t s) {
   a.Kp = c.Kp;
   a.Cout = c.Cout;
   a.M = c.n_img * a.Ho * a.Wo;
-  const int tn1 = c.tn > 128 ? 128 : c.tn;  // v1 grid (the tn 256 case runs conv2 with its own grid)
+  int tn = c.tn, pmode = -1;
+  if (c.variant == 1) tn = tn > 128 ? 128 : tn;
+  if (c.variant == 2 || c.variant == 3) {
+    if (c.Npad % 256) return hipErrorInvalidValue;
+    tn = 256;
+    pmode = c.variant == 3 ? 1 : 0;
+  }
+  const int tn1 = tn > 128 ? 128 : tn;  // v1 grid (the tn 256 case runs conv2 with its own grid)
   const int grid = ((a.M + CV_M - 1) / CV_M) * ((c.Cout + tn1 - 1) / tn1);
   if (a.M <= 0) return hipSuccess;
 #define VGE_CONV_CASE(ACT, OUT, RES)                                                              \
   if (c.act == ACT && c.out_f32 == OUT && c.res_mode == RES)                                      \
-    return c.tn == 64 ? conv_go<64, ACT, OUT, RES>(a, grid, s)                                    \
-                      : c.tn == 128 ? conv_go<128, ACT, OUT, RES>(a, grid, s) : conv_go<256, ACT, OUT, RES>(a, grid, s);
-  if (c.tn != 64 && c.tn != 128 && c.tn != 256) return hipErrorInvalidValue;
+    return tn == 64 ? conv_go<64, ACT, OUT, RES>(a, grid, s, pmode)                               \
+                    : tn == 128 ? conv_go<128, ACT, OUT, RES>(a, grid, s, pmode)                  \
+                                : conv_go<256, ACT, OUT, RES>(a, grid, s, pmode);
+  if (tn != 64 && tn != 128 && tn != 256) return hipErrorInvalidValue;
   VGE_CONV_CASE(ACT_SILU, OUT_BF16, RES_NONE)
   VGE_CONV_CASE(ACT_SILU, OUT_BF16, RES_BF16)
   VGE_CONV_CASE(ACT_NONE, OUT_BF16, RES_NONE)
@@ -980,5 +1323,10 @@ hipError_t launch_upsample2x(const void* x, long ldx, void* y, long ldy, int n_i
 
 extern "C" int vge_debug_set_conv_v1(int on) {  // A/B timing (tools/conv_bench.py)
   vge::g_conv_v1 = on ? 1 : 0;
+  return 0;
+}
+
+extern "C" int vge_debug_set_conv_persist(int mode) {  // A/B timing (tools/conv_bench.py): 0 off, 1 on, 2 one tile each
+  vge::g_conv_persist = mode;
   return 0;
 }

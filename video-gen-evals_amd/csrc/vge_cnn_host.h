@@ -10,6 +10,9 @@
 #include <string>
 #include <unordered_map>
 #include <vector>
+#include <map>
+#include <array>
+#include <cstdlib>
 
 #include "../../include/vge.h"
 #include "vge_cnn.h"
@@ -158,10 +161,67 @@ inline bool fold_pair(WeightMap& wm, const std::string& p0, const std::string& p
   return true;
 }
 
+// Per-layer kernel choice, measured on first use: the implicit-GEMM conv has four bit-identical variants (128-row
+// tiles with 64 or 128 columns, 256 x 256 tiles one per workgroup, 256 x 256 tiles on the persistent grid) whose
+// ranking depends on K, Cout and the tile count (tools/conv_bench.py).  The first launch of each layer shape times
+// every applicable variant on the layer's own operands (one warm launch + 3 timed, hipEvents on its stream) and keeps
+// the fastest; layers whose output is also an input (in-place residual) are not re-run and take the default.
+// VGE_CONV_TUNE=0 turns it off.
+struct ConvTuner {
+  std::map<std::array<long, 10>, int> best;  // (H, W, Cin, Cout, KH, stride, act, out_f32, res, ldo) -> variant / tn
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  int on = -1;
+  ~ConvTuner() {
+    if (e0) (void)hipEventDestroy(e0);
+    if (e1) (void)hipEventDestroy(e1);
+  }
+  bool enabled() {
+    if (on < 0) {
+      const char* e = getenv("VGE_CONV_TUNE");
+      on = (e && atoi(e) == 0) ? 0 : 1;
+    }
+    return on == 1;
+  }
+};
+
 struct ConvCtx {
   const void* zero;      // >= 16 B of device zeros (padding taps)
   double* flops;         // accumulates algorithmic 2 x MACs of every launch
+  ConvTuner* tune = nullptr;
 };
+
+// encoded choice: variant * 1000 + tn
+inline hipError_t conv_tuned_launch(ConvTuner& t, ConvLaunch& c, const std::array<long, 10>& key, hipStream_t s) {
+  auto it = t.best.find(key);
+  if (it == t.best.end()) {
+    if (!t.e0 && (hipEventCreate(&t.e0) != hipSuccess || hipEventCreate(&t.e1) != hipSuccess)) return hipErrorUnknown;
+    std::vector<int> cand = {1000 + 128, 2000 + 256};
+    if (c.Cout <= 192) cand.push_back(1000 + 64);
+    if (c.res_mode == 0 && c.Cout % 4 == 0) cand.push_back(3000 + 256);
+    int pick = -1;
+    float best_ms = 0.f;
+    for (int v : cand) {
+      c.variant = v / 1000;
+      c.tn = v % 1000;
+      hipError_t e = launch_conv_bf16(c, s);
+      if (e != hipSuccess) return e;
+      if ((e = hipEventRecord(t.e0, s)) != hipSuccess) return e;
+      for (int r = 0; r < 3; ++r)
+        if ((e = launch_conv_bf16(c, s)) != hipSuccess) return e;
+      if ((e = hipEventRecord(t.e1, s)) != hipSuccess || (e = hipEventSynchronize(t.e1)) != hipSuccess) return e;
+      float ms = 0.f;
+      if ((e = hipEventElapsedTime(&ms, t.e0, t.e1)) != hipSuccess) return e;
+      if (pick < 0 || ms < best_ms) {
+        pick = v;
+        best_ms = ms;
+      }
+    }
+    it = t.best.emplace(key, pick).first;
+  }
+  c.variant = it->second / 1000;
+  c.tn = it->second % 1000;
+  return launch_conv_bf16(c, s);
+}
 
 // output-channel tile: 256-wide tiles (conv2_bf16_kernel, 8 waves) when Cout fills them, else the 128-row kernel
 // with whichever of 64 / 128 pads Cout least (tools/conv_bench.py: conv2 wins at Cout 256 / 512, loses at 128)
@@ -200,7 +260,12 @@ inline int conv(const ConvCtx& cx, const ConvW& L, const void* x, long ldx, int 
   c.out_f32 = out_f32;
   c.res_mode = res_mode;
   c.tn = conv_tile_n(L.Cout);
-  VGE_HIPCHK(launch_conv_bf16(c, s));
+  if (cx.tune && cx.tune->enabled() && out != x && (res == nullptr || res != out)) {
+    const std::array<long, 10> key = {H, W, L.Cinp, L.Cout, L.KH, stride, act, out_f32, res_mode, ldo};
+    VGE_HIPCHK(conv_tuned_launch(*cx.tune, c, key, s));
+  } else {
+    VGE_HIPCHK(launch_conv_bf16(c, s));
+  }
   const int Ho = (H + 2 * c.pad - L.KH) / stride + 1, Wo = (W + 2 * c.pad - L.KW) / stride + 1;
   if (cx.flops) *cx.flops += 2.0 * n * Ho * Wo * (double)L.Cout * L.KH * L.KW * L.Cin;
   return VGE_OK;

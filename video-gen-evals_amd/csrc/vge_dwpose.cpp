@@ -83,7 +83,8 @@ struct vge_dwpose {
       if (p) (void)hipHostFree(p);
   }
   void* dmalloc(size_t bytes) { return dev.dmalloc(bytes); }
-  ConvCtx cx() { return ConvCtx{zero, &gemm_flops}; }
+  ConvTuner tuner;  // per-layer conv variant, measured on first use
+  ConvCtx cx() { return ConvCtx{zero, &gemm_flops, &tuner}; }
 };
 
 namespace {

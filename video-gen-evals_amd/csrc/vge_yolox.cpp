@@ -44,7 +44,8 @@ struct vge_yolox {
   float* OUT[3] = {nullptr, nullptr, nullptr};
   Profiler prof;
   double gemm_flops = 0;
-  ConvCtx cx() { return ConvCtx{zero, &gemm_flops}; }
+  ConvTuner tuner;  // per-layer conv variant, measured on first use
+  ConvCtx cx() { return ConvCtx{zero, &gemm_flops, &tuner}; }
 };
 
 namespace {
