@@ -161,6 +161,8 @@ def test_conv_bf16_vs_torch(D, n, H, W, Cin, Cout, k, stride, act, outf32, res):
     (33, 41, 37, 128, 512, 3, 1, "silu", False),
     (64, 40, 40, 512, 256, 3, 2, "none", True),
     (300, 1, 1, 512, 768, 1, 1, "silu", False),
+    (16, 48, 36, 32, 64, 3, 1, "silu", False),            # small Cout: 128- vs 256-row tiles with 64 columns
+    (7, 50, 30, 64, 128, 3, 2, "none", True),
 ])
 def test_conv_persistent_matches_one_tile_per_workgroup(D, n, H, W, Cin, Cout, k, stride, act, outf32):
     """conv2p_bf16_kernel (persistent grid, register epilogue) and conv_bf16_kernel (128-row tiles) against
@@ -171,20 +173,23 @@ def test_conv_persistent_matches_one_tile_per_workgroup(D, n, H, W, Cin, Cout, k
     lib = Lb.load()
     lib.vge_debug_set_conv_persist.argtypes = [C.c_int]
     lib.vge_debug_set_conv_v1.argtypes = [C.c_int]
+    lib.vge_debug_set_conv_tall.argtypes = [C.c_int]
     x = _bf((n, H, W, Cin), seed=7).to(DEV)
     w = _bf((Cout, Cin, k, k), (2.0 / (Cin * k * k)) ** 0.5, seed=8).to(DEV)
     b = (torch.randn(Cout, generator=torch.Generator().manual_seed(9)) * 0.1).to(DEV)
     outs = []
     try:
-        for v1, p in ((0, 0), (0, 1), (1, 1)):  # the 128-row kernel too: every conv variant the tuner picks from
+        for v1, p, tall in ((0, 0, 0), (0, 1, 0), (1, 1, 0), (1, 1, 1)):  # every conv variant the tuner picks from
             lib.vge_debug_set_conv_v1(v1)
             lib.vge_debug_set_conv_persist(p)
+            lib.vge_debug_set_conv_tall(tall)
             outs.append(D.conv_bf16(x, w, b, stride=stride, pad=k // 2, act=act, out_f32=outf32))
             torch.cuda.synchronize()
     finally:
         lib.vge_debug_set_conv_persist(1)
         lib.vge_debug_set_conv_v1(0)
-    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+        lib.vge_debug_set_conv_tall(0)
+    assert all(torch.equal(outs[0], o) for o in outs[1:])
 
 
 @gpu

@@ -43,6 +43,7 @@ def timeit(fn, iters=10):
 lib = L.load()
 lib.vge_debug_set_conv_v1.argtypes = [C.c_int]
 lib.vge_debug_set_conv_persist.argtypes = [C.c_int]
+lib.vge_debug_set_conv_tall.argtypes = [C.c_int]
 res = []
 for name, n, H, W, Cin, Cout, k, st in SHAPES:
     x = torch.randn(n, H, W, Cin, device="cuda").to(torch.bfloat16)
@@ -53,14 +54,16 @@ for name, n, H, W, Cin, Cout, k, st in SHAPES:
     out = torch.empty(n, Ho, Wo, Cout, device="cuda", dtype=torch.float32 if out_f32 else torch.bfloat16)
     fl = 2.0 * n * Ho * Wo * Cout * Cin * k * k
     r = {"shape": name, "gflop": fl / 1e9}
-    for name_v, v1, pers in (("v2", 0, 1), ("v2p_grid_ntiles", 0, 2), ("v2_one_tile", 0, 0), ("v1", 1, 1)):
+    for name_v, v1, pers, tall in (("v2", 0, 1, 0), ("v2_one_tile", 0, 0, 0), ("v1", 1, 1, 0), ("v1_tall", 1, 1, 1)):
         lib.vge_debug_set_conv_v1(v1)
         lib.vge_debug_set_conv_persist(pers)
+        lib.vge_debug_set_conv_tall(tall)
         ms = timeit(lambda: D.conv_bf16(x, w, b, stride=st, pad=k // 2, act="none" if out_f32 else "silu",
                                         out_f32=out_f32, out=out))
         r[name_v] = {"ms": ms, "tflops": fl / ms / 1e9}
     lib.vge_debug_set_conv_v1(0)
     lib.vge_debug_set_conv_persist(1)
+    lib.vge_debug_set_conv_tall(0)
     xc = x.permute(0, 3, 1, 2)  # NCHW view of NHWC memory = channels_last
     wc = w.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
     try:

@@ -59,32 +59,35 @@ __device__ __forceinline__ int xcd_remap(int b, int nblk) {  // bijective: each 
 __device__ __forceinline__ float silu(float v) { return v / (1.0f + __expf(-v)); }
 __device__ __forceinline__ float sigm(float v) { return 1.0f / (1.0f + __expf(-v)); }
 
-// 256 threads = 4 waves (2 along M x 2 along N), wave tile 64 x TN/2 on 32x32x16 MFMAs.
-template <int TN, int ACT, int OUT, int RES>
+// 256 threads = 4 waves on 32x32x16 MFMAs.  BM = 128: 2 along M x 2 along N, wave tile 64 x TN/2; BM = 256 ("tall",
+// for small Cout): 4 along M, wave tile 64 x TN, so each A byte in LDS feeds twice the MFMAs of the 128-row form.
+template <int TN, int ACT, int OUT, int RES, int BM = CV_M>
 __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
-  constexpr int TA = CV_M * CV_K * 2;         // 8 KB A stage
+  constexpr int MW = BM / 64, NWV = 4 / MW;   // waves along M / N
+  constexpr int AJ = BM / 64;                 // A wave-instructions (16 rows each) per wave per stage
+  constexpr int TA = BM * CV_K * 2;           // A stage
   constexpr int TB = TN * CV_K * 2;           // B stage
   constexpr int SLOT = TA + TB;
-  constexpr int NB = TN / 64;                 // 32-col MFMA tiles per wave
+  constexpr int NB = TN / (32 * NWV);         // 32-col MFMA tiles per wave
   constexpr int BQ = TN / 16 / 4;             // B wave-instructions per wave per stage
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / NWV, wn = wave % NWV;
   const int ntn = (a.Cout + TN - 1) / TN;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int mt = bid / ntn, nt = bid - mt * ntn;
-  const int m0 = mt * CV_M, n0 = nt * TN;
+  const int m0 = mt * BM, n0 = nt * TN;
   const int nk = a.Kp / CV_K;
   const int cmask = (1 << a.cin_log2) - 1;
 
-  // per-lane gather state of this lane's two A rows (row = 16 q + lane / 4, q = 2 wave + j)
+  // per-lane gather state of this lane's AJ A rows (row = 16 q + lane / 4, q = AJ wave + j)
   const int lc = (lane & 3) ^ ((lane >> 4) & 3);  // logical 16-B chunk this lane fetches (pre-swizzled)
-  int img_hw[2], ih0[2], iw0[2];
-  bool mval[2];
+  int img_hw[AJ], ih0[AJ], iw0[AJ];
+  bool mval[AJ];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int row = 16 * (2 * wave + j) + (lane >> 2);
+  for (int j = 0; j < AJ; ++j) {
+    const int row = 16 * (AJ * wave + j) + (lane >> 2);
     const int m = m0 + row;
     mval[j] = m < a.M;
     const int hw = a.Ho * a.Wo;
@@ -104,11 +107,11 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
     const int tap = k >> a.cin_log2, ci = k & cmask;
     const int kh = (tap * a.kw_magic) >> 16, kw = tap - kh * a.KW;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
+    for (int j = 0; j < AJ; ++j) {
       const int ih = ih0[j] + kh, iw = iw0[j] + kw;
       const bool ok = mval[j] && tap < a.taps && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
       const bf16* src = ok ? a.x + ((size_t)(img_hw[j] + ih) * a.W + iw) * a.ldx + ci : a.zero;
-      glds16(src, slot + (2 * wave + j) * 1024);
+      glds16(src, slot + (AJ * wave + j) * 1024);
     }
 #pragma unroll
     for (int j = 0; j < BQ; ++j) glds16(wrow[j] + st * CV_K, slot + TA + (BQ * wave + j) * 1024);
@@ -125,7 +128,7 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
   const int h = lane >> 5;
   const int swz = (lane >> 2) & 3;
   const int rowoff = (lane & 31) * 64;
-  constexpr int LPS = 2 + BQ;  // global_load_lds per thread per stage
+  constexpr int LPS = AJ + BQ;  // global_load_lds per thread per stage
   for (int st = 0; st < CV_ST - 1; ++st) issue(min(st, nk - 1));
   for (int kt = 0; kt < nk; ++kt) {
     vmcnt_b<LPS>();     // stage kt landed (stage kt + 1 may still be in flight)
@@ -133,7 +136,7 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
     issue(min(kt + CV_ST - 1, nk - 1));  // past the end: re-fetch the last stage into its own slot (same bytes)
     const char* cur = lds + (kt % CV_ST) * SLOT;
     const char* As = cur + wm * 64 * 64 + rowoff;
-    const char* Bs = cur + TA + wn * (TN / 2) * 64 + rowoff;
+    const char* Bs = cur + TA + wn * (TN / NWV) * 64 + rowoff;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       const int co = ((2 * s + h) ^ swz) * 16;
@@ -150,7 +153,8 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
     }
   }
 
-  // epilogue through LDS in two 64-row halves (32 KB of f32 each), row-major re-read: 8 columns per thread
+  // epilogue through LDS in BM / 64 row quarters / halves (64 rows of f32 each), row-major re-read: 8 columns per
+  // thread
   vmcnt_b<0>();
   lds_barrier_b();
   constexpr int LDC = TN + 4;
@@ -158,7 +162,7 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
   constexpr int TPR = TN / 8;       // threads per row
   constexpr int RPP = 256 / TPR;    // rows per pass
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
+  for (int half = 0; half < MW; ++half) {
     if (wm == half) {
 #pragma unroll
       for (int t = 0; t < 2; ++t)
@@ -166,7 +170,7 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
         for (int u = 0; u < NB; ++u)
 #pragma unroll
           for (int r = 0; r < 16; ++r)
-            cs[(t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * LDC + wn * (TN / 2) + u * 32 + (lane & 31)] = acc[t][u][r];
+            cs[(t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * LDC + wn * (TN / NWV) + u * 32 + (lane & 31)] = acc[t][u][r];
     }
     __syncthreads();
     const int c8 = (tid % TPR) * 8;
@@ -1159,6 +1163,23 @@ static hipError_t conv2_go(const ConvArgs& a, hipStream_t s, int pmode) {
 }
 
 static int g_conv_v1 = -1;  // VGE_CONV_V1=1: every layer on the 128-row kernel (A/B timing)
+static int g_conv_tall = 0;  // vge_debug_set_conv_tall(1): 256-row tiles for the 64 / 128-column layers (A/B timing)
+
+template <int TN, int ACT, int OUT, int RES, int BM>
+static hipError_t conv1_go(const ConvArgs& a, int grid, hipStream_t s) {
+  constexpr int LDS = CV_ST * (BM * CV_K * 2 + TN * CV_K * 2);
+  constexpr int EPI = 64 * (TN + 4) * 4;
+  constexpr int BYTES = LDS > EPI ? LDS : EPI;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_bf16_kernel<TN, ACT, OUT, RES, BM>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, BYTES);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL((conv_bf16_kernel<TN, ACT, OUT, RES, BM>), dim3(grid), dim3(256), BYTES, s, a);
+  return hipGetLastError();
+}
 
 template <int TN, int ACT, int OUT, int RES>
 static hipError_t conv_go(const ConvArgs& a, int grid, hipStream_t s, int pmode) {
@@ -1168,19 +1189,10 @@ static hipError_t conv_go(const ConvArgs& a, int grid, hipStream_t s, int pmode)
   }
   if constexpr (TN == 256) {
     return g_conv_v1 && pmode < 0 ? conv_go<128, ACT, OUT, RES>(a, grid, s, pmode) : conv2_go<256, ACT, OUT, RES>(a, s, pmode);
+  } else if (pmode == 5) {  // 256-row ("tall") tiles
+    return conv1_go<TN, ACT, OUT, RES, 256>(a, ((a.M + 255) / 256) * ((a.Cout + TN - 1) / TN), s);
   } else {
-  constexpr int LDS = CV_ST * (CV_M * CV_K * 2 + TN * CV_K * 2);
-  constexpr int EPI = 64 * (TN + 4) * 4;
-  constexpr int BYTES = LDS > EPI ? LDS : EPI;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_bf16_kernel<TN, ACT, OUT, RES>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, BYTES);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
-  hipLaunchKernelGGL((conv_bf16_kernel<TN, ACT, OUT, RES>), dim3(grid), dim3(256), BYTES, s, a);
-  return hipGetLastError();
+    return conv1_go<TN, ACT, OUT, RES, CV_M>(a, grid, s);
   }
 }
 
@@ -1210,7 +1222,8 @@ hipError_t launch_conv_bf16(const ConvLaunch& c, hipStream_t s) {
   a.Cout = c.Cout;
   a.M = c.n_img * a.Ho * a.Wo;
   int tn = c.tn, pmode = -1;
-  if (c.variant == 1) tn = tn > 128 ? 128 : tn;
+  if (c.variant == 1 || c.variant == 5) tn = tn > 128 ? 128 : tn;
+  if (c.variant == 5 || (c.variant == 0 && g_conv_tall && tn < 256)) pmode = 5;  // 256-row tiles, 64 / 128 columns
   if (c.variant == 2 || c.variant == 3) {
     if (c.Npad % 256) return hipErrorInvalidValue;
     tn = 256;
@@ -1323,6 +1336,11 @@ hipError_t launch_upsample2x(const void* x, long ldx, void* y, long ldy, int n_i
 
 extern "C" int vge_debug_set_conv_v1(int on) {  // A/B timing (tools/conv_bench.py)
   vge::g_conv_v1 = on ? 1 : 0;
+  return 0;
+}
+
+extern "C" int vge_debug_set_conv_tall(int on) {  // A/B timing (tools/conv_bench.py)
+  vge::g_conv_tall = on ? 1 : 0;
   return 0;
 }
 

@@ -161,7 +161,7 @@ inline bool fold_pair(WeightMap& wm, const std::string& p0, const std::string& p
   return true;
 }
 
-// Per-layer kernel choice, measured on first use: the implicit-GEMM conv has four bit-identical variants (128-row
+// Per-layer kernel choice, measured on first use: the implicit-GEMM conv has bit-identical variants (128- or 256-row
 // tiles with 64 or 128 columns, 256 x 256 tiles one per workgroup, 256 x 256 tiles on the persistent grid) whose
 // ranking depends on K, Cout and the tile count (tools/conv_bench.py).  The first launch of each layer shape times
 // every applicable variant on the layer's own operands (one warm launch + 3 timed, hipEvents on its stream) and keeps
@@ -195,8 +195,11 @@ inline hipError_t conv_tuned_launch(ConvTuner& t, ConvLaunch& c, const std::arra
   auto it = t.best.find(key);
   if (it == t.best.end()) {
     if (!t.e0 && (hipEventCreate(&t.e0) != hipSuccess || hipEventCreate(&t.e1) != hipSuccess)) return hipErrorUnknown;
-    std::vector<int> cand = {1000 + 128, 2000 + 256};
-    if (c.Cout <= 192) cand.push_back(1000 + 64);
+    std::vector<int> cand = {1000 + 128, 5000 + 128, 2000 + 256};
+    if (c.Cout <= 192) {
+      cand.push_back(1000 + 64);
+      cand.push_back(5000 + 64);
+    }
     if (c.res_mode == 0 && c.Cout % 4 == 0) cand.push_back(3000 + 256);
     int pick = -1;
     float best_ms = 0.f;
