@@ -258,3 +258,43 @@ def test_x3_quad_and_pair_blocks_vs_f32(vg, golden_state_dict, n):
     assert (s3 - s1).abs().max().item() < 2e-5
     assert (f3 - f1).abs().max().item() < 2e-5
     assert (t3 - t1).abs().max().item() < 1e-5
+
+
+def _encoder_images(enc):
+    import ctypes as C
+    lib = enc._lib
+    lib.vge_debug_encoder_images.argtypes = [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t),
+                                             C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]
+    hb, nh, wb, nf = C.c_void_p(), C.c_size_t(), C.c_void_p(), C.c_size_t()
+    assert lib.vge_debug_encoder_images(enc._h, C.byref(hb), C.byref(nh), C.byref(wb), C.byref(nf)) == 0
+    h = torch.empty(nh.value, dtype=torch.int16, device=DEV)
+    w = torch.empty(nf.value, dtype=torch.int32, device=DEV)
+    torch.cuda.synchronize()
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    assert hip.hipMemcpy(h.data_ptr(), hb.value, nh.value * 2, 3) == 0  # hipMemcpyDeviceToDevice
+    assert hip.hipMemcpy(w.data_ptr(), wb.value, nf.value * 4, 3) == 0
+    torch.cuda.synchronize()
+    return h.cpu(), w.cpu()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("big", [False, True])
+def test_x3_device_packing_matches_host_packing(vg, golden_state_dict, big, monkeypatch):
+    """vge_encoder_create packs the 3xfp16 weight image (hi/lo planes, column exponents, chunk layout) on the
+    device; VGE_HOST_PACK=1 runs the host packer.  Both images (fp16 chunks and the f32 image holding the column
+    scales) must be identical bit for bit, including a column far outside the fp16 range."""
+    VE, ops = vg
+    sd = {k: v.copy() for k, v in golden_state_dict.items()}
+    if big:
+        k = next(k for k in sd if k.endswith("proj.weight"))
+        sd[k][3, 7] = 1e5
+        k = next(k for k in sd if k.endswith("conv1.weight"))
+        sd[k][5, 9, 2] = 3e-9
+    dev_enc = VE.load_model(sd, device=DEV, compute="f32x3")
+    monkeypatch.setenv("VGE_HOST_PACK", "1")
+    host_enc = VE.load_model(sd, device=DEV, compute="f32x3")
+    hd, wd = _encoder_images(dev_enc)
+    hh, wh = _encoder_images(host_enc)
+    assert hd.numel() > 10_000_000 and torch.equal(hd, hh)
+    assert torch.equal(wd, wh)

@@ -35,6 +35,8 @@ struct GemmArgsHost {
 };
 hipError_t encoder_kernel_setup();
 hipError_t encoder_x3_kernel_setup();
+hipError_t launch_pack_x3(const float* W, int N, int K_real, int ldk, int conv, int nch, int* sh, float* cs, int* bad,
+                          _Float16* out, hipStream_t s);
 struct EncDescX3Host {
   const _Float16* stem; const _Float16* conv; const _Float16* proj; const float* gn_w; const float* gn_b;
   const float* cs;
@@ -212,6 +214,7 @@ struct vge_encoder {
   // weights: f32 image (all modes: norms, biases, constants; f32-mode matrices) + fp16 hi/lo chunks (x3 mode)
   float* wbuf = nullptr;
   _Float16* hbuf = nullptr;
+  size_t n_half = 0, n_f32 = 0;   // element counts of hbuf / wbuf (vge_debug_encoder_images)
   void* d_encs = nullptr;         // EncDescHost[10] or EncDescX3Host[10]
   std::vector<vge::TxLayerX3Host> tx_layers;  // x3: the fused transformer kernel's layer table
   bool tx_fused = true;           // x3: one fused transformer launch (VGE_X3_UNFUSED=1: per-layer kernels)
@@ -353,27 +356,30 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
 
   const int L = dims->time_layers;
   std::vector<float> pk;      // f32 device image
-  std::vector<_Float16> ph;   // fp16 device image (x3)
-  // a packed matrix lives in pk (f32 mode) or ph (x3 mode); record (is_half, offset)
-  struct Mat { size_t off, cs; };  // packed matrix (pk or ph offset); x3: column scales at pk[cs]
+  // x3: the fp16 hi/lo image is packed on the device after the upload (launch_pack_x3, one job per matrix; the
+  // column scales land in pk's placeholders); VGE_HOST_PACK=1 packs it on host threads instead (A/B check)
+  struct PackJob { const float* W; int N, K_real, ldk, conv, nch; size_t off, cs; };
+  std::vector<PackJob> jobs;
+  size_t ph_n = 0;
+  // a packed matrix lives in pk (f32 mode) or the fp16 image (x3 mode)
+  struct Mat { size_t off, cs; };  // packed matrix (pk or fp16 image offset); x3: column scales at pk[cs]
+  auto add_job = [&](const float* W, int N, int K_real, int ldk, int conv, int chunk_mult) -> Mat {
+    const int nch = ((K_real + 15) / 16 + chunk_mult - 1) / chunk_mult * chunk_mult;
+    const Mat m{ph_n, pk.size()};
+    jobs.push_back(PackJob{W, N, K_real, ldk, conv, nch, ph_n, pk.size()});
+    pk.resize(pk.size() + N, 0.f);
+    ph_n += (size_t)(N / 256) * nch * 8192;
+    return m;
+  };
   auto pack_lin = [&](const float* W, int N, int K_real, int ldk, int P) -> Mat {
-    if (x3) {
-      const Mat m{ph.size(), pk.size()};
-      // the x3 kernels stream weights in groups of 8 chunks (zero chunks pad a short last panel)
-      pack_linear_x3([&](int n, int k) { return W[(size_t)n * ldk + k]; }, N, K_real, ph, pk, 8);
-      return m;
-    }
+    // the x3 kernels stream weights in groups of 8 chunks (zero chunks pad a short last panel)
+    if (x3) return add_job(W, N, K_real, ldk, 0, 8);
     const size_t o = pk.size();
     pack_linear(W, N, K_real, ldk, P, pk);
     return {o, 0};
   };
   auto pack_cv = [&](const float* W) -> Mat {
-    if (x3) {
-      const Mat m{ph.size(), pk.size()};
-      // K index = tap * 256 + ci (tap-major panels)
-      pack_linear_x3([&](int n, int k) { return W[((size_t)n * 256 + (k & 255)) * 5 + (k >> 8)]; }, 256, 5 * 256, ph, pk);
-      return m;
-    }
+    if (x3) return add_job(W, 256, 5 * 256, 0, 1, 1);  // K index = tap * 256 + ci (tap-major panels)
     const size_t o = pk.size();
     pack_conv(W, pk);
     return {o, 0};
@@ -463,12 +469,13 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
   const size_t off_kvb = pk.size();
   pk.insert(pk.end(), kvb, kvb + 256);
   std::vector<float> wov(256 * 256);
-  for (int i = 0; i < 256; ++i)
+  parallel_for(256, [&](int i) {
     for (int j = 0; j < 256; ++j) {
       double a = 0;
       for (int k = 0; k < 256; ++k) a += (double)Wo[(size_t)i * 256 + k] * Wv[(size_t)k * 256 + j];
       wov[(size_t)i * 256 + j] = (float)a;
     }
+  });
   const Mat m_wov = pack_lin(wov.data(), 256, 256, 256, 1);
   const size_t off_cls = pk.size();
   pk.insert(pk.end(), cls, cls + 256);
@@ -536,15 +543,67 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
     return fail(VGE_ERR_HIP, std::string("vge_encoder_create: ") + hipGetErrorString(he));
   };
   // column scaling keeps every finite weight in the fp16 planes' range; a non-finite one cannot be split
-  for (const _Float16 v : ph)
-    if (!std::isfinite((float)v))
-      return fail(VGE_ERR_ARG, "vge_encoder_create: non-finite weight, not representable by the 3xfp16 split; use VGE_F32");
+  const char* hp_env = getenv("VGE_HOST_PACK");
+  const bool host_pack = x3 && hp_env && hp_env[0] == '1';
+  std::vector<_Float16> ph;
+  if (host_pack) {
+    for (const PackJob& j : jobs) {
+      std::vector<float> cs;
+      const float* W = j.W;
+      const int ldk = j.ldk;
+      if (j.conv)
+        pack_linear_x3([&](int n, int k) { return W[((size_t)n * 256 + (k & 255)) * 5 + (k >> 8)]; }, j.N, j.K_real,
+                       ph, cs, 1);
+      else
+        pack_linear_x3([&](int n, int k) { return W[(size_t)n * ldk + k]; }, j.N, j.K_real, ph, cs, 8);
+      std::copy(cs.begin(), cs.end(), pk.begin() + j.cs);
+    }
+    for (const _Float16 v : ph)
+      if (!std::isfinite((float)v)) {
+        vge_encoder_destroy(enc);
+        return fail(VGE_ERR_ARG, "vge_encoder_create: non-finite weight, not representable by the 3xfp16 split; use VGE_F32");
+      }
+  }
   hipError_t he = x3 ? vge::encoder_x3_kernel_setup() : vge::encoder_kernel_setup();
   if (he == hipSuccess) he = hipMalloc(&enc->wbuf, pk.size() * sizeof(float));
   if (he == hipSuccess) he = hipMemcpy(enc->wbuf, pk.data(), pk.size() * sizeof(float), hipMemcpyHostToDevice);
-  if (he == hipSuccess && x3) he = hipMalloc(&enc->hbuf, ph.size() * sizeof(_Float16));
-  if (he == hipSuccess && x3) he = hipMemcpy(enc->hbuf, ph.data(), ph.size() * sizeof(_Float16), hipMemcpyHostToDevice);
+  if (he == hipSuccess && x3) he = hipMalloc(&enc->hbuf, ph_n * sizeof(_Float16));
+  if (he == hipSuccess && host_pack) he = hipMemcpy(enc->hbuf, ph.data(), ph_n * sizeof(_Float16), hipMemcpyHostToDevice);
   if (he != hipSuccess) return hipfail(he);
+  enc->n_half = x3 ? ph_n : 0;
+  enc->n_f32 = pk.size();
+  if (x3 && !host_pack) {
+    // raw f32 weights staged in HBM (one buffer), then packed by launch_pack_x3 straight into hbuf / wbuf
+    size_t raw = 0, ncol = 0;
+    std::vector<size_t> roff(jobs.size());
+    for (size_t i = 0; i < jobs.size(); ++i) {
+      roff[i] = raw;
+      raw += (size_t)jobs[i].N * (jobs[i].conv ? 1280 : jobs[i].ldk);
+      ncol = std::max(ncol, (size_t)jobs[i].N);
+    }
+    float* d_raw = nullptr;
+    int* d_sh = nullptr;  // [jobs][ncol] column exponents, then the non-finite flag
+    he = hipMalloc(&d_raw, raw * sizeof(float));
+    if (he == hipSuccess) he = hipMalloc(&d_sh, (jobs.size() * ncol + 1) * sizeof(int));
+    if (he == hipSuccess) he = hipMemset(d_sh + jobs.size() * ncol, 0, sizeof(int));
+    for (size_t i = 0; i < jobs.size() && he == hipSuccess; ++i) {
+      const PackJob& j = jobs[i];
+      he = hipMemcpyAsync(d_raw + roff[i], j.W, (size_t)j.N * (j.conv ? 1280 : j.ldk) * sizeof(float),
+                          hipMemcpyHostToDevice, nullptr);
+      if (he == hipSuccess)
+        he = vge::launch_pack_x3(d_raw + roff[i], j.N, j.K_real, j.ldk, j.conv, j.nch, d_sh + i * ncol,
+                                 enc->wbuf + j.cs, d_sh + jobs.size() * ncol, enc->hbuf + j.off, nullptr);
+    }
+    int bad = 0;
+    if (he == hipSuccess) he = hipMemcpy(&bad, d_sh + jobs.size() * ncol, sizeof(int), hipMemcpyDeviceToHost);
+    if (d_raw) (void)hipFree(d_raw);
+    if (d_sh) (void)hipFree(d_sh);
+    if (he != hipSuccess) return hipfail(he);
+    if (bad) {
+      vge_encoder_destroy(enc);
+      return fail(VGE_ERR_ARG, "vge_encoder_create: non-finite weight, not representable by the 3xfp16 split; use VGE_F32");
+    }
+  }
   float* wb = enc->wbuf;
   _Float16* hb = enc->hbuf;
   auto mat = [&](const Mat& m) -> const void* { return x3 ? (const void*)(hb + m.off) : (const void*)(wb + m.off); };
@@ -673,6 +732,18 @@ int vge_encoder_profile_read(vge_encoder* enc, double* stage_ms, int* n_calls) {
   }
   *n_calls = n;
   enc->prof_max = 0;
+  return VGE_OK;
+}
+
+// Device images of a created encoder (test hook: tests/test_gpu_parity.py compares the device-packed fp16 image
+// with VGE_HOST_PACK=1's byte for byte).
+extern "C" int vge_debug_encoder_images(const vge_encoder* enc, const void** hbuf, size_t* n_half, const void** wbuf,
+                                        size_t* n_f32) {
+  if (!enc || !hbuf || !n_half || !wbuf || !n_f32) return fail(VGE_ERR_ARG, "vge_debug_encoder_images: null argument");
+  *hbuf = enc->hbuf;
+  *n_half = enc->n_half;
+  *wbuf = enc->wbuf;
+  *n_f32 = enc->n_f32;
   return VGE_OK;
 }
 

@@ -743,10 +743,75 @@ __global__ void __launch_bounds__(512, 4) ffn_x3_kernel(FfnArgsX3 fa) {
   }
 }
 
+// ------------------------------------------------------------------ weight packing (load time)
+// Device twin of vge_api.cpp pack_linear_x3 (the host packer, kept as VGE_HOST_PACK=1): W[N][K] (or the conv
+// weight [256][256][5] read as K = tap * 256 + ci) -> chunks [N/256][nch][plane 2][h 2][n 256][8] fp16 of
+// w * 2^s_n, hi = f16(w'), lo = f16(w' - hi), with the column exponent s_n = min(8 - ilogb(max_k |w|), 100).
+// Same operations in the same order as the host code (RNE conversions, exact ldexp), so the images are
+// bit-identical (tests/test_gpu_parity.py compares them byte for byte).
+__device__ __forceinline__ float pack_w(const float* __restrict__ W, int conv, int ldk, int n, int k) {
+  return conv ? W[((size_t)n * 256 + (k & 255)) * 5 + (k >> 8)] : W[(size_t)n * ldk + k];
+}
+
+// one block per column: s_n and the column scale 2^-s_n; any non-finite weight raises *bad
+__global__ void __launch_bounds__(256) pack_x3_colexp_kernel(const float* __restrict__ W, int K_real, int ldk, int conv,
+                                                             int* __restrict__ sh, float* __restrict__ cs,
+                                                             int* __restrict__ bad) {
+  __shared__ float red[4];
+  const int n = blockIdx.x, tid = threadIdx.x;
+  float m = 0.f;
+  bool nf = false;
+  for (int k = tid; k < K_real; k += 256) {
+    const float v = pack_w(W, conv, ldk, n, k);
+    nf |= !isfinite(v);
+    m = fmaxf(m, fabsf(v));  // NaN-ignoring like the host's std::max(m, |v|)
+  }
+  if (nf) *bad = 1;
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((tid & 63) == 0) red[tid >> 6] = m;
+  __syncthreads();
+  if (tid == 0) {
+    m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    const int s = m > 0.f ? min(8 - ilogbf(m), 100) : 0;
+    sh[n] = s;
+    cs[n] = ldexpf(1.0f, -s);
+  }
+}
+
+// one thread per (column block, chunk, h, column): 8 k-values -> one 16-B store per plane
+__global__ void __launch_bounds__(256) pack_x3_kernel(const float* __restrict__ W, int N, int K_real, int ldk, int conv,
+                                                      int nch, const int* __restrict__ sh, _Float16* __restrict__ out) {
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= (N / 256) * nch * 512) return;
+  const int n = t & 255, h = (t >> 8) & 1, c = (t >> 9) % nch, nb = (t >> 9) / nch;
+  const int col = nb * 256 + n, s = sh[col];
+  half8 hi, lo;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 16 * c + 8 * h + j;
+    const float w = k < K_real ? ldexpf(pack_w(W, conv, ldk, col, k), s) : 0.0f;
+    const _Float16 x = (_Float16)w;
+    hi[j] = x;
+    lo[j] = (_Float16)(w - (float)x);
+  }
+  _Float16* ch = out + ((size_t)nb * nch + c) * 8192;
+  *reinterpret_cast<half8*>(ch + ((0 * 2 + h) * 256 + n) * 8) = hi;
+  *reinterpret_cast<half8*>(ch + ((1 * 2 + h) * 256 + n) * 8) = lo;
+}
+
 }  // namespace
 
 // ================================================================== host launchers
 namespace vge {
+
+hipError_t launch_pack_x3(const float* W, int N, int K_real, int ldk, int conv, int nch, int* sh, float* cs, int* bad,
+                          _Float16* out, hipStream_t s) {
+  if (N % 256 || K_real < 1 || nch * 16 < K_real) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pack_x3_colexp_kernel, dim3(N), dim3(256), 0, s, W, K_real, ldk, conv, sh, cs, bad);
+  const int nt = (N / 256) * nch * 512;
+  hipLaunchKernelGGL(pack_x3_kernel, dim3((nt + 255) / 256), dim3(256), 0, s, W, N, K_real, ldk, conv, nch, sh, out);
+  return hipGetLastError();
+}
 
 struct EncDescX3Host {
   const _Float16* stem; const _Float16* conv; const _Float16* proj; const float* gn_w; const float* gn_b;
