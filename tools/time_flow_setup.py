@@ -39,3 +39,35 @@ for it in range(3):
     res = {n: round((b - a) * 1e3, 2) for n, a, b in zip(names, t, t[1:])}
     res["total_ms"] = round((t[-1] - t[0]) * 1e3, 2)
     print(json.dumps(res), flush=True)
+
+# the flow's last phase ("gen_s"): generated-set scan, window sampling, ingest, encode, AC / TC
+from vge.data import create_dataset_from_generated_meshes, sample_all_windows_npz  # noqa: E402
+
+label_dict = {c: i for i, c in enumerate(sorted(ACTION_CLASSES))}
+centroids = torch.nn.functional.normalize(torch.randn(10, 256, device=dev), dim=-1)
+for it in range(3):
+    torch.cuda.synchronize()
+    t = [time.perf_counter()]
+    gen = create_dataset_from_generated_meshes(p["gen"])
+    items = sorted(gen.items, key=lambda x: x.path)
+    mine = NpzVideoDataset("", items=items)
+    t.append(time.perf_counter())
+    samples = sample_all_windows_npz(mine, 32, 8)
+    t.append(time.perf_counter())
+    fs = VE.load_frame_store(mine.items, p["gen_kp"], True)
+    t.append(time.perf_counter())
+    store = ops.DeviceFrameStore.from_host(fs, dev)
+    torch.cuda.synchronize()
+    t.append(time.perf_counter())
+    feats = VE.extract_window_features(enc, mine, p["gen_kp"], stats, 32, 8, dev, store=store)
+    torch.cuda.synchronize()
+    t.append(time.perf_counter())
+    ac = VE.compute_action_consistency_scores(feats, centroids, label_dict)
+    tc = VE.compute_temporal_coherence_scores(feats, centroids, label_dict)
+    sc = VE.combine_scores(ac, tc)
+    t.append(time.perf_counter())
+    names = ["gen_scan", "sample_windows", "gen_ingest", "gen_h2d", "extract_window_features", "scores"]
+    res = {n: round((b - a) * 1e3, 2) for n, a, b in zip(names, t, t[1:])}
+    res["windows"] = len(samples)
+    res["total_ms"] = round((t[-1] - t[0]) * 1e3, 2)
+    print(json.dumps(res), flush=True)

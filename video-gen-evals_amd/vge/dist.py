@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import json
 import time
+from concurrent.futures import ThreadPoolExecutor
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -100,11 +101,29 @@ def run_eval_distributed(generated_meshes_dir: str, real_meshes_dir: str, model_
     """vge.eval.run_eval sharded over the ranks of the initialised process group.  Returns the merged
     {video: {ac, tc}} dict on rank 0 (None elsewhere); rank 0 writes out_json."""
     from . import eval as VE
-    from . import ops
-    from .data import (ACTION_CLASSES, NpzVideoDataset, create_dataset_from_generated_meshes, load_clip,
-                       train_test_split)
+    from .data import NpzVideoDataset, create_dataset_from_generated_meshes
     rank, ws = world()
     t0 = time.perf_counter()
+    # The generated set's npz decode (host threads, GIL released) runs in the background while the real set's
+    # statistics, the checkpoint load and the centroids proceed; its errors surface where the reference's
+    # generated-set pass would raise them (after the centroids).
+    gen = create_dataset_from_generated_meshes(generated_meshes_dir)
+    gen_items = sorted(gen.items, key=lambda it: it.path)
+    mine = NpzVideoDataset("", items=shard(gen_items, rank, ws))
+    pool = ThreadPoolExecutor(max_workers=1)
+    gen_fs = pool.submit(VE.load_frame_store, mine.items, keypoint_dir, True) if mine.items else None
+    try:
+        return _run_eval_phases(generated_meshes_dir, real_meshes_dir, model_path, keypoint_dir, real_kp_dir,
+                                clip_len, stride, out_json, device, compute, timings, rank, ws, t0, mine, gen_fs)
+    finally:
+        pool.shutdown(wait=True)
+
+
+def _run_eval_phases(generated_meshes_dir, real_meshes_dir, model_path, keypoint_dir, real_kp_dir, clip_len, stride,
+                     out_json, device, compute, timings, rank, ws, t0, mine, gen_fs):
+    from . import eval as VE
+    from . import ops
+    from .data import ACTION_CLASSES, NpzVideoDataset, load_clip, train_test_split
     real_ds = NpzVideoDataset(real_meshes_dir, filter_classes=ACTION_CLASSES)
     train_ds, _ = train_test_split(real_ds, train_ratio=0.8, seed=1337)
     my_train = shard(train_ds.items, rank, ws)
@@ -130,12 +149,10 @@ def run_eval_distributed(generated_meshes_dir: str, real_meshes_dir: str, model_
                                                        device, train_items=my_train, label_dict=label_dict,
                                                        store=real_store, reduce_fn=centroid_reduce_fn)
     t2 = time.perf_counter()
-    gen = create_dataset_from_generated_meshes(generated_meshes_dir)
-    gen_items = sorted(gen.items, key=lambda it: it.path)
-    mine = NpzVideoDataset("", items=shard(gen_items, rank, ws))
     combined = {}
     if mine.items:
-        feats = VE.extract_window_features(model, mine, keypoint_dir, stats, clip_len, stride, device)
+        store = ops.DeviceFrameStore.from_host(gen_fs.result(), device)
+        feats = VE.extract_window_features(model, mine, keypoint_dir, stats, clip_len, stride, device, store=store)
         ac = VE.compute_action_consistency_scores(feats, centroids, label_dict)
         tc = VE.compute_temporal_coherence_scores(feats, centroids, label_dict)
         combined = VE.combine_scores(ac, tc)
