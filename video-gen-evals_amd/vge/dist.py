@@ -14,8 +14,9 @@ tensors and is what the world_size-2 CPU tests use.  Nothing here is specific to
 from __future__ import annotations
 
 import json
+import os
 import time
-from concurrent.futures import ThreadPoolExecutor
+from concurrent.futures import Future, ThreadPoolExecutor
 from typing import Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -110,8 +111,11 @@ def run_eval_distributed(generated_meshes_dir: str, real_meshes_dir: str, model_
     gen = create_dataset_from_generated_meshes(generated_meshes_dir)
     gen_items = sorted(gen.items, key=lambda it: it.path)
     mine = NpzVideoDataset("", items=shard(gen_items, rank, ws))
-    pool = ThreadPoolExecutor(max_workers=1)
-    gen_fs = pool.submit(VE.load_frame_store, mine.items, keypoint_dir, True) if mine.items else None
+    overlap = os.environ.get("VGE_FLOW_OVERLAP", "1") != "0"  # 0: every phase in order (A/B timing)
+    pool = ThreadPoolExecutor(max_workers=2)
+    gen_fs = pool.submit(VE.load_frame_store, mine.items, keypoint_dir, True) if mine.items and overlap else None
+    if overlap and isinstance(model_path, (str, os.PathLike)):  # the checkpoint read overlaps the real set's phases
+        model_path = pool.submit(VE._load_state_dict, model_path)
     try:
         return _run_eval_phases(generated_meshes_dir, real_meshes_dir, model_path, keypoint_dir, real_kp_dir,
                                 clip_len, stride, out_json, device, compute, timings, rank, ws, t0, mine, gen_fs)
@@ -139,6 +143,8 @@ def _run_eval_phases(generated_meshes_dir, real_meshes_dir, model_path, keypoint
         mean, std = ops.stats_finalize(s, c)
         stats = VE.ModalityStatsGPU(mean, std, s, c)
     dims_raw, dims_diff = VE.infer_dims_from_stats(stats)
+    if isinstance(model_path, Future):
+        model_path = model_path.result()  # (state_dict, hyper-parameters); a read error surfaces here, as before
     model = VE.load_model(model_path, dims_raw, dims_diff, device=device, compute=compute)
     t1 = time.perf_counter()
     if real_store is not None:
@@ -151,7 +157,8 @@ def _run_eval_phases(generated_meshes_dir, real_meshes_dir, model_path, keypoint
     t2 = time.perf_counter()
     combined = {}
     if mine.items:
-        store = ops.DeviceFrameStore.from_host(gen_fs.result(), device)
+        fs = gen_fs.result() if gen_fs is not None else VE.load_frame_store(mine.items, keypoint_dir, True)
+        store = ops.DeviceFrameStore.from_host(fs, device)
         feats = VE.extract_window_features(model, mine, keypoint_dir, stats, clip_len, stride, device, store=store)
         ac = VE.compute_action_consistency_scores(feats, centroids, label_dict)
         tc = VE.compute_temporal_coherence_scores(feats, centroids, label_dict)

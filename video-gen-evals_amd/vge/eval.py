@@ -98,6 +98,8 @@ def load_model(model_path, dims_map_raw=None, dims_map_diff=None, device="cuda",
             raise ValueError(f"unsupported modality dims {dims_map_raw} / {dims_map_diff}")
     if isinstance(model_path, dict):
         sd, hp = model_path, {"d_model": 256, "time_layers": 4, "time_heads": 8}
+    elif isinstance(model_path, tuple):  # (state_dict, hyper-parameters) as _load_state_dict returns them
+        sd, hp = model_path
     else:
         sd, hp = _load_state_dict(model_path)
     return ops.Encoder(sd, time_layers=int(hp["time_layers"]), time_heads=int(hp["time_heads"]),
