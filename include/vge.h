@@ -37,7 +37,12 @@ typedef enum {
                                  load_state_dict(strict=False) would silently random-init it) */
   VGE_ERR_WEIGHT_SHAPE = 4,   /* a state_dict tensor has the wrong shape */
   VGE_ERR_NOMEM = 5,
-  VGE_ERR_WORKSPACE = 6       /* vge_encoder_reserve() was not called for this many windows */
+  VGE_ERR_WORKSPACE = 6,      /* vge_encoder_reserve() was not called for this many windows */
+  VGE_ERR_UNSUPPORTED = 7     /* a model shape the kernels are not built for (vge_encoder_create): d_model != 256,
+                                 time_heads != 8, clip_len != 32, or a modality set / input dims other than the
+                                 reference's five (e.g. the keypoint-less layout utils.py:496-514 builds when
+                                 keypoint_dir is None).  load_model (eval.py:136-165) reads these from the
+                                 checkpoint; time_layers is free (any >= 1). */
 } vge_status;
 
 /* Encoder compute modes.  VGE_F32: exact f32 MFMA (v_mfma_f32_16x16x4_f32, bitwise an fmaf chain).
@@ -164,8 +169,10 @@ int vge_score_videos(const float* seq_embed, const float* tc_window, const int32
 
 /* ---------------------------------------------------------------------------------------------
  * Real-class centroids.  Replaces build_train_centroids_subset (utils.py:1018-1045):
- * sums.index_add_(0, y, z); counts.index_add_ -- accumulated in window order (bit-identical
- * sequential f32 sums); finalize = normalize(sums / counts.clamp_min(1)).
+ * sums.index_add_(0, y, z); counts.index_add_ -- a deterministic segmented reduction (segments of 256
+ * windows summed in window order, then the segment partials in segment order: the same bits for any
+ * device or launch, within a few ulps of a sequential index_add_); d <= 256; class ids outside [0, C)
+ * are ignored.  finalize = normalize(sums / counts.clamp_min(1)).
  * sums [C,d] / counts [C] (device float) are ACCUMULATED INTO and are the RCCL all-gather payload.
  */
 int vge_centroid_accumulate(const float* seq_embed, const int32_t* class_id, int n_windows, int C, int d,

@@ -46,9 +46,13 @@ typedef struct {
   int32_t status;    /* VGE_INGEST_OK or an error code above */
 } vge_clip_info;
 
-/* npz_paths[n]; kp_paths[n] (entries may be NULL; kp_paths itself may be NULL).  n_threads <= 0: all
- * hardware threads.  Fills info[n]; returns VGE_INGEST_OK if every video probed cleanly, else the
+/* npz_paths[n]; kp_paths[n] (entries may be NULL; kp_paths itself may be NULL).  n_threads <= 0:
+ * vge_ingest_default_threads().  Fills info[n]; returns VGE_INGEST_OK if every video probed cleanly, else the
  * first failing video's code (the others are still probed). */
+/* Thread count the calls use when n_threads <= 0: VGE_INGEST_THREADS, else OMP_NUM_THREADS if > 1, else
+ * the process's CPU share (cgroup quota / affinity mask) divided by LOCAL_WORLD_SIZE; at most 64. */
+int vge_ingest_default_threads(void);
+
 int vge_ingest_probe(const char* const* npz_paths, const char* const* kp_paths, int n, int n_threads,
                      vge_clip_info* info);
 

@@ -1,0 +1,74 @@
+"""The bench's own workload (bench.py, BASELINE config 2) pinned to the oracle, not to another HIP path.
+
+featurise -> encoder (the persistent quad + pair conv schedule, the fused transformer) -> AC / TC on exactly the
+clips bench.py times (vge.synth clips 0..n-1 of SEED_GEN, 32 frames, one window each), for both compute modes at
+256 windows (quads + a round of pairs on 256 CUs) and 600 windows (quads only), against oracle/featurize.py +
+oracle/encoder.py + the eval.py metrics (oracle pinned to the reference by tests/golden).
+Tolerances: AC / TC 1e-4 (north star), seq / frame embeddings 2e-5, feats 1e-4.
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _oracle(n):
+    """Oracle outputs on bench clips 0..n-1 with bench-like stats (from 16 real clips) -- cached per n."""
+    if n in _oracle.cache:
+        return _oracle.cache[n]
+    import bench
+    from oracle.encoder import OracleEncoder
+    from oracle.featurize import StatsAccumulator, featurize_window
+    from vge import synth
+    real = bench.make_clips(synth.SEED_REAL, 0, 16, 64)
+    acc = StatsAccumulator()
+    for c in real:
+        acc.add_video(c["pose"], c["global_orient"], c["betas"], c["vit"], c["keypoints"])
+    mean, std = acc.finalize().concat()
+    clips = bench.make_clips(synth.SEED_GEN, 0, n, 32)
+    feats = np.stack([(featurize_window(c["pose"], c["global_orient"], c["betas"], c["vit"], c["keypoints"], 0, None)
+                       - mean) / (std + np.float32(1e-6)) for c in clips]).astype(np.float32)
+    sd = synth.make_state_dict(synth.DIMS_RAW, synth.DIMS_DIFF)
+    torch.set_num_threads(max(1, min(16, len(__import__("os").sched_getaffinity(0)))))
+    seq, fe, _ = OracleEncoder(sd, synth.DIMS_RAW, synth.DIMS_DIFF).forward(torch.from_numpy(feats))
+    g = torch.Generator().manual_seed(7)
+    cent = torch.nn.functional.normalize(torch.randn(10, 256, generator=g), dim=-1)
+    vcls = torch.tensor([i % 10 for i in range(n)])
+    f = fe[:, 1:]
+    tc = (f[:, 1:] - f[:, :-1]).norm(dim=-1).mean(dim=1).double()
+    ac = (torch.nn.functional.normalize(seq, dim=-1) - cent[vcls]).norm(dim=-1)
+    out = dict(clips=clips, mean=mean, std=std, feats=feats, seq=seq, fe=fe, tc=tc, ac=ac, cent=cent, vcls=vcls, sd=sd)
+    _oracle.cache[n] = out
+    return out
+
+
+_oracle.cache = {}
+
+
+@pytest.mark.parametrize("n", [256, 600])
+@pytest.mark.parametrize("compute", ["f32x3", "f32"])
+def test_bench_workload_vs_oracle(n, compute):
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vge import ops
+    from vge.data import pack_frame_store
+    o = _oracle(n)
+    store = ops.DeviceFrameStore.from_host(pack_frame_store(o["clips"], [f"g{i}" for i in range(n)], ["X"] * n), DEV)
+    win = torch.tensor([[v, 0] for v in range(n)], dtype=torch.int32, device=DEV)
+    mean, std = torch.from_numpy(o["mean"]).to(DEV), torch.from_numpy(o["std"]).to(DEV)
+    feats = ops.featurize(store, win, mean, std)
+    assert np.abs(feats.cpu().numpy() - o["feats"]).max() < 1e-4
+    enc = ops.Encoder(o["sd"], device=DEV, compute=compute)
+    enc.reserve(n)
+    seq, fe, tcw = enc.encode(feats, frame_embed=True, tc=True)
+    first = torch.arange(n + 1, dtype=torch.int32, device=DEV)
+    ac, tc = ops.score_videos(seq, tcw, first, o["vcls"].to(torch.int32).to(DEV), o["cent"].to(DEV))
+    e_seq = (seq.cpu() - o["seq"]).abs().max().item()
+    e_fe = (fe.cpu() - o["fe"]).abs().max().item()
+    e_ac = (ac.cpu() - o["ac"]).abs().max().item()
+    e_tc = (tc.cpu() - o["tc"]).abs().max().item()
+    print(f"{compute} n={n}: seq {e_seq:.2e} frame {e_fe:.2e} ac {e_ac:.2e} tc {e_tc:.2e}")
+    assert e_seq < 2e-5 and e_fe < 2e-5, (e_seq, e_fe)
+    assert e_ac < 1e-4 and e_tc < 1e-4, (e_ac, e_tc)

@@ -130,3 +130,96 @@ def test_two_rank_gloo_flow_matches_single_process_golden(golden_dataset, golden
     assert sorted(out["scores"]) == sorted(ref)
     worst = max(abs(ref[v][k] - out["scores"][v][k]) for v in ref for k in ref[v])
     assert worst < 1e-4, worst
+
+
+def test_collective_device_policy(monkeypatch):
+    """An nccl (RCCL) process group serves cuda tensors only: host tensors handed to the flow's exchanges (the
+    int64 frame counts of the stats, the status flags of agree()) are staged on the rank's GPU; gloo keeps host
+    tensors; device tensors stay where they are."""
+    import torch.distributed as dist
+    from vge import dist as VD
+    monkeypatch.setattr(VD, "_rank_device", lambda: torch.device("cuda", 3))
+    monkeypatch.setattr(dist, "get_backend", lambda *a, **k: "nccl")
+    assert VD._collective_device(torch.zeros(2, dtype=torch.int64)) == torch.device("cuda", 3)
+    meta = torch.zeros(2, device="meta")
+    assert VD._collective_device(meta) == torch.device("cuda", 3)  # anything not cuda is staged
+    monkeypatch.setattr(dist, "get_backend", lambda *a, **k: "gloo")
+    assert VD._collective_device(torch.zeros(2)) == torch.device("cpu")
+
+
+def test_flow_exchanges_stage_host_tensors_for_nccl(monkeypatch):
+    """Every tensor stats_reduce_fn / centroid_reduce_fn / agree hand to all_gather under an nccl group is on the
+    rank's device (a stand-in device here: the test host has no GPU), including the host int64 counts."""
+    import torch.distributed as dist
+    from vge import dist as VD
+    seen = []
+
+    class Staged(torch.Tensor):
+        pass
+
+    def fake_to(t, dev):
+        assert dev == torch.device("cuda", 0), dev
+        return t.clone().as_subclass(Staged)
+
+    def fake_all_gather(parts, src):
+        seen.append(isinstance(src, Staged))
+        for p in parts:
+            p.copy_(src)
+
+    monkeypatch.setattr(VD, "in_group", lambda: True)
+    monkeypatch.setattr(VD, "world", lambda: (0, 2))
+    monkeypatch.setattr(dist, "get_backend", lambda *a, **k: "nccl")
+    monkeypatch.setattr(dist, "all_gather", fake_all_gather)
+    monkeypatch.setattr(VD, "_rank_device", lambda: torch.device("cuda", 0))
+    orig_to = torch.Tensor.to
+
+    def to(self, *a, **k):
+        if a and isinstance(a[0], torch.device) and a[0].type == "cuda":
+            return fake_to(self, a[0])
+        return orig_to(self, *a, **k)
+
+    monkeypatch.setattr(torch.Tensor, "to", to)
+    s, c = VD.stats_reduce_fn(torch.ones(2, 5, dtype=torch.float64), np.array([3, 4], np.int64))
+    assert s.dtype == torch.float64 and float(s.sum()) == 20.0 and c.tolist() == [6, 8]
+    cs, cc = VD.centroid_reduce_fn(torch.ones(3, 256), torch.ones(3))
+    assert float(cc.sum()) == 6.0
+    VD.agree(None, "test")
+    assert len(seen) == 5 and all(seen), seen
+
+
+def _agree_main(rank, ws, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from vge import dist as VD
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        def phase():
+            if rank == 1:
+                raise FileNotFoundError("Expected keypoints at /nowhere/keypoints.npy")
+            return rank
+        try:
+            VD.guarded("generated-set scoring", phase)
+            q.put((rank, "ok"))
+        except VD.PeerRankFailed as e:
+            q.put((rank, f"peer:{e}"))
+        except FileNotFoundError as e:
+            q.put((rank, f"own:{e}"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_error_on_one_rank_raises_on_every_rank():
+    """A bad file seen by one rank only (its shard) makes every rank raise before the next exchange, instead of
+    leaving the peers blocked in a collective until the backend timeout."""
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_agree_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    got = dict(q.get() for _ in range(2))
+    assert got[1].startswith("own:") and "Expected keypoints" in got[1]
+    assert got[0].startswith("peer:") and "[1]" in got[0]

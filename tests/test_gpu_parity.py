@@ -298,3 +298,38 @@ def test_x3_device_packing_matches_host_packing(vg, golden_state_dict, big, monk
     hh, wh = _encoder_images(host_enc)
     assert hd.numel() > 10_000_000 and torch.equal(hd, hh)
     assert torch.equal(wd, wh)
+
+
+@pytest.mark.parametrize("n,C", [(60_000, 10), (1_000, 70), (5, 3)])
+def test_centroid_segmented_reduction_vs_index_add(vg, n, C):
+    """build_train_centroids_subset (utils.py:1018-1045) at TAG-Bench-size real sets: the segmented device
+    reduction vs torch index_add_ on the host (counts exact, centroids within 2e-5); two launches give the same
+    bits; a second accumulate adds onto the first (the ABI accumulates into sums / counts)."""
+    VE, ops = vg
+    g = torch.Generator().manual_seed(n + C)
+    seq = torch.nn.functional.normalize(torch.randn(n, 256, generator=g), dim=-1)
+    y = torch.randint(0, C, (n,), generator=g)
+    ref_s = torch.zeros(C, 256).index_add_(0, y, seq)
+    ref_c = torch.zeros(C).index_add_(0, y, torch.ones(n))
+    ref = torch.nn.functional.normalize(ref_s / ref_c.clamp_min(1).unsqueeze(1), dim=-1)
+    ds, dy = seq.to(DEV), y.to(torch.int32).to(DEV)
+    outs = []
+    for _ in range(2):
+        s = torch.zeros(C, 256, device=DEV)
+        c = torch.zeros(C, device=DEV)
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        ev[0].record()
+        ops.centroid_accumulate(ds, dy, s, c)
+        ev[1].record()
+        torch.cuda.synchronize()
+        outs.append((s.cpu(), c.cpu(), ev[0].elapsed_time(ev[1])))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    s, c, ms = outs[1]
+    assert torch.equal(c, ref_c)
+    assert (s - ref_s).abs().max().item() < 1e-3
+    cent = ops.centroid_finalize(s.to(DEV), c.to(DEV)).cpu()
+    assert (cent - ref).abs().max().item() < 2e-5
+    print(f"centroid_accumulate n={n} C={C}: {ms * 1e3:.1f} us")
+    s2, c2 = s.to(DEV).clone(), c.to(DEV).clone()
+    ops.centroid_accumulate(ds, dy, s2, c2)
+    assert torch.equal(c2.cpu(), 2 * ref_c)

@@ -107,3 +107,68 @@ def test_sidecar_round_trip(tmp_path):
         f.write(b"XXXX")
     with pytest.raises(RuntimeError):
         ingest.load_sidecar(p, pinned=False)
+
+
+def _zip64_with_wrapping_cd(src: bytes) -> bytes:
+    """`src` (a valid npz) with a zip64 end record whose central-directory offset + size wrap around 2^64."""
+    import struct
+    e = src.rindex(b"PK\x05\x06")
+    z64_off = e
+    rec = struct.pack("<IQHHIIQQQQ", 0x06064B50, 44, 45, 45, 0, 0, 1, 1, 32, (1 << 64) - 16)
+    loc = struct.pack("<IIQI", 0x07064B50, 0, z64_off, 1)
+    eocd = bytearray(src[e:])
+    eocd[10:12] = b"\xff\xff"
+    eocd[12:16] = b"\xff\xff\xff\xff"
+    eocd[16:20] = b"\xff\xff\xff\xff"
+    return src[:e] + rec + loc + bytes(eocd)
+
+
+def _patch_shape(raw: bytes, old: bytes, new: bytes) -> bytes:
+    """Replace an npy header's shape text in place, keeping the header length (the padding absorbs it)."""
+    i = raw.index(old)
+    end = raw.index(b"\n", i)
+    line = raw[i:end].replace(old, new, 1).rstrip(b" ")
+    assert len(line) <= end - i
+    return raw[:i] + line + b" " * (end - i - len(line)) + raw[end:]
+
+
+def test_crafted_sizes_are_rejected_not_read(tmp_path):
+    """Bounds checks on untrusted npz / npy input cannot wrap (zip64 offsets, npy shapes whose element count
+    overflows): each file is refused with an error instead of being read out of bounds."""
+    kp_dir = str(tmp_path / "generated_kps")
+    z = _write(tmp_path, "z", 32, seed=20)
+    Path(z.path).write_bytes(_zip64_with_wrapping_cd(Path(z.path).read_bytes()))
+    with pytest.raises(RuntimeError):
+        ingest.load_frame_store_native([z], kp_dir, require_kp=False)
+    # keypoints.npy whose header claims 2^62 rows of 120 (count * itemsize overflows uint64)
+    k = _write(tmp_path, "kk", 32, seed=21)
+    kp_file = tmp_path / "generated_kps" / "kk" / "keypoints.npy"
+    kp_file.write_bytes(_patch_shape(kp_file.read_bytes(), b"(32, 120)", f"({1 << 62}, 120)".encode()))
+    with pytest.raises(RuntimeError):
+        ingest.load_frame_store_native([k], kp_dir, require_kp=True)
+    # an npz (stored members) whose pose member claims 2^40 frames
+    p = tmp_path / "gen" / "big.npz"
+    np.savez(p, pose=np.zeros((2, 23, 3, 3), np.float32), global_orient=np.zeros((2, 1, 3, 3), np.float32),
+             betas=np.zeros((2, 10), np.float32), vit=np.zeros((2, 64), np.float32))
+    p.write_bytes(_patch_shape(p.read_bytes(), b"(2, 23, 3, 3)", f"({1 << 40}, 23, 3, 3)".encode()))
+    big = VideoItem("Unknown", "big.npz", str(p), 2, 64)
+    with pytest.raises(RuntimeError):
+        ingest.load_frame_store_native([big], None, require_kp=False)
+
+
+def test_default_thread_count_ignores_torchrun_single_thread(monkeypatch):
+    """torchrun exports OMP_NUM_THREADS=1 for nproc_per_node > 1; the decoder must still use the rank's CPU share."""
+    from vge import lib as L
+    lib = L.load()
+    lib.vge_ingest_default_threads.restype = __import__("ctypes").c_int
+    monkeypatch.setenv("VGE_INGEST_THREADS", "5")
+    assert lib.vge_ingest_default_threads() == 5
+    monkeypatch.delenv("VGE_INGEST_THREADS")
+    monkeypatch.setenv("OMP_NUM_THREADS", "3")
+    assert lib.vge_ingest_default_threads() == 3
+    monkeypatch.setenv("OMP_NUM_THREADS", "1")
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
+    share = lib.vge_ingest_default_threads()
+    assert share == min(64, len(os.sched_getaffinity(0))) or share >= 1
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "2")
+    assert lib.vge_ingest_default_threads() == max(1, share // 2)

@@ -73,3 +73,37 @@ def test_erf_branch_free_accuracy():
     erf = np.copysign(np.where(a < 1, small, big), z)
     ref = np.array([math.erf(float(v)) for v in z])
     assert np.abs(erf - ref).max() < 1.5e-7
+
+
+@pytest.mark.parametrize("field,value", [("d_model", 128), ("time_heads", 4), ("n_modalities", 4), ("clip_len", 64)])
+def test_unsupported_model_shape_has_its_own_status(field, value):
+    """load_model (eval.py:136-165) builds HumanActionScorer with d_model / time_layers / time_heads from the
+    checkpoint, and the keypoint-less layout drops kp2d (utils.py:496-514).  Shapes the kernels are not built for
+    are refused before any device work with VGE_ERR_UNSUPPORTED (UnsupportedModelError in Python), distinct from
+    argument errors; time_layers is free."""
+    import ctypes as C
+    from vge import lib as L
+    from vge import ops
+    so = L.load()
+    dims = L.Dims()
+    dims.n_modalities, dims.d_model, dims.time_layers, dims.time_heads, dims.clip_len = 5, 256, 4, 8, 32
+    for i in range(5):
+        dims.dims_raw[i], dims.dims_diff[i] = ops.DIMS_RAW[i], ops.DIMS_DIFF[i]
+    setattr(dims, field, value)
+    h = C.c_void_p()
+    st = so.vge_encoder_create(C.byref(dims), (L.TensorView * 1)(), 0, 1, C.byref(h))
+    assert st == L.VGE_ERR_UNSUPPORTED, st
+    with pytest.raises(L.UnsupportedModelError, match="VGE_ERR_UNSUPPORTED"):
+        L.check(st, "vge_encoder_create")
+    dims.time_layers = 0
+    setattr(dims, field, {"d_model": 256, "time_heads": 8, "n_modalities": 5, "clip_len": 32}[field])
+    assert so.vge_encoder_create(C.byref(dims), (L.TensorView * 1)(), 0, 1, C.byref(h)) == 1  # VGE_ERR_ARG
+
+
+def test_load_model_refuses_keypointless_dims():
+    from vge import eval as VE
+    from vge.lib import UnsupportedModelError
+    raw = {"vit": 1024, "global": 9, "pose": 207, "beta": 10}
+    diff = {"vit": 1024, "global": 3, "pose": 69, "beta": 10}
+    with pytest.raises(UnsupportedModelError):
+        VE.load_model({}, raw, diff, device="cpu")

@@ -328,12 +328,15 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
   *out = nullptr;
   if (compute != VGE_F32 && compute != VGE_F32X3) return fail(VGE_ERR_ARG, "vge_encoder_create: unsupported compute dtype");
   const bool x3 = compute == VGE_F32X3;
-  if (dims->n_modalities != 5 || dims->d_model != 256 || dims->time_heads != 8 || dims->clip_len != 32 ||
-      dims->time_layers < 1)
-    return fail(VGE_ERR_ARG, "vge_encoder_create: kernels are built for 5 modalities, d_model 256, 8 heads, clip 32");
+  if (dims->time_layers < 1) return fail(VGE_ERR_ARG, "vge_encoder_create: time_layers must be >= 1");
+  if (dims->n_modalities != 5 || dims->d_model != 256 || dims->time_heads != 8 || dims->clip_len != 32)
+    return fail(VGE_ERR_UNSUPPORTED,
+                "vge_encoder_create: kernels are built for 5 modalities, d_model 256, 8 heads, clip 32 (got " +
+                    std::to_string(dims->n_modalities) + " modalities, d_model " + std::to_string(dims->d_model) +
+                    ", " + std::to_string(dims->time_heads) + " heads, clip " + std::to_string(dims->clip_len) + ")");
   for (int m = 0; m < 5; ++m)
     if (dims->dims_raw[m] != kDimsRaw[m] || dims->dims_diff[m] != kDimsDiff[m])
-      return fail(VGE_ERR_ARG, std::string("vge_encoder_create: unsupported dims for modality ") + kMods[m]);
+      return fail(VGE_ERR_UNSUPPORTED, std::string("vge_encoder_create: unsupported dims for modality ") + kMods[m]);
 
   std::unordered_map<std::string, const vge_tensor_view*> wm;
   for (int i = 0; i < n_weights; ++i)
@@ -841,7 +844,8 @@ int vge_score_videos(const float* seq, const float* tcw, const int32_t* first, c
 
 int vge_centroid_accumulate(const float* seq, const int32_t* cls, int n, int C, int d, float* sums, float* counts,
                             vge_stream_t stream) {
-  if (!seq || !cls || !sums || !counts || n < 0 || C < 1 || d < 1) return fail(VGE_ERR_ARG, "vge_centroid_accumulate: bad argument");
+  if (!seq || !cls || !sums || !counts || n < 0 || C < 1 || d < 1 || d > 256)
+    return fail(VGE_ERR_ARG, "vge_centroid_accumulate: bad argument");
   if (n == 0) return VGE_OK;
   HIPCHK(vge::launch_centroid_accum(seq, cls, n, C, d, sums, counts, S(stream)));
   return VGE_OK;

@@ -74,21 +74,22 @@ bool zip_members(const Mapped& f, std::vector<Member>& out) {
   if (entries == 0xFFFF || cd_size == 0xFFFFFFFFu || cd_off == 0xFFFFFFFFu) {  // zip64 locator before it
     if (eocd < 20 || rd32(f.p + eocd - 20) != 0x07064b50u) return false;
     const uint64_t z64 = rd64(f.p + eocd - 20 + 8);
-    if (z64 + 56 > f.n || rd32(f.p + z64) != 0x06064b50u) return false;
+    if (z64 > f.n || f.n - z64 < 56 || rd32(f.p + z64) != 0x06064b50u) return false;
     entries = rd64(f.p + z64 + 32);
     cd_size = rd64(f.p + z64 + 40);
     cd_off = rd64(f.p + z64 + 48);
   }
-  if (cd_off + cd_size > f.n) return false;
+  // bounds checks in subtraction form: zip64 fields are 64-bit and a crafted file must not wrap them
+  if (cd_off > f.n || cd_size > f.n - cd_off) return false;
   size_t q = (size_t)cd_off;
   for (uint64_t e = 0; e < entries; ++e) {
-    if (q + 46 > f.n || rd32(f.p + q) != 0x02014b50u) return false;
+    if (q > f.n || f.n - q < 46 || rd32(f.p + q) != 0x02014b50u) return false;
     Member m;
     m.method = rd16(f.p + q + 10);
     uint64_t cs = rd32(f.p + q + 20), us = rd32(f.p + q + 24);
     const uint16_t nl = rd16(f.p + q + 28), xl = rd16(f.p + q + 30), cl = rd16(f.p + q + 32);
     uint64_t loff = rd32(f.p + q + 42);
-    if (q + 46 + nl + xl + cl > f.n) return false;
+    if (f.n - q - 46 < (size_t)nl + xl + cl) return false;
     m.name.assign(reinterpret_cast<const char*>(f.p + q + 46), nl);
     // zip64 extra field (id 1): the 0xFFFFFFFF fields in the order usize, csize, local header offset
     const uint8_t* x = f.p + q + 46 + nl;
@@ -103,9 +104,11 @@ bool zip_members(const Mapped& f, std::vector<Member>& out) {
       }
       k += 4 + sz;
     }
-    if (loff + 30 > f.n || rd32(f.p + loff) != 0x04034b50u) return false;
-    const size_t data = (size_t)loff + 30 + rd16(f.p + loff + 26) + rd16(f.p + loff + 28);
-    if (data + cs > f.n) return false;
+    if (loff > f.n || f.n - loff < 30 || rd32(f.p + loff) != 0x04034b50u) return false;
+    const uint64_t hdr_len = 30 + (uint64_t)rd16(f.p + loff + 26) + rd16(f.p + loff + 28);
+    if (f.n - loff < hdr_len) return false;
+    const size_t data = (size_t)(loff + hdr_len);
+    if (cs > f.n - data) return false;
     m.csize = cs;
     m.usize = us;
     m.data = f.p + data;
@@ -120,9 +123,13 @@ struct NpyHeader {
   size_t header_bytes = 0;  // magic + lengths + dict
   int itemsize = 0;         // 4 (<f4) or 8 (<f8)
   std::vector<int64_t> shape;
+  // element count; -1 when a dimension is negative or the product overflows int64 (a malformed header)
   int64_t count() const {
     int64_t c = 1;
-    for (int64_t s : shape) c *= s;
+    for (int64_t s : shape) {
+      if (s < 0 || (s > 0 && c > INT64_MAX / s)) return -1;
+      c *= s;
+    }
     return c;
   }
 };
@@ -282,8 +289,8 @@ int kp_probe(const char* path, int32_t* rows, NpyHeader* hdr, Mapped** keep) {
   }
   NpyHeader h;
   size_t need = 0;
-  if (!parse_npy(f->p, f->n, h, need) || h.shape.empty() || h.count() % 120 != 0 ||
-      h.header_bytes + (size_t)h.count() * h.itemsize > f->n) {
+  if (!parse_npy(f->p, f->n, h, need) || h.shape.empty() || h.count() < 0 || h.count() % 120 != 0 ||
+      h.header_bytes > f->n || (uint64_t)h.count() > (f->n - h.header_bytes) / (uint64_t)h.itemsize) {
     delete f;
     return VGE_INGEST_ERR_KP;
   }
@@ -309,6 +316,7 @@ int probe_one(const char* npz, const char* kpp, vge_clip_info* info) {
   int64_t T = 0;
   if (!rp.header(hp) || !rv.header(hv)) return VGE_INGEST_ERR_IO;
   if (!shape_is(hp, {23, 3, 3}, &T) || hv.shape.size() != 2 || hv.shape[0] != T) return VGE_INGEST_ERR_SHAPE;
+  if (T < 0 || T > INT32_MAX || hv.shape[1] <= 0 || hv.shape[1] > (1 << 20)) return VGE_INGEST_ERR_SHAPE;  // crafted sizes
   info->n_frames = (int32_t)T;
   info->vit_dim = (int32_t)hv.shape[1];
   int32_t rows = -1;
@@ -369,20 +377,44 @@ int decode_one(const char* npz, const char* kpp, const int32_t* vid, int vit_dim
   return VGE_INGEST_OK;
 }
 
-// Default pool size: VGE_INGEST_THREADS, else OMP_NUM_THREADS (the CPU share a job is given, e.g. 16 on a
-// one-GPU box whose hardware_concurrency counts the whole machine), else the CPUs this process may run on;
-// at most 64.  One thread per file on a many-core host oversubscribes a CPU quota and was measured 2-3x slower.
-int default_threads() {
-  for (const char* var : {"VGE_INGEST_THREADS", "OMP_NUM_THREADS"}) {
-    const char* e = getenv(var);
-    if (e && atoi(e) > 0) return std::min(atoi(e), 64);
-  }
+// CPU share of this process: the cgroup v2 quota (cpu.max "quota period") when one is set, else the
+// affinity mask, else hardware_concurrency (which can count a whole many-socket machine).
+int cpu_share() {
   cpu_set_t set;
   int n = 0;
   if (sched_getaffinity(0, sizeof(set), &set) == 0) n = CPU_COUNT(&set);
   if (n <= 0) n = (int)std::thread::hardware_concurrency();
+  if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char quota[32] = {0};
+    long long period = 0;
+    if (fscanf(f, "%31s %lld", quota, &period) == 2 && strcmp(quota, "max") != 0 && period > 0) {
+      long long q = atoll(quota);
+      if (q > 0) n = std::min<long long>(n, std::max<long long>(1, (q + period - 1) / period));
+    }
+    fclose(f);
+  }
+  return std::max(1, n);
+}
+
+// Decode threads per call: VGE_INGEST_THREADS, else OMP_NUM_THREADS when it asks for more than one thread
+// (torchrun exports OMP_NUM_THREADS=1 for nproc_per_node > 1, which must not serialise the decoder), else
+// this process's CPU share divided among the ranks of this node (LOCAL_WORLD_SIZE).  At most 64.
+int default_threads() {
+  if (const char* e = getenv("VGE_INGEST_THREADS"))
+    if (atoi(e) > 0) return std::min(atoi(e), 64);
+  if (const char* e = getenv("OMP_NUM_THREADS"))
+    if (atoi(e) > 1) return std::min(atoi(e), 64);
+  int n = cpu_share();
+  if (const char* e = getenv("LOCAL_WORLD_SIZE"))
+    if (atoi(e) > 1) n = std::max(1, n / atoi(e));
   return std::max(1, std::min(n, 64));
 }
+
+}  // namespace
+
+extern "C" int vge_ingest_default_threads(void) { return default_threads(); }
+
+namespace {
 
 template <class Fn>
 void parallel_for(int n, int n_threads, Fn fn) {

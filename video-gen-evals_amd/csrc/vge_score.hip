@@ -1,8 +1,15 @@
 // AC / TC reductions and real-class centroid accumulation (gfx950).
 //
-//   centroid_accum_kernel  build_train_centroids_subset (utils.py:1018-1043): sums.index_add_(0, y, z),
-//                          counts.index_add_ -- one thread per (class, dim) walks the windows in order, so the
-//                          f32 sums are bit-identical to index_add_'s sequential accumulation.
+//   centroid_partial_kernel + centroid_combine_kernel
+//                          build_train_centroids_subset (utils.py:1018-1043): sums.index_add_(0, y, z),
+//                          counts.index_add_, as a deterministic segmented reduction: the windows are cut into
+//                          segments of CENT_SEG (a function of n only); one workgroup per (segment, block of 64
+//                          classes) walks its windows in order with thread j owning column j of every class
+//                          row in LDS (no atomics, no races), then one thread per (class, column) adds the
+//                          segment partials in segment order.  Same result for any grid / device; the order
+//                          of the f32 additions differs from a sequential index_add_ only by the segment
+//                          split (a few ulps of the sums, far inside the 2e-5 centroid tolerance).
+//                          HBM-bound: reads n x d x 4 B + 4n B once.
 //   centroid_final_kernel  normalize(sums / counts.clamp_min(1)), eps 1e-12.
 //   tc_windows_kernel      eval.py:216-224 per-window term (mean consecutive L2 over frames 1..T).
 //   score_videos_kernel    eval.py:226 (np.mean over a video's windows, float64) and eval.py:238-255
@@ -13,21 +20,57 @@
 
 namespace {
 
-__global__ void centroid_accum_kernel(const float* __restrict__ seq, const int* __restrict__ cls, int n, int C, int d,
-                                      float* __restrict__ sums, float* __restrict__ counts) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx >= C * d) return;
-  const int c = idx / d, j = idx % d;
-  float s = sums[idx];
-  float cnt = (j == 0) ? counts[c] : 0.f;
-  for (int w = 0; w < n; ++w) {
-    if (cls[w] == c) {
-      s += seq[(size_t)w * d + j];
-      if (j == 0) cnt += 1.0f;
+constexpr int CENT_SEG = 256;     // windows per segment
+constexpr int CENT_CB = 64;       // classes per workgroup (LDS 64 x 256 x 4 B = 64 KB)
+
+// grid (n_seg, ceil(C / 64)), 256 threads; d <= 256.  part [n_seg][C][d], pcnt [n_seg][C]
+__global__ void __launch_bounds__(256) centroid_partial_kernel(const float* __restrict__ seq,
+                                                               const int* __restrict__ cls, int n, int C, int d,
+                                                               float* __restrict__ part, float* __restrict__ pcnt) {
+  __shared__ float acc[CENT_CB][256];
+  __shared__ float cnt[CENT_CB];
+  const int j = threadIdx.x, seg = blockIdx.x, c0 = blockIdx.y * CENT_CB;
+  const int nc = min(CENT_CB, C - c0);
+  for (int c = 0; c < nc; ++c) acc[c][j] = 0.f;
+  if (j < nc) cnt[j] = 0.f;
+  __syncthreads();
+  const int w0 = seg * CENT_SEG, w1 = min(n, w0 + CENT_SEG);
+  // rows in batches of 8: the loads of a batch are issued together, the adds follow in window order
+  for (int w = w0; w < w1; w += 8) {
+    float x[8];
+    int y[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      y[k] = (w + k < w1) ? cls[w + k] - c0 : -1;
+      x[k] = (w + k < w1 && j < d) ? seq[(size_t)(w + k) * d + j] : 0.f;
     }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if ((unsigned)y[k] < (unsigned)nc) {  // uniform over the block
+        acc[y[k]][j] += x[k];
+        if (j == 0) cnt[y[k]] += 1.0f;
+      }
   }
-  sums[idx] = s;
-  if (j == 0) counts[c] = cnt;
+  __syncthreads();
+  if (j < d)
+    for (int c = 0; c < nc; ++c) part[((size_t)seg * C + c0 + c) * d + j] = acc[c][j];
+  if (j < nc) pcnt[(size_t)seg * C + c0 + j] = cnt[j];
+}
+
+// one thread per (class, column) [+ C threads for the counts]: sums += partials in segment order
+__global__ void centroid_combine_kernel(const float* __restrict__ part, const float* __restrict__ pcnt, int n_seg,
+                                        int C, int d, float* __restrict__ sums, float* __restrict__ counts) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx < C * d) {
+    float s = 0.f;
+    for (int g = 0; g < n_seg; ++g) s += part[(size_t)g * C * d + idx];
+    sums[idx] += s;
+  } else if (idx < C * d + C) {
+    const int c = idx - C * d;
+    float s = 0.f;
+    for (int g = 0; g < n_seg; ++g) s += pcnt[(size_t)g * C + c];
+    counts[c] += s;
+  }
 }
 
 __global__ void centroid_final_kernel(const float* __restrict__ sums, const float* __restrict__ counts, int C, int d,
@@ -117,11 +160,24 @@ __global__ void score_videos_kernel(const float* __restrict__ seq, const float* 
 
 namespace vge {
 
+// d <= 256.  The segment partials live in a stream-ordered scratch allocation (n_seg x (C d + C) floats).
 hipError_t launch_centroid_accum(const float* seq, const int* cls, int n, int C, int d, float* sums, float* counts,
                                  hipStream_t s) {
-  const int total = C * d;
-  hipLaunchKernelGGL(centroid_accum_kernel, dim3((total + 255) / 256), dim3(256), 0, s, seq, cls, n, C, d, sums, counts);
-  return hipGetLastError();
+  if (n <= 0) return hipSuccess;
+  const int n_seg = (n + CENT_SEG - 1) / CENT_SEG;
+  float* part = nullptr;
+  const size_t nf = (size_t)n_seg * ((size_t)C * d + C);
+  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&part), nf * sizeof(float), s);
+  if (e != hipSuccess) return e;
+  float* pcnt = part + (size_t)n_seg * C * d;
+  hipLaunchKernelGGL(centroid_partial_kernel, dim3(n_seg, (C + CENT_CB - 1) / CENT_CB), dim3(256), 0, s, seq, cls, n,
+                     C, d, part, pcnt);
+  const int total = C * d + C;
+  hipLaunchKernelGGL(centroid_combine_kernel, dim3((total + 255) / 256), dim3(256), 0, s, part, pcnt, n_seg, C, d,
+                     sums, counts);
+  e = hipGetLastError();
+  const hipError_t f = hipFreeAsync(part, s);
+  return e != hipSuccess ? e : f;
 }
 
 hipError_t launch_centroid_final(const float* sums, const float* counts, int C, int d, float* cent, hipStream_t s) {

@@ -24,10 +24,18 @@ import torch
 import torch.distributed as dist
 
 
+def in_group() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
 def world() -> Tuple[int, int]:
-    if dist.is_available() and dist.is_initialized():
+    if in_group():
         return dist.get_rank(), dist.get_world_size()
     return 0, 1
+
+
+def _rank_device() -> torch.device:
+    return torch.device("cuda", torch.cuda.current_device())
 
 
 def shard_bounds(n: int, rank: int, world_size: int) -> Tuple[int, int]:
@@ -43,16 +51,22 @@ def shard(items: Sequence, rank: int, world_size: int) -> List:
 
 
 def _collective_device(t: torch.Tensor) -> torch.device:
-    # gloo collectives run on host tensors; nccl (RCCL) on device tensors
-    return torch.device("cpu") if dist.get_backend() == "gloo" else t.device
+    """gloo collectives run on host tensors; an nccl (RCCL) process group serves cuda tensors only, so a host
+    tensor (e.g. the int64 frame counts of the stats exchange) is staged on this rank's current GPU."""
+    if dist.get_backend() == "gloo":
+        return torch.device("cpu")
+    if t.device.type == "cuda":
+        return t.device
+    return _rank_device()
 
 
 def allgather_sum(t: torch.Tensor) -> torch.Tensor:
     """All-gather `t` from every rank and sum the parts in rank order (deterministic, identical on all
-    ranks).  Returns a tensor on t's device and dtype."""
-    rank, ws = world()
-    if ws == 1:
+    ranks).  Returns a tensor on t's device and dtype.  Inside a process group the collective runs even for
+    one rank, so a one-GPU run exercises the same RCCL calls as eight."""
+    if not in_group():
         return t
+    rank, ws = world()
     src = t.detach().to(_collective_device(t)).contiguous()
     parts = [torch.empty_like(src) for _ in range(ws)]
     dist.all_gather(parts, src)
@@ -74,11 +88,47 @@ def centroid_reduce_fn(sums: torch.Tensor, counts: torch.Tensor):
     return allgather_sum(sums), allgather_sum(counts)
 
 
+class PeerRankFailed(RuntimeError):
+    """Raised on every rank whose own phase succeeded when another rank's failed (so no rank is left waiting
+    in a collective the failed rank will never reach)."""
+
+
+def agree(err: Optional[BaseException], phase: str) -> None:
+    """One all-gather of a status flag per rank before each exchange of the flow.  The reference is a single
+    process that raises at the first bad file (utils.py:416-417, eval.py:93-95); sharded, only the rank that
+    owns that file sees it, so every rank learns of it here and raises together: the failing rank re-raises
+    its own exception, the others PeerRankFailed naming the failed ranks."""
+    rank, ws = world()
+    if in_group():
+        flag = torch.tensor([0 if err is None else 1], dtype=torch.int32)
+        flag = flag.to(_collective_device(flag))
+        parts = [torch.empty_like(flag) for _ in range(ws)]
+        dist.all_gather(parts, flag)
+        failed = [r for r, p in enumerate(parts) if int(p.item()) != 0]
+    else:
+        failed = [] if err is None else [0]
+    if err is not None:
+        raise err
+    if failed:
+        raise PeerRankFailed(f"{phase}: rank(s) {failed} failed; rank {rank} stops with them")
+
+
+def guarded(phase: str, fn, *args, **kw):
+    """Run one rank-local phase of the flow, then agree() with the other ranks before the next exchange."""
+    err, out = None, None
+    try:
+        out = fn(*args, **kw)
+    except Exception as e:  # re-raised by agree() on this rank, after the peers were told
+        err = e
+    agree(err, phase)
+    return out
+
+
 def gather_to_rank0(obj):
     """Gather a picklable per-rank result (here: the per-video score dicts) to rank 0 (list in rank
     order); other ranks get None."""
     rank, ws = world()
-    if ws == 1:
+    if not in_group():
         return [obj]
     out = [None] * ws if rank == 0 else None
     dist.gather_object(obj, out, dst=0)
@@ -98,9 +148,13 @@ def merge_scores(parts: List[Dict[str, dict]]) -> Dict[str, dict]:
 def run_eval_distributed(generated_meshes_dir: str, real_meshes_dir: str, model_path, keypoint_dir: str,
                          real_kp_dir: str, clip_len: int = 32, stride: int = 8,
                          out_json: Optional[str] = "video_scores.json", device="cuda", compute: str = "f32x3",
-                         timings: Optional[dict] = None):
+                         timings: Optional[dict] = None, human_scores_path: Optional[str] = None,
+                         save_features: Optional[str] = None):
     """vge.eval.run_eval sharded over the ranks of the initialised process group.  Returns the merged
-    {video: {ac, tc}} dict on rank 0 (None elsewhere); rank 0 writes out_json."""
+    {video: {ac, tc}} dict on rank 0 (None elsewhere); rank 0 writes out_json, the Spearman correlations
+    against `human_scores_path` (eval.py:456-464) and, with `save_features`, window_features.pt
+    (eval.py:424, windows of all ranks in the single-process order: the shards are contiguous blocks of the
+    sorted generated list)."""
     from . import eval as VE
     from .data import NpzVideoDataset, create_dataset_from_generated_meshes
     rank, ws = world()
@@ -117,14 +171,17 @@ def run_eval_distributed(generated_meshes_dir: str, real_meshes_dir: str, model_
     if overlap and isinstance(model_path, (str, os.PathLike)):  # the checkpoint read overlaps the real set's phases
         model_path = pool.submit(VE._load_state_dict, model_path)
     try:
-        return _run_eval_phases(generated_meshes_dir, real_meshes_dir, model_path, keypoint_dir, real_kp_dir,
-                                clip_len, stride, out_json, device, compute, timings, rank, ws, t0, mine, gen_fs)
+        return _run_eval_phases(real_meshes_dir, model_path, keypoint_dir, real_kp_dir, clip_len, stride, out_json,
+                                device, compute, timings, rank, ws, t0, mine, gen_fs, human_scores_path,
+                                save_features)
     finally:
         pool.shutdown(wait=True)
 
 
-def _run_eval_phases(generated_meshes_dir, real_meshes_dir, model_path, keypoint_dir, real_kp_dir, clip_len, stride,
-                     out_json, device, compute, timings, rank, ws, t0, mine, gen_fs):
+def _run_eval_phases(real_meshes_dir, model_path, keypoint_dir, real_kp_dir, clip_len, stride, out_json, device,
+                     compute, timings, rank, ws, t0, mine, gen_fs, human_scores_path, save_features):
+    """Three rank-local phases, each closed by agree() before its exchange, so an error on one rank (a missing
+    keypoints.npy, an unreadable checkpoint) makes every rank raise instead of leaving peers in a collective."""
     from . import eval as VE
     from . import ops
     from .data import ACTION_CLASSES, NpzVideoDataset, load_clip, train_test_split
@@ -132,41 +189,69 @@ def _run_eval_phases(generated_meshes_dir, real_meshes_dir, model_path, keypoint
     train_ds, _ = train_test_split(real_ds, train_ratio=0.8, seed=1337)
     my_train = shard(train_ds.items, rank, ws)
     label_dict = {cls: i for i, cls in enumerate(sorted({it.cls for it in real_ds.items}))}
-    real_store = None
-    if my_train:
-        real_store = ops.DeviceFrameStore.from_host(VE.load_frame_store(my_train, real_kp_dir, False), device)
-        stats = VE.compute_stats_from_npz(my_train, real_kp_dir, device=device, store=real_store,
-                                          reduce_fn=stats_reduce_fn)
-    else:  # an empty shard still takes part in the collectives
+
+    # phase 1: this rank's real-train shard -> float64 stats sufficient statistics
+    def local_stats():
         sums = torch.zeros((2, ops.FEAT_DIM), device=device, dtype=torch.float64)
-        s, c = stats_reduce_fn(sums, np.zeros(2, np.int64))
-        mean, std = ops.stats_finalize(s, c)
-        stats = VE.ModalityStatsGPU(mean, std, s, c)
+        counts = np.zeros(2, np.int64)
+        store = None
+        if my_train:  # an empty shard still takes part in the exchange with zeros
+            store = ops.DeviceFrameStore.from_host(VE.load_frame_store(my_train, real_kp_dir, False), device)
+            ops.stats_accumulate(store, range(store.n_videos), sums, counts)
+        return store, sums, counts
+
+    real_store, sums, counts = guarded("real-set statistics", local_stats)
+    s, c = stats_reduce_fn(sums, counts)
+    mean, std = ops.stats_finalize(s, c)
+    stats = VE.ModalityStatsGPU(mean, std, s, c)
     dims_raw, dims_diff = VE.infer_dims_from_stats(stats)
-    if isinstance(model_path, Future):
-        model_path = model_path.result()  # (state_dict, hyper-parameters); a read error surfaces here, as before
-    model = VE.load_model(model_path, dims_raw, dims_diff, device=device, compute=compute)
+
+    # phase 2: checkpoint -> encoder; this rank's real-train windows -> centroid sufficient statistics
+    captured = {}
+
+    def capture(sums_, counts_):  # the exchange happens after agree(), below
+        captured["s"], captured["c"] = sums_, counts_
+        return sums_, counts_
+
+    def local_centroids():
+        mp = model_path.result() if isinstance(model_path, Future) else model_path
+        model = VE.load_model(mp, dims_raw, dims_diff, device=device, compute=compute)
+        if real_store is not None:
+            for i, it in enumerate(my_train):
+                if real_store.host_videos[i, 3] == 0:
+                    load_clip(it, real_kp_dir, require_kp=True)  # raises like utils.py:416-417
+        VE.build_real_centroids(model, real_meshes_dir, real_kp_dir, stats, clip_len, stride, device,
+                                train_items=my_train, label_dict=label_dict, store=real_store, reduce_fn=capture)
+        return model
+
     t1 = time.perf_counter()
-    if real_store is not None:
-        for i, it in enumerate(my_train):
-            if real_store.host_videos[i, 3] == 0:
-                load_clip(it, real_kp_dir, require_kp=True)  # raises like utils.py:416-417
-    centroids, label_dict, _ = VE.build_real_centroids(model, real_meshes_dir, real_kp_dir, stats, clip_len, stride,
-                                                       device, train_items=my_train, label_dict=label_dict,
-                                                       store=real_store, reduce_fn=centroid_reduce_fn)
+    model = guarded("checkpoint / real-set centroids", local_centroids)
+    csum, ccnt = centroid_reduce_fn(captured["s"], captured["c"])
+    centroids = ops.centroid_finalize(csum, ccnt)
     t2 = time.perf_counter()
-    combined = {}
-    if mine.items:
-        fs = gen_fs.result() if gen_fs is not None else VE.load_frame_store(mine.items, keypoint_dir, True)
-        store = ops.DeviceFrameStore.from_host(fs, device)
-        feats = VE.extract_window_features(model, mine, keypoint_dir, stats, clip_len, stride, device, store=store)
-        ac = VE.compute_action_consistency_scores(feats, centroids, label_dict)
-        tc = VE.compute_temporal_coherence_scores(feats, centroids, label_dict)
-        combined = VE.combine_scores(ac, tc)
-    if torch.cuda.is_available() and str(device).startswith("cuda"):
-        torch.cuda.synchronize(device)
+
+    # phase 3: this rank's generated videos -> (ac, tc); no collective until the gather to rank 0
+    def local_scores():
+        combined, feats_host = {}, None
+        if mine.items:
+            fs = gen_fs.result() if gen_fs is not None else VE.load_frame_store(mine.items, keypoint_dir, True)
+            store = ops.DeviceFrameStore.from_host(fs, device)
+            feats = VE.extract_window_features(model, mine, keypoint_dir, stats, clip_len, stride, device,
+                                               store=store, frame_embed=bool(save_features))
+            ac = VE.compute_action_consistency_scores(feats, centroids, label_dict)
+            tc = VE.compute_temporal_coherence_scores(feats, centroids, label_dict)
+            combined = VE.combine_scores(ac, tc)
+            if save_features:
+                feats_host = {"seq_embeds": feats["seq_embeds"].cpu(), "frame_embeds": feats["frame_embeds"].cpu(),
+                              "cls_names": list(feats["cls_names"]), "vid_names": list(feats["vid_names"])}
+        if torch.cuda.is_available() and str(device).startswith("cuda"):
+            torch.cuda.synchronize(device)
+        return combined, feats_host
+
+    combined, feats_host = guarded("generated-set scoring", local_scores)
     t3 = time.perf_counter()
     parts = gather_to_rank0(combined)
+    fparts = gather_to_rank0(feats_host) if save_features else None
     if timings is not None:
         timings.update(stats_s=t1 - t0, centroids_s=t2 - t1, gen_s=t3 - t2, rank=rank, world=ws)
     if rank != 0:
@@ -175,4 +260,27 @@ def _run_eval_phases(generated_meshes_dir, real_meshes_dir, model_path, keypoint
     if out_json:
         with open(out_json, "w") as f:
             json.dump(merged, f, indent=2)
+    if save_features:
+        save_window_features(fparts, save_features)
+    if human_scores_path and os.path.exists(human_scores_path):
+        for key in ("ac", "tc"):
+            sc = {v: e[key] for v, e in merged.items() if key in e}
+            corr, p, m = VE.compute_spearman_correlation(sc, human_scores_path, key)
+            if corr is not None:
+                print(f"{key.upper()} Spearman: {corr:.4f} (p={p:.4e}, matched {len(m)})")
     return merged
+
+
+def save_window_features(parts: List[Optional[dict]], path: str) -> None:
+    """window_features.pt (eval.py:197-204 layout) from the per-rank feature dicts, concatenated in rank order."""
+    parts = [p for p in parts if p is not None]
+    if parts:
+        out = {"seq_embeds": torch.cat([p["seq_embeds"] for p in parts]),
+               "frame_embeds": torch.cat([p["frame_embeds"] for p in parts]),
+               "cls_names": [c for p in parts for c in p["cls_names"]],
+               "vid_names": [v for p in parts for v in p["vid_names"]]}
+    else:
+        out = {"seq_embeds": torch.empty(0, 256), "frame_embeds": torch.empty(0, 33, 256), "cls_names": [],
+               "vid_names": []}
+    torch.save(out, path)
+    print(f"Saved features to {path}")

@@ -95,7 +95,9 @@ def load_model(model_path, dims_map_raw=None, dims_map_diff=None, device="cuda",
     """eval.py:136-165 -> a libvge encoder handle (weights repacked into HBM)."""
     if dims_map_raw is not None:
         if tuple(dims_map_raw.values()) != ops.DIMS_RAW or tuple(dims_map_diff.values()) != ops.DIMS_DIFF:
-            raise ValueError(f"unsupported modality dims {dims_map_raw} / {dims_map_diff}")
+            from .lib import UnsupportedModelError
+            raise UnsupportedModelError(f"unsupported modality dims {dims_map_raw} / {dims_map_diff} (the kernels "
+                                        f"are built for the five-modality layout; VGE_ERR_UNSUPPORTED)")
     if isinstance(model_path, dict):
         sd, hp = model_path, {"d_model": 256, "time_layers": 4, "time_heads": 8}
     elif isinstance(model_path, tuple):  # (state_dict, hyper-parameters) as _load_state_dict returns them
@@ -352,7 +354,8 @@ def main(argv=None):
         try:
             res = run_eval_distributed(a.generated_meshes, a.real_meshes, a.model, a.keypoints, a.real_keypoints,
                                        a.clip_len, a.stride, out_json=a.out, device=f"cuda:{local}",
-                                       compute=a.compute)
+                                       compute=a.compute, human_scores_path=a.human_scores,
+                                       save_features=a.save_features)
         finally:
             dist.destroy_process_group()
     else:

@@ -11,12 +11,14 @@ LIB_PATH = Path(os.environ.get("VGE_LIB", _HERE / "libvge.so"))
 
 VGE_OK = 0
 STATUS = {0: "VGE_OK", 1: "VGE_ERR_ARG", 2: "VGE_ERR_HIP", 3: "VGE_ERR_MISSING_WEIGHT", 4: "VGE_ERR_WEIGHT_SHAPE",
-          5: "VGE_ERR_NOMEM", 6: "VGE_ERR_WORKSPACE"}
+          5: "VGE_ERR_NOMEM", 6: "VGE_ERR_WORKSPACE", 7: "VGE_ERR_UNSUPPORTED"}
+VGE_ERR_UNSUPPORTED = 7
 
 EXPORTS = ["vge_featurize", "vge_stats_workspace_bytes", "vge_stats_accumulate", "vge_stats_finalize",
            "vge_encoder_create", "vge_encoder_reserve", "vge_encoder_destroy", "vge_encode", "vge_tc_windows",
            "vge_score_videos", "vge_centroid_accumulate", "vge_centroid_finalize", "vge_last_error", "vge_version",
            "vge_encoder_profile_begin", "vge_encoder_profile_read", "vge_ingest_probe", "vge_ingest_decode",
+           "vge_ingest_default_threads",
            "vge_hmr_create", "vge_hmr_reserve", "vge_hmr_destroy", "vge_hmr_extract", "vge_hmr_profile_begin",
            "vge_hmr_profile_read", "vge_op_gemm_bf16", "vge_op_vit_attention", "vge_op_layernorm_bf16",
            "vge_dwpose_create", "vge_dwpose_reserve", "vge_dwpose_destroy", "vge_dwpose_keypoints",
@@ -27,6 +29,11 @@ EXPORTS = ["vge_featurize", "vge_stats_workspace_bytes", "vge_stats_accumulate",
 
 class VgeError(RuntimeError):
     pass
+
+
+class UnsupportedModelError(VgeError):
+    """VGE_ERR_UNSUPPORTED: a checkpoint whose d_model / time_heads / modality set the kernels are not built for
+    (load_model, eval.py:136-165, would build such a HumanActionScorer; this library refuses it by name)."""
 
 
 class Dims(C.Structure):
@@ -98,4 +105,5 @@ def load() -> C.CDLL:
 def check(status: int, what: str) -> None:
     if status != VGE_OK:
         msg = load().vge_last_error().decode(errors="replace")
-        raise VgeError(f"{what} failed: {STATUS.get(status, status)}: {msg}")
+        cls = UnsupportedModelError if status == VGE_ERR_UNSUPPORTED else VgeError
+        raise cls(f"{what} failed: {STATUS.get(status, status)}: {msg}")
