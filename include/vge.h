@@ -49,7 +49,11 @@ typedef enum {
  * VGE_F32X3: f32-class split precision -- every GEMM operand carried as fp16 hi + fp16 lo*2^11 and
  * each product formed as hi*hi + 2^-11 (hi*lo + lo*hi) on v_mfma_f32_32x32x16_f16 with f32
  * accumulation (relative error ~2^-21 per product; AC/TC within ~1e-7 of the f32 mode). */
-typedef enum { VGE_F32 = 0, VGE_F32X3 = 1 } vge_dtype;
+typedef enum { VGE_F32 = 0, VGE_F32X3 = 1, VGE_F16 = 2 } vge_dtype;
+/* VGE_F16: the throughput mode (BASELINE config 5, "fp16 MFMA path"): every GEMM operand a single fp16
+ * (the hi planes of the VGE_F32X3 image, same power-of-two scaling), one v_mfma_f32_32x32x16_f16 per
+ * product, f32 accumulation, f32 epilogues (GELU, GroupNorm, LayerNorm, softmax, outputs).  Not a parity
+ * mode: its AC/TC deviation from the reference is measured and reported (bench.py precision). */
 
 #define VGE_FEAT_DIM 2596
 #define VGE_RAW_DIM 1370

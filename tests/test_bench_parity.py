@@ -72,3 +72,27 @@ def test_bench_workload_vs_oracle(n, compute):
     print(f"{compute} n={n}: seq {e_seq:.2e} frame {e_fe:.2e} ac {e_ac:.2e} tc {e_tc:.2e}")
     assert e_seq < 2e-5 and e_fe < 2e-5, (e_seq, e_fe)
     assert e_ac < 1e-4 and e_tc < 1e-4, (e_ac, e_tc)
+
+
+@pytest.mark.parametrize("n", [256, 600])
+def test_f16_throughput_mode_vs_oracle(n):
+    """VGE_F16 (config 5's "fp16 MFMA path"): single-fp16 operands, one MFMA per product.  Not a parity mode; its
+    deviation from the oracle is bounded here (fp16 operand rounding, 2^-11 relative, through ~15 layers) and
+    reported by bench.py.  The same windows must give the same bits in any batch position (deterministic)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vge import ops
+    o = _oracle(n)
+    feats = torch.from_numpy(o["feats"]).to(DEV)
+    enc = ops.Encoder(o["sd"], device=DEV, compute="f16")
+    enc.reserve(n)
+    seq, fe, tcw = enc.encode(feats, frame_embed=True, tc=True)
+    first = torch.arange(n + 1, dtype=torch.int32, device=DEV)
+    ac, tc = ops.score_videos(seq, tcw, first, o["vcls"].to(torch.int32).to(DEV), o["cent"].to(DEV))
+    e_seq = (seq.cpu() - o["seq"]).abs().max().item()
+    e_ac = (ac.cpu() - o["ac"]).abs().max().item()
+    e_tc = (tc.cpu() - o["tc"]).abs().max().item()
+    print(f"f16 n={n}: seq {e_seq:.2e} ac {e_ac:.2e} tc {e_tc:.2e}")
+    assert e_seq < 2e-2 and e_ac < 1e-2 and e_tc < 1e-2, (e_seq, e_ac, e_tc)
+    s2, _, _ = enc.encode(feats[:64].contiguous(), frame_embed=False, tc=True)
+    assert torch.equal(s2, seq[:64])

@@ -48,7 +48,7 @@ struct GemmArgsX3Host {
   const float* bias; const float* res; int ldr; const float* ln_w; const float* ln_b; const float* pe; const float* cls;
   const float* cs;
 };
-hipError_t launch_conv_encoders_x3(const float*, int, const void*, int, float*, hipStream_t);
+hipError_t launch_conv_encoders_x3(const float*, int, const void*, int, float*, bool, hipStream_t);
 hipError_t launch_gemm_x3(int, const GemmArgsX3Host&, hipStream_t);
 struct FfnArgsX3Host {
   const float* X1; float* out; int M;
@@ -74,7 +74,7 @@ struct TxArgsX3Host {
   float* seq; float* frame; float* tc;
 };
 hipError_t transformer_x3_kernel_setup();
-hipError_t launch_transformer_x3(const TxArgsX3Host&, hipStream_t);
+hipError_t launch_transformer_x3(const TxArgsX3Host&, bool, hipStream_t);
 hipError_t launch_conv_encoders(const float*, int, const void*, int, float*, hipStream_t);
 hipError_t launch_fuse(const float*, int, const FuseParamsHost&, float*, hipStream_t);
 hipError_t launch_gemm(int, const GemmArgsHost&, hipStream_t);
@@ -326,8 +326,10 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
                        vge_encoder** out) {
   if (!dims || !weights || !out) return fail(VGE_ERR_ARG, "vge_encoder_create: null argument");
   *out = nullptr;
-  if (compute != VGE_F32 && compute != VGE_F32X3) return fail(VGE_ERR_ARG, "vge_encoder_create: unsupported compute dtype");
-  const bool x3 = compute == VGE_F32X3;
+  if (compute != VGE_F32 && compute != VGE_F32X3 && compute != VGE_F16)
+    return fail(VGE_ERR_ARG, "vge_encoder_create: unsupported compute dtype");
+  // VGE_F16 shares the 3xfp16 weight image (its kernels read the hi planes only)
+  const bool x3 = compute == VGE_F32X3 || compute == VGE_F16;
   if (dims->time_layers < 1) return fail(VGE_ERR_ARG, "vge_encoder_create: time_layers must be >= 1");
   if (dims->n_modalities != 5 || dims->d_model != 256 || dims->time_heads != 8 || dims->clip_len != 32)
     return fail(VGE_ERR_UNSUPPORTED,
@@ -357,6 +359,8 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
   };
   auto bail = [&]() { return fail(err.rfind("missing", 0) == 0 ? VGE_ERR_MISSING_WEIGHT : VGE_ERR_WEIGHT_SHAPE, err); };
 
+  if (compute == VGE_F16 && dims->time_layers > 8)
+    return fail(VGE_ERR_UNSUPPORTED, "vge_encoder_create: VGE_F16 runs the fused transformer, at most 8 layers");
   const int L = dims->time_layers;
   std::vector<float> pk;      // f32 device image
   // x3: the fp16 hi/lo image is packed on the device after the upload (launch_pack_x3, one job per matrix; the
@@ -663,7 +667,7 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
   }
   if (x3) {
     const char* uf = getenv("VGE_X3_UNFUSED");
-    enc->tx_fused = !(uf && uf[0] == '1');
+    enc->tx_fused = !(uf && uf[0] == '1') || compute == VGE_F16;  // the f16 mode has the fused kernel only
     if (L > 8) enc->tx_fused = false;  // the fused kernel takes up to 8 layers
     std::vector<vge::TxLayerX3Host>& tl = enc->tx_layers;
     tl.resize(L);
@@ -772,7 +776,7 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
   hipEvent_t* ev = nullptr;
   if (enc->prof_calls < enc->prof_max) ev = enc->prof_ev.data() + (size_t)(enc->prof_calls++) * (VGE_N_STAGES + 1);
   auto mark = [&](int k) -> hipError_t { return ev ? hipEventRecord(ev[k], s) : hipSuccess; };
-  const bool x3 = enc->mode == VGE_F32X3;
+  const bool x3 = enc->mode == VGE_F32X3 || enc->mode == VGE_F16, split = enc->mode != VGE_F16;
   // one GEMM launcher for both modes (same epilogues; x3 = 3xfp16 split MFMA, f32 = exact f32 MFMA)
   auto gemm = [&](int epi, const float* A, int lda, const void* W, const float* cs, float* o, int ldo, int Mr, int K,
                   int N, const float* bias, const float* res, const float* lw, const float* lb) -> hipError_t {
@@ -784,7 +788,7 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
     return vge::launch_gemm(epi, g, s);
   };
   HIPCHK(mark(0));
-  if (x3) HIPCHK(vge::launch_conv_encoders_x3(feats, B, enc->d_encs, 10, enc->enc_out, s));
+  if (x3) HIPCHK(vge::launch_conv_encoders_x3(feats, B, enc->d_encs, 10, enc->enc_out, split, s));
   else HIPCHK(vge::launch_conv_encoders(feats, B, enc->d_encs, 10, enc->enc_out, s));
   HIPCHK(mark(1));
   HIPCHK(vge::launch_fuse(enc->enc_out, frames, enc->fuse, enc->pooled, s));
@@ -793,7 +797,7 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
     HIPCHK(mark(3));
     const vge::TxArgsX3Host ta{enc->pooled, B, enc->n_layers, (const _Float16*)enc->Wov, enc->Wov_cs, enc->cls, enc->pe,
                                enc->tx_layers.data(), seq_embed, frame_embed, tc_window};
-    HIPCHK(vge::launch_transformer_x3(ta, s));
+    HIPCHK(vge::launch_transformer_x3(ta, split, s));
     HIPCHK(mark(4));
     HIPCHK(mark(5));
     return VGE_OK;

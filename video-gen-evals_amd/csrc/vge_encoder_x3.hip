@@ -71,7 +71,7 @@ constexpr int conv_lds_bytes() {
 
 // blocks [0, n_quad) take 4 windows, the rest 2: quads stream each weight byte for twice the rows, pairs
 // fill the last round (see launch_conv_encoders_x3)
-template <int W, int CW>
+template <int W, int CW, bool SP>
 __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feats, int n_windows, int win0,
                                                   const EncDescX3& ed, int e, float* __restrict__ enc_out,
                                                   char* lds_raw, [[maybe_unused]] bool tr_on) {
@@ -95,7 +95,7 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
   floatx16 res[R][N];
   for (int c = tid; c < XS; c += 64 * CW) {  // the zero row
     Xh[ROWS * XS + c] = (_Float16)0.0f;
-    Xl[ROWS * XS + c] = (_Float16)0.0f;
+    if constexpr (SP) Xl[ROWS * XS + c] = (_Float16)0.0f;
   }
 
   // Combine one value per window over the 8 waves.  `slot` picks one of 4 partial buffers so back-to-back
@@ -163,8 +163,10 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
           *reinterpret_cast<_Float16*>(bh + off) = hi[0];
           *reinterpret_cast<_Float16*>(bh + off + XSB) = hi[1];
 #if !(VGE_ABL & 256)  // timing ablation: hi plane only (wrong results)
-          *reinterpret_cast<_Float16*>(bl + off) = lo[0];
-          *reinterpret_cast<_Float16*>(bl + off + XSB) = lo[1];
+          if constexpr (SP) {
+            *reinterpret_cast<_Float16*>(bl + off) = lo[0];
+            *reinterpret_cast<_Float16*>(bl + off + XSB) = lo[1];
+          }
 #endif
         }
       }
@@ -176,7 +178,7 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
     for (int t = 0; t < R; ++t) {
       const char* q = xa + (t * 32 + i) * XSB + c * 32;
       f.h[t] = *reinterpret_cast<const half8*>(q);
-      f.l[t] = *reinterpret_cast<const half8*>(q + XROWS * XSB);
+      if constexpr (SP) f.l[t] = *reinterpret_cast<const half8*>(q + XROWS * XSB);
     }
   };
 
@@ -217,7 +219,8 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
 #pragma unroll
         for (int jc = 0; jc < 4; ++jc) {
           const int c = lane + 64 * jc;
-          split_store(Xh + r * XS + c, Xl + r * XS + c, ldexpf(a[jr][jc], -ex));
+          if constexpr (SP) split_store(Xh + r * XS + c, Xl + r * XS + c, ldexpf(a[jr][jc], -ex));
+          else Xh[r * XS + c] = (_Float16)ldexpf(a[jr][jc], -ex);
         }
       }
     }
@@ -234,7 +237,7 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
           for (int n = 0; n < N; ++n) acc.c[t][n][r] *= f;
         }
     }
-    run_stream<CONV_PF>(acc, reinterpret_cast<const char*>(ed.stem) + (size_t)p * 16 * CHUNK_B,
+    run_stream<CONV_PF, SP>(acc, reinterpret_cast<const char*>(ed.stem) + (size_t)p * 16 * CHUNK_B,
                         ((kw + 127) >> 7) * STREAM_GROUP, loff, afn_rows);
     __syncthreads();  // every wave is done reading X
   }
@@ -269,10 +272,10 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
           const int row = in ? t * 32 + tt : ROWS;  // out of the window -> zero row
           const char* q = xa + row * XSB + cc * 32;
           f.h[t] = *reinterpret_cast<const half8*>(q);
-          f.l[t] = *reinterpret_cast<const half8*>(q + XROWS * XSB);
+          if constexpr (SP) f.l[t] = *reinterpret_cast<const half8*>(q + XROWS * XSB);
         }
       };
-      run_stream<CONV_PF>(acc, reinterpret_cast<const char*>(ed.conv) + (size_t)(blk * 2 + cv) * 5 * 16 * CHUNK_B,
+      run_stream<CONV_PF, SP>(acc, reinterpret_cast<const char*>(ed.conv) + (size_t)(blk * 2 + cv) * 5 * 16 * CHUNK_B,
                           5 * 16, loff, afn);
       STAMP(4 + (blk * 2 + cv) * 2);
       // epilogue in packed f32 (v_pk_fma_f32: two rows per instruction), in place:
@@ -356,7 +359,7 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
 
   // ---------------- proj: Linear(256 -> 256, no bias)
   acc.zero();
-  run_stream<CONV_PF>(acc, reinterpret_cast<const char*>(ed.proj), 16, loff, afn_rows);
+  run_stream<CONV_PF, SP>(acc, reinterpret_cast<const char*>(ed.proj), 16, loff, afn_rows);
   STAMP(20);
 #pragma unroll
   for (int t = 0; t < R; ++t) {
@@ -391,6 +394,7 @@ __device__ __forceinline__ int xcd_remap(int b, int nblk) {
   return (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (b >> 3);
 }
 
+template <bool SP>
 __global__ void __launch_bounds__(512, 1) conv_encoder_x3_kernel(const float* __restrict__ feats,
                                                                   const EncDescX3* __restrict__ encs, ConvSched cs,
                                                                   float* __restrict__ enc_out) {
@@ -405,14 +409,14 @@ __global__ void __launch_bounds__(512, 1) conv_encoder_x3_kernel(const float* __
       const int big = cs.qr * (cs.qa + 1);
       const int e = u < big ? u / (cs.qa + 1) : cs.qr + (u - big) / cs.qa;
       const int j = u < big ? u % (cs.qa + 1) : (u - big) % cs.qa;
-      conv_encoder_body<4, 8>(feats, n, 4 * j, encs[e], e, enc_out, lds_raw, round == VGE_TRACE_ROUND);
+      conv_encoder_body<4, 8, SP>(feats, n, 4 * j, encs[e], e, enc_out, lds_raw, round == VGE_TRACE_ROUND);
     } else {
       const int v = u - cs.Q;
       const int big = cs.qr * p_big;
       const int e = v < big ? v / p_big : cs.qr + (v - big) / p_small;
       const int j = v < big ? v % p_big : (v - big) % p_small;
       const int q_e = cs.qa + (e < cs.qr);
-      conv_encoder_body<2, 8>(feats, n, 4 * q_e + 2 * j, encs[e], e, enc_out, lds_raw, round == VGE_TRACE_ROUND);
+      conv_encoder_body<2, 8, SP>(feats, n, 4 * q_e + 2 * j, encs[e], e, enc_out, lds_raw, round == VGE_TRACE_ROUND);
     }
   }
 }
@@ -829,8 +833,11 @@ struct GemmArgsX3Host {
 static_assert(sizeof(GemmArgsX3Host) == sizeof(GemmArgsX3), "GemmArgsX3 layout");
 
 hipError_t encoder_x3_kernel_setup() {
-  hipError_t e = hipFuncSetAttribute((const void*)conv_encoder_x3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                     conv_lds_bytes<4, 8>());
+  hipError_t e = hipFuncSetAttribute((const void*)conv_encoder_x3_kernel<true>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, conv_lds_bytes<4, 8>());
+  if (e != hipSuccess) return e;
+  e = hipFuncSetAttribute((const void*)conv_encoder_x3_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          conv_lds_bytes<4, 8>());
   if (e != hipSuccess) return e;
   const void* gk[4] = {(const void*)gemm_x3_kernel<EPI_TOKENS, GEMM_RT>, (const void*)gemm_x3_kernel<EPI_BIAS, GEMM_RT>,
                        (const void*)gemm_x3_kernel<EPI_BIAS_RELU, GEMM_RT>,
@@ -846,7 +853,7 @@ hipError_t encoder_x3_kernel_setup() {
 // units) persistent blocks and m = ceil(pair units / G) per block, Q = G * floor(m / 2) quads (as many as
 // fit) make every block run floor(m / 2) quads and at most one pair.
 hipError_t launch_conv_encoders_x3(const float* feats, int n_windows, const void* encs, int n_enc, float* enc_out,
-                                   hipStream_t s) {
+                                   bool split, hipStream_t s) {
   static int n_cu = 0;
   if (n_cu == 0) {
     int dev = 0;
@@ -869,8 +876,12 @@ hipError_t launch_conv_encoders_x3(const float* feats, int n_windows, const void
   for (int e = 0; e < n_enc; ++e) pairs += (n_windows - 4 * (cs.qa + (e < cs.qr)) + 1) / 2;
   cs.n_units = Q + pairs;
   cs.G = std::min(n_cu, cs.n_units);
-  hipLaunchKernelGGL(conv_encoder_x3_kernel, dim3(cs.G), dim3(512), (conv_lds_bytes<4, 8>()), s, feats,
-                     reinterpret_cast<const EncDescX3*>(encs), cs, enc_out);
+  if (split)
+    hipLaunchKernelGGL(conv_encoder_x3_kernel<true>, dim3(cs.G), dim3(512), (conv_lds_bytes<4, 8>()), s, feats,
+                       reinterpret_cast<const EncDescX3*>(encs), cs, enc_out);
+  else
+    hipLaunchKernelGGL(conv_encoder_x3_kernel<false>, dim3(cs.G), dim3(512), (conv_lds_bytes<4, 8>()), s, feats,
+                       reinterpret_cast<const EncDescX3*>(encs), cs, enc_out);
   return hipGetLastError();
 }
 

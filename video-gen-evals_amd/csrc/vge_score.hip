@@ -3,10 +3,10 @@
 //   centroid_partial_kernel + centroid_combine_kernel
 //                          build_train_centroids_subset (utils.py:1018-1043): sums.index_add_(0, y, z),
 //                          counts.index_add_, as a deterministic segmented reduction: the windows are cut into
-//                          segments of CENT_SEG (a function of n only); one workgroup per (segment, block of 64
-//                          classes) walks its windows in order with thread j owning column j of every class
-//                          row in LDS (no atomics, no races), then one thread per (class, column) adds the
-//                          segment partials in segment order.  Same result for any grid / device; the order
+//                          segments of CENT_SEG (a function of n only); one workgroup per (segment, 64 columns,
+//                          block of 64 classes) walks its windows in order, lane j owning column j of every
+//                          class row in LDS (no atomics, no races), then the segment partials are added in a
+//                          fixed order.  Same result for any grid / device; the order
 //                          of the f32 additions differs from a sequential index_add_ only by the segment
 //                          split (a few ulps of the sums, far inside the 2e-5 centroid tolerance).
 //                          HBM-bound: reads n x d x 4 B + 4n B once.
@@ -20,22 +20,25 @@
 
 namespace {
 
-constexpr int CENT_SEG = 256;     // windows per segment
-constexpr int CENT_CB = 64;       // classes per workgroup (LDS 64 x 256 x 4 B = 64 KB)
+constexpr int CENT_SEG = 512;     // windows per segment (a function of nothing but n: the result is launch-independent)
+constexpr int CENT_CB = 64;       // classes per workgroup
 
-// grid (n_seg, ceil(C / 64)), 256 threads; d <= 256.  part [n_seg][C][d], pcnt [n_seg][C]
+// grid (n_seg, ceil(d / 64), ceil(C / 64)), 4 waves; lane = column (64 per workgroup).  Wave q walks windows
+// [q SEG/4, (q+1) SEG/4) of the segment in order into its own LDS rows, then the 4 wave partials are added in
+// wave order.  part [n_seg][C][d], pcnt [n_seg][C].
 __global__ void __launch_bounds__(256) centroid_partial_kernel(const float* __restrict__ seq,
                                                                const int* __restrict__ cls, int n, int C, int d,
                                                                float* __restrict__ part, float* __restrict__ pcnt) {
-  __shared__ float acc[CENT_CB][256];
-  __shared__ float cnt[CENT_CB];
-  const int j = threadIdx.x, seg = blockIdx.x, c0 = blockIdx.y * CENT_CB;
+  __shared__ float acc[4][CENT_CB][64];
+  __shared__ float cnt[4][CENT_CB];
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int seg = blockIdx.x, j = blockIdx.y * 64 + lane, c0 = blockIdx.z * CENT_CB;
   const int nc = min(CENT_CB, C - c0);
-  for (int c = 0; c < nc; ++c) acc[c][j] = 0.f;
-  if (j < nc) cnt[j] = 0.f;
-  __syncthreads();
-  const int w0 = seg * CENT_SEG, w1 = min(n, w0 + CENT_SEG);
-  // rows in batches of 8: the loads of a batch are issued together, the adds follow in window order
+  for (int c = 0; c < nc; ++c) acc[q][c][lane] = 0.f;
+  if (lane < nc) cnt[q][lane] = 0.f;
+  constexpr int QW = CENT_SEG / 4;
+  const int w0 = seg * CENT_SEG + q * QW, w1 = min(n, w0 + QW);
+  // rows in batches of 8: the batch's loads are issued together, the adds follow in window order
   for (int w = w0; w < w1; w += 8) {
     float x[8];
     int y[8];
@@ -46,30 +49,47 @@ __global__ void __launch_bounds__(256) centroid_partial_kernel(const float* __re
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k)
-      if ((unsigned)y[k] < (unsigned)nc) {  // uniform over the block
-        acc[y[k]][j] += x[k];
-        if (j == 0) cnt[y[k]] += 1.0f;
+      if ((unsigned)y[k] < (unsigned)nc) {  // uniform over the wave
+        acc[q][y[k]][lane] += x[k];
+        if (lane == 0) cnt[q][y[k]] += 1.0f;
       }
   }
   __syncthreads();
-  if (j < d)
-    for (int c = 0; c < nc; ++c) part[((size_t)seg * C + c0 + c) * d + j] = acc[c][j];
-  if (j < nc) pcnt[(size_t)seg * C + c0 + j] = cnt[j];
+  for (int c = q; c < nc; c += 4)
+    if (j < d) part[((size_t)seg * C + c0 + c) * d + j] = ((acc[0][c][lane] + acc[1][c][lane]) + acc[2][c][lane]) +
+                                                          acc[3][c][lane];
+  if (blockIdx.y == 0 && q == 0 && lane < nc)
+    pcnt[(size_t)seg * C + c0 + lane] = ((cnt[0][lane] + cnt[1][lane]) + cnt[2][lane]) + cnt[3][lane];
 }
 
-// one thread per (class, column) [+ C threads for the counts]: sums += partials in segment order
-__global__ void centroid_combine_kernel(const float* __restrict__ part, const float* __restrict__ pcnt, int n_seg,
-                                        int C, int d, float* __restrict__ sums, float* __restrict__ counts) {
-  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
-  if (idx < C * d) {
-    float s = 0.f;
-    for (int g = 0; g < n_seg; ++g) s += part[(size_t)g * C * d + idx];
-    sums[idx] += s;
-  } else if (idx < C * d + C) {
-    const int c = idx - C * d;
-    float s = 0.f;
-    for (int g = 0; g < n_seg; ++g) s += pcnt[(size_t)g * C + c];
-    counts[c] += s;
+// sums[e] += sum over segments of part[g][e] (e over C d sums then C counts): 64 elements per workgroup, wave q
+// adds segments q, q + 4, ... (8 loads in flight), then the 4 wave partials in wave order.
+__global__ void __launch_bounds__(256) centroid_combine_kernel(const float* __restrict__ part,
+                                                               const float* __restrict__ pcnt, int n_seg, int C,
+                                                               int d, float* __restrict__ sums,
+                                                               float* __restrict__ counts) {
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + lane, n_sum = C * d;
+  const bool is_cnt = e >= n_sum;
+  const float* src = is_cnt ? pcnt + (e - n_sum) : part + e;
+  const size_t stride = is_cnt ? (size_t)C : (size_t)n_sum;
+  float s = 0.f;
+  if (e < n_sum + C) {
+    for (int g = q; g < n_seg; g += 32) {
+      float x[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) x[k] = (g + 4 * k < n_seg) ? src[(size_t)(g + 4 * k) * stride] : 0.f;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += x[k];
+    }
+  }
+  red[q][lane] = s;
+  __syncthreads();
+  if (q == 0 && e < n_sum + C) {
+    const float t = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    if (is_cnt) counts[e - n_sum] += t;
+    else sums[e] += t;
   }
 }
 
@@ -170,11 +190,11 @@ hipError_t launch_centroid_accum(const float* seq, const int* cls, int n, int C,
   hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&part), nf * sizeof(float), s);
   if (e != hipSuccess) return e;
   float* pcnt = part + (size_t)n_seg * C * d;
-  hipLaunchKernelGGL(centroid_partial_kernel, dim3(n_seg, (C + CENT_CB - 1) / CENT_CB), dim3(256), 0, s, seq, cls, n,
-                     C, d, part, pcnt);
+  hipLaunchKernelGGL(centroid_partial_kernel, dim3(n_seg, (d + 63) / 64, (C + CENT_CB - 1) / CENT_CB), dim3(256), 0,
+                     s, seq, cls, n, C, d, part, pcnt);
   const int total = C * d + C;
-  hipLaunchKernelGGL(centroid_combine_kernel, dim3((total + 255) / 256), dim3(256), 0, s, part, pcnt, n_seg, C, d,
-                     sums, counts);
+  hipLaunchKernelGGL(centroid_combine_kernel, dim3((total + 63) / 64), dim3(256), 0, s, part, pcnt, n_seg, C, d, sums,
+                     counts);
   e = hipGetLastError();
   const hipError_t f = hipFreeAsync(part, s);
   return e != hipSuccess ? e : f;

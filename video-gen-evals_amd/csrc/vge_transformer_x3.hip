@@ -72,18 +72,24 @@ struct AFragT {  // one chunk's A operand: the 32 frame rows (MFMA) and the CLS 
 };
 
 // CLS row on the VALU: c += x . w over this lane's 8 k of the chunk, the same 3 products as the MFMAs
+template <bool SP>
 __device__ __forceinline__ float cls_dot(float c, half8 xh, half8 xl, half8 wh, half8 wl) {
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
-    const half2v a = {xh[2 * p], xh[2 * p + 1]}, al = {xl[2 * p], xl[2 * p + 1]};
-    const half2v b = {wh[2 * p], wh[2 * p + 1]}, bl = {wl[2 * p], wl[2 * p + 1]};
-    c = __builtin_amdgcn_fdot2(al, b, c, false);
-    c = __builtin_amdgcn_fdot2(a, bl, c, false);
+    const half2v a = {xh[2 * p], xh[2 * p + 1]};
+    const half2v b = {wh[2 * p], wh[2 * p + 1]};
+    if constexpr (SP) {
+      const half2v al = {xl[2 * p], xl[2 * p + 1]}, bl = {wl[2 * p], wl[2 * p + 1]};
+      c = __builtin_amdgcn_fdot2(al, b, c, false);
+      c = __builtin_amdgcn_fdot2(a, bl, c, false);
+    }
     c = __builtin_amdgcn_fdot2(a, b, c, false);
   }
   return c;
 }
 
+// SP: 3xfp16 (VGE_F32X3); !SP: single fp16 planes, one MFMA per product (VGE_F16 throughput mode)
+template <bool SP>
 __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* Ap = lds;                                   // A planes: hi rows [0, AROWS), lo at + AROWS * XSB
@@ -195,14 +201,16 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
         const int off = ((r & 3) + 8 * (r >> 2)) * XSB;
         *reinterpret_cast<_Float16*>(bh + off) = hi[0];
         *reinterpret_cast<_Float16*>(bh + off + XSB) = hi[1];
-        *reinterpret_cast<_Float16*>(bh + off + AROWS * XSB) = lo[0];
-        *reinterpret_cast<_Float16*>(bh + off + XSB + AROWS * XSB) = lo[1];
+        if constexpr (SP) {
+          *reinterpret_cast<_Float16*>(bh + off + AROWS * XSB) = lo[0];
+          *reinterpret_cast<_Float16*>(bh + off + XSB + AROWS * XSB) = lo[1];
+        }
       }
       if (h == 0) {
         const float y = v0[n] * sc;
         const _Float16 hi = (_Float16)y;
         reinterpret_cast<_Float16*>(plane)[col0 + 32 * n] = hi;
-        reinterpret_cast<_Float16*>(plane + AROWS * XSB)[col0 + 32 * n] = (_Float16)(y - (float)hi);
+        if constexpr (SP) reinterpret_cast<_Float16*>(plane + AROWS * XSB)[col0 + 32 * n] = (_Float16)(y - (float)hi);
       }
     }
     return e;
@@ -233,9 +241,13 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
     }
     ax = fp16_range_exp(block_max(m));
 #pragma unroll
-    for (int j = 0; j < 32; ++j)
-      split_store(reinterpret_cast<_Float16*>(Ap + (1 + j) * XSB) + tid,
-                  reinterpret_cast<_Float16*>(Ap + (AROWS + 1 + j) * XSB) + tid, ldexpf(a[j], -ax));
+    for (int j = 0; j < 32; ++j) {
+      if constexpr (SP)
+        split_store(reinterpret_cast<_Float16*>(Ap + (1 + j) * XSB) + tid,
+                    reinterpret_cast<_Float16*>(Ap + (AROWS + 1 + j) * XSB) + tid, ldexpf(a[j], -ax));
+      else
+        reinterpret_cast<_Float16*>(Ap + (1 + j) * XSB)[tid] = (_Float16)ldexpf(a[j], -ax);
+    }
   }
   __syncthreads();
 
@@ -272,7 +284,7 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
   BFrag<2> b[TX_PF];
   gchar seg_next = seg_base(0);
 #pragma unroll
-  for (int j = 0; j < TX_PF - 1; ++j) load_b(seg_next, j, loff, b[j]);
+  for (int j = 0; j < TX_PF - 1; ++j) load_b<2, SP>(seg_next, j, loff, b[j]);
 
   for (int s = 0; s < nseg; ++s) {
     {  // lane-derived values re-derived per segment: stops the compiler from hoisting the ~100 (64-bit,
@@ -289,9 +301,11 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
     const char* abase = use_h ? U : Ap;
     auto afn = [&](int c, AFragT& f) {
       f.h = *reinterpret_cast<const half8*>(abase + aoff + c * 32);
-      f.l = *reinterpret_cast<const half8*>(abase + aoff + c * 32 + AROWS * XSB);
       f.h0 = *reinterpret_cast<const half8*>(abase + aoff0 + c * 32);
-      f.l0 = *reinterpret_cast<const half8*>(abase + aoff0 + c * 32 + AROWS * XSB);
+      if constexpr (SP) {
+        f.l = *reinterpret_cast<const half8*>(abase + aoff + c * 32 + AROWS * XSB);
+        f.l0 = *reinterpret_cast<const half8*>(abase + aoff0 + c * 32 + AROWS * XSB);
+      }
     };
     TSTAMP(2 * s);
     // this segment's epilogue parameters (column scales, bias, LayerNorm affine), loaded before its weight
@@ -334,8 +348,8 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
 #if !(VGE_ABL & 2)
-      if (c + TX_PF - 1 < 16) load_b(seg_cur, c + TX_PF - 1, loff, b[(c + TX_PF - 1) % TX_PF]);
-      else load_b(seg_next, c + TX_PF - 1 - 16, loff, b[(c + TX_PF - 1) % TX_PF]);
+      if (c + TX_PF - 1 < 16) load_b<2, SP>(seg_cur, c + TX_PF - 1, loff, b[(c + TX_PF - 1) % TX_PF]);
+      else load_b<2, SP>(seg_next, c + TX_PF - 1 - 16, loff, b[(c + TX_PF - 1) % TX_PF]);
 #endif
       if (c + 1 < 16) afn(c + 1, a[(c + 1) & 1]);
       const AFragT& f = a[c & 1];
@@ -344,13 +358,15 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
       for (int n = 0; n < 2; ++n) {
 #if !(VGE_ABL & 1)
         acc.c[0][n] = mfma32(f.h, bb.h[n], acc.c[0][n]);
-        acc.c[0][n] = mfma32(f.h, bb.l[n], acc.c[0][n]);
-        acc.c[0][n] = mfma32(f.l, bb.h[n], acc.c[0][n]);
+        if constexpr (SP) {
+          acc.c[0][n] = mfma32(f.h, bb.l[n], acc.c[0][n]);
+          acc.c[0][n] = mfma32(f.l, bb.h[n], acc.c[0][n]);
+        }
 #else
         asm volatile("" ::"v"(f.h), "v"(f.l), "v"(bb.h[n]), "v"(bb.l[n]));
 #endif
 #if !(VGE_ABL & 64)
-        c0[n] = cls_dot(c0[n], f.h0, f.l0, bb.h[n], bb.l[n]);
+        c0[n] = cls_dot<SP>(c0[n], f.h0, f.l0, bb.h[n], bb.l[n]);
 #endif
       }
       // the CLS dot products stay in their step (else they are sunk past the loop and the ring stays live)
@@ -506,13 +522,14 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
                 lv[k] = (_Float16)(y - (float)hv[k]);
               }
               *reinterpret_cast<half4v*>(rh + (8 * g + 4 * h) * 2) = hv;
-              *reinterpret_cast<half4v*>(rh + (8 * g + 4 * h) * 2 + AROWS * XSB) = lv;
+              if constexpr (SP) *reinterpret_cast<half4v*>(rh + (8 * g + 4 * h) * 2 + AROWS * XSB) = lv;
             }
             if (h == 0) {
               const float y = oc[e] * scl;
               const _Float16 hi = (_Float16)y;
               reinterpret_cast<_Float16*>(Ap)[(2 * wave + e) * 32 + i] = hi;
-              reinterpret_cast<_Float16*>(Ap + AROWS * XSB)[(2 * wave + e) * 32 + i] = (_Float16)(y - (float)hi);
+              if constexpr (SP)
+                reinterpret_cast<_Float16*>(Ap + AROWS * XSB)[(2 * wave + e) * 32 + i] = (_Float16)(y - (float)hi);
             }
           }
         }
@@ -668,11 +685,14 @@ struct TxArgsX3Host {
 };
 
 hipError_t transformer_x3_kernel_setup() {
-  return hipFuncSetAttribute((const void*)transformer_x3_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+  const hipError_t e = hipFuncSetAttribute((const void*)transformer_x3_kernel<true>,
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, TX_LDS_BYTES);
+  if (e != hipSuccess) return e;
+  return hipFuncSetAttribute((const void*)transformer_x3_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
                              TX_LDS_BYTES);
 }
 
-hipError_t launch_transformer_x3(const TxArgsX3Host& a, hipStream_t s) {
+hipError_t launch_transformer_x3(const TxArgsX3Host& a, bool split, hipStream_t s) {
   if (a.n_windows < 1) return hipSuccess;
   if (a.n_layers < 0 || a.n_layers > TX_MAX_LAYERS) return hipErrorInvalidValue;
   TxArgsX3 t;
@@ -688,7 +708,8 @@ hipError_t launch_transformer_x3(const TxArgsX3Host& a, hipStream_t s) {
   t.frame = a.frame;
   t.tc = a.tc;
   memcpy(t.layers, a.layers, sizeof(TxLayerX3) * a.n_layers);
-  hipLaunchKernelGGL(transformer_x3_kernel, dim3(a.n_windows), dim3(256), TX_LDS_BYTES, s, t);
+  if (split) hipLaunchKernelGGL(transformer_x3_kernel<true>, dim3(a.n_windows), dim3(256), TX_LDS_BYTES, s, t);
+  else hipLaunchKernelGGL(transformer_x3_kernel<false>, dim3(a.n_windows), dim3(256), TX_LDS_BYTES, s, t);
   return hipGetLastError();
 }
 

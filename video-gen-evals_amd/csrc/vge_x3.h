@@ -71,7 +71,9 @@ struct BFrag {  // B fragments (hi, lo) of one 16-K chunk for N column tiles
   half8 h[N], l[N];
 };
 
-template <int R, int N>
+// SP (split): true = the 3xfp16 product (hi*hi + hi*lo + lo*hi); false = the single-fp16 throughput mode
+// (VGE_F16: hi planes only, one MFMA per product; the lo fragments are never loaded)
+template <bool SP = true, int R, int N>
 __device__ __forceinline__ void mma_chunk(Acc<R, N>& acc, const AFrag<R>& a, const BFrag<N>& b) {
 #if !(VGE_ABL & 1)
 #pragma unroll
@@ -79,8 +81,10 @@ __device__ __forceinline__ void mma_chunk(Acc<R, N>& acc, const AFrag<R>& a, con
 #pragma unroll
     for (int t = 0; t < R; ++t) {
       acc.c[t][n] = mfma32(a.h[t], b.h[n], acc.c[t][n]);
-      acc.c[t][n] = mfma32(a.h[t], b.l[n], acc.c[t][n]);
-      acc.c[t][n] = mfma32(a.l[t], b.h[n], acc.c[t][n]);
+      if constexpr (SP) {
+        acc.c[t][n] = mfma32(a.h[t], b.l[n], acc.c[t][n]);
+        acc.c[t][n] = mfma32(a.l[t], b.h[n], acc.c[t][n]);
+      }
     }
 #else
   asm volatile("" ::"v"(a.h[0]), "v"(a.l[R - 1]), "v"(b.h[0]), "v"(b.l[N - 1]));
@@ -91,13 +95,13 @@ typedef const __attribute__((address_space(1))) char* gchar;  // global (not fla
 typedef const __attribute__((address_space(1))) half8* ghalf8;
 
 // column tile n of this lane sits 32 columns (512 B) after tile n - 1
-template <int N>
+template <int N, bool SP = true>
 __device__ __forceinline__ void load_b(gchar g, int c, unsigned loff, BFrag<N>& b) {
   gchar p = g + (size_t)c * CHUNK_B + loff;
 #pragma unroll
   for (int n = 0; n < N; ++n) {
     b.h[n] = *reinterpret_cast<ghalf8>(p + n * 512);
-    b.l[n] = *reinterpret_cast<ghalf8>(p + n * 512 + PLANE_B);
+    if constexpr (SP) b.l[n] = *reinterpret_cast<ghalf8>(p + n * 512 + PLANE_B);
   }
 }
 
@@ -105,12 +109,12 @@ __device__ __forceinline__ void load_b(gchar g, int c, unsigned loff, BFrag<N>& 
 // reads the A fragments of chunk c from LDS (one chunk ahead).  B fragments are loaded PF - 1 chunks ahead
 // into a register ring; the loop is unrolled by PF so every ring index is static and the compiler's counted
 // vmcnt waits retire exactly the chunk being consumed.
-template <int PF, int R, int N, class AFn>
+template <int PF, bool SP = true, int R, int N, class AFn>
 __device__ __forceinline__ void run_stream(Acc<R, N>& acc, const void* gw, int n, unsigned loff, AFn afn) {
   const gchar g = (gchar)gw;
   BFrag<N> b[PF];
 #pragma unroll
-  for (int j = 0; j < PF - 1; ++j) load_b(g, j, loff, b[j]);
+  for (int j = 0; j < PF - 1; ++j) load_b<N, SP>(g, j, loff, b[j]);
   AFrag<R> a[2];
   afn(0, a[0]);
   for (int c0 = 0; c0 < n; c0 += PF) {
@@ -118,12 +122,12 @@ __device__ __forceinline__ void run_stream(Acc<R, N>& acc, const void* gw, int n
     for (int j = 0; j < PF; ++j) {
       const int c = c0 + j;
 #if !(VGE_ABL & 2)
-      load_b(g, min(c + PF - 1, n - 1), loff, b[(j + PF - 1) % PF]);
+      load_b<N, SP>(g, min(c + PF - 1, n - 1), loff, b[(j + PF - 1) % PF]);
 #endif
 #if !(VGE_ABL & 4)
       afn(min(c + 1, n - 1), a[(j + 1) & 1]);
 #endif
-      mma_chunk(acc, a[j & 1], b[j]);
+      mma_chunk<SP>(acc, a[j & 1], b[j]);
       // pin this step's loads in place: without it the compiler hoists every A read of the unrolled group
       // and sinks the B loads next to their use, which collapses the prefetch to vmcnt(0) waits
       asm volatile("" ::: "memory");

@@ -102,7 +102,7 @@ def stats_finalize(sums: torch.Tensor, counts: np.ndarray) -> Tuple[torch.Tensor
     return mean, std
 
 
-COMPUTE = {"f32": 0, "f32x3": 1}
+COMPUTE = {"f32": 0, "f32x3": 1, "f16": 2}
 
 
 class Encoder:
