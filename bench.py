@@ -5,21 +5,26 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Workload (config 2 of BASELINE.json): 256 synthetic 32-frame clips per GPU with pre-extracted
-per-frame features (SMPL rotations, betas, 1024-d token, 120-d keypoints) resident in HBM.  One
-step = featurise all windows (HIP) -> HumanActionScorer forward (MFMA) -> per-video AC + TC
-(HIP reductions) -> scores copied to pinned host memory.  ModalityStats and the real-class
-centroids (the real set is sharded over ranks, sufficient statistics all-reduced over RCCL) are
-built once in the setup phase and reported separately (`setup_s`).  Weak scaling: every rank
-scores its own 256 clips; no collective in the step.
+Workload (config 2 of BASELINE.json, "1 MI355X bf16"): 256 synthetic 32-frame clips per GPU with
+pre-extracted per-frame features (SMPL rotations, betas, 1024-d token, 120-d keypoints) resident in
+HBM.  One step = featurise all windows (HIP) -> HumanActionScorer forward (MFMA) -> per-video AC + TC
+(HIP reductions) -> scores copied to pinned host memory.  ModalityStats and the real-class centroids
+(the real set is sharded over ranks, sufficient statistics all-gathered over RCCL) are built once in
+the setup phase (`setup_s`).  Weak scaling: every rank scores its own 256 clips; no collective in the
+step.  Compute mode: `f16` (VGE_F16: fp16 MFMA conv encoders, 3xfp16 transformer -- the config's 16-bit
+path; its |dAC|, |dTC| vs the oracle over every clip of the step are in `precision`), with the
+f32-class `f32x3` parity mode run on the same workload and reported as `parity_mode`.
 
 Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (the 10 MovementConvEncoders,
-MFMA-bound): achieved = its algorithmic (f32) FLOPs per launch / its average duration from hipEvents
-recorded around it on its stream inside the timed steps; peak = the MFMA ceiling of the compute mode
-(exact f32: 157.3 TF; 3xfp16 split: dense F16 / 3 = 838.9 TF).  `traffic` = HBM bytes per launch from
-the committed PMC pass (profiles/pmc_conv_encoder.json, FETCH_SIZE x2 + WRITE_SIZE per the guide).  `cpu_baseline`
-is the oracle CPU restatement of eval.py (torch-fp32 encoder + numpy featuriser, same work split as
-the reference) timed on this host on a bounded sample of the same workload.
+MFMA-bound): achieved = its algorithmic FLOPs per launch (1.7622 GFLOP per window)
+/ its average duration from hipEvents recorded around it on its stream inside the timed steps; peak =
+the MFMA ceiling of the compute mode (f16: dense F16 2516.6 TF; 3xfp16 split: / 3 = 838.9 TF; exact
+f32: 157.3 TF).  `traffic` = HBM bytes per launch from the committed PMC pass
+(profiles/pmc_conv_encoder.json, FETCH_SIZE x2 + WRITE_SIZE per the guide), reported only when that pass
+was taken on this tree's kernel sources, else null.  `cpu_baseline` is the oracle CPU restatement of
+eval.py in the reference's structure (DataLoader workers=4, bs 32, torch-fp32 on the CPU share) timed on
+this host on a bounded sample before the GPU is touched.  `--workload cfg5` runs config 5 (10k 64-frame
+clips, strong scaling); `tag` config 4's flow; `e2e` config 3.
 """
 from __future__ import annotations
 
@@ -56,8 +61,9 @@ PEAK_BY_COMPUTE = {"f32": (F32_MFMA_PEAK_TFLOPS, "conv_encoder_kernel (10 Moveme
 ARITH = {"f32": "f32 in, f32 accumulate (v_mfma_f32_16x16x4_f32)",
          "f32x3": "f32 operands as fp16 hi + fp16 residual lo (power-of-two scaled per row/window/column), 3 f16 "
                   "MFMAs per product (hi*hi + hi*lo + lo*hi), f32 accumulate",
-         "f16": "operands rounded to fp16 (power-of-two scaled per row/window/column), 1 f16 MFMA per product, f32 "
-                "accumulate and f32 epilogues (throughput mode, not the parity mode)"}
+         "f16": "MovementConvEncoders (85% of the FLOPs): operands rounded to fp16 (power-of-two scaled per "
+                "row/window/column), 1 f16 MFMA per product, f32 accumulate, f32 GELU/GroupNorm epilogues; "
+                "transformer: 3xfp16 split (VGE_F16 default)"}
 HBM_PEAK_GBS = 8000.0
 FEAT_BYTES_PER_WINDOW = 32 * (1024 + 207 + 9 + 10 + 120) * 4 + 32 * 2596 * 4   # read + write
 
@@ -214,6 +220,8 @@ def main():
                     help="f32x3: 3xfp16 split-precision MFMA (f32-class, default of score/tag/e2e); f32: exact f32 "
                          "MFMA; f16: single-fp16 MFMA throughput mode (default of cfg5)")
     ap.add_argument("--chunk", type=int, default=4096, help="cfg5: windows per featurise + encode launch")
+    ap.add_argument("--no-parity-mode", action="store_true",
+                    help="score: skip the second (f32x3) run reported as parity_mode beside an f16 headline")
     ap.add_argument("--serial-extract", action="store_true",
                     help="e2e: run TokenHMR and DWPose one after the other on one stream (default: two streams)")
     ap.add_argument("--no-detector", action="store_true",
@@ -225,7 +233,7 @@ def main():
                          "(default 10000) 64-frame clips sharded over the ranks, f16 MFMA path by default")
     args = ap.parse_args()
     if args.compute is None:
-        args.compute = "f16" if args.workload == "cfg5" else "f32x3"
+        args.compute = "f16" if args.workload in ("cfg5", "score") else "f32x3"
     if args.workload == "cfg5" and args.clips == 256:
         args.clips = 10_000
 
@@ -254,6 +262,15 @@ def main():
             dist.destroy_process_group()
         return
     out = run_score(args, world, rank, dev)
+    if args.workload == "score" and args.compute != "f32x3" and not args.no_parity_mode:
+        # the f32-class parity mode (3xfp16 split) on the same workload, reported beside the headline
+        import copy
+        pa = copy.copy(args)
+        pa.compute, pa.steps, pa.warmup = "f32x3", max(5, args.steps // 2), 2
+        par = run_score(pa, world, rank, dev)
+        if rank == 0:
+            out["parity_mode"] = {k: par[k] for k in ("dtype", "value", "ms_per_step", "steps", "precision",
+                                                      "roofline", "stage_ms")}
     if rank == 0:
         out["cpu_baseline"] = cpu
         print(json.dumps(out))
@@ -376,7 +393,7 @@ def run_score(args, world, rank, dev):
     # precision evidence for the timed mode: the untimed first step's scores vs the oracle on a sample of clips
     ac_a, tc_a = step()
     precision = oracle_precision(gen_clips, stats.mean, stats.std, centroids, vcls, seq, ac_a, tc_a, starts,
-                                 n=16 if cfg5 else 64) if rank == 0 else None
+                                 n=16 if cfg5 else V) if rank == 0 else None
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t_setup
 

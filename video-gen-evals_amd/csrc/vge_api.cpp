@@ -48,7 +48,7 @@ struct GemmArgsX3Host {
   const float* bias; const float* res; int ldr; const float* ln_w; const float* ln_b; const float* pe; const float* cls;
   const float* cs;
 };
-hipError_t launch_conv_encoders_x3(const float*, int, const void*, int, float*, bool, hipStream_t);
+hipError_t launch_conv_encoders_x3(const float*, int, const void*, int, float*, bool, bool, hipStream_t);
 hipError_t launch_gemm_x3(int, const GemmArgsX3Host&, hipStream_t);
 struct FfnArgsX3Host {
   const float* X1; float* out; int M;
@@ -218,6 +218,7 @@ struct vge_encoder {
   void* d_encs = nullptr;         // EncDescHost[10] or EncDescX3Host[10]
   std::vector<vge::TxLayerX3Host> tx_layers;  // x3: the fused transformer kernel's layer table
   bool tx_fused = true;           // x3: one fused transformer launch (VGE_X3_UNFUSED=1: per-layer kernels)
+  int f16_mix = 0;                // VGE_F16: stages kept in 3xfp16 (bit 0 stem, bit 1 transformer; VGE_F16_MIX)
   vge::FuseParamsHost fuse{};
   const void* Wov = nullptr;      // packed (f32 chunks or fp16 chunks)
   const float* Wov_cs = nullptr;  // x3: its column scales
@@ -544,6 +545,10 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
 
   vge_encoder* enc = new vge_encoder();
   enc->mode = compute;
+  if (compute == VGE_F16) {  // default: the transformer keeps the split (most of the f16 error, ~10% of the FLOPs)
+    const char* mx = getenv("VGE_F16_MIX");
+    enc->f16_mix = mx ? atoi(mx) : 2;
+  }
   enc->n_layers = L;
   auto hipfail = [&](hipError_t he) {
     vge_encoder_destroy(enc);
@@ -788,7 +793,7 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
     return vge::launch_gemm(epi, g, s);
   };
   HIPCHK(mark(0));
-  if (x3) HIPCHK(vge::launch_conv_encoders_x3(feats, B, enc->d_encs, 10, enc->enc_out, split, s));
+  if (x3) HIPCHK(vge::launch_conv_encoders_x3(feats, B, enc->d_encs, 10, enc->enc_out, split, enc->f16_mix & 1, s));
   else HIPCHK(vge::launch_conv_encoders(feats, B, enc->d_encs, 10, enc->enc_out, s));
   HIPCHK(mark(1));
   HIPCHK(vge::launch_fuse(enc->enc_out, frames, enc->fuse, enc->pooled, s));
@@ -797,7 +802,7 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
     HIPCHK(mark(3));
     const vge::TxArgsX3Host ta{enc->pooled, B, enc->n_layers, (const _Float16*)enc->Wov, enc->Wov_cs, enc->cls, enc->pe,
                                enc->tx_layers.data(), seq_embed, frame_embed, tc_window};
-    HIPCHK(vge::launch_transformer_x3(ta, split, s));
+    HIPCHK(vge::launch_transformer_x3(ta, split || (enc->f16_mix & 2), s));
     HIPCHK(mark(4));
     HIPCHK(mark(5));
     return VGE_OK;

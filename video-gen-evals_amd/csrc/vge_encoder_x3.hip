@@ -71,7 +71,9 @@ constexpr int conv_lds_bytes() {
 
 // blocks [0, n_quad) take 4 windows, the rest 2: quads stream each weight byte for twice the rows, pairs
 // fill the last round (see launch_conv_encoders_x3)
-template <int W, int CW, bool SP>
+// SP: the 3xfp16 split for the conv blocks and proj; SPS: for the stem (its z-scored inputs carry the widest
+// dynamic range; the f16 mode may keep the stem split)
+template <int W, int CW, bool SP, bool SPS = SP>
 __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feats, int n_windows, int win0,
                                                   const EncDescX3& ed, int e, float* __restrict__ enc_out,
                                                   char* lds_raw, [[maybe_unused]] bool tr_on) {
@@ -181,6 +183,14 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
       if constexpr (SP) f.l[t] = *reinterpret_cast<const half8*>(q + XROWS * XSB);
     }
   };
+  auto afn_stem = [&](int c, AFrag<R>& f) {
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+      const char* q = xa + (t * 32 + i) * XSB + c * 32;
+      f.h[t] = *reinterpret_cast<const half8*>(q);
+      if constexpr (SPS) f.l[t] = *reinterpret_cast<const half8*>(q + XROWS * XSB);
+    }
+  };
 
   STAMP(0);
   // ---------------- stem: Conv1d(d_in -> 256, k=1, no bias), K streamed in 256-wide panels.
@@ -219,7 +229,7 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
 #pragma unroll
         for (int jc = 0; jc < 4; ++jc) {
           const int c = lane + 64 * jc;
-          if constexpr (SP) split_store(Xh + r * XS + c, Xl + r * XS + c, ldexpf(a[jr][jc], -ex));
+          if constexpr (SPS) split_store(Xh + r * XS + c, Xl + r * XS + c, ldexpf(a[jr][jc], -ex));
           else Xh[r * XS + c] = (_Float16)ldexpf(a[jr][jc], -ex);
         }
       }
@@ -237,8 +247,8 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
           for (int n = 0; n < N; ++n) acc.c[t][n][r] *= f;
         }
     }
-    run_stream<CONV_PF, SP>(acc, reinterpret_cast<const char*>(ed.stem) + (size_t)p * 16 * CHUNK_B,
-                        ((kw + 127) >> 7) * STREAM_GROUP, loff, afn_rows);
+    run_stream<CONV_PF, SPS>(acc, reinterpret_cast<const char*>(ed.stem) + (size_t)p * 16 * CHUNK_B,
+                             ((kw + 127) >> 7) * STREAM_GROUP, loff, afn_stem);
     __syncthreads();  // every wave is done reading X
   }
   {
@@ -394,7 +404,7 @@ __device__ __forceinline__ int xcd_remap(int b, int nblk) {
   return (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (b >> 3);
 }
 
-template <bool SP>
+template <bool SP, bool SPS>
 __global__ void __launch_bounds__(512, 1) conv_encoder_x3_kernel(const float* __restrict__ feats,
                                                                   const EncDescX3* __restrict__ encs, ConvSched cs,
                                                                   float* __restrict__ enc_out) {
@@ -409,14 +419,14 @@ __global__ void __launch_bounds__(512, 1) conv_encoder_x3_kernel(const float* __
       const int big = cs.qr * (cs.qa + 1);
       const int e = u < big ? u / (cs.qa + 1) : cs.qr + (u - big) / cs.qa;
       const int j = u < big ? u % (cs.qa + 1) : (u - big) % cs.qa;
-      conv_encoder_body<4, 8, SP>(feats, n, 4 * j, encs[e], e, enc_out, lds_raw, round == VGE_TRACE_ROUND);
+      conv_encoder_body<4, 8, SP, SPS>(feats, n, 4 * j, encs[e], e, enc_out, lds_raw, round == VGE_TRACE_ROUND);
     } else {
       const int v = u - cs.Q;
       const int big = cs.qr * p_big;
       const int e = v < big ? v / p_big : cs.qr + (v - big) / p_small;
       const int j = v < big ? v % p_big : (v - big) % p_small;
       const int q_e = cs.qa + (e < cs.qr);
-      conv_encoder_body<2, 8, SP>(feats, n, 4 * q_e + 2 * j, encs[e], e, enc_out, lds_raw, round == VGE_TRACE_ROUND);
+      conv_encoder_body<2, 8, SP, SPS>(feats, n, 4 * q_e + 2 * j, encs[e], e, enc_out, lds_raw, round == VGE_TRACE_ROUND);
     }
   }
 }
@@ -833,12 +843,13 @@ struct GemmArgsX3Host {
 static_assert(sizeof(GemmArgsX3Host) == sizeof(GemmArgsX3), "GemmArgsX3 layout");
 
 hipError_t encoder_x3_kernel_setup() {
-  hipError_t e = hipFuncSetAttribute((const void*)conv_encoder_x3_kernel<true>,
-                                     hipFuncAttributeMaxDynamicSharedMemorySize, conv_lds_bytes<4, 8>());
-  if (e != hipSuccess) return e;
-  e = hipFuncSetAttribute((const void*)conv_encoder_x3_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                          conv_lds_bytes<4, 8>());
-  if (e != hipSuccess) return e;
+  const void* ck[3] = {(const void*)conv_encoder_x3_kernel<true, true>, (const void*)conv_encoder_x3_kernel<false, true>,
+                       (const void*)conv_encoder_x3_kernel<false, false>};
+  hipError_t e = hipSuccess;
+  for (auto k : ck) {
+    e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, conv_lds_bytes<4, 8>());
+    if (e != hipSuccess) return e;
+  }
   const void* gk[4] = {(const void*)gemm_x3_kernel<EPI_TOKENS, GEMM_RT>, (const void*)gemm_x3_kernel<EPI_BIAS, GEMM_RT>,
                        (const void*)gemm_x3_kernel<EPI_BIAS_RELU, GEMM_RT>,
                        (const void*)gemm_x3_kernel<EPI_BIAS_RES_LN, GEMM_RT>};
@@ -852,8 +863,9 @@ hipError_t encoder_x3_kernel_setup() {
 // Quads (4 windows per block) halve the weight bytes per row; pairs fill the remainder.  With G = min(CUs,
 // units) persistent blocks and m = ceil(pair units / G) per block, Q = G * floor(m / 2) quads (as many as
 // fit) make every block run floor(m / 2) quads and at most one pair.
+// split: 3xfp16 (VGE_F32X3); otherwise single fp16 with the stem split (stem_split) or not
 hipError_t launch_conv_encoders_x3(const float* feats, int n_windows, const void* encs, int n_enc, float* enc_out,
-                                   bool split, hipStream_t s) {
+                                   bool split, bool stem_split, hipStream_t s) {
   static int n_cu = 0;
   if (n_cu == 0) {
     int dev = 0;
@@ -876,12 +888,10 @@ hipError_t launch_conv_encoders_x3(const float* feats, int n_windows, const void
   for (int e = 0; e < n_enc; ++e) pairs += (n_windows - 4 * (cs.qa + (e < cs.qr)) + 1) / 2;
   cs.n_units = Q + pairs;
   cs.G = std::min(n_cu, cs.n_units);
-  if (split)
-    hipLaunchKernelGGL(conv_encoder_x3_kernel<true>, dim3(cs.G), dim3(512), (conv_lds_bytes<4, 8>()), s, feats,
-                       reinterpret_cast<const EncDescX3*>(encs), cs, enc_out);
-  else
-    hipLaunchKernelGGL(conv_encoder_x3_kernel<false>, dim3(cs.G), dim3(512), (conv_lds_bytes<4, 8>()), s, feats,
-                       reinterpret_cast<const EncDescX3*>(encs), cs, enc_out);
+  auto k = split ? conv_encoder_x3_kernel<true, true>
+                 : (stem_split ? conv_encoder_x3_kernel<false, true> : conv_encoder_x3_kernel<false, false>);
+  hipLaunchKernelGGL(k, dim3(cs.G), dim3(512), (conv_lds_bytes<4, 8>()), s, feats,
+                     reinterpret_cast<const EncDescX3*>(encs), cs, enc_out);
   return hipGetLastError();
 }
 

@@ -342,7 +342,7 @@ def main(argv=None):
     ap.add_argument("--save-features", default=None, help="e.g. window_features.pt")
     ap.add_argument("--clip-len", type=int, default=32)
     ap.add_argument("--stride", type=int, default=8)
-    ap.add_argument("--compute", default="f32x3", choices=["f32x3", "f32"])
+    ap.add_argument("--compute", default="f32x3", choices=["f32x3", "f32", "f16"])
     a = ap.parse_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
