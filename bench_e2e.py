@@ -5,10 +5,14 @@ fusion encoder (f32x3) -> AC/TC, per step `--clips` 32-frame clips per GPU.
 
 The reference pipeline is extract_mesh.py (TokenHMR per frame, modifications/mesh_generator.py:119-171) + DWPose
 (modifications/process_video.py) -> npz / keypoints.npy on disk -> eval.py.  Here the frames-to-scores path stays
-in HBM.  DWPose runs as the reference's Wholebody does: YOLOX-L person detector (640x640 letterbox) -> RTMPose-l on
-persons 0 / 1 (the whole frame when nobody is found) -> keypoints.npy rows; `--no-detector` takes the no-detection
-path for every frame instead.  TokenHMR's frames are already person crops (its detectron2 ViTDet gate is upstream
-of the extractor boundary).  Parity for the upstream models is unpinned.
+in HBM and both extractors start from the full frames.  One YOLOX-L person detection per frame (640x640 letterbox)
+serves both: DWPose runs as the reference's Wholebody does (RTMPose-l on persons 0 / 1, the whole frame when nobody
+is found -> keypoints.npy rows), and TokenHMR's front end (mesh_generator.py:101-145; YOLOX-L stands in for its
+detectron2 Faster R-CNN, absent offline) applies the single-person gate (exactly one person > 0.5) and crops every
+frame with ViTDetDataset's warp (vge_hmr_crop).  The gate's decision is computed and reported (`front_end`); a frame
+it rejects is still cropped (whole-frame box) and extracted, so the timed work is the every-frame-valid upper bound
+whatever the random-weight detector finds.  `--no-detector`: whole-frame boxes for both extractors.  Parity for the
+upstream models is unpinned.
 
 Roofline: the backbone GEMM kernel (gemm_bf16_kernel, MFMA bound): achieved = algorithmic FLOPs of every backbone
 GEMM launch / their summed durations (hipEvents recorded around each launch on the extract stream inside the timed
@@ -67,8 +71,9 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
     from vge import ops, synth
     from vge.data import ACTION_CLASSES, pack_frame_store
     from vge.dist import shard
-    from vge.dwpose import RTMPOSE_L, YOLOX_L, DwposeExtractor, Wholebody, YoloxDetector
-    from vge.hmr import TOKENHMR, HmrExtractor
+    from vge.dwpose import RTMPOSE_L, YOLOX_L, DwposeExtractor, YoloxDetector
+    from vge.extract import single_person_mask
+    from vge.hmr import TOKENHMR, HmrExtractor, crop_persons
 
     C, T = args.clips, 32
     F = C * T
@@ -106,7 +111,6 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
     dw = DwposeExtractor(synth.make_rtmpose_state_dict(RTMPOSE_L), RTMPOSE_L, device=dev, max_instances=2 * F)
     det = None if args.no_detector else YoloxDetector(synth.make_yolox_state_dict(YOLOX_L), YOLOX_L, device=dev,
                                                       chunk=min(F, 64))
-    wholebody = Wholebody(det, dw) if det is not None else None
     no_box = np.zeros(F, np.int32)
     frames = torch.from_numpy(synth.make_frames(1000 + rank, F)).to(dev)
     gen_clips = make_clips(synth.SEED_GEN, rank * C, C, T)
@@ -129,26 +133,51 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
     s_hmr, s_pose = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
     concurrent = not getattr(args, "serial_extract", False)
 
-    def keypoints():
-        if wholebody is not None:
-            wholebody(frames, out=gstore.kp)
-        else:
-            dw.keypoints(frames, None, no_box, out=gstore.kp)
+    Hf, Wf = int(frames.shape[1]), int(frames.shape[2])
+    whole = np.tile(np.array([0, 0, Wf, Hf], np.float32), (F, 1))
+    pin_b = torch.empty((F, 2, 4), dtype=torch.float32, pin_memory=True)
+    pin_n = torch.empty((F,), dtype=torch.int32, pin_memory=True)
+    pin_s = torch.empty((F, 2), dtype=torch.float32, pin_memory=True)
+    gate = {"frames": 0, "single_person": 0}
+
+    def detect():
+        """the shared person detection -> host (the pose model's instance table and the TokenHMR gate / crop boxes
+        are built on the host, as the reference's numpy NMS output is)"""
+        if det is None:
+            return None, no_box, whole
+        boxes, npers, scores = det.detect(frames, with_scores=True)
+        pin_b.copy_(boxes, non_blocking=True)
+        pin_n.copy_(npers, non_blocking=True)
+        pin_s.copy_(scores, non_blocking=True)
+        torch.cuda.current_stream(dev).synchronize()
+        hb, hn = pin_b.numpy(), pin_n.numpy()
+        keep = single_person_mask(pin_s.numpy())
+        gate["frames"] += F
+        gate["single_person"] += int(keep.sum())
+        return hb, hn, np.where(keep[:, None], hb[:, 0], whole)
+
+    def hmr(hbox):
+        crops = crop_persons(frames, hbox)
+        ex.extract(crops, out=outs)
+
+    def keypoints(hb, hn):
+        dw.keypoints(frames, hb, hn, out=gstore.kp)
 
     def step():
+        hb, hn, hbox = detect()
         if concurrent:
             cur = torch.cuda.current_stream(dev)
             s_hmr.wait_stream(cur)
             s_pose.wait_stream(cur)
             with torch.cuda.stream(s_hmr):
-                ex.extract(frames, out=outs)
+                hmr(hbox)
             with torch.cuda.stream(s_pose):
-                keypoints()
+                keypoints(hb, hn)
             cur.wait_stream(s_hmr)
             cur.wait_stream(s_pose)
         else:
-            ex.extract(frames, out=outs)
-            keypoints()
+            hmr(hbox)
+            keypoints(hb, hn)
         ops.featurize(gstore, windows, stats.mean, stats.std, out=feats)
         seq, _, tcw = enc.encode(feats, frame_embed=False, tc=True)
         ac, tc = ops.score_videos(seq, tcw, first, vcls, centroids)
@@ -215,8 +244,9 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
         "data": "synthetic 256x256 RGB frames (vge.synth.make_frames); random-init weights of the TokenHMR "
                 "(ViT-H/16 + decoder), YOLOX-L, RTMPose-l whole-body and scorer architectures",
         "config": {"workload": "BASELINE config 3: TokenHMR + DWPose (YOLOX-L + RTMPose-l) extract -> featurise -> "
-                               "encoder -> AC/TC, 32-frame 256x256 clips, frames resident in HBM (TokenHMR frames are "
-                               "person crops)" + (" [--no-detector: whole-frame pose boxes]" if det is None else ""),
+                               "encoder -> AC/TC, 32-frame 256x256 clips, full frames resident in HBM (one YOLOX-L "
+                               "detection per frame for DWPose and TokenHMR's single-person gate; ViTDetDataset crops)"
+                               + (" [--no-detector: whole-frame boxes]" if det is None else ""),
                    "clips_per_gpu": C, "frames_per_step_per_gpu": F,
                    "parallelism": f"video-sharded x{world}"},
         "roofline": {"bound": "mfma", "kernel": "gemm_bf16_kernel (ViT-H/16 backbone: patch-embed, qkv, proj, fc1, "
@@ -230,6 +260,11 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
         "yolox_gemm_tflops": (y_flops / (yst["gemm"] / ycalls * 1e-3) / 1e12) if ycalls else None,
         "dwpose_gemm_tflops": dw_flops / (dst["gemm"] / max(dcalls, 1) * 1e-3) / 1e12,
         "frames_per_s": world * F * args.steps / dt,
+        "front_end": {"detector": "YOLOX-L (stand-in for detectron2 Faster R-CNN X101-FPN)" if det is not None else None,
+                      "gate": "exactly one person box with score > 0.5 (mesh_generator.py:103-111)",
+                      "single_person_fraction": (gate["single_person"] / gate["frames"]) if gate["frames"] else None,
+                      "crop": "ViTDetDataset warp to 256x256 (vge_hmr_crop); gate-rejected frames take the whole "
+                              "frame, so every frame is extracted"},
         "extractors": ("concurrent (TokenHMR and DWPose on two HIP streams; stage_ms / roofline from hipEvents on "
                        "serial steps after the timed region)") if concurrent else "serial",
         "setup_s": setup_s,

@@ -98,6 +98,13 @@ int vge_yolox_destroy(vge_yolox* m);
  * every anchor's decoded box and score (A = 3 * 16^2 * (in_size / 128)^2 ... = 8400 at 640), for tests. */
 int vge_yolox_detect(vge_yolox* m, const uint8_t* frames, int n_frames, int H, int W, float* boxes, int* n_persons,
                      float* cand, vge_stream_t stream);
+/* The same, plus scores: device float [F][2] = the scores of persons 0 and 1 (0 where absent).  The TokenHMR
+ * front end's single-person gate (mesh_generator.py:103-111: exactly one person box with score > 0.5 after NMS)
+ * reads them: since persons 0 / 1 are the first two boxes the greedy NMS keeps, "exactly one box > 0.5" is
+ * scores[f][0] > 0.5 && scores[f][1] <= 0.5.  (The reference's detector there is detectron2's Faster R-CNN
+ * X101-FPN, absent offline; this YOLOX-L is its stand-in: parity unpinned.) */
+int vge_yolox_detect_scored(vge_yolox* m, const uint8_t* frames, int n_frames, int H, int W, float* boxes,
+                            int* n_persons, float* scores, float* cand, vge_stream_t stream);
 /* stage_ms[0] = convolutions (implicit GEMMs), [1] = letterbox / upsample / pooling / decode + NMS */
 int vge_yolox_profile_begin(vge_yolox* m, int max_calls);
 int vge_yolox_profile_read(vge_yolox* m, double* stage_ms, int* n_calls, double* gemm_flops_per_call);

@@ -10,8 +10,8 @@
  *                                     attention decoder -> readouts -> rot6d_to_rotmat)
  *   extract_mesh.py:35-43             the npz arrays pose[T,23,3,3] / global_orient[T,1,3,3] / betas[T,10] /
  *                                     vit[T,1024] (here: rows of the HBM frame store, no npz round trip)
- * The person detector (detectron2 ViTDet, mesh_generator.py:103-117) and the crop warp are upstream of this
- * boundary: frames arrive as 256x256 RGB person crops.  The ViT backbone, pose_transformer and the
+ * The person crop (ViTDetDataset) is vge_hmr_crop below; the person detector of mesh_generator.py:103-117
+ * (detectron2 Faster R-CNN) is stood in for by the YOLOX-L of vge_dwpose.h (vge_yolox_detect_scored).  The ViT backbone, pose_transformer and the
  * TokenHMR tokenizer are third-party code absent from /root/reference (TokenHMR / 4D-Humans at HEAD, no
  * pinned version, no weights offline): their structure is restated from the published models, the
  * token classifier's codebook decoder is a documented stand-in, and parity vs the upstream weights is
@@ -52,6 +52,16 @@ typedef struct vge_hmr vge_hmr;
 int vge_hmr_create(const vge_hmr_config* cfg, const vge_tensor_view* weights, int n_weights, vge_hmr** out);
 int vge_hmr_reserve(vge_hmr* m, int max_frames);
 int vge_hmr_destroy(vge_hmr* m);
+
+/* The TokenHMR front end's crop (ViTDetDataset.__getitem__ in 4D-Humans, driven by mesh_generator.py:119-145):
+ * crop i is the 256 x 256 RGB patch of frame frame_of[i] (frame_of NULL: frame i) around boxes[i] (HOST float
+ * [n_crops][4] xyxy frame pixels -- the single-person box of the frame, after the gate of mesh_generator.py:103-117):
+ * center, 2.5x box scale expanded to the 192:256 aspect, the anti-alias Gaussian when the patch is downsampled by
+ * more than 2.2x, cv2.warpAffine INTER_LINEAR with border 0, rounded to uint8.  frames: device uint8 [n_frames][H][W]
+ * [3] RGB; crops: device uint8 [n_crops][256][256][3], the input of vge_hmr_extract.  Synchronises `stream`
+ * before returning (the host instance table is released).  Parity unpinned (third-party geometry, restated). */
+int vge_hmr_crop(const uint8_t* frames, int n_frames, int H, int W, const float* boxes, const int32_t* frame_of,
+                 int n_crops, uint8_t* crops, vge_stream_t stream);
 
 /* frames: device uint8 [F, in_h, in_w, 3] RGB.  Outputs (device float32, row strides as in the frame store):
  * pose [F,207] (23 rotation matrices, row-major), gori [F,9], betas [F,10], vit [F,dec_dim] (token_out). */

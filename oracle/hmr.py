@@ -143,3 +143,84 @@ class OracleHmr:
     @torch.no_grad()
     def forward(self, frames_u8: np.ndarray):
         return self.head(self.backbone(frames_u8))
+
+
+# ------------------------------------------------------------------------- the TokenHMR front end (crop + gate)
+# ViTDetDataset (4D-Humans hmr2/datasets/vitdet_dataset.py, no pinned version; driven by
+# modifications/mesh_generator.py:119-145) restated: rescale_factor 2.5, BBOX_SHAPE [192, 256], IMAGE_SIZE 256,
+# skimage.filters.gaussian anti-aliasing (mode 'nearest', truncate 4) when the patch is downsampled > 2.2x,
+# generate_image_patch_cv2 -> cv2.warpAffine(INTER_LINEAR, BORDER_CONSTANT 0).  cv2's bilinear is restated in
+# float32 without contraction (the kernel vge_hmr_front.hip runs the same operations), rounded like a uint8 warp.
+
+def expand_to_aspect_ratio(wh, target=(192, 256)):
+    w, h = float(wh[0]), float(wh[1])
+    wt, ht = target
+    if h / w < ht / wt:
+        return np.array([w, max(w * ht / wt, h)])
+    return np.array([max(h * wt / ht, w), h])
+
+
+def vitdet_geometry(box):
+    """box xyxy -> (cx, cy, k = bbox_size / 256, sigma or 0) in ViTDetDataset's float32 / float64 arithmetic."""
+    b = np.asarray(box, np.float32)
+    c = (b[2:4] + b[0:2]) / np.float32(2.0)
+    scale = np.float32(2.5) * (b[2:4] - b[0:2]) / np.float32(200.0)
+    bbox = float(expand_to_aspect_ratio((float(scale[0] * np.float32(200)), float(scale[1] * np.float32(200)))).max())
+    df = bbox / 256.0 / 2.0
+    return float(c[0]), float(c[1]), np.float32(bbox / 256.0), ((df - 1.0) / 2.0 if df > 1.1 else 0.0)
+
+
+def _gauss_nearest(img: np.ndarray, sigma: float) -> np.ndarray:
+    """skimage.filters.gaussian(img, sigma, channel_axis=2, preserve_range=True): separable, mode 'nearest',
+    truncate 4 (scipy.ndimage.gaussian_filter1d's radius int(4 sigma + 0.5)); float32 here."""
+    r = min(8, int(4.0 * sigma + 0.5))
+    t = np.exp(-0.5 * np.arange(r + 1) ** 2 / sigma ** 2)
+    t = (t / (t[0] + 2 * t[1:].sum())).astype(np.float32)
+    x = img.astype(np.float32)
+    H, W = x.shape[:2]
+    out = np.zeros_like(x)
+    for dy in range(-r, r + 1):
+        ry = np.clip(np.arange(H) + dy, 0, H - 1)
+        row = np.zeros_like(x)
+        for dx in range(-r, r + 1):
+            rx = np.clip(np.arange(W) + dx, 0, W - 1)
+            row += t[abs(dx)] * x[ry][:, rx]
+        out += t[abs(dy)] * row
+    return out
+
+
+def vitdet_crop(frame_rgb: np.ndarray, box) -> np.ndarray:
+    """uint8 [H, W, 3] RGB frame + xyxy box -> uint8 [256, 256, 3] RGB patch (ViTDetDataset.__getitem__ before its
+    mean / std normalisation, which patchify applies)."""
+    cx, cy, k, sigma = vitdet_geometry(box)
+    src = _gauss_nearest(frame_rgb, sigma) if sigma > 0 else frame_rgb.astype(np.float32)
+    H, W = frame_rgb.shape[:2]
+    f32 = np.float32
+    u = np.arange(256, dtype=np.float32)
+    sx = f32(cx) + (u - f32(128.0)) * k
+    sy = f32(cy) + (u - f32(128.0)) * k
+    x0 = np.floor(sx)
+    y0 = np.floor(sy)
+    fx = (sx - x0)[None, :]
+    fy = (sy - y0)[:, None]
+    x0 = x0.astype(np.int64)
+    y0 = y0.astype(np.int64)
+    pad = np.zeros((H + 2, W + 2, 3), np.float32)  # BORDER_CONSTANT 0 around the frame
+    pad[1:-1, 1:-1] = src
+
+    def px(yy, xx):
+        yy = np.clip(yy + 1, 0, H + 1)
+        xx = np.clip(xx + 1, 0, W + 1)
+        return pad[yy[:, None], xx[None, :]]
+
+    one = f32(1.0)
+    top = (one - fx)[..., None] * px(y0, x0) + fx[..., None] * px(y0, x0 + 1)
+    bot = (one - fx)[..., None] * px(y0 + 1, x0) + fx[..., None] * px(y0 + 1, x0 + 1)
+    val = (one - fy)[..., None] * top + fy[..., None] * bot
+    return np.rint(np.clip(val, 0, 255)).astype(np.uint8)
+
+
+def single_person_mask(scores: np.ndarray, thresh: float = 0.5) -> np.ndarray:
+    """mesh_generator.py:103-111 on the detector's first two NMS-kept persons: exactly one box with score > 0.5."""
+    s = np.asarray(scores, np.float32).reshape(-1, 2)
+    return (s[:, 0] > thresh) & ~(s[:, 1] > thresh)

@@ -42,7 +42,7 @@ struct DetLevel {      // one YOLOX head level: f32 [n][g*g][8] = reg xywh, obj 
   int grid, stride;
 };
 hipError_t launch_yolox_decode_nms(DetLevel l0, DetLevel l1, DetLevel l2, int F, float ratio, float* boxes, int* n_out,
-                                   float* cand, hipStream_t s);
+                                   float* scores, float* cand, hipStream_t s);
 hipError_t launch_head_sn_t(const float* y, long ldy, int hw, int K, int Kp, float g, long n_rows, void* out,
                             hipStream_t s);
 hipError_t launch_scalenorm_rows(const float* x, int D, float g, long rows, void* y, hipStream_t s);

@@ -22,6 +22,7 @@ struct GemmBf16 {
   int M, N, K;
 };
 hipError_t vit_kernels_setup();
+hipError_t launch_hmr_crop(const uint8_t*, int, int, const float*, const int*, int, uint8_t*, hipStream_t);
 hipError_t launch_gemm_bf16(int, const GemmBf16&, hipStream_t);
 hipError_t launch_ln_bf16(const float*, long, void*, long, const float*, const float*, int, int, float, hipStream_t);
 hipError_t launch_cast_bf16(const float*, long, void*, long, int, int, hipStream_t);
@@ -391,6 +392,21 @@ int vge_hmr_profile_read(vge_hmr* m, double* stage_ms, int* n_calls, double* gem
   }
   *n_calls = m->prof_calls;
   if (gemm_flops_per_call) *gemm_flops_per_call = m->gemm_flops;
+  return VGE_OK;
+}
+
+int vge_hmr_crop(const uint8_t* frames, int n_frames, int H, int W, const float* boxes, const int32_t* frame_of,
+                 int n_crops, uint8_t* crops, vge_stream_t stream) {
+  if (n_crops < 0 || n_frames < 0 || (n_crops > 0 && (!frames || !boxes || !crops || H <= 0 || W <= 0)))
+    return fail(VGE_ERR_ARG, "vge_hmr_crop: bad argument");
+  for (int i = 0; i < n_crops; ++i) {
+    const int f = frame_of ? frame_of[i] : i;
+    const float* b = boxes + 4 * (size_t)i;
+    if (f < 0 || f >= n_frames) return fail(VGE_ERR_ARG, "vge_hmr_crop: frame index out of range");
+    if (!(b[2] > b[0]) || !(b[3] > b[1]) || !std::isfinite(b[0] + b[1] + b[2] + b[3]))
+      return fail(VGE_ERR_ARG, "vge_hmr_crop: empty or non-finite box");
+  }
+  HIPCHK(vge::launch_hmr_crop(frames, H, W, boxes, frame_of, n_crops, crops, S(stream)));
   return VGE_OK;
 }
 

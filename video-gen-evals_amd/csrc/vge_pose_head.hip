@@ -368,7 +368,8 @@ __device__ int block_argmax(const vge::DetLevel& L0, const vge::DetLevel& L1, co
 
 __global__ void __launch_bounds__(256) yolox_decode_nms_kernel(vge::DetLevel L0, vge::DetLevel L1, vge::DetLevel L2,
                                                                float ratio, float* __restrict__ boxes,
-                                                               int* __restrict__ n_out, float* __restrict__ cand) {
+                                                               int* __restrict__ n_out, float* __restrict__ scores,
+                                                               float* __restrict__ cand) {
   __shared__ float s_best[4];
   __shared__ int s_idx[4];
   const int f = blockIdx.x;
@@ -395,6 +396,7 @@ __global__ void __launch_bounds__(256) yolox_decode_nms_kernel(vge::DetLevel L0,
       v = c == 0 ? b.x0 : c == 1 ? b.y0 : c == 2 ? b.x1 : b.y1;
     }
     boxes[(long)f * 8 + threadIdx.x] = v;
+    if (scores && c == 0) scores[(long)f * 2 + p] = ii >= 0 ? det_anchor(L0, L1, L2, f, ii, ratio).score : 0.f;
   }
   if (threadIdx.x == 0) n_out[f] = i0 < 0 ? 0 : (i1 < 0 ? 1 : 2);
 }
@@ -470,9 +472,9 @@ hipError_t launch_simcc_decode(const float* logits, long ld, int WX, int WY, flo
 }
 
 hipError_t launch_yolox_decode_nms(DetLevel l0, DetLevel l1, DetLevel l2, int F, float ratio, float* boxes, int* n_out,
-                                   float* cand, hipStream_t s) {
+                                   float* scores, float* cand, hipStream_t s) {
   if (F == 0) return hipSuccess;
-  hipLaunchKernelGGL(yolox_decode_nms_kernel, dim3(F), dim3(256), 0, s, l0, l1, l2, ratio, boxes, n_out, cand);
+  hipLaunchKernelGGL(yolox_decode_nms_kernel, dim3(F), dim3(256), 0, s, l0, l1, l2, ratio, boxes, n_out, scores, cand);
   return hipGetLastError();
 }
 

@@ -258,6 +258,11 @@ int vge_yolox_profile_read(vge_yolox* m, double* stage_ms, int* n_calls, double*
 
 int vge_yolox_detect(vge_yolox* m, const uint8_t* frames, int F, int H, int W, float* boxes, int* n_persons,
                      float* cand, vge_stream_t stream) {
+  return vge_yolox_detect_scored(m, frames, F, H, W, boxes, n_persons, nullptr, cand, stream);
+}
+
+int vge_yolox_detect_scored(vge_yolox* m, const uint8_t* frames, int F, int H, int W, float* boxes, int* n_persons,
+                            float* scores, float* cand, vge_stream_t stream) {
   if (!m || F < 0 || (F > 0 && (!frames || !boxes || !n_persons || H <= 0 || W <= 0)))
     return fail(VGE_ERR_ARG, "vge_yolox_detect: bad argument");
   if (F == 0) return VGE_OK;
@@ -342,6 +347,7 @@ int vge_yolox_detect(vge_yolox* m, const uint8_t* frames, int F, int H, int W, f
     }
     const vge::DetLevel L0{m->OUT[0], h8, 8}, L1{m->OUT[1], h16, 16}, L2{m->OUT[2], h32, 32};
     OTHER(vge::launch_yolox_decode_nms(L0, L1, L2, n, (float)r, boxes + (size_t)f0 * 8, n_persons + f0,
+                                       scores ? scores + (size_t)f0 * 2 : nullptr,
                                        cand ? cand + (size_t)f0 * A * 5 : nullptr, s));
   }
 #undef OTHER

@@ -170,6 +170,7 @@ def _sig(lib):
         "vge_yolox_reserve": [vp, i32],
         "vge_yolox_destroy": [vp],
         "vge_yolox_detect": [vp, vp, i32, i32, i32, vp, vp, vp, vp],
+        "vge_yolox_detect_scored": [vp, vp, i32, i32, i32, vp, vp, vp, vp, vp],
         "vge_yolox_profile_begin": [vp, i32],
         "vge_yolox_profile_read": [vp, C.POINTER(C.c_double), C.POINTER(C.c_int), C.POINTER(C.c_double)],
     }
@@ -297,18 +298,21 @@ class YoloxDetector:
         S = self.cfg.in_size
         return (S // 8) ** 2 + (S // 16) ** 2 + (S // 32) ** 2
 
-    def detect(self, frames: torch.Tensor, cand: Optional[torch.Tensor] = None):
+    def detect(self, frames: torch.Tensor, cand: Optional[torch.Tensor] = None, with_scores: bool = False):
         """frames uint8 [F, H, W, 3] RGB on the device -> (boxes float [F, 2, 4] xyxy frame pixels of persons 0 and 1,
-        n_persons int32 [F] = min(count, 2)), both on the device (inference_detector's final_boxes, first two)."""
+        n_persons int32 [F] = min(count, 2)), both on the device (inference_detector's final_boxes, first two);
+        with_scores: + scores float [F, 2] of those persons (0 where absent; vge_yolox_detect_scored)."""
         if frames.dtype != torch.uint8 or frames.dim() != 4 or frames.shape[3] != 3:
             raise L.VgeError("frames must be uint8 [F,H,W,3]")
         F_, H_, W_ = (int(v) for v in frames.shape[:3])
         boxes = torch.empty((F_, 2, 4), device=frames.device, dtype=torch.float32)
         npers = torch.empty((F_,), device=frames.device, dtype=torch.int32)
-        L.check(self.lib.vge_yolox_detect(self.h, _ptr(frames), F_, H_, W_, _ptr(boxes), _ptr(npers),
-                                          _ptr(cand) if cand is not None else None, _stream(frames.device)),
+        scores = torch.empty((F_, 2), device=frames.device, dtype=torch.float32) if with_scores else None
+        L.check(self.lib.vge_yolox_detect_scored(self.h, _ptr(frames), F_, H_, W_, _ptr(boxes), _ptr(npers),
+                                                 _ptr(scores) if with_scores else None,
+                                                 _ptr(cand) if cand is not None else None, _stream(frames.device)),
                 "vge_yolox_detect")
-        return boxes, npers
+        return (boxes, npers, scores) if with_scores else (boxes, npers)
 
     def profile_begin(self, max_calls: int) -> None:
         L.check(self.lib.vge_yolox_profile_begin(self.h, int(max_calls)), "vge_yolox_profile_begin")

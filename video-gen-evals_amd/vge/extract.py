@@ -3,6 +3,9 @@
 Mirrors the reference's extraction scripts, minus video decoding (cv2 is not part of this framework: callers pass
 decoded uint8 RGB frames):
 
+  mesh_generator.py:101-145   the TokenHMR front end: person detection, the single-person gate (exactly one person box
+                              with score > 0.5 per frame, >= 80 % of the frames), ViTDetDataset's crop (vge_hmr_crop)
+
   extract_mesh.py:12-43       mesh_info_to_arrays / save_video_npz -- one np.savez_compressed per video with
                               pose / betas / global_orient / vit / frame_idx / meta (JSON string); the file the scorer's
                               npz reader (vge.ingest, utils.py:383-424) consumes
@@ -23,6 +26,7 @@ from typing import Dict, Optional, Sequence, Union
 import numpy as np
 
 SINGLE_PERSON_MIN_FRACTION = 0.8   # mesh_generator.py:116 (len(valid_frames) < 0.8 * len(frames) -> False)
+PERSON_SCORE_THRESH = 0.5          # mesh_generator.py:107 (pred_classes == 0) & (scores > 0.5)
 
 
 def mesh_info_to_arrays(mesh_info: dict):
@@ -57,6 +61,48 @@ def single_person_frames(person_counts: Sequence[int]) -> Optional[np.ndarray]:
     return valid
 
 
+def single_person_mask(scores) -> np.ndarray:
+    """mesh_generator.py:103-111 per frame: exactly one person box with score > 0.5.  `scores` [F, 2] are the scores
+    of the first two boxes the detector's greedy NMS keeps (vge_yolox_detect_scored), so a frame has one such box
+    iff the first is above the threshold and the second is not."""
+    s = np.asarray(scores, np.float32).reshape(-1, 2)
+    return (s[:, 0] > PERSON_SCORE_THRESH) & ~(s[:, 1] > PERSON_SCORE_THRESH)
+
+
+def tokenhmr_front(detector, frames, detections=None):
+    """TokenHMRMeshGenerator.process_video's front end (mesh_generator.py:101-145) on the device: person detection
+    (the YOLOX-L of vge.dwpose standing in for detectron2's Faster R-CNN X101-FPN, absent offline), the per-frame
+    single-person gate, the 80 % rule, and ViTDetDataset's crop of every kept frame.
+    frames: uint8 [F, H, W, 3] RGB on the device; detections: optional (boxes [F,2,4], n_persons [F], scores [F,2])
+    host arrays already computed for these frames.  Returns (kept frame indices, uint8 crops [n, 256, 256, 3] on the
+    device), or None when the reference rejects the video (process_video returns False)."""
+    from .hmr import crop_persons
+    if detections is None:
+        b, _, sc = detector.detect(frames, with_scores=True)
+        boxes, scores = b.cpu().numpy(), sc.cpu().numpy()
+    else:
+        boxes, scores = np.asarray(detections[0]), np.asarray(detections[2])
+    keep = np.flatnonzero(single_person_mask(scores))
+    F = int(frames.shape[0])
+    if keep.size == 0 or keep.size < SINGLE_PERSON_MIN_FRACTION * F:
+        return None
+    return keep, crop_persons(frames, boxes.reshape(F, 2, 4)[keep, 0], keep)
+
+
+def process_video_frames(hmr, detector, frames, detections=None):
+    """TokenHMRMeshGenerator.process_video (mesh_generator.py:91-171) from full frames: front end (detector, gate,
+    crops) then TokenHMR on the kept frames -> {frame_idx: {pose [23,3,3], betas, global_orient [1,3,3], vit}} or
+    False."""
+    front = tokenhmr_front(detector, frames, detections)
+    if front is None:
+        return False
+    idx, crops = front
+    out = {k: v.cpu().numpy() for k, v in hmr.extract(crops).items()}
+    return {int(f): {"pose": out["pose"][j].reshape(23, 3, 3), "betas": out["betas"][j],
+                     "global_orient": out["global_orient"][j].reshape(1, 3, 3), "vit": out["vit"][j]}
+            for j, f in enumerate(idx)}
+
+
 def process_video(hmr, crops, person_counts: Optional[Sequence[int]] = None):
     """MeshGenerator.process_video: TokenHMR on the single-person frames' crops -> mesh_info {frame_idx: {...}}, or
     False for a rejected video.  crops: uint8 [F, 256, 256, 3] RGB person crops on the device (one per frame; the
@@ -89,11 +135,16 @@ def save_keypoints(rows: np.ndarray, root: Union[str, Path], action: str, vid_id
 
 
 def extract_video(hmr, wholebody, frames, crops, action: str, video: str, mesh_root, kp_root,
-                  person_counts: Optional[Sequence[int]] = None, source_path: str = "") -> Dict[str, Optional[str]]:
+                  person_counts: Optional[Sequence[int]] = None, source_path: str = "",
+                  detector=None) -> Dict[str, Optional[str]]:
     """One video of extract_mesh.py:main + process_video.py: npz (or None when the single-person gate rejects the
-    video, the reference's not-single list) and keypoints.npy paths."""
+    video, the reference's not-single list) and keypoints.npy paths.  crops None: the TokenHMR front end runs on the
+    full frames with `detector` (process_video_frames); otherwise crops are ready-made person crops."""
     stem = Path(video).stem
-    mesh_info = process_video(hmr, crops, person_counts)
+    if crops is None:
+        mesh_info = process_video_frames(hmr, detector if detector is not None else wholebody.det, frames)
+    else:
+        mesh_info = process_video(hmr, crops, person_counts)
     npz = None
     if mesh_info:
         npz = save_video_npz(str(Path(action) / stem), mesh_info, out_root=mesh_root,

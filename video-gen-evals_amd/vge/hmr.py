@@ -67,6 +67,7 @@ def _sig(lib):
         "vge_op_gemm_bf16": [i32, vp, C.c_long, vp, C.c_long, vp, C.c_long, vp, vp, C.c_long, vp, i32, i32, i32, i32,
                              vp],
         "vge_op_vit_attention": [vp, vp, i32, i32, i32, vp],
+        "vge_hmr_crop": [vp, i32, i32, i32, vp, vp, i32, vp, vp],
         "vge_op_layernorm_bf16": [vp, vp, vp, vp, i32, i32, C.c_float, vp],
     }
     for name, args in sig.items():
@@ -193,3 +194,23 @@ def layernorm_bf16(x: torch.Tensor, w: torch.Tensor, b: torch.Tensor, eps: float
     L.check(lib.vge_op_layernorm_bf16(_ptr(x), _ptr(out), _ptr(w), _ptr(b), rows, D, eps, _stream(x.device)),
             "vge_op_layernorm_bf16")
     return out
+
+
+def crop_persons(frames: torch.Tensor, boxes, frame_of=None) -> torch.Tensor:
+    """ViTDetDataset's person crop (mesh_generator.py:119-145; vge_hmr_crop): frames uint8 [F, H, W, 3] RGB on the
+    device, boxes host float [n, 4] xyxy, frame_of host int [n] (None: crop i from frame i) -> uint8 [n, 256, 256, 3]
+    device crops, the input of HmrExtractor.extract."""
+    lib = _sig(L.load())
+    if frames.dtype != torch.uint8 or frames.dim() != 4 or frames.shape[3] != 3:
+        raise L.VgeError("frames must be uint8 [F,H,W,3]")
+    b = np.ascontiguousarray(np.asarray(boxes, np.float32).reshape(-1, 4))
+    n = b.shape[0]
+    fo = None if frame_of is None else np.ascontiguousarray(np.asarray(frame_of, np.int32).reshape(-1))
+    if fo is not None and fo.shape[0] != n:
+        raise L.VgeError("frame_of must have one entry per box")
+    out = torch.empty((n, 256, 256, 3), dtype=torch.uint8, device=frames.device)
+    F_, H_, W_ = (int(v) for v in frames.shape[:3])
+    L.check(lib.vge_hmr_crop(_ptr(frames), F_, H_, W_, b.ctypes.data, None if fo is None else fo.ctypes.data, n,
+                             _ptr(out), _stream(frames.device)), "vge_hmr_crop")
+    return out
+

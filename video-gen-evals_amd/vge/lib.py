@@ -23,7 +23,8 @@ EXPORTS = ["vge_featurize", "vge_stats_workspace_bytes", "vge_stats_accumulate",
            "vge_hmr_profile_read", "vge_op_gemm_bf16", "vge_op_vit_attention", "vge_op_layernorm_bf16",
            "vge_dwpose_create", "vge_dwpose_reserve", "vge_dwpose_destroy", "vge_dwpose_keypoints",
            "vge_dwpose_profile_begin", "vge_dwpose_profile_read", "vge_op_conv_bf16",
-           "vge_yolox_create", "vge_yolox_reserve", "vge_yolox_destroy", "vge_yolox_detect",
+           "vge_yolox_create", "vge_yolox_reserve", "vge_yolox_destroy", "vge_yolox_detect", "vge_yolox_detect_scored",
+           "vge_hmr_crop",
            "vge_yolox_profile_begin", "vge_yolox_profile_read"]
 
 
