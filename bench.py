@@ -220,6 +220,7 @@ def main():
                     help="f32x3: 3xfp16 split-precision MFMA (f32-class, default of score/tag/e2e); f32: exact f32 "
                          "MFMA; f16: single-fp16 MFMA throughput mode (default of cfg5)")
     ap.add_argument("--chunk", type=int, default=4096, help="cfg5: windows per featurise + encode launch")
+    ap.add_argument("--chunk-clips", type=int, default=32, help="e2e: clips per extraction pass (frames in HBM)")
     ap.add_argument("--no-parity-mode", action="store_true",
                     help="score: skip the second (f32x3) run reported as parity_mode beside an f16 headline")
     ap.add_argument("--serial-extract", action="store_true",

@@ -77,6 +77,7 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
 
     C, T = args.clips, 32
     F = C * T
+    FC = min(F, max(1, getattr(args, "chunk_clips", 32)) * T)   # frames per extraction pass
     t_setup = time.perf_counter()
     # scoring model, stats and centroids from the (sharded) pre-extracted real set, as in config 2
     n_real_per_class, T_real = 8, 64
@@ -106,13 +107,21 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
     # extractors + generated clips: frames resident in HBM; the frame store's SMPL / token arrays (TokenHMR) and
     # keypoint rows (DWPose, whole-frame boxes) are written by the extractors every step
     hsd = synth.make_hmr_state_dict(TOKENHMR)
-    ex = HmrExtractor(hsd, TOKENHMR, device=dev, max_frames=F)
+    ex = HmrExtractor(hsd, TOKENHMR, device=dev, max_frames=FC)
     del hsd
-    dw = DwposeExtractor(synth.make_rtmpose_state_dict(RTMPOSE_L), RTMPOSE_L, device=dev, max_instances=2 * F)
+    dw = DwposeExtractor(synth.make_rtmpose_state_dict(RTMPOSE_L), RTMPOSE_L, device=dev, max_instances=2 * FC)
     det = None if args.no_detector else YoloxDetector(synth.make_yolox_state_dict(YOLOX_L), YOLOX_L, device=dev,
-                                                      chunk=min(F, 64))
-    no_box = np.zeros(F, np.int32)
-    frames = torch.from_numpy(synth.make_frames(1000 + rank, F)).to(dev)
+                                                      chunk=min(FC, 64))
+    no_box = np.zeros(FC, np.int32)
+    base = torch.from_numpy(synth.make_frames(1000 + rank, FC)).to(dev)
+    if F == FC:
+        frames = base
+    else:  # distinct frames for every pass, derived on the device from one pass's worth of generated frames
+        frames = torch.empty((F,) + tuple(base.shape[1:]), dtype=torch.uint8, device=dev)
+        for f0 in range(0, F, FC):
+            n = min(FC, F - f0)
+            frames[f0:f0 + n] = ((base[:n].to(torch.int16) + (f0 // FC) * 37) % 256).to(torch.uint8)
+        del base
     gen_clips = make_clips(synth.SEED_GEN, rank * C, C, T)
     names = [synth.generated_name(rank * C + i) for i in range(C)]
     gstore = ops.DeviceFrameStore.from_host(pack_frame_store(gen_clips, names, ["X"] * C), dev)
@@ -134,50 +143,53 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
     concurrent = not getattr(args, "serial_extract", False)
 
     Hf, Wf = int(frames.shape[1]), int(frames.shape[2])
-    whole = np.tile(np.array([0, 0, Wf, Hf], np.float32), (F, 1))
-    pin_b = torch.empty((F, 2, 4), dtype=torch.float32, pin_memory=True)
-    pin_n = torch.empty((F,), dtype=torch.int32, pin_memory=True)
-    pin_s = torch.empty((F, 2), dtype=torch.float32, pin_memory=True)
+    whole = np.tile(np.array([0, 0, Wf, Hf], np.float32), (FC, 1))
+    pin_b = torch.empty((FC, 2, 4), dtype=torch.float32, pin_memory=True)
+    pin_n = torch.empty((FC,), dtype=torch.int32, pin_memory=True)
+    pin_s = torch.empty((FC, 2), dtype=torch.float32, pin_memory=True)
     gate = {"frames": 0, "single_person": 0}
 
-    def detect():
+    def detect(fr):
         """the shared person detection -> host (the pose model's instance table and the TokenHMR gate / crop boxes
         are built on the host, as the reference's numpy NMS output is)"""
+        n = int(fr.shape[0])
         if det is None:
-            return None, no_box, whole
-        boxes, npers, scores = det.detect(frames, with_scores=True)
-        pin_b.copy_(boxes, non_blocking=True)
-        pin_n.copy_(npers, non_blocking=True)
-        pin_s.copy_(scores, non_blocking=True)
+            return None, no_box[:n], whole[:n]
+        boxes, npers, scores = det.detect(fr, with_scores=True)
+        pin_b[:n].copy_(boxes, non_blocking=True)
+        pin_n[:n].copy_(npers, non_blocking=True)
+        pin_s[:n].copy_(scores, non_blocking=True)
         torch.cuda.current_stream(dev).synchronize()
-        hb, hn = pin_b.numpy(), pin_n.numpy()
-        keep = single_person_mask(pin_s.numpy())
-        gate["frames"] += F
+        hb, hn = pin_b[:n].numpy(), pin_n[:n].numpy()
+        keep = single_person_mask(pin_s[:n].numpy())
+        gate["frames"] += n
         gate["single_person"] += int(keep.sum())
-        return hb, hn, np.where(keep[:, None], hb[:, 0], whole)
+        return hb, hn, np.where(keep[:, None], hb[:, 0], whole[:n])
 
-    def hmr(hbox):
-        crops = crop_persons(frames, hbox)
-        ex.extract(crops, out=outs)
+    def hmr(fr, hbox, f0):
+        crops = crop_persons(fr, hbox)
+        ex.extract(crops, out={k: v[f0:f0 + int(fr.shape[0])] for k, v in outs.items()})
 
-    def keypoints(hb, hn):
-        dw.keypoints(frames, hb, hn, out=gstore.kp)
+    def keypoints(fr, hb, hn, f0):
+        dw.keypoints(fr, hb, hn, out=gstore.kp[f0:f0 + int(fr.shape[0])])
 
     def step():
-        hb, hn, hbox = detect()
-        if concurrent:
-            cur = torch.cuda.current_stream(dev)
-            s_hmr.wait_stream(cur)
-            s_pose.wait_stream(cur)
-            with torch.cuda.stream(s_hmr):
-                hmr(hbox)
-            with torch.cuda.stream(s_pose):
-                keypoints(hb, hn)
-            cur.wait_stream(s_hmr)
-            cur.wait_stream(s_pose)
-        else:
-            hmr(hbox)
-            keypoints(hb, hn)
+        for f0 in range(0, F, FC):
+            fr = frames[f0:f0 + FC]
+            hb, hn, hbox = detect(fr)
+            if concurrent:
+                cur = torch.cuda.current_stream(dev)
+                s_hmr.wait_stream(cur)
+                s_pose.wait_stream(cur)
+                with torch.cuda.stream(s_hmr):
+                    hmr(fr, hbox, f0)
+                with torch.cuda.stream(s_pose):
+                    keypoints(fr, hb, hn, f0)
+                cur.wait_stream(s_hmr)
+                cur.wait_stream(s_pose)
+            else:
+                hmr(fr, hbox, f0)
+                keypoints(fr, hb, hn, f0)
         ops.featurize(gstore, windows, stats.mean, stats.std, out=feats)
         seq, _, tcw = enc.encode(feats, frame_embed=False, tc=True)
         ac, tc = ops.score_videos(seq, tcw, first, vcls, centroids)
@@ -189,12 +201,13 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
     torch.cuda.synchronize()
     # per-kernel hipEvents inside concurrent streams would time shared GPU wall time, so with concurrent extractors
     # the stage / roofline events are recorded on serial steps right after the timed region instead
-    prof_steps = args.steps
+    n_chunks = -(-F // FC)
+    prof_steps = args.steps if n_chunks == 1 else 1   # large runs: one serial profiled step
     if not concurrent:
-        ex.profile_begin(prof_steps)
-        dw.profile_begin(prof_steps)
+        ex.profile_begin(prof_steps * n_chunks)
+        dw.profile_begin(prof_steps * n_chunks)
         if det is not None:
-            det.profile_begin(prof_steps)
+            det.profile_begin(prof_steps * n_chunks)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -211,10 +224,10 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
     dt = float(dt_t.item())
     if concurrent:
-        ex.profile_begin(prof_steps)
-        dw.profile_begin(prof_steps)
+        ex.profile_begin(prof_steps * n_chunks)
+        dw.profile_begin(prof_steps * n_chunks)
         if det is not None:
-            det.profile_begin(prof_steps)
+            det.profile_begin(prof_steps * n_chunks)
         concurrent = False
         for _ in range(prof_steps):
             step()
@@ -228,7 +241,7 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
         return None
     n = max(ncalls, 1)
     gemm_ms = st["gemm"] / n
-    achieved = gemm_flops_per_frame * F / (gemm_ms * 1e-3) / 1e12
+    achieved = gemm_flops_per_frame * FC / (gemm_ms * 1e-3) / 1e12
     out = {
         "metric": metric,
         "value": world * C * args.steps / dt,
@@ -247,13 +260,13 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
                                "encoder -> AC/TC, 32-frame 256x256 clips, full frames resident in HBM (one YOLOX-L "
                                "detection per frame for DWPose and TokenHMR's single-person gate; ViTDetDataset crops)"
                                + (" [--no-detector: whole-frame boxes]" if det is None else ""),
-                   "clips_per_gpu": C, "frames_per_step_per_gpu": F,
+                   "clips_per_gpu": C, "frames_per_step_per_gpu": F, "frames_per_extraction_pass": FC,
                    "parallelism": f"video-sharded x{world}"},
         "roofline": {"bound": "mfma", "kernel": "gemm_bf16_kernel (ViT-H/16 backbone: patch-embed, qkv, proj, fc1, "
                                                 "fc2; dense bf16 MFMA peak)",
                      "achieved": achieved, "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / BF16_MFMA_PEAK_TFLOPS, "traffic": None,
-                     "flop_per_call": gemm_flops_per_frame * F, "gemm_ms_per_call": gemm_ms},
+                     "flop_per_call": gemm_flops_per_frame * FC, "gemm_ms_per_call": gemm_ms},
         "stage_ms": {**{f"hmr_{k}": v / n for k, v in st.items()},
                      **{f"dwpose_{k}": v / max(dcalls, 1) for k, v in dst.items()},
                      **{f"yolox_{k}": v / max(ycalls, 1) for k, v in yst.items()}},
