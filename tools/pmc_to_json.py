@@ -17,6 +17,8 @@ import shutil
 from pathlib import Path
 
 ROOT = Path(__file__).resolve().parent.parent
+import sys  # noqa: E402
+sys.path.insert(0, str(ROOT))
 ap = argparse.ArgumentParser()
 ap.add_argument("tag")
 ap.add_argument("compute")
@@ -24,7 +26,8 @@ ap.add_argument("--windows", type=int, default=256)
 ap.add_argument("--last", type=int, default=6)
 a = ap.parse_args()
 out_dir = ROOT / "gpurun_out"
-KNAME = {"f32x3": "conv_encoder_x3_kernel", "f32": "conv_encoder_kernel("}[a.compute]
+KNAME = {"f32x3": "conv_encoder_x3_kernel<true", "f16": "conv_encoder_x3_kernel<false",
+         "f32": "conv_encoder_kernel("}[a.compute]
 
 
 def rows(kind):
@@ -58,7 +61,7 @@ for f in glob.glob(str(out_dir / f"prof_{a.tag}_trace" / "**" / "*kernel_trace.c
     tr += [int(r["End_Timestamp"]) - int(r["Start_Timestamp"]) for r in rs[-a.last:]]
 hbm = fetch["FETCH_SIZE"] * 1024 * 2 + write["WRITE_SIZE"] * 1024
 res = {
-    "kernel": KNAME.rstrip("("), "windows_per_launch": a.windows, "dispatches": {"fetch": nf, "write": nw},
+    "kernel": KNAME.rstrip("("), "source_sha": __import__("bench")._kernel_sources_sha(), "windows_per_launch": a.windows, "dispatches": {"fetch": nf, "write": nw},
     "fetch_size_kb_raw": fetch["FETCH_SIZE"], "write_size_kb": write["WRITE_SIZE"],
     "hbm_bytes_per_launch": hbm, "hbm_bytes_per_window": hbm / a.windows,
     "l2_hit_rate": l2["TCC_HIT_sum"] / (l2["TCC_HIT_sum"] + l2["TCC_MISS_sum"]) if l2 else None,

@@ -5,12 +5,12 @@
 # Writes gpurun_out/prof_TAG_{trace,fetch,write,sq,l2}/ ; summarise with tools/pmc_to_json.py.
 set -u
 TAG=$1
-COMPUTE=${2:-f32x3}
+COMPUTE=${2:-f16}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-BENCH="$R/bench.py --steps 6 --warmup 2 --no-cpu-baseline --compute $COMPUTE"
+BENCH="$R/bench.py --steps 6 --warmup 2 --no-cpu-baseline --no-parity-mode --compute $COMPUTE"
 run() {  # name, extra rocprofv3 args...
   local name=$1; shift
   timeout -k 10 300 rocprofv3 "$@" --output-format csv -d "$OUT/prof_${TAG}_$name" -o run -- python3 $BENCH \
