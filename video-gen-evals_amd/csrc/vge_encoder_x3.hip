@@ -247,7 +247,7 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
           for (int n = 0; n < N; ++n) acc.c[t][n][r] *= f;
         }
     }
-    run_stream<CONV_PF, SPS>(acc, reinterpret_cast<const char*>(ed.stem) + (size_t)p * 16 * CHUNK_B,
+    run_stream<SPS ? CONV_PF : CONV_PF16, SPS>(acc, reinterpret_cast<const char*>(ed.stem) + (size_t)p * 16 * CHUNK_B,
                              ((kw + 127) >> 7) * STREAM_GROUP, loff, afn_stem);
     __syncthreads();  // every wave is done reading X
   }
@@ -285,7 +285,7 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
           if constexpr (SP) f.l[t] = *reinterpret_cast<const half8*>(q + XROWS * XSB);
         }
       };
-      run_stream<CONV_PF, SP>(acc, reinterpret_cast<const char*>(ed.conv) + (size_t)(blk * 2 + cv) * 5 * 16 * CHUNK_B,
+      run_stream<SP ? CONV_PF : CONV_PF16, SP>(acc, reinterpret_cast<const char*>(ed.conv) + (size_t)(blk * 2 + cv) * 5 * 16 * CHUNK_B,
                           5 * 16, loff, afn);
       STAMP(4 + (blk * 2 + cv) * 2);
       // epilogue in packed f32 (v_pk_fma_f32: two rows per instruction), in place:
@@ -369,7 +369,7 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
 
   // ---------------- proj: Linear(256 -> 256, no bias)
   acc.zero();
-  run_stream<CONV_PF, SP>(acc, reinterpret_cast<const char*>(ed.proj), 16, loff, afn_rows);
+  run_stream<SP ? CONV_PF : CONV_PF16, SP>(acc, reinterpret_cast<const char*>(ed.proj), 16, loff, afn_rows);
   STAMP(20);
 #pragma unroll
   for (int t = 0; t < R; ++t) {

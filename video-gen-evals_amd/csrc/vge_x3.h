@@ -21,6 +21,10 @@ constexpr int CHUNK_B = 16384;       // bytes per weight chunk
 constexpr int PLANE_B = 8192;        // bytes between the hi and lo planes of a chunk
 constexpr int STREAM_GROUP = 8;      // weight streams are packed as multiples of 8 chunks
 constexpr int CONV_PF = 4;           // weight chunks in flight per wave: conv (a quad wave holds 128 x 64 outputs)
+#ifndef VGE_CONV_PF16
+#define VGE_CONV_PF16 8
+#endif
+constexpr int CONV_PF16 = VGE_CONV_PF16;  // ... in the single-fp16 mode (half the bytes per chunk)
 constexpr int GEMM_PF = 4;           // ... and GEMM waves (32 x 32 outputs, 4 waves per SIMD)
 
 __device__ __forceinline__ floatx16 mfma32(half8 a, half8 b, floatx16 c) {
