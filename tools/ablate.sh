@@ -11,7 +11,7 @@ HIPCC="/opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950"
 link() {
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$1/libvge.so" "${FEAT:-build/vge_featurize.o}" \
     build/vge_encoder.o "$1/x3.o" "$1/tx.o" build/vge_score.o build/vge_api.o build/vge_ingest.o build/vge_vit.o \
-    build/vge_cnn.o build/vge_pose_head.o build/vge_hmr.o build/vge_dwpose.o build/vge_yolox.o -lz -lpthread
+    build/vge_cnn.o build/vge_pose_head.o build/vge_hmr.o build/vge_hmr_front.o build/vge_dwpose.o build/vge_yolox.o -lz -lpthread
 }
 for v in "$@"; do
   mkdir -p build/abl$v

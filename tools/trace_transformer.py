@@ -24,10 +24,11 @@ from vge import lib, ops, synth  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--windows", type=int, default=256)
+ap.add_argument("--compute", default="f32x3")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 sd = synth.make_state_dict(synth.DIMS_RAW, synth.DIMS_DIFF)
-enc = ops.Encoder(sd, device=dev, compute="f32x3")
+enc = ops.Encoder(sd, device=dev, compute=a.compute)
 x = torch.randn(a.windows, 32, 2596, device=dev)
 enc.reserve(a.windows)
 for _ in range(3):

@@ -5,8 +5,8 @@
 //                          counts.index_add_, as a deterministic segmented reduction: the windows are cut into
 //                          segments of CENT_SEG (a function of n only); one workgroup per (segment, 64 columns,
 //                          block of 64 classes) walks its windows in order, lane j owning column j of every
-//                          class row in LDS (no atomics, no races), then the segment partials are added in a
-//                          fixed order.  Same result for any grid / device; the order
+//                          class row in LDS (runs of one class summed in a register first; no atomics, no
+//                          races), then the segment partials are added in a fixed order.  Same result for any grid / device; the order
 //                          of the f32 additions differs from a sequential index_add_ only by the segment
 //                          split (a few ulps of the sums, far inside the 2e-5 centroid tolerance).
 //                          HBM-bound: reads n x d x 4 B + 4n B once.
@@ -24,8 +24,11 @@ constexpr int CENT_SEG = 512;     // windows per segment (a function of nothing 
 constexpr int CENT_CB = 64;       // classes per workgroup
 
 // grid (n_seg, ceil(d / 64), ceil(C / 64)), 4 waves; lane = column (64 per workgroup).  Wave q walks windows
-// [q SEG/4, (q+1) SEG/4) of the segment in order into its own LDS rows, then the 4 wave partials are added in
-// wave order.  part [n_seg][C][d], pcnt [n_seg][C].
+// [q SEG/4, (q+1) SEG/4) of the segment in order: consecutive windows of one class (real-set windows come grouped by
+// video and class) are summed in a register and flushed to the wave's own LDS row when the class changes; rows are
+// loaded 32 ahead (one memory round trip per 32 windows).  Then the 4 wave partials are added in wave order.
+// part [n_seg][C][d], pcnt [n_seg][C].
+constexpr int CENT_QW = CENT_SEG / 4, CENT_B = 32;
 __global__ void __launch_bounds__(256) centroid_partial_kernel(const float* __restrict__ seq,
                                                                const int* __restrict__ cls, int n, int C, int d,
                                                                float* __restrict__ part, float* __restrict__ pcnt) {
@@ -36,23 +39,53 @@ __global__ void __launch_bounds__(256) centroid_partial_kernel(const float* __re
   const int nc = min(CENT_CB, C - c0);
   for (int c = 0; c < nc; ++c) acc[q][c][lane] = 0.f;
   if (lane < nc) cnt[q][lane] = 0.f;
-  constexpr int QW = CENT_SEG / 4;
-  const int w0 = seg * CENT_SEG + q * QW, w1 = min(n, w0 + QW);
-  // rows in batches of 8: the batch's loads are issued together, the adds follow in window order
-  for (int w = w0; w < w1; w += 8) {
-    float x[8];
-    int y[8];
+  const int w0 = seg * CENT_SEG + q * CENT_QW, w1 = min(n, w0 + CENT_QW);
+  // the wave's 128 class ids, two per lane; read back as scalars with v_readlane (no LDS round trip per window)
+  int yv[CENT_QW / 64];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      y[k] = (w + k < w1) ? cls[w + k] - c0 : -1;
-      x[k] = (w + k < w1 && j < d) ? seq[(size_t)(w + k) * d + j] : 0.f;
-    }
+  for (int h = 0; h < CENT_QW / 64; ++h) {
+    const int k = h * 64 + lane;
+    const int y = (w0 + k < w1) ? cls[w0 + k] - c0 : -1;
+    yv[h] = (unsigned)y < (unsigned)nc ? y : -1;
+  }
+  __syncthreads();  // the zeroed LDS rows
+  float run = 0.f, rcnt = 0.f;
+  int cur = -1;
+  auto load = [&](int b, float (&x)[CENT_B]) {
 #pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if ((unsigned)y[k] < (unsigned)nc) {  // uniform over the wave
-        acc[q][y[k]][lane] += x[k];
-        if (lane == 0) cnt[q][y[k]] += 1.0f;
+    for (int k = 0; k < CENT_B; ++k)
+      x[k] = (w0 + b + k < w1 && j < d) ? seq[(size_t)(w0 + b + k) * d + j] : 0.f;
+  };
+  float xa[CENT_B], xb[CENT_B];
+  load(0, xa);
+#pragma unroll
+  for (int b = 0; b < CENT_QW; b += 2 * CENT_B) {
+    load(b + CENT_B, xb);  // rows past the segment read as 0 and carry class -1
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float (&x)[CENT_B] = h ? xb : xa;
+      const int bb = b + h * CENT_B;
+      if (h == 1 && bb + CENT_B < CENT_QW) load(bb + CENT_B, xa);
+#pragma unroll
+      for (int k = 0; k < CENT_B; ++k) {
+        const int y = __builtin_amdgcn_readlane(yv[(bb + k) >> 6], (bb + k) & 63);
+        if (y != cur) {  // uniform: flush the finished run of class `cur`
+          if (cur >= 0) {
+            acc[q][cur][lane] += run;
+            if (lane == 0) cnt[q][cur] += rcnt;
+          }
+          run = 0.f;
+          rcnt = 0.f;
+          cur = y;
+        }
+        run += x[k];
+        rcnt += 1.0f;
       }
+    }
+  }
+  if (cur >= 0) {
+    acc[q][cur][lane] += run;
+    if (lane == 0) cnt[q][cur] += rcnt;
   }
   __syncthreads();
   for (int c = q; c < nc; c += 4)
