@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Precision / time of the f16 throughput mode per stage kept in 3xfp16 (VGE_F16_MIX bits: 1 stem, 2 transformer)
+"""Precision / time of the f16 throughput mode per stage kept in 3xfp16 (VGE_F16_MIX bits: 1 stem, 2 transformer split, 4 transformer activations split)
 against the oracle on bench.py's config-2 clips (256 windows, bench-like stats and centroids).
 
     python tools/f16_precision.py [--n 256]
@@ -29,7 +29,7 @@ feats = torch.from_numpy(o["feats"]).to(dev)
 first = torch.arange(a.n + 1, dtype=torch.int32, device=dev)
 vcls = o["vcls"].to(torch.int32).to(dev)
 cent = o["cent"].to(dev)
-for compute, mix in (("f32x3", 0), ("f16", 0), ("f16", 1), ("f16", 2), ("f16", 3)):
+for compute, mix in (("f32x3", 0), ("f16", 0), ("f16", 2), ("f16", 4), ("f16", 5), ("f16", 3)):
     os.environ["VGE_F16_MIX"] = str(mix)
     enc = ops.Encoder(o["sd"], device=dev, compute=compute)
     enc.reserve(a.n)

@@ -74,7 +74,7 @@ struct TxArgsX3Host {
   float* seq; float* frame; float* tc;
 };
 hipError_t transformer_x3_kernel_setup();
-hipError_t launch_transformer_x3(const TxArgsX3Host&, bool, hipStream_t);
+hipError_t launch_transformer_x3(const TxArgsX3Host&, int, hipStream_t);
 hipError_t launch_conv_encoders(const float*, int, const void*, int, float*, hipStream_t);
 hipError_t launch_fuse(const float*, int, const FuseParamsHost&, float*, hipStream_t);
 hipError_t launch_gemm(int, const GemmArgsHost&, hipStream_t);
@@ -802,7 +802,7 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
     HIPCHK(mark(3));
     const vge::TxArgsX3Host ta{enc->pooled, B, enc->n_layers, (const _Float16*)enc->Wov, enc->Wov_cs, enc->cls, enc->pe,
                                enc->tx_layers.data(), seq_embed, frame_embed, tc_window};
-    HIPCHK(vge::launch_transformer_x3(ta, split || (enc->f16_mix & 2), s));
+    HIPCHK(vge::launch_transformer_x3(ta, (split || (enc->f16_mix & 2)) ? 2 : ((enc->f16_mix & 4) ? 1 : 0), s));
     HIPCHK(mark(4));
     HIPCHK(mark(5));
     return VGE_OK;

@@ -72,15 +72,18 @@ struct AFragT {  // one chunk's A operand: the 32 frame rows (MFMA) and the CLS 
 };
 
 // CLS row on the VALU: c += x . w over this lane's 8 k of the chunk, the same 3 products as the MFMAs
-template <bool SP>
+template <bool SPA, bool SPW>
 __device__ __forceinline__ float cls_dot(float c, half8 xh, half8 xl, half8 wh, half8 wl) {
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
     const half2v a = {xh[2 * p], xh[2 * p + 1]};
     const half2v b = {wh[2 * p], wh[2 * p + 1]};
-    if constexpr (SP) {
-      const half2v al = {xl[2 * p], xl[2 * p + 1]}, bl = {wl[2 * p], wl[2 * p + 1]};
+    if constexpr (SPA) {
+      const half2v al = {xl[2 * p], xl[2 * p + 1]};
       c = __builtin_amdgcn_fdot2(al, b, c, false);
+    }
+    if constexpr (SPW) {
+      const half2v bl = {wl[2 * p], wl[2 * p + 1]};
       c = __builtin_amdgcn_fdot2(a, bl, c, false);
     }
     c = __builtin_amdgcn_fdot2(a, b, c, false);
@@ -88,8 +91,10 @@ __device__ __forceinline__ float cls_dot(float c, half8 xh, half8 xl, half8 wh, 
   return c;
 }
 
-// SP: 3xfp16 (VGE_F32X3); !SP: single fp16 planes, one MFMA per product (VGE_F16 throughput mode)
-template <bool SP>
+// SPA / SPW: activations / weights carried as hi + lo fp16 planes.  Both: 3xfp16 (VGE_F32X3, hi*hi + hi*lo +
+// lo*hi); neither: single fp16, one MFMA per product; SPA only: (hi_a + lo_a) * hi_w, two MFMAs on the fp16 weight
+// stream (half the bytes of the split).
+template <bool SPA, bool SPW = SPA>
 __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   char* Ap = lds;                                   // A planes: hi rows [0, AROWS), lo at + AROWS * XSB
@@ -201,7 +206,7 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
         const int off = ((r & 3) + 8 * (r >> 2)) * XSB;
         *reinterpret_cast<_Float16*>(bh + off) = hi[0];
         *reinterpret_cast<_Float16*>(bh + off + XSB) = hi[1];
-        if constexpr (SP) {
+        if constexpr (SPA) {
           *reinterpret_cast<_Float16*>(bh + off + AROWS * XSB) = lo[0];
           *reinterpret_cast<_Float16*>(bh + off + XSB + AROWS * XSB) = lo[1];
         }
@@ -210,7 +215,7 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
         const float y = v0[n] * sc;
         const _Float16 hi = (_Float16)y;
         reinterpret_cast<_Float16*>(plane)[col0 + 32 * n] = hi;
-        if constexpr (SP) reinterpret_cast<_Float16*>(plane + AROWS * XSB)[col0 + 32 * n] = (_Float16)(y - (float)hi);
+        if constexpr (SPA) reinterpret_cast<_Float16*>(plane + AROWS * XSB)[col0 + 32 * n] = (_Float16)(y - (float)hi);
       }
     }
     return e;
@@ -242,7 +247,7 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
     ax = fp16_range_exp(block_max(m));
 #pragma unroll
     for (int j = 0; j < 32; ++j) {
-      if constexpr (SP)
+      if constexpr (SPA)
         split_store(reinterpret_cast<_Float16*>(Ap + (1 + j) * XSB) + tid,
                     reinterpret_cast<_Float16*>(Ap + (AROWS + 1 + j) * XSB) + tid, ldexpf(a[j], -ax));
       else
@@ -284,7 +289,7 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
   BFrag<2> b[TX_PF];
   gchar seg_next = seg_base(0);
 #pragma unroll
-  for (int j = 0; j < TX_PF - 1; ++j) load_b<2, SP>(seg_next, j, loff, b[j]);
+  for (int j = 0; j < TX_PF - 1; ++j) load_b<2, SPW>(seg_next, j, loff, b[j]);
 
   for (int s = 0; s < nseg; ++s) {
     {  // lane-derived values re-derived per segment: stops the compiler from hoisting the ~100 (64-bit,
@@ -302,7 +307,7 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
     auto afn = [&](int c, AFragT& f) {
       f.h = *reinterpret_cast<const half8*>(abase + aoff + c * 32);
       f.h0 = *reinterpret_cast<const half8*>(abase + aoff0 + c * 32);
-      if constexpr (SP) {
+      if constexpr (SPA) {
         f.l = *reinterpret_cast<const half8*>(abase + aoff + c * 32 + AROWS * XSB);
         f.l0 = *reinterpret_cast<const half8*>(abase + aoff0 + c * 32 + AROWS * XSB);
       }
@@ -348,8 +353,8 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
 #if !(VGE_ABL & 2)
-      if (c + TX_PF - 1 < 16) load_b<2, SP>(seg_cur, c + TX_PF - 1, loff, b[(c + TX_PF - 1) % TX_PF]);
-      else load_b<2, SP>(seg_next, c + TX_PF - 1 - 16, loff, b[(c + TX_PF - 1) % TX_PF]);
+      if (c + TX_PF - 1 < 16) load_b<2, SPW>(seg_cur, c + TX_PF - 1, loff, b[(c + TX_PF - 1) % TX_PF]);
+      else load_b<2, SPW>(seg_next, c + TX_PF - 1 - 16, loff, b[(c + TX_PF - 1) % TX_PF]);
 #endif
       if (c + 1 < 16) afn(c + 1, a[(c + 1) & 1]);
       const AFragT& f = a[c & 1];
@@ -358,15 +363,13 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
       for (int n = 0; n < 2; ++n) {
 #if !(VGE_ABL & 1)
         acc.c[0][n] = mfma32(f.h, bb.h[n], acc.c[0][n]);
-        if constexpr (SP) {
-          acc.c[0][n] = mfma32(f.h, bb.l[n], acc.c[0][n]);
-          acc.c[0][n] = mfma32(f.l, bb.h[n], acc.c[0][n]);
-        }
+        if constexpr (SPW) acc.c[0][n] = mfma32(f.h, bb.l[n], acc.c[0][n]);
+        if constexpr (SPA) acc.c[0][n] = mfma32(f.l, bb.h[n], acc.c[0][n]);
 #else
         asm volatile("" ::"v"(f.h), "v"(f.l), "v"(bb.h[n]), "v"(bb.l[n]));
 #endif
 #if !(VGE_ABL & 64)
-        c0[n] = cls_dot<SP>(c0[n], f.h0, f.l0, bb.h[n], bb.l[n]);
+        c0[n] = cls_dot<SPA, SPW>(c0[n], f.h0, f.l0, bb.h[n], bb.l[n]);
 #endif
       }
       // the CLS dot products stay in their step (else they are sunk past the loop and the ring stays live)
@@ -522,13 +525,13 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
                 lv[k] = (_Float16)(y - (float)hv[k]);
               }
               *reinterpret_cast<half4v*>(rh + (8 * g + 4 * h) * 2) = hv;
-              if constexpr (SP) *reinterpret_cast<half4v*>(rh + (8 * g + 4 * h) * 2 + AROWS * XSB) = lv;
+              if constexpr (SPA) *reinterpret_cast<half4v*>(rh + (8 * g + 4 * h) * 2 + AROWS * XSB) = lv;
             }
             if (h == 0) {
               const float y = oc[e] * scl;
               const _Float16 hi = (_Float16)y;
               reinterpret_cast<_Float16*>(Ap)[(2 * wave + e) * 32 + i] = hi;
-              if constexpr (SP)
+              if constexpr (SPA)
                 reinterpret_cast<_Float16*>(Ap + AROWS * XSB)[(2 * wave + e) * 32 + i] = (_Float16)(y - (float)hi);
             }
           }
@@ -685,14 +688,17 @@ struct TxArgsX3Host {
 };
 
 hipError_t transformer_x3_kernel_setup() {
-  const hipError_t e = hipFuncSetAttribute((const void*)transformer_x3_kernel<true>,
-                                           hipFuncAttributeMaxDynamicSharedMemorySize, TX_LDS_BYTES);
-  if (e != hipSuccess) return e;
-  return hipFuncSetAttribute((const void*)transformer_x3_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             TX_LDS_BYTES);
+  const void* k[3] = {(const void*)transformer_x3_kernel<true, true>, (const void*)transformer_x3_kernel<true, false>,
+                      (const void*)transformer_x3_kernel<false, false>};
+  for (auto f : k) {
+    const hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, TX_LDS_BYTES);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
-hipError_t launch_transformer_x3(const TxArgsX3Host& a, bool split, hipStream_t s) {
+// mode: 0 single fp16, 1 activations split (fp16 weights), 2 3xfp16
+hipError_t launch_transformer_x3(const TxArgsX3Host& a, int mode, hipStream_t s) {
   if (a.n_windows < 1) return hipSuccess;
   if (a.n_layers < 0 || a.n_layers > TX_MAX_LAYERS) return hipErrorInvalidValue;
   TxArgsX3 t;
@@ -708,8 +714,9 @@ hipError_t launch_transformer_x3(const TxArgsX3Host& a, bool split, hipStream_t 
   t.frame = a.frame;
   t.tc = a.tc;
   memcpy(t.layers, a.layers, sizeof(TxLayerX3) * a.n_layers);
-  if (split) hipLaunchKernelGGL(transformer_x3_kernel<true>, dim3(a.n_windows), dim3(256), TX_LDS_BYTES, s, t);
-  else hipLaunchKernelGGL(transformer_x3_kernel<false>, dim3(a.n_windows), dim3(256), TX_LDS_BYTES, s, t);
+  auto k = mode == 2 ? transformer_x3_kernel<true, true>
+                     : (mode == 1 ? transformer_x3_kernel<true, false> : transformer_x3_kernel<false, false>);
+  hipLaunchKernelGGL(k, dim3(a.n_windows), dim3(256), TX_LDS_BYTES, s, t);
   return hipGetLastError();
 }
 
