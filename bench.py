@@ -449,7 +449,10 @@ def run_score(args, world, rank, dev):
         "scaling": "strong" if cfg5 else "weak",
         "vs_baseline": None,
         "dtype": args.compute,
-        "precision": {"arith": ARITH[args.compute], **precision},
+        "precision": {"arith": ARITH[args.compute] if not (args.compute == "f16" and
+                                                             os.environ.get("VGE_F16_MIX", "2") == "0") else
+                      ARITH["f16"].replace("transformer: 3xfp16 split (VGE_F16 default)",
+                                           "transformer: fp16 too (VGE_F16_MIX=0)"), **precision},
         "data": "synthetic (deterministic generator vge.synth: quaternion-walk SMPL rotations, N(0,1) betas/tokens, "
                 "U[0,1] keypoints with 5% invisible; random-init weights of the reference architecture)",
         "config": {"workload": workload, "clips_per_gpu": V, "frames_per_clip": T, "windows_per_step_per_gpu": NW,
