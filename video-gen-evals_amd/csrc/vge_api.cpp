@@ -260,7 +260,7 @@ int vge_featurize(const vge_frame_store* st, const int32_t* windows, int n_windo
 }
 
 // ------------------------------------------------------------------ stats
-static const int kColChunk = 64;  // tiles per column-sum partial
+static const int kColChunk = 4;   // tiles per column-sum partial (128 rows: enough chunks to fill the chip)
 
 size_t vge_stats_workspace_bytes(int ct) {
   if (ct < 1) ct = 1;
