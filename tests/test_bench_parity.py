@@ -96,3 +96,34 @@ def test_f16_throughput_mode_vs_oracle(n):
     assert e_seq < 2e-2 and e_ac < 1e-2 and e_tc < 1e-2, (e_seq, e_ac, e_tc)
     s2, _, _ = enc.encode(feats[:64].contiguous(), frame_embed=False, tc=True)
     assert torch.equal(s2, seq[:64])
+
+
+@pytest.mark.parametrize("n", [1, 37, 256, 293, 600])
+def test_f16_unit_kernel_matches_quad_kernel(n, monkeypatch):
+    """The fp16 conv kernel on 1..6-window units from the host-built table (conv_encoder_f16w_kernel, the VGE_F16
+    default) against the 8-wave quad / pair kernel (VGE_F16W=0): the same chunk order and MFMA per output; its GELU is
+    gelu2_fast (|error| < 5e-7, against ocml erff's 7.4e-8), which moves a few fp16 operand roundings, so the two
+    agree to 1e-4 on the embeddings, and both are bounded against the oracle."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vge import ops
+    o = _oracle(max(n, 256)) if n <= 256 else _oracle(n)
+    feats = torch.from_numpy(o["feats"][:n]).to(DEV)
+    monkeypatch.setenv("VGE_F16W", "0")
+    quad = ops.Encoder(o["sd"], device=DEV, compute="f16")
+    monkeypatch.delenv("VGE_F16W")
+    unit = ops.Encoder(o["sd"], device=DEV, compute="f16")
+    for e in (quad, unit):
+        e.reserve(n)
+    s_q, f_q, t_q = quad.encode(feats, frame_embed=True, tc=True)
+    s_u, f_u, t_u = unit.encode(feats, frame_embed=True, tc=True)
+    d_seq = (s_u - s_q).abs().max().item()
+    d_fe = (f_u - f_q).abs().max().item()
+    d_tc = (t_u - t_q).abs().max().item()
+    e_seq = (s_u.cpu() - o["seq"][:n]).abs().max().item()
+    print(f"n={n}: unit vs quad seq {d_seq:.2e} frame {d_fe:.2e} tc {d_tc:.2e}; unit vs oracle seq {e_seq:.2e}")
+    assert d_seq < 1e-4 and d_fe < 1e-4 and d_tc < 1e-4, (d_seq, d_fe, d_tc)
+    assert e_seq < 2e-2
+    if n >= 64:  # deterministic per window whatever unit it lands in
+        s2, _, _ = unit.encode(feats[:64].contiguous(), frame_embed=False, tc=True)
+        assert torch.equal(s2, s_u[:64])

@@ -75,6 +75,27 @@ def test_erf_branch_free_accuracy():
     assert np.abs(erf - ref).max() < 1.5e-7
 
 
+def test_gelu_fast_accuracy():
+    """Host restatement (float32 numpy) of the fp16 conv path's GELU (vge_common.h gelu2_fast): erf(|x|/sqrt 2) =
+    1 - 2^(-a P(a)), a = min(|x|, 4 sqrt 2), GELU = 0.5 x + |x| (0.5 - 0.5 * 2^(-a P(a))).  |error| vs the exact
+    GELU stays below 5e-7 over [-10, 10] (that path's operands are fp16: 2^-11 relative)."""
+    import math
+    import numpy as np
+    f = np.float32
+    c = [f(_hexf(x)) for x in ("-0x1.f5fbdcp-16", "0x1.83e48ap-11", "-0x1.05672ep-7", "0x1.b42062p-5",
+                               "0x1.d5ee02p-2", "0x1.26b194p+0")]
+    x = np.linspace(-10, 10, 400001, dtype=np.float32)
+    a = np.minimum(np.abs(x), f(_hexf("0x1.6a09e6p+2")))
+    p = a * c[0] + c[1]
+    for k in c[2:]:
+        p = a * p + k
+    p = p * a
+    eh = np.exp2(-p.astype(np.float64)).astype(np.float32) * f(-0.5) + f(0.5)
+    out = np.abs(x) * eh + x * f(0.5)
+    ref = np.array([0.5 * float(v) * (1 + math.erf(float(v) / math.sqrt(2))) for v in x])
+    assert np.abs(out - ref).max() < 5e-7
+
+
 @pytest.mark.parametrize("field,value", [("d_model", 128), ("time_heads", 4), ("n_modalities", 4), ("clip_len", 64)])
 def test_unsupported_model_shape_has_its_own_status(field, value):
     """load_model (eval.py:136-165) builds HumanActionScorer with d_model / time_layers / time_heads from the
@@ -107,3 +128,40 @@ def test_load_model_refuses_keypointless_dims():
     diff = {"vit": 1024, "global": 3, "pose": 69, "beta": 10}
     with pytest.raises(UnsupportedModelError):
         VE.load_model({}, raw, diff, device="cpu")
+
+
+@pytest.mark.parametrize("n_windows", [1, 3, 37, 64, 255, 256, 293, 512, 600, 4096])
+def test_conv_unit_schedule_covers_every_window_once(n_windows):
+    """Host-side unit table of the fp16 conv kernel (vge_encoder_x3.hip conv_f16w_schedule, host only, 256 CUs
+    assumed without a GPU): every (encoder, window) pair in exactly one unit of 1..6 consecutive windows; the fewest
+    rounds; per-CU windows within one unit of balance.  At the bench's 256 windows: two units per CU (quint + quint
+    or hex + quad), 10 windows each."""
+    import collections
+    import ctypes as C
+
+    import numpy as np
+    from vge import lib as L
+    so = L.load()
+    cap = 10 * n_windows + 1024
+    tab = np.zeros(cap, np.int32)
+    G, R = C.c_int(), C.c_int()
+    n = so.vge_debug_conv_schedule(n_windows, 6, tab.ctypes.data_as(C.c_void_p), cap, C.byref(G), C.byref(R))
+    assert n == G.value * R.value > 0
+    tab = tab[:n].reshape(R.value, G.value)
+    seen = collections.Counter()
+    per_cu = np.zeros(G.value, np.int64)
+    for u in tab.ravel():
+        if u < 0:
+            continue
+        e, w, w0 = u & 15, (u >> 4) & 7, u >> 8
+        assert 1 <= w <= 6 and 0 <= w0 and w0 + w <= n_windows and e < 10
+        for k in range(w0, w0 + w):
+            seen[(e, k)] += 1
+    for r in range(R.value):
+        for p in range(G.value):
+            if tab[r, p] >= 0:
+                per_cu[p] += (tab[r, p] >> 4) & 7
+    assert len(seen) == 10 * n_windows and set(seen.values()) == {1}
+    assert per_cu.max() - per_cu.min() <= 6
+    if n_windows == 256:
+        assert (G.value, R.value) == (256, 2) and set(per_cu.tolist()) == {10}

@@ -53,4 +53,14 @@ for j, n in enumerate(names):
 for k in range(8):
     g = t[:, :, 22 + k] - t[:, :, 4 + 2 * k]
     out[f"conv{k}_gelu"] = {"w0": round(float(g[:, 0].mean())), "max": round(float(g.max(axis=1).mean()))}
+W = t[:, 0, 30]  # f16 unit kernel: windows of each block's unit (0 in the quad kernel's trace)
+if W.any():
+    out["unit_windows"] = {int(w): {"blocks": int((W == w).sum()),
+                                    "total_cycles_w0": float((t[W == w, 0, 21] - t[W == w, 0, 0]).mean()),
+                                    "conv_stream_w0": float(np.mean([(t[W == w, 0, 4 + 2 * k] - t[W == w, 0, 3 + 2 * k]
+                                                                      if k else t[W == w, 0, 4] - t[W == w, 0, 3])
+                                                                     for k in range(8)])),
+                                    "conv_epi_w0": float(np.mean([t[W == w, 0, 5 + 2 * k] - t[W == w, 0, 4 + 2 * k]
+                                                                  for k in range(8)]))}
+                             for w in sorted(set(W.tolist()))}
 print(json.dumps(out))

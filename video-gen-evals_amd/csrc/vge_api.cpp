@@ -49,6 +49,8 @@ struct GemmArgsX3Host {
   const float* cs;
 };
 hipError_t launch_conv_encoders_x3(const float*, int, const void*, int, float*, bool, bool, hipStream_t);
+bool conv_f16w_schedule(int n_windows, int n_enc, int wmax, std::vector<int>& table, int& G, int& R);
+hipError_t launch_conv_encoders_f16w(const float*, int, const void*, float*, const int*, int, int, hipStream_t);
 hipError_t launch_gemm_x3(int, const GemmArgsX3Host&, hipStream_t);
 struct FfnArgsX3Host {
   const float* X1; float* out; int M;
@@ -219,6 +221,13 @@ struct vge_encoder {
   std::vector<vge::TxLayerX3Host> tx_layers;  // x3: the fused transformer kernel's layer table
   bool tx_fused = true;           // x3: one fused transformer launch (VGE_X3_UNFUSED=1: per-layer kernels)
   int f16_mix = 0;                // VGE_F16: stages kept in 3xfp16 (bit 0 stem, bit 1 transformer; VGE_F16_MIX)
+  // VGE_F16 with the stem unsplit: the 4-wave conv kernel with units of up to `f16w` windows (VGE_F16W; 0 = the 8-wave
+  // quad/pair kernel); its unit table for batch units_B lives in d_units (uploaded from units_host on the stream)
+  int f16w = 6;
+  int* d_units = nullptr;
+  size_t units_cap = 0;
+  int units_B = 0, units_G = 0, units_R = 0;
+  std::vector<int> units_host;
   vge::FuseParamsHost fuse{};
   const void* Wov = nullptr;      // packed (f32 chunks or fp16 chunks)
   const float* Wov_cs = nullptr;  // x3: its column scales
@@ -548,6 +557,8 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
   if (compute == VGE_F16) {  // default: the transformer keeps the split (most of the f16 error, ~10% of the FLOPs)
     const char* mx = getenv("VGE_F16_MIX");
     enc->f16_mix = mx ? atoi(mx) : 2;
+    const char* fw = getenv("VGE_F16W");
+    enc->f16w = fw ? atoi(fw) : 6;
   }
   enc->n_layers = L;
   auto hipfail = [&](hipError_t he) {
@@ -765,6 +776,7 @@ int vge_encoder_destroy(vge_encoder* enc) {
   if (enc->ws) (void)hipFree(enc->ws);
   if (enc->d_encs) (void)hipFree(enc->d_encs);
   if (enc->wbuf) (void)hipFree(enc->wbuf);
+  if (enc->d_units) (void)hipFree(enc->d_units);
   if (enc->hbuf) (void)hipFree(enc->hbuf);
   delete enc;
   return VGE_OK;
@@ -793,8 +805,33 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
     return vge::launch_gemm(epi, g, s);
   };
   HIPCHK(mark(0));
-  if (x3) HIPCHK(vge::launch_conv_encoders_x3(feats, B, enc->d_encs, 10, enc->enc_out, split, enc->f16_mix & 1, s));
-  else HIPCHK(vge::launch_conv_encoders(feats, B, enc->d_encs, 10, enc->enc_out, s));
+  if (x3 && !split && !(enc->f16_mix & 1) && enc->f16w > 0) {
+    if (B != enc->units_B) {  // new batch size: build and upload the unit table (stream-ordered)
+      std::vector<int> tab;
+      int G = 0, R = 0;
+      if (!vge::conv_f16w_schedule(B, 10, enc->f16w, tab, G, R)) return fail(VGE_ERR_ARG, "vge_encode: batch too large");
+      HIPCHK(hipStreamSynchronize(s));  // the previous table's upload has completed
+      if (tab.size() > enc->units_cap) {
+        if (enc->d_units) HIPCHK(hipFree(enc->d_units));
+        enc->d_units = nullptr;
+        enc->units_cap = 0;
+        HIPCHK(hipMalloc(&enc->d_units, tab.size() * sizeof(int)));
+        enc->units_cap = tab.size();
+      }
+      enc->units_host.swap(tab);
+      HIPCHK(hipMemcpyAsync(enc->d_units, enc->units_host.data(), enc->units_host.size() * sizeof(int),
+                            hipMemcpyHostToDevice, s));
+      enc->units_B = B;
+      enc->units_G = G;
+      enc->units_R = R;
+    }
+    HIPCHK(vge::launch_conv_encoders_f16w(feats, B, enc->d_encs, enc->enc_out, enc->d_units, enc->units_G,
+                                          enc->units_R, s));
+  } else if (x3) {
+    HIPCHK(vge::launch_conv_encoders_x3(feats, B, enc->d_encs, 10, enc->enc_out, split, enc->f16_mix & 1, s));
+  } else {
+    HIPCHK(vge::launch_conv_encoders(feats, B, enc->d_encs, 10, enc->enc_out, s));
+  }
   HIPCHK(mark(1));
   HIPCHK(vge::launch_fuse(enc->enc_out, frames, enc->fuse, enc->pooled, s));
   HIPCHK(mark(2));

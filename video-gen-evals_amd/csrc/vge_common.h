@@ -154,6 +154,44 @@ __device__ __forceinline__ void gelu2_many(floatx2 (&y)[K]) {
 #endif
 }
 
+// GELU for the single-fp16 conv path (VGE_F16), whose operands are rounded to fp16 (2^-11) anyway: one exp2 and no
+// branch pieces.  erf(|x| / sqrt 2) = 1 - 2^(-a P(a)), a = min(|x|, 4 sqrt 2), P of degree 5 (weighted least-squares
+// fit of -log2(erfc(a / sqrt 2)) / a), and GELU(x) = 0.5 x + |x| (0.5 - 0.5 * 2^(-a P(a))), which is
+// 0.5 x (1 + erf(x / sqrt 2)) for either sign.  Max |error| vs the exact GELU 4.8e-7 over [-10, 10] in f32
+// (host restatement: tests/test_lib_abi.py::test_gelu_fast_accuracy); ~2/3 of gelu2_many's VALU slots.
+template <int K>
+__device__ __forceinline__ void gelu2_fast(floatx2 (&y)[K]) {
+#if !(defined(VGE_ABL) && (VGE_ABL & 16))
+  floatx2 a[K], p[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    a[k].x = fminf(fabsf(y[k].x), 0x1.6a09e6p+2f);
+    a[k].y = fminf(fabsf(y[k].y), 0x1.6a09e6p+2f);
+    p[k] = __builtin_elementwise_fma(a[k], (floatx2)(-0x1.f5fbdcp-16f), (floatx2)(0x1.83e48ap-11f));
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) p[k] = __builtin_elementwise_fma(a[k], p[k], (floatx2)(-0x1.05672ep-7f));
+#pragma unroll
+  for (int k = 0; k < K; ++k) p[k] = __builtin_elementwise_fma(a[k], p[k], (floatx2)(0x1.b42062p-5f));
+#pragma unroll
+  for (int k = 0; k < K; ++k) p[k] = __builtin_elementwise_fma(a[k], p[k], (floatx2)(0x1.d5ee02p-2f));
+#pragma unroll
+  for (int k = 0; k < K; ++k) p[k] = __builtin_elementwise_fma(a[k], p[k], (floatx2)(0x1.26b194p+0f)) * a[k];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    p[k].x = __builtin_amdgcn_exp2f(-p[k].x);
+    p[k].y = __builtin_amdgcn_exp2f(-p[k].y);
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const floatx2 eh = __builtin_elementwise_fma(p[k], (floatx2)(-0.5f), (floatx2)(0.5f));
+    const floatx2 hx = y[k] * 0.5f;
+    y[k].x = fmaf(fabsf(y[k].x), eh.x, hx.x);
+    y[k].y = fmaf(fabsf(y[k].y), eh.y, hx.y);
+  }
+#endif
+}
+
 // v_mfma_f32_16x16x4_f32: exact f32 (bitwise an fmaf chain over k).  Lane l supplies
 // A[i = l&15][k = l>>4] and B[k = l>>4][j = l&15]; C/D: col = l&15, row = (l>>4)*4 + r.
 __device__ __forceinline__ floatx4 mfma16x16x4(float a, float b, floatx4 c) {

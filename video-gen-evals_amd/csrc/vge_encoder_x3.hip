@@ -25,6 +25,7 @@
 // is one 16-B load per plane and a wave's 32 columns are two contiguous 512-B runs per plane.
 #include "vge_x3.h"
 #include <algorithm>
+#include <vector>
 #include <cstdlib>
 #include <cstring>
 
@@ -64,9 +65,23 @@ struct EncDescX3 {
 // workgroup feeds 32 W rows.  Used as W = 4 / 2 with CW = 8 (one workgroup per CU, two waves per SIMD).
 // (Measured alternative, not kept: pairs on 4 waves with two unsynchronised workgroups per CU -- equal
 // steady-state rate, twice the L2->CU weight traffic, worse tail at 256 windows.)
-template <int W, int CW>
+// Row tiles whose residual lives in LDS (f32, lane-private) instead of registers in conv_f16w_body: from 4 windows
+// on, the last one or two tiles' residuals go to LDS (what the 160 KB leave beside the single activation plane), so
+// a hex unit's accumulators (96) + residuals (80) + fragments fit a wave's 256 VGPRs.
+template <int W, int CW, bool F16W = true>
+constexpr int res_lds_tiles() {
+  return !F16W ? 0 : (W == 6 ? 1 : (W >= 4 ? 2 : 0));
+}
+// NPL activation planes: 2 (hi, lo) when the convs or the stem are split, 1 in the pure fp16 mode
+template <int W, int CW, int NPL = 2>
 constexpr int conv_lds_bytes() {
-  return 2 * (32 * W + 1) * XSB + (6 * W * CW + 2 * 32 * W) * 4;
+  return NPL * (32 * W + 1) * XSB + (6 * W * CW + 2 * 32 * W) * 4 + (NPL == 1 ? res_lds_tiles<W, CW>() : 0) * 32 * 256 * 4;
+}
+template <int CW, int NPL>
+constexpr int conv_lds_bytes_max() {  // over W = 1..6
+  return std::max({conv_lds_bytes<1, CW, NPL>(), conv_lds_bytes<2, CW, NPL>(), conv_lds_bytes<3, CW, NPL>(),
+                   conv_lds_bytes<4, CW, NPL>(), conv_lds_bytes<5, CW, NPL>(), conv_lds_bytes<6, CW, NPL>()});
+  // (W = 6 only in VGE_F16W6 builds; it fits: 1 residual tile in LDS)
 }
 
 // blocks [0, n_quad) take 4 windows, the rest 2: quads stream each weight byte for twice the rows, pairs
@@ -79,11 +94,19 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
                                                   char* lds_raw, [[maybe_unused]] bool tr_on) {
   constexpr int R = W, N = 8 / CW, ROWS = 32 * W, XROWS = ROWS + 1;
   constexpr int CONV_WAVES = CW;
+  constexpr int NPL = (SP || SPS) ? 2 : 1;  // the lo plane exists only when something is split
+  // GELU pairs evaluated together: 8 independent chains on 8-wave blocks; 4 on 4-wave blocks, whose waves hold
+  // twice the accumulators and residuals (up to 6 x 2 x 16 of each) and need the registers
+  constexpr int GK = CW == 4 ? 4 : 8;
   static_assert(CW * N == 8, "8 column tiles of 32 per workgroup");
   _Float16* Xh = reinterpret_cast<_Float16*>(lds_raw);                   // [XROWS][XS]
-  _Float16* Xl = Xh + XROWS * XS;                                        // [XROWS][XS]
-  float* red = reinterpret_cast<float*>(lds_raw + 2 * XROWS * XSB);      // [6 slots][W][waves] partials
+  _Float16* Xl = Xh + XROWS * XS;                                        // [XROWS][XS] (NPL == 2 only)
+  float* red = reinterpret_cast<float*>(lds_raw + NPL * XROWS * XSB);    // [6 slots][W][waves] partials
   int* rexp = reinterpret_cast<int*>(red + 6 * W * CONV_WAVES);          // [2][ROWS] stem row exponents
+  // residuals: tiles t < RREG in registers, the rest in LDS as [tile][n][r / 4][lane][4] f32 (one ds_*_b128 per
+  // 4 rows of a lane: conflict-free, and only the lane itself touches its slots -- no barrier needed)
+  constexpr int RL = res_lds_tiles<W, CW, false>(), RREG = R - RL;
+  floatx4* resl = reinterpret_cast<floatx4*>(rexp + 2 * ROWS) + (threadIdx.x & 63);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -94,7 +117,26 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
   auto crow = [&](int t, int r) { return t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h; };  // C-layout row
 
   Acc<R, N> acc;
-  floatx16 res[R][N];
+  floatx16 res[RREG > 0 ? RREG : 1][N];
+  auto res_set = [&](int t, int n, const floatx16& x) {
+    if (t < RREG) {
+      res[t][n] = x;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        resl[(((t - RREG) * N + n) * 4 + q) * 64] = (floatx4){x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]};
+    }
+  };
+  auto res_get = [&](int t, int n) -> floatx16 {
+    if (t < RREG) return res[t][n];
+    floatx16 x;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const floatx4 y = resl[(((t - RREG) * N + n) * 4 + q) * 64];
+      x[4 * q] = y.x; x[4 * q + 1] = y.y; x[4 * q + 2] = y.z; x[4 * q + 3] = y.w;
+    }
+    return x;
+  };
   for (int c = tid; c < XS; c += 64 * CW) {  // the zero row
     Xh[ROWS * XS + c] = (_Float16)0.0f;
     if constexpr (SP) Xl[ROWS * XS + c] = (_Float16)0.0f;
@@ -247,7 +289,7 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
           for (int n = 0; n < N; ++n) acc.c[t][n][r] *= f;
         }
     }
-    run_stream<SPS ? CONV_PF : CONV_PF16, SPS>(acc, reinterpret_cast<const char*>(ed.stem) + (size_t)p * 16 * CHUNK_B,
+    run_stream<SPS ? CONV_PF : (CW == 4 ? CONV_PF16W : CONV_PF16), SPS>(acc, reinterpret_cast<const char*>(ed.stem) + (size_t)p * 16 * CHUNK_B,
                              ((kw + 127) >> 7) * STREAM_GROUP, loff, afn_stem);
     __syncthreads();  // every wave is done reading X
   }
@@ -259,12 +301,16 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
 #pragma unroll
       for (int t = 0; t < R; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) res[t][n][r] = ldexpf(acc.c[t][n][r] * wcs, efin[crow(t, r)]);
+        for (int r = 0; r < 16; ++r) acc.c[t][n][r] = ldexpf(acc.c[t][n][r] * wcs, efin[crow(t, r)]);
     }
+#pragma unroll
+    for (int t = 0; t < R; ++t)
+#pragma unroll
+      for (int n = 0; n < N; ++n) res_set(t, n, acc.c[t][n]);
   }
   STAMP(2);
   int xexp[R];
-  store_x(res, xexp, nullptr);
+  store_x(acc.c, xexp, nullptr);
   __syncthreads();
   STAMP(3);
 
@@ -285,7 +331,7 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
           if constexpr (SP) f.l[t] = *reinterpret_cast<const half8*>(q + XROWS * XSB);
         }
       };
-      run_stream<SP ? CONV_PF : CONV_PF16, SP>(acc, reinterpret_cast<const char*>(ed.conv) + (size_t)(blk * 2 + cv) * 5 * 16 * CHUNK_B,
+      run_stream<SP ? CONV_PF : (CW == 4 ? CONV_PF16W : CONV_PF16), SP>(acc, reinterpret_cast<const char*>(ed.conv) + (size_t)(blk * 2 + cv) * 5 * 16 * CHUNK_B,
                           5 * 16, loff, afn);
       STAMP(4 + (blk * 2 + cv) * 2);
       // epilogue in packed f32 (v_pk_fma_f32: two rows per instruction), in place:
@@ -300,20 +346,25 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
 #pragma unroll
         for (int t = 0; t < R; ++t) {
           const float xs = ldexpf(1.0f, xexp[t]) * wcs;
-          floatx2 y[8];
+          floatx16 rt;
+          if (cv == 1) rt = res_get(t, n);
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            y[k] = (floatx2){v[t][n][2 * k], v[t][n][2 * k + 1]} * xs;
-            if (cv == 1) y[k] += (floatx2){res[t][n][2 * k], res[t][n][2 * k + 1]};
-          }
-          gelu2_many(y);  // 8 independent chains interleaved
+          for (int k0 = 0; k0 < 8; k0 += GK) {
+            floatx2 y[GK];
 #pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            s2[t] += y[k];
-            v[t][n][2 * k] = y[k].x;
-            v[t][n][2 * k + 1] = y[k].y;
+            for (int k = 0; k < GK; ++k) {
+              y[k] = (floatx2){v[t][n][2 * (k0 + k)], v[t][n][2 * (k0 + k) + 1]} * xs;
+              if (cv == 1) y[k] += (floatx2){rt[2 * (k0 + k)], rt[2 * (k0 + k) + 1]};
+            }
+            gelu2_many(y);  // GK independent chains interleaved
+#pragma unroll
+            for (int k = 0; k < GK; ++k) {
+              s2[t] += y[k];
+              v[t][n][2 * (k0 + k)] = y[k].x;
+              v[t][n][2 * (k0 + k) + 1] = y[k].y;
+            }
+            __builtin_amdgcn_sched_barrier(0);  // one batch's temporaries at a time
           }
-          __builtin_amdgcn_sched_barrier(0);  // one tile's temporaries at a time
         }
       }
       STAMP(22 + blk * 2 + cv);
@@ -353,9 +404,10 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
             for (int r = 0; r < 16; r += 2) {
               const floatx2 y =
                   __builtin_elementwise_fma((floatx2){v[t][n][r], v[t][n][r + 1]}, (floatx2)sc, (floatx2)sh);
-              v[t][n][r] = res[t][n][r] = y.x;
-              v[t][n][r + 1] = res[t][n][r + 1] = y.y;
+              v[t][n][r] = y.x;
+              v[t][n][r + 1] = y.y;
             }
+            res_set(t, n, v[t][n]);
           }
         }
       }
@@ -369,7 +421,7 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
 
   // ---------------- proj: Linear(256 -> 256, no bias)
   acc.zero();
-  run_stream<SP ? CONV_PF : CONV_PF16, SP>(acc, reinterpret_cast<const char*>(ed.proj), 16, loff, afn_rows);
+  run_stream<SP ? CONV_PF : (CW == 4 ? CONV_PF16W : CONV_PF16), SP>(acc, reinterpret_cast<const char*>(ed.proj), 16, loff, afn_rows);
   STAMP(20);
 #pragma unroll
   for (int t = 0; t < R; ++t) {
@@ -428,6 +480,414 @@ __global__ void __launch_bounds__(512, 1) conv_encoder_x3_kernel(const float* __
       const int q_e = cs.qa + (e < cs.qr);
       conv_encoder_body<2, 8, SP, SPS>(feats, n, 4 * q_e + 2 * j, encs[e], e, enc_out, lds_raw, round == VGE_TRACE_ROUND);
     }
+  }
+}
+
+// Multiply a wave's output tile by a stream of n weight chunks (the single-fp16 form of run_stream) with ONE A
+// fragment per row tile: tile t's fragment of chunk c + 1 is read from LDS right after the N MFMAs of chunk c that
+// use it, so its latency hides behind the other tiles' MFMAs and no second A buffer is live (a hex unit needs
+// those registers).  afn1(c, t) returns tile t's fragment of chunk c.
+template <int PF, int R, int N, class AFn1>
+__device__ __forceinline__ void run_stream1(Acc<R, N>& acc, const void* gw, int n, unsigned loff, AFn1 afn1) {
+  const gchar g = (gchar)gw;
+  BFrag<N> b[PF];
+#pragma unroll
+  for (int j = 0; j < PF - 1; ++j) load_b<N, false>(g, j, loff, b[j]);
+  half8 a[R];
+#pragma unroll
+  for (int t = 0; t < R; ++t) a[t] = afn1(0, t);
+  for (int c0 = 0; c0 < n; c0 += PF) {
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      const int c = c0 + j;
+#if !(VGE_ABL & 2)
+      load_b<N, false>(g, min(c + PF - 1, n - 1), loff, b[(j + PF - 1) % PF]);
+#endif
+      const int cn = min(c + 1, n - 1);
+#pragma unroll
+      for (int t = 0; t < R; ++t) {
+#if !(VGE_ABL & 1)
+#pragma unroll
+        for (int q = 0; q < N; ++q) acc.c[t][q] = mfma32(a[t], b[j].h[q], acc.c[t][q]);
+#endif
+#if !(VGE_ABL & 4)
+        a[t] = afn1(cn, t);
+#endif
+      }
+      asm volatile("" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#if !(VGE_ABL & 8)
+    lds_barrier();
+#endif
+  }
+}
+
+// The MovementConvEncoder chain of one unit = one encoder x W windows on CW waves (wave w: columns 32Nw..32Nw+32N-1
+// of all 32 W rows, N = 8 / CW), single fp16 operands (VGE_F16, nothing split).  Same arithmetic as conv_encoder_body<W, CW,
+// false> -- same chunk order and MFMA per output, same epilogue operations -- with epilogues that stream tile by
+// tile instead of holding the unit's activations in registers: each exponent comes from a max pass over the
+// accumulators (stem output; |pre-GELU value| for the first conv of a block, an upper bound of |GELU|) or from the
+// GroupNorm bound, so every tile is computed, stored and dropped in one pass.  Only the second conv of a block holds
+// its GELU outputs for the GroupNorm statistics, while the residuals it consumes die.
+template <int W, int CW>
+__device__ __forceinline__ void conv_f16w_body(const float* __restrict__ feats, int n_windows, int win0,
+                                               const EncDescX3& ed, int e, float* __restrict__ enc_out,
+                                               char* lds_raw, [[maybe_unused]] bool tr_on) {
+  constexpr int R = W, N = 8 / CW, NWV = CW, ROWS = 32 * W, XROWS = ROWS + 1;
+  constexpr int RL = res_lds_tiles<W, CW>(), RREG = R - RL;
+#ifndef VGE_HEX_PF
+#define VGE_HEX_PF CONV_PF16W
+#endif
+  constexpr int PFW = W >= 6 ? VGE_HEX_PF : 2 * CONV_PF16W;  // weight chunks in flight (registers allowing)
+  _Float16* X = reinterpret_cast<_Float16*>(lds_raw);                 // [XROWS][XS]
+  float* red = reinterpret_cast<float*>(lds_raw + XROWS * XSB);       // [6 slots][W][waves]
+  int* rexp = reinterpret_cast<int*>(red + 6 * W * NWV);              // [2][ROWS] stem row exponents
+  // residual tiles in LDS: [RL][waves][N][4][64 lanes] floatx4 (tile stride = 32 rows x 256 columns)
+  floatx4* resl = reinterpret_cast<floatx4*>(rexp + 2 * ROWS) + (threadIdx.x >> 6) * (N * 4 * 64) + (threadIdx.x & 63);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int i = lane & 31, h = lane >> 5;
+  const int col0 = wave * 32 * N + i;                          // this lane's columns: col0 + 32 n
+  const unsigned loff = (unsigned)((h * 256 + col0) * 16);     // its B fragment (column tile 0) in a chunk
+  const char* xa = reinterpret_cast<const char*>(X) + h * 16;  // its 8 k-values of a 16-K chunk column
+  auto crow = [&](int t, int r) { return t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h; };  // C-layout row
+  char* xb = reinterpret_cast<char*>(X) + (4 * h * XS + col0) * 2;  // this lane's column, row 4h of tile 0
+
+  Acc<R, N> acc;
+  floatx16 res[RREG > 0 ? RREG : 1][N];
+  auto res_set = [&](int t, int n, const floatx16& x) {
+    if (t < RREG) {
+      res[t][n] = x;
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        resl[(t - RREG) * (NWV * N * 4 * 64) + (n * 4 + q) * 64] = (floatx4){x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]};
+    }
+  };
+  auto res_get = [&](int t, int n) -> floatx16 {
+    if (t < RREG) return res[t][n];
+    floatx16 x;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const floatx4 y = resl[(t - RREG) * (NWV * N * 4 * 64) + (n * 4 + q) * 64];
+      x[4 * q] = y.x; x[4 * q + 1] = y.y; x[4 * q + 2] = y.z; x[4 * q + 3] = y.w;
+    }
+    return x;
+  };
+  for (int c = tid; c < XS; c += 64 * NWV) X[ROWS * XS + c] = (_Float16)0.0f;  // the zero row
+
+  auto block_reduce = [&](const float (&v)[R], int slot, bool is_max, float (&out)[R]) {
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+      const float w = is_max ? wave_max_last(v[t]) : wave_sum_last(v[t]);
+      if (lane == 63) red[(slot * R + t) * NWV + wave] = w;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+      const float* p = red + (slot * R + t) * NWV;
+      float a = p[0];
+#pragma unroll
+      for (int w = 1; w < NWV; ++w) a = is_max ? fmaxf(a, p[w]) : a + p[w];
+      out[t] = a;
+    }
+  };
+  // fp16 store of a lane's 16 values of column tile n of row tile t, scaled by 2^-ex (immediate-offset ds_write_b16)
+  auto store_tile = [&](const floatx16& v, int t, int n, int ex) {
+    const float sc = ldexpf(1.0f, -ex);
+    char* bh = xb + (t * 32 * XS + 32 * n) * 2;
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {
+      const floatx2 y = (floatx2){v[r], v[r + 1]} * sc;
+      const half2v hv = __builtin_convertvector(y, half2v);
+      const int off = ((r & 3) + 8 * (r >> 2)) * XSB;
+      *reinterpret_cast<_Float16*>(bh + off) = hv[0];
+      *reinterpret_cast<_Float16*>(bh + off + XSB) = hv[1];
+    }
+  };
+  auto afn_rows = [&](int c, int t) { return *reinterpret_cast<const half8*>(xa + (t * 32 + i) * XSB + c * 32); };
+
+  // ---------------- stem: Conv1d(d_in -> 256, k=1, no bias), K in 256-wide panels, per-row exponents (see
+  // conv_encoder_body)
+  STAMP(0);
+  acc.zero();
+  for (int p = 0; p < ed.n_stem_panels; ++p) {
+    const int kw = min(256, ed.d_in - p * 256);
+    int* ecur = rexp + (p & 1) * ROWS;
+    constexpr int RPW = 32 * W / NWV;
+    // every row load of the panel in flight at once (the staging is HBM-latency bound: ~20 k cycles per unit with
+    // 16 loads in flight per wave); the acc registers are zero and no residual is live yet
+    float a[RPW][4];
+#pragma unroll
+    for (int jr = 0; jr < RPW; ++jr) {
+      const int r = wave * RPW + jr;
+      const int w = win0 + (r >> 5);
+      const float* src = feats + ((size_t)w * VGE_T + (r & 31)) * VGE_FD + ed.in_col + p * 256;
+#pragma unroll
+      for (int jc = 0; jc < 4; ++jc) {
+        const int c = lane + 64 * jc;
+        a[jr][jc] = (c < kw && w < n_windows) ? src[c] : 0.f;
+      }
+    }
+#pragma unroll
+    for (int jr = 0; jr < RPW; ++jr) {
+      float m = fmaxf(fmaxf(fabsf(a[jr][0]), fabsf(a[jr][1])), fmaxf(fabsf(a[jr][2]), fabsf(a[jr][3])));
+      m = wave_max_all(m);
+      const int ex = fp16_range_exp(m);
+      const int r = wave * RPW + jr;
+      if (lane == 0) ecur[r] = ex;
+#pragma unroll
+      for (int jc = 0; jc < 4; ++jc) X[r * XS + lane + 64 * jc] = (_Float16)ldexpf(a[jr][jc], -ex);
+    }
+    __syncthreads();  // X and ecur complete
+    if (p == 0) STAMP(1);
+    if (p > 0) {
+      const int* eprev = rexp + ((p - 1) & 1) * ROWS;
+#pragma unroll
+      for (int t = 0; t < R; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float f = ldexpf(1.0f, eprev[crow(t, r)] - ecur[crow(t, r)]);
+#pragma unroll
+          for (int n = 0; n < N; ++n) acc.c[t][n][r] *= f;
+        }
+    }
+    run_stream1<PFW>(acc, reinterpret_cast<const char*>(ed.stem) + (size_t)p * 16 * CHUNK_B,
+                            ((kw + 127) >> 7) * STREAM_GROUP, loff, afn_rows);
+    __syncthreads();  // every wave is done reading X
+  }
+  STAMP(2);
+  int xexp[R];
+  {
+    const int* efin = rexp + ((ed.n_stem_panels - 1) & 1) * ROWS;
+    float wcs[N];
+#pragma unroll
+    for (int n = 0; n < N; ++n) wcs[n] = ed.cs[col0 + 32 * n];
+    auto stem_out = [&](int t, int n, int r) { return ldexpf(acc.c[t][n][r] * wcs[n], efin[crow(t, r)]); };
+    float m[R], mm[R];
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+      m[t] = 0.f;
+#pragma unroll
+      for (int n = 0; n < N; ++n)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) m[t] = fmaxf(m[t], fabsf(stem_out(t, n, r)));
+    }
+    block_reduce(m, 3, true, mm);
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+      xexp[t] = fp16_range_exp(mm[t]);
+#pragma unroll
+      for (int n = 0; n < N; ++n) {
+        floatx16 v;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) v[r] = stem_out(t, n, r);
+        res_set(t, n, v);
+        store_tile(v, t, n, xexp[t]);
+      }
+    }
+  }
+  __syncthreads();
+  STAMP(3);
+
+  // ---------------- 4 TemporalConvBlocks (the two convs of a block written out: each epilogue is its own code)
+#pragma unroll 1
+  for (int blk = 0; blk < 4; ++blk) {
+    const int dil = 1 << blk;
+#pragma unroll
+    for (int cv = 0; cv < 2; ++cv) {
+      acc.zero();
+      auto afn = [&](int c, int t) {
+        const int tap = c >> 4, cc = c & 15;
+        const int tt = i + (tap - 2) * dil;
+        const int row = (unsigned)tt < 32u ? t * 32 + tt : ROWS;  // out of the window -> zero row
+        return *reinterpret_cast<const half8*>(xa + row * XSB + cc * 32);
+      };
+      run_stream1<PFW>(acc, reinterpret_cast<const char*>(ed.conv) + (size_t)(blk * 2 + cv) * 5 * 16 * CHUNK_B,
+                              5 * 16, loff, afn);
+      STAMP(4 + (blk * 2 + cv) * 2);
+      float wcs[N];
+#pragma unroll
+      for (int n = 0; n < N; ++n) wcs[n] = ed.cs[(1 + blk * 2 + cv) * 256 + col0 + 32 * n];
+      if (cv == 0) {
+        // GELU(y) with y = acc * 2^xexp * column scale; |GELU(y)| <= max(|y|, 0.17), so the pre-GELU block max
+        // gives the next operand's exponent without holding the GELU outputs
+        float m[R], mm[R];
+#pragma unroll
+        for (int t = 0; t < R; ++t) {
+          m[t] = 0.17f;
+#pragma unroll
+          for (int n = 0; n < N; ++n) {
+            float a0 = 0.f;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) a0 = fmaxf(a0, fabsf(acc.c[t][n][r]));
+            m[t] = fmaxf(m[t], a0 * fabsf(ldexpf(1.0f, xexp[t]) * wcs[n]));
+          }
+        }
+        STAMP(22 + blk * 2 + cv);
+        block_reduce(m, 3, true, mm);  // its barrier also orders the stores after every wave's reads of X
+#pragma unroll
+        for (int t = 0; t < R; ++t) {
+          const int ex = fp16_range_exp(mm[t]);
+#pragma unroll
+          for (int n = 0; n < N; ++n) {
+            const float xs = ldexpf(1.0f, xexp[t]) * wcs[n];
+            floatx16 v;
+#pragma unroll
+            for (int k0 = 0; k0 < 8; k0 += 4) {
+              floatx2 y[4];
+#pragma unroll
+              for (int k = 0; k < 4; ++k) y[k] = (floatx2){acc.c[t][n][2 * (k0 + k)], acc.c[t][n][2 * (k0 + k) + 1]} * xs;
+              gelu2_fast(y);
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                v[2 * (k0 + k)] = y[k].x;
+                v[2 * (k0 + k) + 1] = y[k].y;
+              }
+            }
+            store_tile(v, t, n, ex);
+            __builtin_amdgcn_sched_barrier(0);  // one tile's temporaries at a time
+          }
+          xexp[t] = ex;
+        }
+      } else {
+        // GELU(acc * scale + residual) -> GroupNorm(1, 256) per window -> the next block's input and residual
+        floatx2 s2[R];
+#pragma unroll
+        for (int t = 0; t < R; ++t) {
+          s2[t] = 0.f;
+#pragma unroll
+          for (int n = 0; n < N; ++n) {
+            const float xs = ldexpf(1.0f, xexp[t]) * wcs[n];
+            const floatx16 rt = res_get(t, n);
+#pragma unroll
+            for (int k0 = 0; k0 < 8; k0 += 4) {
+              floatx2 y[4];
+#pragma unroll
+              for (int k = 0; k < 4; ++k)
+                y[k] = (floatx2){acc.c[t][n][2 * (k0 + k)], acc.c[t][n][2 * (k0 + k) + 1]} * xs +
+                       (floatx2){rt[2 * (k0 + k)], rt[2 * (k0 + k) + 1]};
+              gelu2_fast(y);
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                s2[t] += y[k];
+                acc.c[t][n][2 * (k0 + k)] = y[k].x;
+                acc.c[t][n][2 * (k0 + k) + 1] = y[k].y;
+              }
+            }
+            __builtin_amdgcn_sched_barrier(0);
+          }
+        }
+        float sm[R], mean[R], q[R], var[R];
+#pragma unroll
+        for (int t = 0; t < R; ++t) sm[t] = s2[t].x + s2[t].y;
+        STAMP(22 + blk * 2 + cv);
+        block_reduce(sm, 0, false, mean);
+#pragma unroll
+        for (int t = 0; t < R; ++t) {
+          mean[t] *= 1.0f / 8192.0f;
+          floatx2 q2 = 0.f;
+#pragma unroll
+          for (int n = 0; n < N; ++n)
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) {
+              const floatx2 d = (floatx2){acc.c[t][n][r], acc.c[t][n][r + 1]} - mean[t];
+              q2 = __builtin_elementwise_fma(d, d, q2);
+            }
+          q[t] = q2.x + q2.y;
+        }
+        block_reduce(q, 1, false, var);
+        const int ex = fp16_range_exp(90.51f * ed.gn_gmax[blk] + ed.gn_bmax[blk]);  // as conv_encoder_body
+#pragma unroll
+        for (int t = 0; t < R; ++t) {
+          const float rstd = 1.0f / sqrtf(var[t] * (1.0f / 8192.0f) + 1e-5f);
+#pragma unroll
+          for (int n = 0; n < N; ++n) {
+            const float gw = ed.gn_w[blk * 256 + col0 + 32 * n], gb = ed.gn_b[blk * 256 + col0 + 32 * n];
+            const float sc = rstd * gw, sh = gb - mean[t] * sc;
+            floatx16 v;
+#pragma unroll
+            for (int r = 0; r < 16; r += 2) {
+              const floatx2 y =
+                  __builtin_elementwise_fma((floatx2){acc.c[t][n][r], acc.c[t][n][r + 1]}, (floatx2)sc, (floatx2)sh);
+              v[r] = y.x;
+              v[r + 1] = y.y;
+            }
+            res_set(t, n, v);
+            store_tile(v, t, n, ex);
+          }
+          xexp[t] = ex;
+        }
+      }
+      __syncthreads();
+      STAMP(5 + (blk * 2 + cv) * 2);
+    }
+  }
+
+  // ---------------- proj: Linear(256 -> 256, no bias)
+  acc.zero();
+  run_stream1<PFW>(acc, reinterpret_cast<const char*>(ed.proj), 16, loff, afn_rows);
+  STAMP(20);
+#pragma unroll
+  for (int t = 0; t < R; ++t) {
+    const int win = win0 + t;
+    if (win < n_windows) {
+      float* o = enc_out + ((size_t)e * n_windows * VGE_T + (size_t)win * VGE_T) * VGE_D;
+#pragma unroll
+      for (int n = 0; n < N; ++n) {
+        const float xs = ldexpf(1.0f, xexp[t]) * ed.cs[9 * 256 + col0 + 32 * n];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[crow(0, r) * VGE_D + col0 + 32 * n] = acc.c[t][n][r] * xs;
+      }
+    }
+  }
+  STAMP(21);
+#ifdef VGE_TRACE
+  if (tr_on && blockIdx.x < 64 && threadIdx.x == 0) {
+    g_vge_trace[blockIdx.x * 8 * 32 + 31] = e;
+    g_vge_trace[blockIdx.x * 8 * 32 + 30] = W;
+  }
+#endif
+}
+
+// Pure fp16 mode (VGE_F16 with nothing split): one 512-thread workgroup per CU (8 waves, wave w = columns 32w..32w+31
+// of all rows), units of 1..6 windows of one encoder from a host-built table (conv_f16w_schedule), run by
+// conv_f16w_body.  The weight stream is paid per unit (~28.5 k cycles per conv whatever the unit's rows), so the
+// number of units per CU is what sets the time: at 256 windows every CU runs two units (quint + quint, or hex +
+// quad; 10 windows) instead of the quad kernel's three (quad + quad + pair).  Measured (256 / 4,096 windows):
+// 0.61 / 8.07 ms against 0.745 / 10.55 ms for conv_encoder_x3_kernel<false, false>.  Measured and dropped: the same
+// body on 4 waves (one per SIMD, accumulators in AGPRs, at most 5 windows: the hex spills) -- 0.65-0.67 / 9.5 ms.
+// Table entry: encoder | W << 4 | first window << 8, -1 = idle; [round][position], position = xcd_remap(block).
+constexpr int F16W_MAX = 6;  // windows per unit
+
+constexpr int F16W_WAVES = 8;
+
+__global__ void __launch_bounds__(512, 1) conv_encoder_f16w_kernel(const float* __restrict__ feats,
+                                                                    const EncDescX3* __restrict__ encs, int n_windows,
+                                                                    int G, int n_rounds, const int* __restrict__ units,
+                                                                    float* __restrict__ enc_out) {
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  const int pos = xcd_remap(blockIdx.x, G);
+  for (int round = 0; round < n_rounds; ++round) {
+    const int u = __builtin_amdgcn_readfirstlane(units[round * G + pos]);
+    if (u < 0) continue;  // uniform over the block
+    if (round > 0) __syncthreads();  // the previous unit's LDS is free
+    const int e = u & 15, w = (u >> 4) & 7, w0 = u >> 8;
+#ifdef VGE_F16W_ONLY  // register-pressure probes: one instantiation only
+    conv_f16w_body<VGE_F16W_ONLY, F16W_WAVES>(feats, n_windows, w0, encs[e], e, enc_out, lds_raw, round == VGE_TRACE_ROUND);
+    (void)w;
+#else
+    switch (w) {
+      case 6: conv_f16w_body<6, F16W_WAVES>(feats, n_windows, w0, encs[e], e, enc_out, lds_raw, round == VGE_TRACE_ROUND); break;
+      case 5: conv_f16w_body<5, F16W_WAVES>(feats, n_windows, w0, encs[e], e, enc_out, lds_raw, round == VGE_TRACE_ROUND); break;
+      case 4: conv_f16w_body<4, F16W_WAVES>(feats, n_windows, w0, encs[e], e, enc_out, lds_raw, round == VGE_TRACE_ROUND); break;
+      case 3: conv_f16w_body<3, F16W_WAVES>(feats, n_windows, w0, encs[e], e, enc_out, lds_raw, round == VGE_TRACE_ROUND); break;
+      case 2: conv_f16w_body<2, F16W_WAVES>(feats, n_windows, w0, encs[e], e, enc_out, lds_raw, round == VGE_TRACE_ROUND); break;
+      default: conv_f16w_body<1, F16W_WAVES>(feats, n_windows, w0, encs[e], e, enc_out, lds_raw, round == VGE_TRACE_ROUND); break;
+    }
+#endif
   }
 }
 
@@ -818,6 +1278,8 @@ __global__ void __launch_bounds__(256) pack_x3_kernel(const float* __restrict__ 
 // ================================================================== host launchers
 namespace vge {
 
+static int conv_cu_count();
+
 hipError_t launch_pack_x3(const float* W, int N, int K_real, int ldk, int conv, int nch, int* sh, float* cs, int* bad,
                           _Float16* out, hipStream_t s) {
   if (N % 256 || K_real < 1 || nch * 16 < K_real) return hipErrorInvalidValue;
@@ -850,6 +1312,9 @@ hipError_t encoder_x3_kernel_setup() {
     e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, conv_lds_bytes<4, 8>());
     if (e != hipSuccess) return e;
   }
+  e = hipFuncSetAttribute((const void*)conv_encoder_f16w_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                          conv_lds_bytes_max<F16W_WAVES, 1>());
+  if (e != hipSuccess) return e;
   const void* gk[4] = {(const void*)gemm_x3_kernel<EPI_TOKENS, GEMM_RT>, (const void*)gemm_x3_kernel<EPI_BIAS, GEMM_RT>,
                        (const void*)gemm_x3_kernel<EPI_BIAS_RELU, GEMM_RT>,
                        (const void*)gemm_x3_kernel<EPI_BIAS_RES_LN, GEMM_RT>};
@@ -866,13 +1331,7 @@ hipError_t encoder_x3_kernel_setup() {
 // split: 3xfp16 (VGE_F32X3); otherwise single fp16 with the stem split (stem_split) or not
 hipError_t launch_conv_encoders_x3(const float* feats, int n_windows, const void* encs, int n_enc, float* enc_out,
                                    bool split, bool stem_split, hipStream_t s) {
-  static int n_cu = 0;
-  if (n_cu == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu < 1)
-      n_cu = 256;
-  }
+  const int n_cu = conv_cu_count();
   if (n_windows < 1 || n_enc < 1) return hipSuccess;
   const int pair_units = n_enc * ((n_windows + 1) / 2);
   const int G0 = std::min(n_cu, pair_units);
@@ -892,6 +1351,66 @@ hipError_t launch_conv_encoders_x3(const float* feats, int n_windows, const void
                  : (stem_split ? conv_encoder_x3_kernel<false, true> : conv_encoder_x3_kernel<false, false>);
   hipLaunchKernelGGL(k, dim3(cs.G), dim3(512), (conv_lds_bytes<4, 8>()), s, feats,
                      reinterpret_cast<const EncDescX3*>(encs), cs, enc_out);
+  return hipGetLastError();
+}
+
+static int conv_cu_count() {
+  static int n_cu = 0;
+  if (n_cu == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu < 1)
+      n_cu = 256;
+  }
+  return n_cu;
+}
+
+// Unit table of conv_encoder_f16w_kernel for n_windows x n_enc (window, encoder) pairs on G = min(CUs, units)
+// persistent blocks and R rounds: the fewest rounds whose units fit wmax (<= F16W_MAX) windows; encoder e is cut into u_e
+// nearly equal units of consecutive windows (u_e = U / n_enc, +1 for the first U % n_enc encoders).  The units,
+// encoder-major, are sorted by size (largest first, stable: the same encoder's units stay together) and dealt in
+// snake order over the positions (round 0 left to right, round 1 right to left, ...), so a position holding a
+// large unit in one round holds a small one in the next and consecutive positions -- one XCD's CUs, xcd_remap -- run the same encoder's units together.
+// Returns false if n_enc > 16 or n_windows > 2^23 (the entry's bit fields).
+bool conv_f16w_schedule(int n_windows, int n_enc, int wmax, std::vector<int>& table, int& G, int& R) {
+  if (n_windows < 1 || n_enc < 1 || n_enc > 16 || n_windows > (1 << 23)) return false;
+  wmax = std::max(1, std::min(wmax, F16W_MAX));
+  const long long P = (long long)n_windows * n_enc;
+  const int n_cu = conv_cu_count();
+  struct U { int e, w0, w; };
+  std::vector<U> units;
+  for (R = 1;; ++R) {
+    const long long Ul = std::min<long long>((long long)n_cu * R, P);
+    const int Ut = (int)Ul;
+    units.clear();
+    bool ok = true;
+    for (int e = 0; e < n_enc && ok; ++e) {
+      const int ue = std::min(n_windows, Ut / n_enc + (e < Ut % n_enc));
+      if (ue < 1 || (n_windows + ue - 1) / ue > wmax) { ok = false; break; }
+      for (int k = 0; k < ue; ++k) {
+        const int a = (int)((long long)k * n_windows / ue), b = (int)((long long)(k + 1) * n_windows / ue);
+        units.push_back({e, a, b - a});
+      }
+    }
+    if (ok) break;
+  }
+  const int Ut = (int)units.size();
+  G = std::min(n_cu, Ut);
+  R = (Ut + G - 1) / G;
+  std::stable_sort(units.begin(), units.end(), [](const U& x, const U& y) { return x.w > y.w; });
+  table.assign((size_t)R * G, -1);
+  for (int k = 0; k < Ut; ++k) {
+    const int r = k / G, j = k % G, p = (r & 1) ? G - 1 - j : j;
+    table[(size_t)r * G + p] = units[k].e | (units[k].w << 4) | (units[k].w0 << 8);
+  }
+  return true;
+}
+
+hipError_t launch_conv_encoders_f16w(const float* feats, int n_windows, const void* encs, float* enc_out,
+                                     const int* d_units, int G, int R, hipStream_t s) {
+  if (n_windows < 1) return hipSuccess;
+  hipLaunchKernelGGL(conv_encoder_f16w_kernel, dim3(G), dim3(512), (conv_lds_bytes_max<F16W_WAVES, 1>()), s, feats,
+                     reinterpret_cast<const EncDescX3*>(encs), n_windows, G, R, d_units, enc_out);
   return hipGetLastError();
 }
 
@@ -925,6 +1444,14 @@ hipError_t launch_ffn_x3(const FfnArgsX3Host& a, hipStream_t s) {
 }
 
 }  // namespace vge
+
+// Test hook (host only, tests/test_lib_abi.py): the f16w unit table for n_windows x 10 encoders, n_cu CUs.
+extern "C" int vge_debug_conv_schedule(int n_windows, int wmax, int* table, int cap, int* G, int* R) {
+  std::vector<int> t;
+  if (!vge::conv_f16w_schedule(n_windows, 10, wmax, t, *G, *R) || (int)t.size() > cap) return -1;
+  std::copy(t.begin(), t.end(), table);
+  return (int)t.size();
+}
 
 #ifdef VGE_TRACE
 extern "C" int vge_debug_x3_trace(long long* host, int n) {

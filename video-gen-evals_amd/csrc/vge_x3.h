@@ -25,6 +25,10 @@ constexpr int CONV_PF = 4;           // weight chunks in flight per wave: conv (
 #define VGE_CONV_PF16 8
 #endif
 constexpr int CONV_PF16 = VGE_CONV_PF16;  // ... in the single-fp16 mode (half the bytes per chunk)
+#ifndef VGE_CONV_PF16W
+#define VGE_CONV_PF16W 4
+#endif
+constexpr int CONV_PF16W = VGE_CONV_PF16W;  // ... 4-wave fp16 blocks (a wave's chunk = 2 column tiles)
 constexpr int GEMM_PF = 4;           // ... and GEMM waves (32 x 32 outputs, 4 waves per SIMD)
 
 __device__ __forceinline__ floatx16 mfma32(half8 a, half8 b, floatx16 c) {
