@@ -56,14 +56,14 @@ F16_MFMA_PEAK_TFLOPS = 2516.6
 PEAK_BY_COMPUTE = {"f32": (F32_MFMA_PEAK_TFLOPS, "conv_encoder_kernel (10 MovementConvEncoders, exact f32 MFMA)"),
                    "f32x3": (F16_MFMA_PEAK_TFLOPS / 3, "conv_encoder_x3_kernel (10 MovementConvEncoders, "
                                                       "3xfp16 split MFMA, peak = dense F16 MFMA / 3)"),
-                   "f16": (F16_MFMA_PEAK_TFLOPS, "conv_encoder_x3_kernel<f16> (10 MovementConvEncoders, single "
-                                                 "fp16 MFMA per product, peak = dense F16 MFMA)")}
+                   "f16": (F16_MFMA_PEAK_TFLOPS, "conv_encoder_f16w_kernel (10 MovementConvEncoders on 1..6-window "
+                                                 "units, single fp16 MFMA per product, peak = dense F16 MFMA)")}
 ARITH = {"f32": "f32 in, f32 accumulate (v_mfma_f32_16x16x4_f32)",
          "f32x3": "f32 operands as fp16 hi + fp16 residual lo (power-of-two scaled per row/window/column), 3 f16 "
                   "MFMAs per product (hi*hi + hi*lo + lo*hi), f32 accumulate",
          "f16": "MovementConvEncoders (85% of the FLOPs): operands rounded to fp16 (power-of-two scaled per "
-                "row/window/column), 1 f16 MFMA per product, f32 accumulate, f32 GELU/GroupNorm epilogues; "
-                "transformer: 3xfp16 split (VGE_F16 default)"}
+                "row/window/column), 1 f16 MFMA per product, f32 accumulate, f32 GELU (one-exp2 erf, |err| < 5e-7) "
+                "and GroupNorm epilogues; transformer: 3xfp16 split (VGE_F16 default)"}
 HBM_PEAK_GBS = 8000.0
 FEAT_BYTES_PER_WINDOW = 32 * (1024 + 207 + 9 + 10 + 120) * 4 + 32 * 2596 * 4   # read + write
 

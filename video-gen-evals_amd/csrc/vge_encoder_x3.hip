@@ -68,20 +68,19 @@ struct EncDescX3 {
 // Row tiles whose residual lives in LDS (f32, lane-private) instead of registers in conv_f16w_body: from 4 windows
 // on, the last one or two tiles' residuals go to LDS (what the 160 KB leave beside the single activation plane), so
 // a hex unit's accumulators (96) + residuals (80) + fragments fit a wave's 256 VGPRs.
-template <int W, int CW, bool F16W = true>
+template <int W>
 constexpr int res_lds_tiles() {
-  return !F16W ? 0 : (W == 6 ? 1 : (W >= 4 ? 2 : 0));
+  return W == 6 ? 1 : (W >= 4 ? 2 : 0);
 }
 // NPL activation planes: 2 (hi, lo) when the convs or the stem are split, 1 in the pure fp16 mode
 template <int W, int CW, int NPL = 2>
 constexpr int conv_lds_bytes() {
-  return NPL * (32 * W + 1) * XSB + (6 * W * CW + 2 * 32 * W) * 4 + (NPL == 1 ? res_lds_tiles<W, CW>() : 0) * 32 * 256 * 4;
+  return NPL * (32 * W + 1) * XSB + (6 * W * CW + 2 * 32 * W) * 4 + (NPL == 1 ? res_lds_tiles<W>() : 0) * 32 * 256 * 4;
 }
 template <int CW, int NPL>
 constexpr int conv_lds_bytes_max() {  // over W = 1..6
   return std::max({conv_lds_bytes<1, CW, NPL>(), conv_lds_bytes<2, CW, NPL>(), conv_lds_bytes<3, CW, NPL>(),
                    conv_lds_bytes<4, CW, NPL>(), conv_lds_bytes<5, CW, NPL>(), conv_lds_bytes<6, CW, NPL>()});
-  // (W = 6 only in VGE_F16W6 builds; it fits: 1 residual tile in LDS)
 }
 
 // blocks [0, n_quad) take 4 windows, the rest 2: quads stream each weight byte for twice the rows, pairs
@@ -94,19 +93,11 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
                                                   char* lds_raw, [[maybe_unused]] bool tr_on) {
   constexpr int R = W, N = 8 / CW, ROWS = 32 * W, XROWS = ROWS + 1;
   constexpr int CONV_WAVES = CW;
-  constexpr int NPL = (SP || SPS) ? 2 : 1;  // the lo plane exists only when something is split
-  // GELU pairs evaluated together: 8 independent chains on 8-wave blocks; 4 on 4-wave blocks, whose waves hold
-  // twice the accumulators and residuals (up to 6 x 2 x 16 of each) and need the registers
-  constexpr int GK = CW == 4 ? 4 : 8;
   static_assert(CW * N == 8, "8 column tiles of 32 per workgroup");
   _Float16* Xh = reinterpret_cast<_Float16*>(lds_raw);                   // [XROWS][XS]
-  _Float16* Xl = Xh + XROWS * XS;                                        // [XROWS][XS] (NPL == 2 only)
-  float* red = reinterpret_cast<float*>(lds_raw + NPL * XROWS * XSB);    // [6 slots][W][waves] partials
+  _Float16* Xl = Xh + XROWS * XS;                                        // [XROWS][XS]
+  float* red = reinterpret_cast<float*>(lds_raw + 2 * XROWS * XSB);      // [6 slots][W][waves] partials
   int* rexp = reinterpret_cast<int*>(red + 6 * W * CONV_WAVES);          // [2][ROWS] stem row exponents
-  // residuals: tiles t < RREG in registers, the rest in LDS as [tile][n][r / 4][lane][4] f32 (one ds_*_b128 per
-  // 4 rows of a lane: conflict-free, and only the lane itself touches its slots -- no barrier needed)
-  constexpr int RL = res_lds_tiles<W, CW, false>(), RREG = R - RL;
-  floatx4* resl = reinterpret_cast<floatx4*>(rexp + 2 * ROWS) + (threadIdx.x & 63);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -117,26 +108,7 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
   auto crow = [&](int t, int r) { return t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h; };  // C-layout row
 
   Acc<R, N> acc;
-  floatx16 res[RREG > 0 ? RREG : 1][N];
-  auto res_set = [&](int t, int n, const floatx16& x) {
-    if (t < RREG) {
-      res[t][n] = x;
-    } else {
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        resl[(((t - RREG) * N + n) * 4 + q) * 64] = (floatx4){x[4 * q], x[4 * q + 1], x[4 * q + 2], x[4 * q + 3]};
-    }
-  };
-  auto res_get = [&](int t, int n) -> floatx16 {
-    if (t < RREG) return res[t][n];
-    floatx16 x;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const floatx4 y = resl[(((t - RREG) * N + n) * 4 + q) * 64];
-      x[4 * q] = y.x; x[4 * q + 1] = y.y; x[4 * q + 2] = y.z; x[4 * q + 3] = y.w;
-    }
-    return x;
-  };
+  floatx16 res[R][N];
   for (int c = tid; c < XS; c += 64 * CW) {  // the zero row
     Xh[ROWS * XS + c] = (_Float16)0.0f;
     if constexpr (SP) Xl[ROWS * XS + c] = (_Float16)0.0f;
@@ -289,7 +261,7 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
           for (int n = 0; n < N; ++n) acc.c[t][n][r] *= f;
         }
     }
-    run_stream<SPS ? CONV_PF : (CW == 4 ? CONV_PF16W : CONV_PF16), SPS>(acc, reinterpret_cast<const char*>(ed.stem) + (size_t)p * 16 * CHUNK_B,
+    run_stream<SPS ? CONV_PF : CONV_PF16, SPS>(acc, reinterpret_cast<const char*>(ed.stem) + (size_t)p * 16 * CHUNK_B,
                              ((kw + 127) >> 7) * STREAM_GROUP, loff, afn_stem);
     __syncthreads();  // every wave is done reading X
   }
@@ -301,16 +273,12 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
 #pragma unroll
       for (int t = 0; t < R; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc.c[t][n][r] = ldexpf(acc.c[t][n][r] * wcs, efin[crow(t, r)]);
+        for (int r = 0; r < 16; ++r) res[t][n][r] = ldexpf(acc.c[t][n][r] * wcs, efin[crow(t, r)]);
     }
-#pragma unroll
-    for (int t = 0; t < R; ++t)
-#pragma unroll
-      for (int n = 0; n < N; ++n) res_set(t, n, acc.c[t][n]);
   }
   STAMP(2);
   int xexp[R];
-  store_x(acc.c, xexp, nullptr);
+  store_x(res, xexp, nullptr);
   __syncthreads();
   STAMP(3);
 
@@ -331,7 +299,7 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
           if constexpr (SP) f.l[t] = *reinterpret_cast<const half8*>(q + XROWS * XSB);
         }
       };
-      run_stream<SP ? CONV_PF : (CW == 4 ? CONV_PF16W : CONV_PF16), SP>(acc, reinterpret_cast<const char*>(ed.conv) + (size_t)(blk * 2 + cv) * 5 * 16 * CHUNK_B,
+      run_stream<SP ? CONV_PF : CONV_PF16, SP>(acc, reinterpret_cast<const char*>(ed.conv) + (size_t)(blk * 2 + cv) * 5 * 16 * CHUNK_B,
                           5 * 16, loff, afn);
       STAMP(4 + (blk * 2 + cv) * 2);
       // epilogue in packed f32 (v_pk_fma_f32: two rows per instruction), in place:
@@ -346,25 +314,20 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
 #pragma unroll
         for (int t = 0; t < R; ++t) {
           const float xs = ldexpf(1.0f, xexp[t]) * wcs;
-          floatx16 rt;
-          if (cv == 1) rt = res_get(t, n);
+          floatx2 y[8];
 #pragma unroll
-          for (int k0 = 0; k0 < 8; k0 += GK) {
-            floatx2 y[GK];
-#pragma unroll
-            for (int k = 0; k < GK; ++k) {
-              y[k] = (floatx2){v[t][n][2 * (k0 + k)], v[t][n][2 * (k0 + k) + 1]} * xs;
-              if (cv == 1) y[k] += (floatx2){rt[2 * (k0 + k)], rt[2 * (k0 + k) + 1]};
-            }
-            gelu2_many(y);  // GK independent chains interleaved
-#pragma unroll
-            for (int k = 0; k < GK; ++k) {
-              s2[t] += y[k];
-              v[t][n][2 * (k0 + k)] = y[k].x;
-              v[t][n][2 * (k0 + k) + 1] = y[k].y;
-            }
-            __builtin_amdgcn_sched_barrier(0);  // one batch's temporaries at a time
+          for (int k = 0; k < 8; ++k) {
+            y[k] = (floatx2){v[t][n][2 * k], v[t][n][2 * k + 1]} * xs;
+            if (cv == 1) y[k] += (floatx2){res[t][n][2 * k], res[t][n][2 * k + 1]};
           }
+          gelu2_many(y);  // 8 independent chains interleaved
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {
+            s2[t] += y[k];
+            v[t][n][2 * k] = y[k].x;
+            v[t][n][2 * k + 1] = y[k].y;
+          }
+          __builtin_amdgcn_sched_barrier(0);  // one tile's temporaries at a time
         }
       }
       STAMP(22 + blk * 2 + cv);
@@ -404,10 +367,9 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
             for (int r = 0; r < 16; r += 2) {
               const floatx2 y =
                   __builtin_elementwise_fma((floatx2){v[t][n][r], v[t][n][r + 1]}, (floatx2)sc, (floatx2)sh);
-              v[t][n][r] = y.x;
-              v[t][n][r + 1] = y.y;
+              v[t][n][r] = res[t][n][r] = y.x;
+              v[t][n][r + 1] = res[t][n][r + 1] = y.y;
             }
-            res_set(t, n, v[t][n]);
           }
         }
       }
@@ -421,7 +383,7 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
 
   // ---------------- proj: Linear(256 -> 256, no bias)
   acc.zero();
-  run_stream<SP ? CONV_PF : (CW == 4 ? CONV_PF16W : CONV_PF16), SP>(acc, reinterpret_cast<const char*>(ed.proj), 16, loff, afn_rows);
+  run_stream<SP ? CONV_PF : CONV_PF16, SP>(acc, reinterpret_cast<const char*>(ed.proj), 16, loff, afn_rows);
   STAMP(20);
 #pragma unroll
   for (int t = 0; t < R; ++t) {
@@ -535,7 +497,7 @@ __device__ __forceinline__ void conv_f16w_body(const float* __restrict__ feats, 
                                                const EncDescX3& ed, int e, float* __restrict__ enc_out,
                                                char* lds_raw, [[maybe_unused]] bool tr_on) {
   constexpr int R = W, N = 8 / CW, NWV = CW, ROWS = 32 * W, XROWS = ROWS + 1;
-  constexpr int RL = res_lds_tiles<W, CW>(), RREG = R - RL;
+  constexpr int RL = res_lds_tiles<W>(), RREG = R - RL;
 #ifndef VGE_HEX_PF
 #define VGE_HEX_PF CONV_PF16W
 #endif
