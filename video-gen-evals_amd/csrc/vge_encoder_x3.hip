@@ -479,9 +479,9 @@ __device__ __forceinline__ void run_stream1(Acc<R, N>& acc, const void* gw, int 
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
     }
-#if !(VGE_ABL & 8)
-    lds_barrier();
-#endif
+    // no per-group barrier (unlike run_stream): measured without it the waves drift within a conv and meet at the
+    // epilogue's first block reduction -- 443 k -> 419 k cycles per 5-window unit; every LDS write that could race a
+    // slower wave's A reads comes after that reduction's barrier
   }
 }
 
