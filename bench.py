@@ -18,8 +18,8 @@ f32-class `f32x3` parity mode run on the same workload and reported as `parity_m
 Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (the 10 MovementConvEncoders,
 MFMA-bound): achieved = its algorithmic FLOPs per launch (1.7622 GFLOP per window)
 / its average duration from hipEvents recorded around it on its stream inside the timed steps; peak =
-the MFMA ceiling of the compute mode (f16: dense F16 2516.6 TF; 3xfp16 split: / 3 = 838.9 TF; exact
-f32: 157.3 TF).  `traffic` = HBM bytes per launch from the committed PMC pass
+the MFMA ceiling of the compute mode from rocminfo (CUs x max clock: f16 dense 4096 FLOP/clk/CU, 2516.6 TF on
+MI355X; 3xfp16 split: / 3 = 838.9 TF; exact f32 256 FLOP/clk/CU, 157.3 TF; `peak_source`).  `traffic` = HBM bytes per launch from the committed PMC pass
 (profiles/pmc_conv_encoder.json, FETCH_SIZE x2 + WRITE_SIZE per the guide), reported only when that pass
 was taken on this tree's kernel sources, else null.  `cpu_baseline` is the oracle CPU restatement of
 eval.py in the reference's structure (DataLoader workers=4, bs 32, torch-fp32 on the CPU share) timed on
@@ -66,6 +66,26 @@ ARITH = {"f32": "f32 in, f32 accumulate (v_mfma_f32_16x16x4_f32)",
                 "and GroupNorm epilogues; transformer: 3xfp16 split (VGE_F16 default)"}
 HBM_PEAK_GBS = 8000.0
 FEAT_BYTES_PER_WINDOW = 32 * (1024 + 207 + 9 + 10 + 120) * 4 + 32 * 2596 * 4   # read + write
+
+
+def device_peaks() -> dict:
+    """MFMA peaks of the visible GPU from rocminfo (CU count x max engine clock x MFMA FLOP/CU/clk):
+    dense f16 4 SIMDs x 1024 FLOP/clk, exact f32 4 x 64.  Falls back to the MI355X_MICROARCH.md figures (256 CUs,
+    2.4 GHz) when rocminfo is unavailable; `source` says which."""
+    import re
+    import subprocess
+    try:
+        txt = subprocess.run(["rocminfo"], capture_output=True, text=True, timeout=60).stdout
+        for agent in txt.split("*******")[1:]:
+            if re.search(r"Device Type:\s+GPU", agent) and "gfx950" in agent:
+                cus = int(re.search(r"Compute Unit:\s+(\d+)", agent).group(1))
+                mhz = int(re.search(r"Max Clock Freq\. \(MHz\):\s+(\d+)", agent).group(1))
+                return {"f16": cus * 4 * 1024 * mhz * 1e6 / 1e12, "f32": cus * 4 * 64 * mhz * 1e6 / 1e12,
+                        "source": f"rocminfo: {cus} CUs x {mhz} MHz"}
+    except (OSError, subprocess.SubprocessError, AttributeError, ValueError):
+        pass
+    return {"f16": F16_MFMA_PEAK_TFLOPS, "f32": F32_MFMA_PEAK_TFLOPS,
+            "source": "MI355X_MICROARCH.md (rocminfo unavailable): 256 CUs x 2400 MHz"}
 
 
 def make_clips(seed, start, n, T, kp_len=None):
@@ -383,13 +403,7 @@ def run_score(args, world, rank, dev):
             ops.featurize(gstore, windows[b0:b1], stats.mean, stats.std, out=feats[: b1 - b0])
             if i is not None:
                 fe1[i * n_chunks + c].record()
-            s_, _, t_ = enc.encode(feats[: b1 - b0], frame_embed=False, tc=True)
-            if n_chunks > 1:
-                seq[b0:b1] = s_
-                tcw[b0:b1] = t_
-            else:
-                seq.copy_(s_)
-                tcw.copy_(t_)
+            enc.encode(feats[: b1 - b0], frame_embed=False, tc=True, seq_out=seq[b0:b1], tc_out=tcw[b0:b1])
         ac, tc = ops.score_videos(seq, tcw, first, vcls, centroids)
         host_ac.copy_(ac, non_blocking=True)
         host_tc.copy_(tc, non_blocking=True)
@@ -428,7 +442,9 @@ def run_score(args, world, rank, dev):
         return None
     conv_ms = stage_ms["conv_encoders"] / max(ncalls, 1)
     achieved = CONV_FLOP_PER_WINDOW * CH / (conv_ms * 1e-3) / 1e12
-    peak, kname = PEAK_BY_COMPUTE[args.compute]
+    _, kname = PEAK_BY_COMPUTE[args.compute]
+    pk = device_peaks()
+    peak = {"f16": pk["f16"], "f32x3": pk["f16"] / 3, "f32": pk["f32"]}[args.compute]
     total_videos = (args.clips if cfg5 else world * V) * args.steps
     if cfg5:
         workload = (f"BASELINE config 5: {args.clips} synthetic 64-frame clips (5 windows each) sharded over "
@@ -458,7 +474,7 @@ def run_score(args, world, rank, dev):
         "config": {"workload": workload, "clips_per_gpu": V, "frames_per_clip": T, "windows_per_step_per_gpu": NW,
                    "windows_per_encode": CH, "parallelism": f"video-sharded x{world}"},
         "roofline": {"bound": "mfma", "kernel": kname,
-                     "achieved": achieved, "peak": peak, "unit": "TFLOP/s",
+                     "achieved": achieved, "peak": peak, "peak_source": pk["source"], "unit": "TFLOP/s",
                      "frac": achieved / peak, "traffic": pmc_traffic(args.compute, CH),
                      "flop_per_launch": CONV_FLOP_PER_WINDOW * CH, "avg_launch_ms": conv_ms},
         "stage_ms": {k: v / max(ncalls, 1) for k, v in stage_ms.items()},

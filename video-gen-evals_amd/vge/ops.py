@@ -146,15 +146,21 @@ class Encoder:
                 L.check(self._lib.vge_encoder_reserve(self._h, int(max_windows)), "vge_encoder_reserve")
             self.capacity = int(max_windows)
 
-    def encode(self, feats: torch.Tensor, frame_embed: bool = False, tc: bool = True):
-        """feats [B,32,2596] -> (seq_embed [B,256], frame_embeds [B,33,256] | None, tc_window [B] | None)."""
+    def encode(self, feats: torch.Tensor, frame_embed: bool = False, tc: bool = True,
+               seq_out: Optional[torch.Tensor] = None, tc_out: Optional[torch.Tensor] = None):
+        """feats [B,32,2596] -> (seq_embed [B,256], frame_embeds [B,33,256] | None, tc_window [B] | None).
+        seq_out / tc_out: optional contiguous float32 destinations ([B,256] / [B]) written in place."""
         B, T, D = feats.shape
         if D != FEAT_DIM:
             raise L.VgeError(f"feats last dim {D} != {FEAT_DIM}")
+        for t, shape in ((seq_out, (B, D_MODEL)), (tc_out, (B,))):
+            if t is not None and (tuple(t.shape) != shape or t.dtype != torch.float32 or not t.is_contiguous()
+                                  or t.device != feats.device):
+                raise L.VgeError(f"encode: output must be a contiguous float32 {shape} tensor on {feats.device}")
         self.reserve(B)
-        seq = torch.empty((B, D_MODEL), device=feats.device, dtype=torch.float32)
+        seq = seq_out if seq_out is not None else torch.empty((B, D_MODEL), device=feats.device, dtype=torch.float32)
         fe = torch.empty((B, T + 1, D_MODEL), device=feats.device, dtype=torch.float32) if frame_embed else None
-        tcw = torch.empty((B,), device=feats.device, dtype=torch.float32) if tc else None
+        tcw = (tc_out if tc_out is not None else torch.empty((B,), device=feats.device, dtype=torch.float32)) if tc else None
         L.check(self._lib.vge_encode(self._h, _ptr(feats), B, T, _ptr(seq), _ptr(fe), _ptr(tcw), _stream(feats.device)),
                 "vge_encode")
         return seq, fe, tcw
