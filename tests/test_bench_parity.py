@@ -127,3 +127,23 @@ def test_f16_unit_kernel_matches_quad_kernel(n, monkeypatch):
     if n >= 64:  # deterministic per window whatever unit it lands in
         s2, _, _ = unit.encode(feats[:64].contiguous(), frame_embed=False, tc=True)
         assert torch.equal(s2, s_u[:64])
+
+
+def test_f16_unit_kernel_is_position_independent_at_4096_windows():
+    """Config 5's encode chunk (4,096 windows: 27 rounds of 5- and 6-window units) checked without the oracle, by a
+    property that pins the schedule: every window's outputs depend only on that window (per-window exponents, the
+    same chunk order), so encoding a 256-window slice alone (two rounds, quint / hex / quad units) must reproduce its
+    rows of the 4,096-window encode bit for bit, wherever the big schedule placed them."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vge import ops, synth
+    sd = synth.make_state_dict(synth.DIMS_RAW, synth.DIMS_DIFF)
+    g = torch.Generator(device=DEV).manual_seed(11)
+    feats = torch.randn((4096, 32, ops.FEAT_DIM), device=DEV, generator=g)
+    enc = ops.Encoder(sd, device=DEV, compute="f16")
+    enc.reserve(4096)
+    seq, _, tcw = enc.encode(feats, frame_embed=False, tc=True)
+    assert torch.isfinite(seq).all() and torch.isfinite(tcw).all()
+    for lo in (0, 1000, 3840):
+        s2, _, t2 = enc.encode(feats[lo:lo + 256].contiguous(), frame_embed=False, tc=True)
+        assert torch.equal(s2, seq[lo:lo + 256]) and torch.equal(t2, tcw[lo:lo + 256]), lo
