@@ -243,6 +243,9 @@ def main():
     ap.add_argument("--chunk-clips", type=int, default=32, help="e2e: clips per extraction pass (frames in HBM)")
     ap.add_argument("--no-parity-mode", action="store_true",
                     help="score: skip the second (f32x3) run reported as parity_mode beside an f16 headline")
+    ap.add_argument("--serial-featurize", action="store_true",
+                    help="score/cfg5: featurise each chunk on the encode stream right before it (default: the next "
+                         "chunk is featurised on a second stream beside the current chunk's fusion + transformer)")
     ap.add_argument("--serial-extract", action="store_true",
                     help="e2e: run TokenHMR and DWPose one after the other on one stream (default: two streams)")
     ap.add_argument("--no-detector", action="store_true",
@@ -391,19 +394,48 @@ def run_score(args, world, rank, dev):
     host_ac = torch.empty((V,), dtype=torch.float32, pin_memory=True)
     host_tc = torch.empty((V,), dtype=torch.float64, pin_memory=True)
     n_chunks = (NW + CH - 1) // CH
-    fe0 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps * n_chunks)]
-    fe1 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps * n_chunks)]
+    fe0 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps * n_chunks + 1)]
+    fe1 = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps * n_chunks + 1)]
+    n_fe = [0]  # featurise launches timed so far (inside the timed steps)
+    timing = [False]
+    side = torch.cuda.Stream(device=dev)
+    feat_ready = torch.cuda.Event()
+    pending = [None]  # the chunk whose featurise is already enqueued on `side`
+
+    def featurize_chunk(c, stream):
+        b0, b1 = c * CH, min(NW, (c + 1) * CH)
+        k = n_fe[0] if timing[0] else None
+        if k is not None:
+            fe0[k].record(stream)
+        ops.featurize(gstore, windows[b0:b1], stats.mean, stats.std, out=feats[: b1 - b0])
+        if k is not None:
+            fe1[k].record(stream)
+            n_fe[0] += 1
+
+    def launch_feat(c):
+        # featurise chunk c on the side stream once the last encode's conv stage (the last reader of feats) is done:
+        # it runs beside that chunk's fusion + transformer (a featurise workgroup fits next to a transformer
+        # workgroup on a CU: 16 KB of LDS and 141 registers per lane on top of 139 KB and 325)
+        with torch.cuda.stream(side):
+            enc.wait_conv(side)
+            featurize_chunk(c, side)
+            feat_ready.record(side)
+        pending[0] = c
 
     def step(i=None):
         ac = tc = None
+        cur = torch.cuda.current_stream()
         for c in range(n_chunks):
             b0, b1 = c * CH, min(NW, (c + 1) * CH)
-            if i is not None:
-                fe0[i * n_chunks + c].record()
-            ops.featurize(gstore, windows[b0:b1], stats.mean, stats.std, out=feats[: b1 - b0])
-            if i is not None:
-                fe1[i * n_chunks + c].record()
+            if args.serial_featurize:
+                featurize_chunk(c, cur)
+            else:
+                if pending[0] != c:
+                    launch_feat(c)
+                cur.wait_event(feat_ready)
             enc.encode(feats[: b1 - b0], frame_embed=False, tc=True, seq_out=seq[b0:b1], tc_out=tcw[b0:b1])
+            if not args.serial_featurize:
+                launch_feat((c + 1) % n_chunks)  # the next chunk, or the next step's first
         ac, tc = ops.score_videos(seq, tcw, first, vcls, centroids)
         host_ac.copy_(ac, non_blocking=True)
         host_tc.copy_(tc, non_blocking=True)
@@ -423,10 +455,12 @@ def run_score(args, world, rank, dev):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    timing[0] = True
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
     torch.cuda.synchronize()
+    timing[0] = False
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
@@ -436,7 +470,7 @@ def run_score(args, world, rank, dev):
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
     dt = float(dt_t.item())
     stage_ms, ncalls = enc.profile_read()
-    feat_ms = sum(a.elapsed_time(b) for a, b in zip(fe0, fe1)) / max(1, args.steps * n_chunks)
+    feat_ms = sum(fe0[k].elapsed_time(fe1[k]) for k in range(n_fe[0])) / max(1, n_fe[0])
     assert np.isfinite(host_ac.numpy()).all() and np.isfinite(host_tc.numpy()).all()
     if rank != 0:
         return None
@@ -478,7 +512,7 @@ def run_score(args, world, rank, dev):
                      "frac": achieved / peak, "traffic": pmc_traffic(args.compute, CH),
                      "flop_per_launch": CONV_FLOP_PER_WINDOW * CH, "avg_launch_ms": conv_ms},
         "stage_ms": {k: v / max(ncalls, 1) for k, v in stage_ms.items()},
-        "featurize": {"avg_ms": feat_ms, "bound": "hbm",
+        "featurize": {"avg_ms": feat_ms, "bound": "hbm", "overlapped": not args.serial_featurize,
                       "achieved_GBs": FEAT_BYTES_PER_WINDOW * CH / (feat_ms * 1e-3) / 1e9, "peak_GBs": HBM_PEAK_GBS},
         "encoder_tflops_2.0203GF_per_window": ENCODER_FLOP_PER_WINDOW * NW * args.steps / dt / 1e12,
         "setup_s": setup_s,

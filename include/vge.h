@@ -149,6 +149,11 @@ int vge_encoder_reserve(vge_encoder* enc, int max_windows);
 int vge_encoder_destroy(vge_encoder* enc);
 int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_embed, float* frame_embed,
                float* tc_window, vge_stream_t stream);
+/* Pipelining hook (no reference counterpart; the reference featurises batch k+1 in DataLoader workers while batch k
+ * is encoded, eval.py:410-418): make `stream` wait until the conv stage of the most recent vge_encode on this
+ * encoder -- the last reader of its feats -- has finished, so the next batch's vge_featurize can overwrite feats on
+ * `stream` while this batch's fusion / transformer still run. */
+int vge_encoder_wait_conv(vge_encoder* enc, vge_stream_t stream);
 
 /* Per-stage device time of vge_encode, measured with hipEvents recorded on the encode stream around
  * each stage (used by bench.py for the roofline line).  profile_begin pre-creates events for up to

@@ -147,3 +147,31 @@ def test_f16_unit_kernel_is_position_independent_at_4096_windows():
     for lo in (0, 1000, 3840):
         s2, _, t2 = enc.encode(feats[lo:lo + 256].contiguous(), frame_embed=False, tc=True)
         assert torch.equal(s2, seq[lo:lo + 256]) and torch.equal(t2, tcw[lo:lo + 256]), lo
+
+
+@pytest.mark.parametrize("n", [1, 37, 256, 293, 4096])
+def test_f16_unit_table_built_on_device_matches_host_spec(n):
+    """vge_encode builds the unit table on the device (conv_f16w_table_kernel: no host round trip inside encode); it
+    must equal the host specification (conv_f16w_schedule via vge_debug_conv_schedule) entry for entry."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import ctypes as C
+
+    import numpy as np
+    from vge import lib, ops, synth
+    so = lib.load()
+    sd = synth.make_state_dict(synth.DIMS_RAW, synth.DIMS_DIFF)
+    enc = ops.Encoder(sd, device=DEV, compute="f16")
+    enc.reserve(n)
+    enc.encode(torch.zeros((n, 32, ops.FEAT_DIM), device=DEV), tc=False)
+    torch.cuda.synchronize()
+    ptr, G, R = C.c_void_p(), C.c_int(), C.c_int()
+    assert so.vge_debug_encoder_units(enc._h, C.byref(ptr), C.byref(G), C.byref(R)) == 0
+    dev_tab = torch.empty(G.value * R.value, dtype=torch.int32, device=DEV)
+    C.CDLL("libamdhip64.so").hipMemcpy(C.c_void_p(dev_tab.data_ptr()), ptr, C.c_size_t(dev_tab.numel() * 4), 3)
+    cap = 10 * n + 1024
+    host = np.zeros(cap, np.int32)
+    Gh, Rh = C.c_int(), C.c_int()
+    m = so.vge_debug_conv_schedule(n, 6, host.ctypes.data_as(C.c_void_p), cap, C.byref(Gh), C.byref(Rh))
+    assert (Gh.value, Rh.value) == (G.value, R.value) and m == G.value * R.value
+    assert np.array_equal(dev_tab.cpu().numpy(), host[:m])

@@ -49,7 +49,8 @@ struct GemmArgsX3Host {
   const float* cs;
 };
 hipError_t launch_conv_encoders_x3(const float*, int, const void*, int, float*, bool, bool, hipStream_t);
-bool conv_f16w_schedule(int n_windows, int n_enc, int wmax, std::vector<int>& table, int& G, int& R);
+bool conv_f16w_plan(int n_windows, int n_enc, int wmax, int& G, int& R, int& U);
+hipError_t launch_conv_f16w_table(int n_windows, int n_enc, int G, int R, int U, int* d_table, hipStream_t s);
 hipError_t launch_conv_encoders_f16w(const float*, int, const void*, float*, const int*, int, int, hipStream_t);
 hipError_t launch_gemm_x3(int, const GemmArgsX3Host&, hipStream_t);
 struct FfnArgsX3Host {
@@ -221,13 +222,13 @@ struct vge_encoder {
   std::vector<vge::TxLayerX3Host> tx_layers;  // x3: the fused transformer kernel's layer table
   bool tx_fused = true;           // x3: one fused transformer launch (VGE_X3_UNFUSED=1: per-layer kernels)
   int f16_mix = 0;                // VGE_F16: stages kept in 3xfp16 (bit 0 stem, bit 1 transformer; VGE_F16_MIX)
-  // VGE_F16 with the stem unsplit: the 4-wave conv kernel with units of up to `f16w` windows (VGE_F16W; 0 = the 8-wave
-  // quad/pair kernel); its unit table for batch units_B lives in d_units (uploaded from units_host on the stream)
+  // VGE_F16 with the stem unsplit: the unit-table conv kernel with units of up to `f16w` windows (VGE_F16W; 0 = the
+  // quad / pair kernel); its table for batch units_B lives in d_units (sized by vge_encoder_reserve, built on the
+  // device by vge_encode when the batch size changes)
   int f16w = 6;
   int* d_units = nullptr;
-  size_t units_cap = 0;
   int units_B = 0, units_G = 0, units_R = 0;
-  std::vector<int> units_host;
+  hipEvent_t conv_done = nullptr;  // recorded after the conv stage of every vge_encode (vge_encoder_wait_conv)
   vge::FuseParamsHost fuse{};
   const void* Wov = nullptr;      // packed (f32 chunks or fp16 chunks)
   const float* Wov_cs = nullptr;  // x3: its column scales
@@ -696,6 +697,8 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
     he = vge::transformer_x3_kernel_setup();
     if (he != hipSuccess) return hipfail(he);
   }
+  he = hipEventCreateWithFlags(&enc->conv_done, hipEventDisableTiming);
+  if (he != hipSuccess) return hipfail(he);
   *out = enc;
   return VGE_OK;
 }
@@ -723,7 +726,18 @@ int vge_encoder_reserve(vge_encoder* enc, int B) {
   enc->att = p; p += n_att;
   enc->x1 = p; p += n_x1;
   enc->h = p;
+  if (enc->d_units) (void)hipFree(enc->d_units);
+  enc->d_units = nullptr;
+  enc->units_B = 0;
+  he = hipMalloc(&enc->d_units, ((size_t)10 * B + 1024) * sizeof(int));  // >= R * G for any batch <= B
+  if (he != hipSuccess) return fail(VGE_ERR_NOMEM, std::string("vge_encoder_reserve: ") + hipGetErrorString(he));
   enc->cap = B;
+  return VGE_OK;
+}
+
+int vge_encoder_wait_conv(vge_encoder* enc, vge_stream_t stream) {
+  if (!enc) return fail(VGE_ERR_ARG, "vge_encoder_wait_conv: null encoder");
+  HIPCHK(hipStreamWaitEvent(S(stream), enc->conv_done, 0));
   return VGE_OK;
 }
 
@@ -770,6 +784,16 @@ extern "C" int vge_debug_encoder_images(const vge_encoder* enc, const void** hbu
   return VGE_OK;
 }
 
+// Test hook: the device-built unit table of the last vge_encode's batch (tests compare it with the host spec,
+// vge_debug_conv_schedule).
+extern "C" int vge_debug_encoder_units(const vge_encoder* enc, const void** table, int* G, int* R) {
+  if (!enc || !table || !G || !R) return fail(VGE_ERR_ARG, "vge_debug_encoder_units: null argument");
+  *table = enc->d_units;
+  *G = enc->units_G;
+  *R = enc->units_R;
+  return VGE_OK;
+}
+
 int vge_encoder_destroy(vge_encoder* enc) {
   if (!enc) return VGE_OK;
   for (hipEvent_t e : enc->prof_ev) (void)hipEventDestroy(e);
@@ -777,6 +801,7 @@ int vge_encoder_destroy(vge_encoder* enc) {
   if (enc->d_encs) (void)hipFree(enc->d_encs);
   if (enc->wbuf) (void)hipFree(enc->wbuf);
   if (enc->d_units) (void)hipFree(enc->d_units);
+  if (enc->conv_done) (void)hipEventDestroy(enc->conv_done);
   if (enc->hbuf) (void)hipFree(enc->hbuf);
   delete enc;
   return VGE_OK;
@@ -806,21 +831,10 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
   };
   HIPCHK(mark(0));
   if (x3 && !split && !(enc->f16_mix & 1) && enc->f16w > 0) {
-    if (B != enc->units_B) {  // new batch size: build and upload the unit table (stream-ordered)
-      std::vector<int> tab;
-      int G = 0, R = 0;
-      if (!vge::conv_f16w_schedule(B, 10, enc->f16w, tab, G, R)) return fail(VGE_ERR_ARG, "vge_encode: batch too large");
-      HIPCHK(hipStreamSynchronize(s));  // the previous table's upload has completed
-      if (tab.size() > enc->units_cap) {
-        if (enc->d_units) HIPCHK(hipFree(enc->d_units));
-        enc->d_units = nullptr;
-        enc->units_cap = 0;
-        HIPCHK(hipMalloc(&enc->d_units, tab.size() * sizeof(int)));
-        enc->units_cap = tab.size();
-      }
-      enc->units_host.swap(tab);
-      HIPCHK(hipMemcpyAsync(enc->d_units, enc->units_host.data(), enc->units_host.size() * sizeof(int),
-                            hipMemcpyHostToDevice, s));
+    if (B != enc->units_B) {  // new batch size: the unit table, built on the device (stream-ordered, no host copy)
+      int G = 0, R = 0, U = 0;
+      if (!vge::conv_f16w_plan(B, 10, enc->f16w, G, R, U)) return fail(VGE_ERR_ARG, "vge_encode: batch too large");
+      HIPCHK(vge::launch_conv_f16w_table(B, 10, G, R, U, enc->d_units, s));
       enc->units_B = B;
       enc->units_G = G;
       enc->units_R = R;
@@ -832,6 +846,7 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
   } else {
     HIPCHK(vge::launch_conv_encoders(feats, B, enc->d_encs, 10, enc->enc_out, s));
   }
+  HIPCHK(hipEventRecord(enc->conv_done, s));
   HIPCHK(mark(1));
   HIPCHK(vge::launch_fuse(enc->enc_out, frames, enc->fuse, enc->pooled, s));
   HIPCHK(mark(2));

@@ -815,7 +815,8 @@ __device__ __forceinline__ void conv_f16w_body(const float* __restrict__ feats, 
 }
 
 // Pure fp16 mode (VGE_F16 with nothing split): one 512-thread workgroup per CU (8 waves, wave w = columns 32w..32w+31
-// of all rows), units of 1..6 windows of one encoder from a host-built table (conv_f16w_schedule), run by
+// of all rows), units of 1..6 windows of one encoder from a table (conv_f16w_schedule; built on the device by
+// conv_f16w_table_kernel), run by
 // conv_f16w_body.  The weight stream is paid per unit (~28.5 k cycles per conv whatever the unit's rows), so the
 // number of units per CU is what sets the time: at 256 windows every CU runs two units (quint + quint, or hex +
 // quad; 10 windows) instead of the quad kernel's three (quad + quad + pair).  Measured (256 / 4,096 windows):
@@ -1366,6 +1367,59 @@ bool conv_f16w_schedule(int n_windows, int n_enc, int wmax, std::vector<int>& ta
     table[(size_t)r * G + p] = units[k].e | (units[k].w << 4) | (units[k].w0 << 8);
   }
   return true;
+}
+
+// The plan of conv_f16w_schedule without the table: grid G, rounds R and unit count U (upper bound of the table:
+// R * G <= 10 * n_windows + CUs).
+bool conv_f16w_plan(int n_windows, int n_enc, int wmax, int& G, int& R, int& U) {
+  if (n_windows < 1 || n_enc < 1 || n_enc > 16 || n_windows > (1 << 23)) return false;
+  wmax = std::max(1, std::min(wmax, F16W_MAX));
+  const long long P = (long long)n_windows * n_enc;
+  const int n_cu = conv_cu_count();
+  for (R = 1;; ++R) {
+    const int Ut = (int)std::min<long long>((long long)n_cu * R, P);
+    bool ok = true;
+    U = 0;
+    for (int e = 0; e < n_enc && ok; ++e) {
+      const int ue = std::min(n_windows, Ut / n_enc + (e < Ut % n_enc));
+      ok = ue >= 1 && (n_windows + ue - 1) / ue <= wmax;
+      U += ue;
+    }
+    if (ok) break;
+  }
+  G = std::min(n_cu, U);
+  R = (U + G - 1) / G;
+  return true;
+}
+
+}  // namespace vge
+namespace {
+// Device twin of conv_f16w_schedule's table (so vge_encode builds it without host round trips: capture-safe): the
+// same units (encoder e cut into u_e nearly equal runs), the same stable order (size descending, then encoder-major)
+// as a counting pass per size, the same snake dealing.  One thread: it runs only when the batch size changes.
+__global__ void conv_f16w_table_kernel(int n_windows, int n_enc, int G, int R, int U, int* __restrict__ table) {
+  for (int i = threadIdx.x; i < G * R; i += blockDim.x) table[i] = -1;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  int k = 0;
+  for (int sz = F16W_MAX; sz >= 1; --sz)
+    for (int e = 0; e < n_enc; ++e) {
+      const int ue = min(n_windows, U / n_enc + (e < U % n_enc));
+      for (int j = 0; j < ue; ++j) {
+        const int a = (int)((long long)j * n_windows / ue), b = (int)((long long)(j + 1) * n_windows / ue);
+        if (b - a != sz) continue;
+        const int r = k / G, q = k % G, pos = (r & 1) ? G - 1 - q : q;
+        table[r * G + pos] = e | (sz << 4) | (a << 8);
+        ++k;
+      }
+    }
+}
+}  // namespace
+namespace vge {
+
+hipError_t launch_conv_f16w_table(int n_windows, int n_enc, int G, int R, int U, int* d_table, hipStream_t s) {
+  hipLaunchKernelGGL(conv_f16w_table_kernel, dim3(1), dim3(256), 0, s, n_windows, n_enc, G, R, U, d_table);
+  return hipGetLastError();
 }
 
 hipError_t launch_conv_encoders_f16w(const float* feats, int n_windows, const void* encs, float* enc_out,

@@ -17,7 +17,8 @@ VGE_ERR_UNSUPPORTED = 7
 EXPORTS = ["vge_featurize", "vge_stats_workspace_bytes", "vge_stats_accumulate", "vge_stats_finalize",
            "vge_encoder_create", "vge_encoder_reserve", "vge_encoder_destroy", "vge_encode", "vge_tc_windows",
            "vge_score_videos", "vge_centroid_accumulate", "vge_centroid_finalize", "vge_last_error", "vge_version",
-           "vge_encoder_profile_begin", "vge_encoder_profile_read", "vge_ingest_probe", "vge_ingest_decode",
+           "vge_encoder_profile_begin", "vge_encoder_profile_read", "vge_encoder_wait_conv", "vge_ingest_probe",
+           "vge_ingest_decode",
            "vge_ingest_default_threads",
            "vge_hmr_create", "vge_hmr_reserve", "vge_hmr_destroy", "vge_hmr_extract", "vge_hmr_profile_begin",
            "vge_hmr_profile_read", "vge_op_gemm_bf16", "vge_op_vit_attention", "vge_op_layernorm_bf16",
@@ -85,6 +86,7 @@ def load() -> C.CDLL:
         "vge_centroid_accumulate": [vp, vp, i32, i32, i32, vp, vp, vp],
         "vge_centroid_finalize": [vp, vp, i32, i32, vp, vp],
         "vge_encoder_profile_begin": [vp, i32],
+        "vge_encoder_wait_conv": [vp, vp],
         "vge_encoder_profile_read": [vp, C.POINTER(C.c_double), C.POINTER(C.c_int)],
         "vge_last_error": [],
         "vge_version": [],

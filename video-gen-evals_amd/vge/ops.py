@@ -165,6 +165,13 @@ class Encoder:
                 "vge_encode")
         return seq, fe, tcw
 
+    def wait_conv(self, stream: Optional[torch.cuda.Stream] = None) -> None:
+        """Make `stream` (default: the current stream) wait until the conv stage of the last encode() -- the last
+        reader of its feats -- has finished (vge_encoder_wait_conv): the next batch can be featurised into the same
+        buffer on another stream while this batch's fusion / transformer run."""
+        st = (stream if stream is not None else torch.cuda.current_stream()).cuda_stream
+        L.check(self._lib.vge_encoder_wait_conv(self._h, st), "vge_encoder_wait_conv")
+
     STAGES = ("conv_encoders", "fusion_pool", "token_gemm", "transformer", "outputs_tc")
 
     def profile_begin(self, max_calls: int) -> None:
