@@ -175,3 +175,42 @@ def test_f16_unit_table_built_on_device_matches_host_spec(n):
     m = so.vge_debug_conv_schedule(n, 6, host.ctypes.data_as(C.c_void_p), cap, C.byref(Gh), C.byref(Rh))
     assert (Gh.value, Rh.value) == (G.value, R.value) and m == G.value * R.value
     assert np.array_equal(dev_tab.cpu().numpy(), host[:m])
+
+
+def test_featurize_pipelined_on_a_side_stream_matches_serial():
+    """bench.py's pipelining protocol: chunk c+1 is featurised into the SAME feats buffer on a side stream after
+    vge_encoder_wait_conv (encode c's conv stage has consumed feats) while encode c's fusion / transformer run; the
+    encode of c+1 waits for that featurise.  Outputs must equal the serial order bit for bit."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vge import ops
+    from vge.data import pack_frame_store
+    o = _oracle(256)
+    store = ops.DeviceFrameStore.from_host(pack_frame_store(o["clips"], [f"g{i}" for i in range(256)], ["X"] * 256), DEV)
+    mean, std = torch.from_numpy(o["mean"]).to(DEV), torch.from_numpy(o["std"]).to(DEV)
+    win = torch.tensor([[v, 0] for v in range(256)], dtype=torch.int32, device=DEV)
+    enc = ops.Encoder(o["sd"], device=DEV, compute="f16")
+    enc.reserve(64)
+    chunks = [(c * 64, (c + 1) * 64) for c in range(4)]
+    feats = torch.empty((64, 32, ops.FEAT_DIM), device=DEV)
+    serial = torch.empty((256, 256), device=DEV)
+    for b0, b1 in chunks:
+        ops.featurize(store, win[b0:b1], mean, std, out=feats)
+        enc.encode(feats, tc=False, seq_out=serial[b0:b1])
+    piped = torch.empty((256, 256), device=DEV)
+    side, ready = torch.cuda.Stream(device=DEV), torch.cuda.Event()
+    cur = torch.cuda.current_stream()
+    with torch.cuda.stream(side):
+        side.wait_stream(cur)
+        ops.featurize(store, win[0:64], mean, std, out=feats)
+        ready.record(side)
+    for c, (b0, b1) in enumerate(chunks):
+        cur.wait_event(ready)
+        enc.encode(feats, tc=False, seq_out=piped[b0:b1])
+        if c + 1 < len(chunks):
+            with torch.cuda.stream(side):
+                enc.wait_conv(side)
+                ops.featurize(store, win[chunks[c + 1][0]:chunks[c + 1][1]], mean, std, out=feats)
+                ready.record(side)
+    torch.cuda.synchronize()
+    assert torch.equal(piped, serial)
