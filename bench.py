@@ -8,7 +8,9 @@
 Workload (config 2 of BASELINE.json, "1 MI355X bf16"): 256 synthetic 32-frame clips per GPU with
 pre-extracted per-frame features (SMPL rotations, betas, 1024-d token, 120-d keypoints) resident in
 HBM.  One step = featurise all windows (HIP) -> HumanActionScorer forward (MFMA) -> per-video AC + TC
-(HIP reductions) -> scores copied to pinned host memory.  ModalityStats and the real-class centroids
+(HIP reductions) -> scores copied to pinned host memory; each chunk's featurise is issued on a side stream once the
+previous encode's conv stage has consumed the feats buffer (vge_encoder_wait_conv), so it overlaps that chunk's
+fusion + transformer (--serial-featurize: the plain serial order; every step's work stays inside the timed region).  ModalityStats and the real-class centroids
 (the real set is sharded over ranks, sufficient statistics all-gathered over RCCL) are built once in
 the setup phase (`setup_s`).  Weak scaling: every rank scores its own 256 clips; no collective in the
 step.  Compute mode: `f16` (VGE_F16: fp16 MFMA conv encoders, 3xfp16 transformer -- the config's 16-bit
