@@ -453,6 +453,9 @@ def run_score(args, world, rank, dev):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    # inside the timed steps only the conv stage's two events are recorded (each event is a queue marker: all six
+    # stage markers measured -1.3 % videos/s); the other stages are timed on untimed steps afterwards
+    enc.profile_mask(0x3)
     enc.profile_begin(args.steps * n_chunks)
     if world > 1:
         dist.barrier()
@@ -472,6 +475,15 @@ def run_score(args, world, rank, dev):
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
     dt = float(dt_t.item())
     stage_ms, ncalls = enc.profile_read()
+    n_extra = 5
+    enc.profile_mask(0x3F)
+    enc.profile_begin(n_extra * n_chunks)
+    for _ in range(n_extra):
+        step()
+    torch.cuda.synchronize()
+    stage_x, ncalls_x = enc.profile_read()
+    stage_out = {k: (v / max(ncalls, 1) if k == "conv_encoders" else stage_x[k] / max(ncalls_x, 1))
+                 for k, v in stage_ms.items()}
     feat_ms = sum(fe0[k].elapsed_time(fe1[k]) for k in range(n_fe[0])) / max(1, n_fe[0])
     assert np.isfinite(host_ac.numpy()).all() and np.isfinite(host_tc.numpy()).all()
     if rank != 0:
@@ -513,7 +525,8 @@ def run_score(args, world, rank, dev):
                      "achieved": achieved, "peak": peak, "peak_source": pk["source"], "unit": "TFLOP/s",
                      "frac": achieved / peak, "traffic": pmc_traffic(args.compute, CH),
                      "flop_per_launch": CONV_FLOP_PER_WINDOW * CH, "avg_launch_ms": conv_ms},
-        "stage_ms": {k: v / max(ncalls, 1) for k, v in stage_ms.items()},
+        "stage_ms": stage_out,
+        "stage_ms_source": "conv_encoders: hipEvents in the timed steps; the other stages: 5 untimed steps after them",
         "featurize": {"avg_ms": feat_ms, "bound": "hbm", "overlapped": not args.serial_featurize,
                       "achieved_GBs": FEAT_BYTES_PER_WINDOW * CH / (feat_ms * 1e-3) / 1e9, "peak_GBs": HBM_PEAK_GBS},
         "encoder_tflops_2.0203GF_per_window": ENCODER_FLOP_PER_WINDOW * NW * args.steps / dt / 1e12,

@@ -164,6 +164,10 @@ int vge_encoder_wait_conv(vge_encoder* enc, vge_stream_t stream);
 #define VGE_N_STAGES 5
 int vge_encoder_profile_begin(vge_encoder* enc, int max_calls);
 int vge_encoder_profile_read(vge_encoder* enc, double* stage_ms, int* n_calls);
+/* Which of the VGE_N_STAGES + 1 stage-boundary events profiled vge_encode calls record (bit k = event before stage k;
+ * default all): each event is a queue marker, so a timed loop that only needs the conv stage records 0x3 and
+ * profile_read reports the stages both of whose events were recorded (the others as 0). */
+int vge_encoder_profile_mask(vge_encoder* enc, int event_mask);
 
 /* ---------------------------------------------------------------------------------------------
  * Metrics.

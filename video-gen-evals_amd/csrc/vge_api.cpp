@@ -244,6 +244,8 @@ struct vge_encoder {
   // profiling (hipEvents recorded around the stages of vge_encode)
   std::vector<hipEvent_t> prof_ev;   // (VGE_N_STAGES + 1) per call
   int prof_max = 0, prof_calls = 0;
+  int prof_mask = (1 << (VGE_N_STAGES + 1)) - 1;  // which stage-boundary events vge_encode records (profile_mask)
+  hipEvent_t last_conv = nullptr;                 // the event vge_encoder_wait_conv waits on
   // workspace
   int cap = 0;
   float* ws = nullptr;
@@ -735,9 +737,16 @@ int vge_encoder_reserve(vge_encoder* enc, int B) {
   return VGE_OK;
 }
 
+int vge_encoder_profile_mask(vge_encoder* enc, int event_mask) {
+  if (!enc || event_mask < 0 || event_mask >= (1 << (VGE_N_STAGES + 1)))
+    return fail(VGE_ERR_ARG, "vge_encoder_profile_mask: bad argument");
+  enc->prof_mask = event_mask;
+  return VGE_OK;
+}
+
 int vge_encoder_wait_conv(vge_encoder* enc, vge_stream_t stream) {
   if (!enc) return fail(VGE_ERR_ARG, "vge_encoder_wait_conv: null encoder");
-  HIPCHK(hipStreamWaitEvent(S(stream), enc->conv_done, 0));
+  if (enc->last_conv) HIPCHK(hipStreamWaitEvent(S(stream), enc->last_conv, 0));
   return VGE_OK;
 }
 
@@ -758,10 +767,13 @@ int vge_encoder_profile_read(vge_encoder* enc, double* stage_ms, int* n_calls) {
   if (!enc || !stage_ms || !n_calls) return fail(VGE_ERR_ARG, "vge_encoder_profile_read: bad argument");
   for (int k = 0; k < VGE_N_STAGES; ++k) stage_ms[k] = 0.0;
   const int n = std::min(enc->prof_calls, enc->prof_max);
+  int last = VGE_N_STAGES;
+  while (last > 0 && !((enc->prof_mask >> last) & 1)) --last;
   for (int c = 0; c < n; ++c) {
     hipEvent_t* ev = enc->prof_ev.data() + (size_t)c * (VGE_N_STAGES + 1);
-    HIPCHK(hipEventSynchronize(ev[VGE_N_STAGES]));
+    HIPCHK(hipEventSynchronize(ev[last]));
     for (int k = 0; k < VGE_N_STAGES; ++k) {
+      if (!((enc->prof_mask >> k) & 1) || !((enc->prof_mask >> (k + 1)) & 1)) continue;  // stage not bracketed
       float ms = 0.f;
       HIPCHK(hipEventElapsedTime(&ms, ev[k], ev[k + 1]));
       stage_ms[k] += ms;
@@ -817,7 +829,9 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
   const int frames = B * 32, M = B * 33;
   hipEvent_t* ev = nullptr;
   if (enc->prof_calls < enc->prof_max) ev = enc->prof_ev.data() + (size_t)(enc->prof_calls++) * (VGE_N_STAGES + 1);
-  auto mark = [&](int k) -> hipError_t { return ev ? hipEventRecord(ev[k], s) : hipSuccess; };
+  auto mark = [&](int k) -> hipError_t {
+    return (ev && ((enc->prof_mask >> k) & 1)) ? hipEventRecord(ev[k], s) : hipSuccess;
+  };
   const bool x3 = enc->mode == VGE_F32X3 || enc->mode == VGE_F16, split = enc->mode != VGE_F16;
   // one GEMM launcher for both modes (same epilogues; x3 = 3xfp16 split MFMA, f32 = exact f32 MFMA)
   auto gemm = [&](int epi, const float* A, int lda, const void* W, const float* cs, float* o, int ldo, int Mr, int K,
@@ -846,8 +860,14 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
   } else {
     HIPCHK(vge::launch_conv_encoders(feats, B, enc->d_encs, 10, enc->enc_out, s));
   }
-  HIPCHK(hipEventRecord(enc->conv_done, s));
-  HIPCHK(mark(1));
+  if (ev && (enc->prof_mask & 2)) {  // the conv-end profiling event doubles as the conv-done event (one marker)
+    HIPCHK(mark(1));
+    enc->last_conv = ev[1];
+  } else {
+    HIPCHK(hipEventRecord(enc->conv_done, s));
+    enc->last_conv = enc->conv_done;
+    HIPCHK(mark(1));
+  }
   HIPCHK(vge::launch_fuse(enc->enc_out, frames, enc->fuse, enc->pooled, s));
   HIPCHK(mark(2));
   if (x3 && enc->tx_fused) {  // tokens + all layers + outputs in one launch, one window per workgroup

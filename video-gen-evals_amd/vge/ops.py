@@ -165,6 +165,10 @@ class Encoder:
                 "vge_encode")
         return seq, fe, tcw
 
+    def profile_mask(self, event_mask: int) -> None:
+        """Stage-boundary events recorded by profiled encodes (bit k = before stage k; 0x3 = the conv stage only)."""
+        L.check(self._lib.vge_encoder_profile_mask(self._h, event_mask), "vge_encoder_profile_mask")
+
     def wait_conv(self, stream: Optional[torch.cuda.Stream] = None) -> None:
         """Make `stream` (default: the current stream) wait until the conv stage of the last encode() -- the last
         reader of its feats -- has finished (vge_encoder_wait_conv): the next batch can be featurised into the same
