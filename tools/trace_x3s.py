@@ -1,0 +1,76 @@
+#!/usr/bin/env python3
+"""Per-phase timeline of conv_encoder_x3s_kernel (the staggered split conv kernel) from a VGE_TRACE build
+(tools/build_x3s_variant.sh trace_s "-DVGE_TRACE"; s_memtime stamps of every wave of blocks 0..63, first unit):
+
+    VGE_LIB=.../build/trace_s/libvge.so python tools/trace_x3s.py [--windows 256]
+
+Phase p of a wave: task = [barrier exit of p-1, arrival at barrier p], wait = [arrival, exit].  Reported per half
+(A = waves 0-3, B = waves 4-7) as mean cycles over blocks and the half's waves, with the task kind (stem-epi, P1,
+P2, E<g>, idle) each half runs in that phase.
+"""
+import argparse
+import ctypes as C
+import json
+import sys
+from pathlib import Path
+
+import numpy as np
+
+ROOT = Path(__file__).resolve().parent.parent
+sys.path.insert(0, str(ROOT / "video-gen-evals_amd"))
+
+import torch  # noqa: E402
+
+from vge import lib, ops, synth  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--windows", type=int, default=256)
+a = ap.parse_args()
+dev = torch.device("cuda", 0)
+sd = synth.make_state_dict(synth.DIMS_RAW, synth.DIMS_DIFF)
+enc = ops.Encoder(sd, device=dev, compute="f32x3")
+x = torch.randn(a.windows, 32, 2596, device=dev)
+enc.reserve(a.windows)
+for _ in range(3):
+    enc.encode(x)
+torch.cuda.synchronize()
+enc.profile_begin(1)
+enc.encode(x)  # the traced launch is the last one: its wall time from the stage events
+torch.cuda.synchronize()
+conv_ms = enc.profile_read()[0]["conv_encoders"]
+L = lib.load()
+buf = (C.c_longlong * (64 * 8 * 128))()
+assert L.vge_debug_x3s_trace(buf, 64 * 8 * 128) == 0
+t = np.array(buf, dtype=np.int64).reshape(64, 8, 128).astype(np.float64)
+tasks = ["stem-epi"] + [f"{k}({g})" for g in range(9) for k in ("P1", "P2", "E")] + ["idle"]
+kc = float((t[:, 0, 121] - t[:, 0, 120]).mean())
+out = {"conv_ms": conv_ms, "kernel_cycles_block": kc, "clock_ghz": kc / (conv_ms * 1e6),
+       "blocks": 64, "unit_cycles": float((t[:, :, 59] - t[:, :, 0]).max(axis=1).mean()),
+       "stem_cycles": float((t[:, :, 1] - t[:, :, 0]).mean()), "phases": []}
+for p in range(29):
+    start = t[:, :, 1] if p == 0 else t[:, :, 3 + 2 * (p - 1)]
+    task = t[:, :, 2 + 2 * p] - start
+    wait = t[:, :, 3 + 2 * p] - t[:, :, 2 + 2 * p]
+    ka = tasks[p] if p < 28 else "idle"
+    kb = "idle" if p == 0 else tasks[p - 1]
+    out["phases"].append({"p": p, "A": ka, "B": kb, "phase": round(float((t[:, :, 3 + 2 * p] - start).mean())),
+                          "A_task": round(float(task[:, :4].mean())), "B_task": round(float(task[:, 4:].mean())),
+                          "A_wait": round(float(wait[:, :4].mean())), "B_wait": round(float(wait[:, 4:].mean()))})
+# epilogue internals (stem epilogue + 8 conv epilogues; the proj's has no exchange): compute, exchange, store
+names = ["stem"] + [f"E({g})" for g in range(8)]
+out["epilogues"] = {}
+for k, nm in enumerate(names):
+    b = 64 + 4 * k
+    d = {}
+    for half, ws in (("A", slice(0, 4)), ("B", slice(4, 8))):
+        x = t[:, ws, b:b + 4]
+        d[half] = [round(float((x[:, :, j + 1] - x[:, :, j]).mean())) for j in range(3)]
+    out["epilogues"][nm] = d
+print(json.dumps(out))
+print(f"conv {conv_ms:.4f} ms, kernel {kc:.0f} cycles per block -> {kc / (conv_ms * 1e6):.3f} GHz; unit "
+      f"{out['unit_cycles']:.0f} cycles, stem {out['stem_cycles']:.0f}")
+for nm, d in out["epilogues"].items():
+    print(f"{nm:>5s}  A compute/exchange/store {d['A']}   B {d['B']}")
+for ph in out["phases"]:
+    print(f"{ph['p']:2d} A {ph['A']:>8s} {ph['A_task']:7d} (+{ph['A_wait']:6d})   B {ph['B']:>8s} {ph['B_task']:7d} "
+          f"(+{ph['B_wait']:6d})   phase {ph['phase']:7d}")

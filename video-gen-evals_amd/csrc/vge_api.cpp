@@ -39,7 +39,7 @@ hipError_t launch_pack_x3(const float* W, int N, int K_real, int ldk, int conv, 
                           _Float16* out, hipStream_t s);
 struct EncDescX3Host {
   const _Float16* stem; const _Float16* conv; const _Float16* proj; const float* gn_w; const float* gn_b;
-  const float* cs;
+  const float* cs; const float* fold;
   int in_col, d_in, n_stem_panels, pad;
   float gn_gmax[4], gn_bmax[4];  // max |gamma|, max |beta| per GroupNorm
 };
@@ -49,6 +49,8 @@ struct GemmArgsX3Host {
   const float* cs;
 };
 hipError_t launch_conv_encoders_x3(const float*, int, const void*, int, float*, bool, bool, hipStream_t);
+hipError_t encoder_x3s_kernel_setup();
+hipError_t launch_conv_encoders_x3s(const float*, int, const void*, int, float*, hipStream_t);
 bool conv_f16w_plan(int n_windows, int n_enc, int wmax, int& G, int& R, int& U);
 hipError_t launch_conv_f16w_table(int n_windows, int n_enc, int G, int R, int U, int* d_table, hipStream_t s);
 hipError_t launch_conv_encoders_f16w(const float*, int, const void*, float*, const int*, int, int, hipStream_t);
@@ -221,6 +223,7 @@ struct vge_encoder {
   void* d_encs = nullptr;         // EncDescHost[10] or EncDescX3Host[10]
   std::vector<vge::TxLayerX3Host> tx_layers;  // x3: the fused transformer kernel's layer table
   bool tx_fused = true;           // x3: one fused transformer launch (VGE_X3_UNFUSED=1: per-layer kernels)
+  bool x3s = false;               // VGE_F32X3: the staggered conv kernel on GroupNorm-folded weights (VGE_X3S=0: off)
   int f16_mix = 0;                // VGE_F16: stages kept in 3xfp16 (bit 0 stem, bit 1 transformer; VGE_F16_MIX)
   // VGE_F16 with the stem unsplit: the unit-table conv kernel with units of up to `f16w` windows (VGE_F16W; 0 = the
   // quad / pair kernel); its table for batch units_B lives in d_units (sized by vge_encoder_reserve, built on the
@@ -405,7 +408,13 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
     return {o, 0};
   };
 
-  struct Off { Mat stem, conv, proj; size_t gnw, gnb; int in_col, d_in, P; };
+  // VGE_F32X3 runs the staggered conv kernel (vge_encoder_x3s.hip) unless VGE_X3S=0: each block's GroupNorm is folded
+  // into the next GEMM -- conv1 of blocks 1..3 and proj packed as W diag(gamma) -- plus the per-row corrections
+  // (sums of W gamma and W beta over the taps that fall inside the window; double, then f32)
+  const char* x3s_env = getenv("VGE_X3S");
+  const bool x3s = compute == VGE_F32X3 && !(x3s_env && x3s_env[0] == '0');
+  std::vector<std::vector<float>> folded;  // folded weight copies, alive until packed
+  struct Off { Mat stem, conv, proj; size_t gnw, gnb, fold; int in_col, d_in, P; };
   std::vector<Off> eoff(10);
   int col_raw = 0, col_diff = VGE_RAW_DIM;
   for (int kind = 0; kind < 2; ++kind) {
@@ -430,10 +439,47 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
         gb[b] = get(pre + ".blocks." + std::to_string(b) + ".norm.bias", {256});
       }
       if (!err.empty()) return bail();
+      const float* projw = proj;
+      o.fold = 0;
+      if (x3s) {
+        pk.resize((pk.size() + 63) / 64 * 64, 0.f);  // 256-B aligned: the kernel reads 16-B vectors
+        o.fold = pk.size();
+        pk.resize(pk.size() + 3 * 256 * 16 + 512, 0.f);
+        for (int b = 1; b <= 4; ++b) {  // GroupNorm b-1 folded into block b's conv1 (b < 4) or the proj (b == 4)
+          const float* g = gw[b - 1];
+          const float* be = gb[b - 1];
+          const float* src = b < 4 ? cw[2 * b] : proj;
+          const int ntap = b < 4 ? 5 : 1;
+          folded.emplace_back((size_t)256 * 256 * ntap);
+          float* f = folded.back().data();
+          for (size_t q = 0; q < folded.back().size(); ++q) f[q] = src[q] * g[(q / ntap) & 255];
+          parallel_for(256, [&](int n) {
+            double sg[5] = {0, 0, 0, 0, 0}, sb[5] = {0, 0, 0, 0, 0};
+            for (int ci = 0; ci < 256; ++ci)
+              for (int tap = 0; tap < ntap; ++tap) {
+                const size_t q = ((size_t)n * 256 + ci) * ntap + tap;
+                sg[tap] += f[q];
+                sb[tap] += (double)src[q] * be[ci];
+              }
+            if (b == 4) {
+              pk[o.fold + 3 * 256 * 16 + n * 2] = (float)sg[0];
+              pk[o.fold + 3 * 256 * 16 + n * 2 + 1] = (float)sb[0];
+              return;
+            }
+            // per-tap sums: the kernel adds the taps that fall inside the window for each of its rows
+            for (int tap = 0; tap < 5; ++tap) {
+              pk[o.fold + ((size_t)(b - 1) * 256 + n) * 16 + tap] = (float)sg[tap];
+              pk[o.fold + ((size_t)(b - 1) * 256 + n) * 16 + 8 + tap] = (float)sb[tap];
+            }
+          });
+          if (b < 4) cw[2 * b] = f;
+          else projw = f;
+        }
+      }
       o.stem = pack_lin(stem, 256, d_in, d_in, o.P);
       o.conv = pack_cv(cw[0]);
       for (int c = 1; c < 8; ++c) pack_cv(cw[c]);
-      o.proj = pack_lin(proj, 256, 256, 256, 1);
+      o.proj = pack_lin(projw, 256, 256, 256, 1);
       o.gnw = pk.size();
       for (int b = 0; b < 4; ++b) pk.insert(pk.end(), gw[b], gw[b] + 256);
       o.gnb = pk.size();
@@ -590,7 +636,9 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
         return fail(VGE_ERR_ARG, "vge_encoder_create: non-finite weight, not representable by the 3xfp16 split; use VGE_F32");
       }
   }
+  enc->x3s = x3s;
   hipError_t he = x3 ? vge::encoder_x3_kernel_setup() : vge::encoder_kernel_setup();
+  if (he == hipSuccess && x3s) he = vge::encoder_x3s_kernel_setup();
   if (he == hipSuccess) he = hipMalloc(&enc->wbuf, pk.size() * sizeof(float));
   if (he == hipSuccess) he = hipMemcpy(enc->wbuf, pk.data(), pk.size() * sizeof(float), hipMemcpyHostToDevice);
   if (he == hipSuccess && x3) he = hipMalloc(&enc->hbuf, ph_n * sizeof(_Float16));
@@ -639,7 +687,8 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
     {
       descs[e] = vge::EncDescX3Host{hb + eoff[e].stem.off, hb + eoff[e].conv.off, hb + eoff[e].proj.off,
                                     wb + eoff[e].gnw, wb + eoff[e].gnb, wb + eoff[e].stem.cs,  // [10][256] scales
-                                    eoff[e].in_col, eoff[e].d_in, eoff[e].P, 0, {}, {}};
+                                    x3s ? wb + eoff[e].fold : nullptr, eoff[e].in_col, eoff[e].d_in, eoff[e].P, 0,
+                                    {}, {}};
       for (int b = 0; b < 4; ++b) {
         float gm = 0.f, bm = 0.f;
         for (int c = 0; c < 256; ++c) {
@@ -855,6 +904,8 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
     }
     HIPCHK(vge::launch_conv_encoders_f16w(feats, B, enc->d_encs, enc->enc_out, enc->d_units, enc->units_G,
                                           enc->units_R, s));
+  } else if (x3 && enc->x3s) {
+    HIPCHK(vge::launch_conv_encoders_x3s(feats, B, enc->d_encs, 10, enc->enc_out, s));
   } else if (x3) {
     HIPCHK(vge::launch_conv_encoders_x3(feats, B, enc->d_encs, 10, enc->enc_out, split, enc->f16_mix & 1, s));
   } else {

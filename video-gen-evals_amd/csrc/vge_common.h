@@ -192,6 +192,84 @@ __device__ __forceinline__ void gelu2_fast(floatx2 (&y)[K]) {
 #endif
 }
 
+// Scalar forms of gelu2_many / gelu2_fast (same operations, so the same results), for code that runs beside MFMA
+// streams: packed f32 VALU (v_pk_fma_f32 ...) issued next to a busy matrix pipe costs ~22 cycles more than two scalar
+// ops (MI355X_MICROARCH.md, filler price row); build such files with -fno-slp-vectorize so they stay scalar.
+template <int K>
+__device__ __forceinline__ void gelu_many_s(float (&y)[K]) {
+#if !(defined(VGE_ABL) && (VGE_ABL & 16))
+  float z[K], a[K], s[K], q[K], p[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    z[k] = y[k] * 0.70710678118654752440f;
+    a[k] = fabsf(z[k]);
+    s[k] = a[k] * a[k];
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    q[k] = fmaf(s[k], -0x1.268bc2p-11f, 0x1.420828p-8f);
+    p[k] = fmaf(a[k], 0x1.1d3156p-16f, -0x1.8d129p-12f);
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    q[k] = fmaf(s[k], q[k], -0x1.b5937p-6f);
+    p[k] = fmaf(a[k], p[k], 0x1.f9a6d2p-9f);
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    q[k] = fmaf(s[k], q[k], 0x1.ce077cp-4f);
+    p[k] = fmaf(a[k], p[k], -0x1.8c3164p-6f);
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    q[k] = fmaf(s[k], q[k], -0x1.81266p-2f);
+    p[k] = fmaf(a[k], p[k], 0x1.b4e9c8p-4f);
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    q[k] = fmaf(s[k], q[k], 0x1.06eba0p-3f);
+    p[k] = fmaf(a[k], p[k], 0x1.4515fap-1f);
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    q[k] = fmaf(a[k], q[k], a[k]);  // erf(a), a < 1
+    p[k] = fmaf(a[k], p[k], 0x1.078e5p-3f);
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) p[k] = __builtin_amdgcn_exp2f(fmaf(a[k], p[k], a[k]) * -1.44269504f);
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const float r = a[k] < 1.0f ? q[k] : 1.0f - p[k];
+    const float hx = y[k] * 0.5f;
+    y[k] = fmaf(hx, copysignf(r, z[k]), hx);
+  }
+#endif
+}
+template <int K>
+__device__ __forceinline__ void gelu_fast_s(float (&y)[K]) {
+#if !(defined(VGE_ABL) && (VGE_ABL & 16))
+  float a[K], p[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    a[k] = fminf(fabsf(y[k]), 0x1.6a09e6p+2f);
+    p[k] = fmaf(a[k], -0x1.f5fbdcp-16f, 0x1.83e48ap-11f);
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) p[k] = fmaf(a[k], p[k], -0x1.05672ep-7f);
+#pragma unroll
+  for (int k = 0; k < K; ++k) p[k] = fmaf(a[k], p[k], 0x1.b42062p-5f);
+#pragma unroll
+  for (int k = 0; k < K; ++k) p[k] = fmaf(a[k], p[k], 0x1.d5ee02p-2f);
+#pragma unroll
+  for (int k = 0; k < K; ++k) p[k] = fmaf(a[k], p[k], 0x1.26b194p+0f) * a[k];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const float eh = fmaf(__builtin_amdgcn_exp2f(-p[k]), -0.5f, 0.5f);
+    y[k] = fmaf(fabsf(y[k]), eh, y[k] * 0.5f);
+  }
+#endif
+}
+
 // v_mfma_f32_16x16x4_f32: exact f32 (bitwise an fmaf chain over k).  Lane l supplies
 // A[i = l&15][k = l>>4] and B[k = l>>4][j = l&15]; C/D: col = l&15, row = (l>>4)*4 + r.
 __device__ __forceinline__ floatx4 mfma16x16x4(float a, float b, floatx4 c) {

@@ -48,18 +48,7 @@ __device__ long long g_vge_trace[64 * 8 * 32];
 
 namespace {
 
-// ------------------------------------------------------------------ conv encoder chain
-struct EncDescX3 {
-  const _Float16* stem;  // stem chunks; panel p (256 K) starts at chunk 16p, padded to STREAM_GROUP chunks
-  const _Float16* conv;  // 8 convs x 5 taps x 16 chunks
-  const _Float16* proj;  // 16 chunks
-  const float* gn_w;     // [4][256]
-  const float* gn_b;     // [4][256]
-  const float* cs;       // [10][256] weight column scales: stem, conv 0..7, proj
-  int in_col, d_in, n_stem_panels, pad;
-  float gn_gmax[4], gn_bmax[4];  // max |gamma|, max |beta| of each GroupNorm (split-exponent bounds)
-};
-
+// ------------------------------------------------------------------ conv encoder chain (EncDescX3: vge_x3.h)
 // One workgroup = one encoder x W windows (32 W rows) on CW waves; wave w owns output columns
 // 32 N w .. 32 N w + 32 N - 1 (N = 8 / CW column tiles) of all rows, so every weight byte streamed into the
 // workgroup feeds 32 W rows.  Used as W = 4 / 2 with CW = 8 (one workgroup per CU, two waves per SIMD).
@@ -409,18 +398,11 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
 // Grid = G blocks (one per CU); unit u runs on block u % G in round u / G, so with Q a multiple of G every
 // CU does the same number of quads and at most one pair.  Within a round the block index is remapped so the
 // 8 XCDs (blocks dealt round robin) take contiguous units, i.e. the same encoders' weights in their L2.
-struct ConvSched {
-  int n_windows, n_enc, G, Q, qa, qr, n_units;
-};
-
-__device__ __forceinline__ int xcd_remap(int b, int nblk) {
-  const int q8 = nblk >> 3, r8 = nblk & 7, x8 = b & 7;
-  return (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (b >> 3);
-}
+// (ConvSched, xcd_remap: vge_x3.h)
 
 template <bool SP, bool SPS>
 __global__ void __launch_bounds__(512, 1) conv_encoder_x3_kernel(const float* __restrict__ feats,
-                                                                  const EncDescX3* __restrict__ encs, ConvSched cs,
+                                                                  const EncDescX3* __restrict__ encs, vge::ConvSched cs,
                                                                   float* __restrict__ enc_out) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   const int n = cs.n_windows;
@@ -1254,7 +1236,7 @@ hipError_t launch_pack_x3(const float* W, int N, int K_real, int ldk, int conv, 
 
 struct EncDescX3Host {
   const _Float16* stem; const _Float16* conv; const _Float16* proj; const float* gn_w; const float* gn_b;
-  const float* cs;
+  const float* cs; const float* fold;
   int in_col, d_in, n_stem_panels, pad;
   float gn_gmax[4], gn_bmax[4];
 };
@@ -1292,10 +1274,8 @@ hipError_t encoder_x3_kernel_setup() {
 // units) persistent blocks and m = ceil(pair units / G) per block, Q = G * floor(m / 2) quads (as many as
 // fit) make every block run floor(m / 2) quads and at most one pair.
 // split: 3xfp16 (VGE_F32X3); otherwise single fp16 with the stem split (stem_split) or not
-hipError_t launch_conv_encoders_x3(const float* feats, int n_windows, const void* encs, int n_enc, float* enc_out,
-                                   bool split, bool stem_split, hipStream_t s) {
+ConvSched conv_quad_sched(int n_windows, int n_enc) {
   const int n_cu = conv_cu_count();
-  if (n_windows < 1 || n_enc < 1) return hipSuccess;
   const int pair_units = n_enc * ((n_windows + 1) / 2);
   const int G0 = std::min(n_cu, pair_units);
   const int m = (pair_units + G0 - 1) / G0;
@@ -1310,6 +1290,13 @@ hipError_t launch_conv_encoders_x3(const float* feats, int n_windows, const void
   for (int e = 0; e < n_enc; ++e) pairs += (n_windows - 4 * (cs.qa + (e < cs.qr)) + 1) / 2;
   cs.n_units = Q + pairs;
   cs.G = std::min(n_cu, cs.n_units);
+  return cs;
+}
+
+hipError_t launch_conv_encoders_x3(const float* feats, int n_windows, const void* encs, int n_enc, float* enc_out,
+                                   bool split, bool stem_split, hipStream_t s) {
+  if (n_windows < 1 || n_enc < 1) return hipSuccess;
+  const ConvSched cs = conv_quad_sched(n_windows, n_enc);
   auto k = split ? conv_encoder_x3_kernel<true, true>
                  : (stem_split ? conv_encoder_x3_kernel<false, true> : conv_encoder_x3_kernel<false, false>);
   hipLaunchKernelGGL(k, dim3(cs.G), dim3(512), (conv_lds_bytes<4, 8>()), s, feats,

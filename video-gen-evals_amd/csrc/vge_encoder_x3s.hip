@@ -1,0 +1,601 @@
+// Staggered split-precision ("3xfp16") MovementConvEncoder chain (model.py:21-58, x10), gfx950.
+//
+// Same arithmetic as conv_encoder_x3_kernel (vge_encoder_x3.hip: hi/lo fp16 planes, three v_mfma_f32_32x32x16_f16
+// per product, power-of-two scaled operands, f32 accumulation and epilogues), same units (an encoder x 4 or 2
+// windows per 512-thread workgroup, wave w = output columns 32w..32w+31 of all rows), but the two halves of the
+// workgroup run half a conv apart so that every epilogue of one half runs beside the other half's MFMA stream.
+// In the unstaggered kernel all 8 waves reach each epilogue together and the matrix pipes idle through it (~20 %
+// of a quad's cycles: tools/trace_encoder.py).
+//
+// Group A = waves 0-3 (output columns 0..127), group B = waves 4-7 (128..255); SIMD s holds waves s and s + 4, one
+// of each group.  A GEMM's K (tap x 256 input channels) is streamed in two parts: P1 = the channels group A
+// produced (0..127; 5 taps x 8 chunks for a conv), P2 = group B's.  Each half runs the task sequence
+// stem-epilogue, then P1(g), P2(g), E(g) for g = conv 0..7, proj; B runs one phase behind A and every phase ends
+// with a workgroup barrier:
+//
+//   phase 3g+1: A P1(g) | B E(g-1)      phase 3g+2: A P2(g) | B P1(g)      phase 3g+3: A E(g) | B P2(g)
+//
+// One buffer of activations satisfies every dependency: A's P2(g) reads what B's E(g-1) wrote a phase earlier; A's
+// E(g) overwrites channels 0..127 after B's P1(g) read them (previous phase); B's E(g) overwrites 128..255 after
+// A's P2(g) and B's own P2(g).  In phases 3g+1 and 3g+3 one wave per SIMD streams -- one accumulation chain of
+// this MFMA keeps a SIMD's matrix pipe busy on its own (MI355X_MICROARCH.md, cycle constants) -- while its partner
+// runs the epilogue's VALU work.
+//
+// Two reductions of the unstaggered kernel span the whole 256-column row, which one half cannot finish alone:
+// * GroupNorm(1, 256) (per window over its 32 x 256 values).  A's epilogue of a block's second conv runs while B
+//   is still streaming that conv, so the normalisation is folded into the next GEMM: the epilogue stores
+//   x = GELU(conv2 + res) itself, keeps it as the residual and writes per-wave partial statistics; the next GEMM's
+//   weights were packed as W diag(gamma) (vge_encoder_create) and its epilogue, which runs after both halves' E,
+//   corrects per window: conv(GN(x)) = rstd (conv_{W gamma}(x) - mu C_gamma(r)) + C_beta(r), with C(r) the sums of
+//   W gamma / W beta over the taps of row r that fall inside the window (EncDescX3::fold, host-computed in double);
+//   the residual becomes (x - mu) rstd gamma + beta in registers.  Statistics: each wave's mean and M2 (two-pass in
+//   registers) combined in a fixed order (Chan et al.), identical in every wave.
+// * the split exponent of stored activations.  Each half stores its channels with its own per-window exponent (the
+//   max over its 4 waves, exchanged through LDS with an arrival counter -- no barrier, the other half is
+//   streaming), and a consumer rescales its accumulators between P1 and P2 (exact powers of two).
+#include "vge_x3.h"
+#include <type_traits>
+
+#ifdef VGE_TRACE  // timing-only builds (tools/trace_x3s.py): s_memtime stamps of every wave of blocks 0..63, first unit
+__device__ long long g_x3s_trace[64 * 8 * 128];
+#define XTS(k)                                                                                                       \
+  do {                                                                                                              \
+    if (tr_on && blockIdx.x < 64 && (threadIdx.x & 63) == 0)                                                        \
+      g_x3s_trace[(blockIdx.x * 8 + (threadIdx.x >> 6)) * 128 + (k)] = __builtin_amdgcn_s_memtime();                 \
+  } while (0)
+#else
+#define XTS(k) \
+  do {         \
+  } while (0)
+#endif
+
+namespace {
+
+#ifndef X3S_TRACE_ROUND
+#define X3S_TRACE_ROUND 0  // VGE_TRACE builds stamp the units of this round of the persistent schedule
+#endif
+#ifndef X3S_GELU
+#define X3S_GELU 0  // 0: gelu2_many (exact-erf pieces), 1: gelu2_fast (one exp2)
+#endif
+#ifndef X3S_PRIO
+#define X3S_PRIO 1  // s_setprio 1 for the streaming half
+#endif
+constexpr int X3S_PF = 4;       // weight chunks in flight per wave
+constexpr int X3S_WMAX = 4;     // windows per unit (quads; pairs fill the remainder)
+// Activation rows in LDS interleave the planes: [hi 256 + 8 pad | lo 256 + 8 pad | 8 pad] fp16 = 1,072 B, so one row
+// base addresses both planes with immediate offsets (lo at +528 B) and the ds_read_b128 fragment reads of 32
+// consecutive rows stay conflict-free (row r starts at bank 12 r mod 64).
+constexpr int XR = 536;                         // fp16 per row
+constexpr int XRB = 2 * XR;                     // bytes per row
+constexpr int XLO = 528;                        // byte offset of the lo plane in a row
+constexpr int X3S_AUX_OFF = (32 * X3S_WMAX + 1) * XRB;  // fixed LDS offset of the auxiliary area
+
+struct X3sAux {
+  int rexp[2][32 * X3S_WMAX];       // stem row exponents, by panel parity
+  float stats[2][X3S_WMAX][8][2];   // [block parity][window][wave] (mean, M2) of x = GELU(conv2 + res)
+  float mx[2][2][X3S_WMAX][4];      // [exchange parity][group][window][wave in group] maxima
+  int ex[2][2][X3S_WMAX];           // [GEMM-input parity][group][window] exponents of the stored activations
+  int cnt[2];                       // exchange arrivals per group (monotonic over the launch)
+};
+constexpr int X3S_LDS_BYTES = X3S_AUX_OFF + (int)sizeof(X3sAux);
+static_assert(X3S_AUX_OFF % 16 == 0, "aux alignment");
+
+// One part of a conv / proj GEMM without barriers: ntap taps x 8 chunks (input-channel blocks cb0..cb0+7 of each
+// tap).  B fragments 3 chunks ahead in a register ring; A fragments single-buffered per row tile (tile t's fragments
+// of the next chunk are read right after the three MFMAs of this chunk that use them: their latency hides behind the
+// other tiles' MFMAs).  Addresses are formed once per tap -- LDS row bases (the zero row for taps outside the window)
+// plus immediate chunk offsets, uniform weight pointers plus the lane's offset -- so the stream issues almost no VALU
+// work besides its MFMAs (its partner wave's epilogue shares the SIMD's issue slots).
+template <int R, int ROWS>
+__device__ __forceinline__ void stream_part(Acc<R, 1>& acc, const char* wb, int ntap, unsigned loff, const char* xa,
+                                            int i, int dil, int ctr) {
+  // chunks in flight: a pair's chunk is only 6 MFMAs (192 cycles) -- 3 chunks ahead would not cover the weight
+  // stream's L2 latency while one wave per SIMD streams -- and it has the registers for 7
+  constexpr int PF = R >= 4 ? 4 : 8;
+  auto rowp = [&](int k, int t) -> const char* {
+    const int tt = i + (k - ctr) * dil;
+    return xa + ((unsigned)tt < 32u ? t * 32 + tt : ROWS) * XRB;
+  };
+  // weights through a buffer resource: the chunk offset in an SGPR, the lane's offset (+ the lo plane) in VGPRs
+  const __amdgpu_buffer_rsrc_t rs =
+      __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(wb), (short)0, 0x7FFFFFF0, 0x00020000);
+  const unsigned loff_l = loff + PLANE_B;
+  auto ldb = [&](int k, int j, BFrag<1>& b) {  // chunk j (0..7) of tap k
+    const int so = (k * 16 + j) * CHUNK_B;
+    b.h[0] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(rs, loff, so, 0));
+    b.l[0] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(rs, loff_l, so, 0));
+  };
+  BFrag<1> b[PF];
+#pragma unroll
+  for (int j = 0; j < PF - 1; ++j) ldb(0, j, b[j]);
+  half8 ah[R], al[R];
+  const char* pt[R];
+#pragma unroll
+  for (int t = 0; t < R; ++t) {
+    pt[t] = rowp(0, t);
+    ah[t] = *reinterpret_cast<const half8*>(pt[t]);
+    al[t] = *reinterpret_cast<const half8*>(pt[t] + XLO);
+  }
+  for (int k = 0; k < ntap; ++k) {
+    const bool more = k + 1 < ntap;
+    const int kn = more ? k + 1 : k;
+    const char* pn[R];
+#pragma unroll
+    for (int t = 0; t < R; ++t) pn[t] = rowp(kn, t);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+#if !(VGE_ABL & 2)
+      if (j + PF - 1 < 8) ldb(k, j + PF - 1, b[(j + PF - 1) % PF]);
+      else ldb(kn, more ? j + PF - 1 - 8 : 7, b[(j + PF - 1) % PF]);  // (past the end: reload the last chunk)
+#endif
+#pragma unroll
+      for (int t = 0; t < R; ++t) {
+#if !(VGE_ABL & 1)
+        acc.c[t][0] = mfma32(ah[t], b[j % PF].h[0], acc.c[t][0]);
+        acc.c[t][0] = mfma32(ah[t], b[j % PF].l[0], acc.c[t][0]);
+        acc.c[t][0] = mfma32(al[t], b[j % PF].h[0], acc.c[t][0]);
+#endif
+#if !(VGE_ABL & 4)
+        const char* q = j < 7 ? pt[t] + (j + 1) * 32 : pn[t];
+        ah[t] = *reinterpret_cast<const half8*>(q);
+        al[t] = *reinterpret_cast<const half8*>(q + XLO);
+#endif
+        __builtin_amdgcn_sched_barrier(0);  // tile by tile: the next fragments reuse this tile's registers
+      }
+      asm volatile("" ::: "memory");
+    }
+#pragma unroll
+    for (int t = 0; t < R; ++t) pt[t] = pn[t];
+  }
+}
+
+// a global-address-space load (a generic pointer would become a flat load, which also counts on lgkmcnt)
+__device__ __forceinline__ float gload(const float* p) {
+  return *(const __attribute__((address_space(1))) float*)p;
+}
+
+template <int W>
+__device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, int n_windows, int win0,
+                                              const EncDescX3& ed, int e, float* __restrict__ enc_out, char* lds_raw,
+                                              int& n_ex, [[maybe_unused]] bool tr_on) {
+  constexpr int R = W, ROWS = 32 * W, XROWS = ROWS + 1;
+  _Float16* X = reinterpret_cast<_Float16*>(lds_raw);  // [XROWS][XR]: hi at +0, lo at +XLO bytes
+  X3sAux& ax = *reinterpret_cast<X3sAux*>(lds_raw + X3S_AUX_OFF);
+
+  const int tid = threadIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wave >> 2, wg = wave & 3;
+  // Lane-derived values are recomputed from an opaque copy of the thread index at the top of every phase: hoisted
+  // out of the phase loop (per-row addresses of every task kind) they would stay live across all of it and spill.
+  int lane, i, h, col;
+  unsigned loff;
+  const char* xa;
+  auto lane_setup = [&]() {
+    int t = tid;
+    asm volatile("" : "+v"(t));
+    lane = t & 63;
+    i = lane & 31;
+    h = lane >> 5;
+    col = wave * 32 + i;                                   // this lane's output column
+    loff = (unsigned)((h * 256 + col) * 16);               // its B fragment in a chunk
+    xa = reinterpret_cast<const char*>(X) + h * 16;        // its 8 k-values of a 16-K chunk column
+  };
+  lane_setup();
+  auto crow = [&](int t, int r) { return t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h; };  // C-layout row
+
+  Acc<R, 1> acc;
+  floatx16 res[R];
+  for (int c = tid; c < XR; c += 512) X[ROWS * XR + c] = (_Float16)0.0f;  // the zero row (out-of-window taps)
+
+  // ---------------- stem: Conv1d(d_in -> 256, k=1, no bias), both halves together (conv_encoder_body's staging:
+  // per-row power-of-two exponents, K in 256-wide panels)
+  auto afn_stem = [&](int c, AFrag<R>& f) {
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+      const char* q = xa + (t * 32 + i) * XRB + c * 32;
+      f.h[t] = *reinterpret_cast<const half8*>(q);
+      f.l[t] = *reinterpret_cast<const half8*>(q + XLO);
+    }
+  };
+  XTS(0);
+  acc.zero();
+  for (int p = 0; p < ed.n_stem_panels; ++p) {
+    const int kw = min(256, ed.d_in - p * 256);
+    int* ecur = ax.rexp[p & 1];
+    constexpr int RPW = 32 * W / 8;
+#pragma unroll
+    for (int g8 = 0; g8 < RPW / 4; ++g8) {
+      float a[4][4];
+#pragma unroll
+      for (int jr = 0; jr < 4; ++jr) {
+        const int r = wave * RPW + g8 * 4 + jr;
+        const int w = win0 + (r >> 5);
+        const float* src = feats + ((size_t)w * VGE_T + (r & 31)) * VGE_FD + ed.in_col + p * 256;
+#pragma unroll
+        for (int jc = 0; jc < 4; ++jc) {
+          const int c = lane + 64 * jc;
+          a[jr][jc] = (c < kw && w < n_windows) ? src[c] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int jr = 0; jr < 4; ++jr) {
+        float m = fmaxf(fmaxf(fabsf(a[jr][0]), fabsf(a[jr][1])), fmaxf(fabsf(a[jr][2]), fabsf(a[jr][3])));
+        m = wave_max_all(m);
+        const int ex = fp16_range_exp(m);
+        const int r = wave * RPW + g8 * 4 + jr;
+        if (lane == 0) ecur[r] = ex;
+#pragma unroll
+        for (int jc = 0; jc < 4; ++jc) {
+          const int c = lane + 64 * jc;
+          split_store(X + r * XR + c, X + r * XR + XLO / 2 + c, ldexpf(a[jr][jc], -ex));
+        }
+      }
+    }
+    __syncthreads();  // X and ecur complete
+    if (p > 0) {
+      const int* eprev = ax.rexp[(p - 1) & 1];
+#pragma unroll
+      for (int t = 0; t < R; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc.c[t][0][r] *= ldexpf(1.0f, eprev[crow(t, r)] - ecur[crow(t, r)]);
+    }
+    run_stream<CONV_PF, true>(acc, reinterpret_cast<const char*>(ed.stem) + (size_t)p * 16 * CHUNK_B,
+                              ((kw + 127) >> 7) * STREAM_GROUP, loff, afn_stem);
+    __syncthreads();  // every wave is done reading X
+  }
+
+  // ---------------- the staggered chain
+  // An epilogue computes every tile in place in the accumulators, then exchanges the windows' maxima with the other
+  // 3 waves of its half once, then stores.
+  // max over the group's 4 waves of one value per window (every wave of the group gets the same results)
+  auto group_max = [&](float (&m)[R]) {
+    const int par = n_ex & 1;
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+      const float w = wave_max_last(m[t]);
+      if (lane == 63) ax.mx[par][grp][t][wg] = w;
+    }
+    ++n_ex;
+    if (lane == 63) __hip_atomic_fetch_add(&ax.cnt[grp], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    // (bounded: a wave that never arrives would be a bug; the bound ends the wait -- with wrong results -- instead of
+    // hanging the device)
+    for (int spin = 0; spin < (1 << 22) &&
+                       __builtin_amdgcn_readfirstlane(__hip_atomic_load(&ax.cnt[grp], __ATOMIC_ACQUIRE,
+                                                                        __HIP_MEMORY_SCOPE_WORKGROUP)) < 4 * n_ex;
+         ++spin)
+      __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+    for (int t = 0; t < R; ++t)
+      m[t] = fmaxf(fmaxf(ax.mx[par][grp][t][0], ax.mx[par][grp][t][1]),
+                   fmaxf(ax.mx[par][grp][t][2], ax.mx[par][grp][t][3]));
+  };
+  // Store this wave's columns of the next GEMM's input (v = the accumulators or the residuals), window t scaled by
+  // 2^-ex[t] with the group's largest |value| in [2^8, 2^9) (exact), and publish the exponents for parity `par`.  Two
+  // rows per packed conversion, row r of a tile at an immediate offset of ds_write_b16.
+  [[maybe_unused]] int tslot = 64;  // trace: epilogue stamp base (64 + 4 * epilogue index)
+  auto store_act = [&](auto get, int par) {
+    XTS(tslot + 1);
+    float m[R];
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+      const floatx16& v = get(t);
+      float a = fmaxf(fabsf(v[0]), fabsf(v[1])), b = fmaxf(fabsf(v[2]), fabsf(v[3]));
+#pragma unroll
+      for (int r = 4; r < 16; r += 2) {
+        a = fmaxf(a, fabsf(v[r]));
+        b = fmaxf(b, fabsf(v[r + 1]));
+      }
+      m[t] = fmaxf(a, b);
+    }
+    group_max(m);
+    XTS(tslot + 2);
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+      const floatx16& v = get(t);
+      const int ex = fp16_range_exp(m[t]);
+      if (wg == 0 && lane == 0) ax.ex[par][grp][t] = ex;
+      const float sc = ldexpf(1.0f, -ex);
+      char* bh = reinterpret_cast<char*>(X) + ((t * 32 + 4 * h) * XR + col) * 2;
+      char* bl = bh + XLO;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float y = v[r] * sc;
+        const _Float16 hi = (_Float16)y;
+        const int off = ((r & 3) + 8 * (r >> 2)) * XRB;
+        *reinterpret_cast<_Float16*>(bh + off) = hi;
+        *reinterpret_cast<_Float16*>(bl + off) = (_Float16)(y - (float)hi);
+      }
+    }
+    XTS(tslot + 3);
+    tslot += 4;
+  };
+  // GroupNorm statistics of block b's x over both halves, window t: mean and 1 / sqrt(var + eps)
+  auto gn_stats = [&](int b, int t, float& mu, float& rstd) {
+    const float(*s)[2] = ax.stats[b & 1][t];
+    const float m = (((s[0][0] + s[1][0]) + (s[2][0] + s[3][0])) + ((s[4][0] + s[5][0]) + (s[6][0] + s[7][0]))) * 0.125f;
+    float q = 0.f, d = 0.f;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) {
+      q += s[w][1];
+      const float dm = s[w][0] - m;
+      d = fmaf(dm, dm, d);
+    }
+    mu = m;
+    rstd = 1.0f / sqrtf(fmaf(d, 1024.0f, q) * (1.0f / 8192.0f) + 1e-5f);
+  };
+  // GELU of a tile's 16 values in place (8 independent packed chains)
+  auto gelu_tile = [&](floatx16& v) {
+    float y[16];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) y[k] = v[k];
+#if X3S_GELU
+    gelu_fast_s(y);
+#else
+    gelu_many_s(y);
+#endif
+#pragma unroll
+    for (int k = 0; k < 16; ++k) v[k] = y[k];
+  };
+
+  // this half's stem epilogue: the stem output is block 0's residual and conv 0's input
+  auto stem_epilogue = [&]() {
+    XTS(tslot);
+    const int* efin = ax.rexp[(ed.n_stem_panels - 1) & 1];
+    const float wcs = gload(ed.cs + col);
+#pragma unroll
+    for (int t = 0; t < R; ++t) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) res[t][r] = ldexpf(acc.c[t][0][r] * wcs, efin[crow(t, r)]);
+    }
+    store_act([&](int t) -> const floatx16& { return res[t]; }, 0);
+  };
+
+  // epilogue of GEMM gi; KIND (compile time) = 0: a block's conv1, 1: its conv2, 2: the proj
+  // The epilogue's global operands (column scale; GroupNorm affine and folded corrections; the proj's corrections)
+  // are loaded at the start of the phase before it (P2 of the same GEMM), so their latency -- long while the other
+  // half streams weights -- hides behind that stream.
+  float pre_wcs = 0.f, pre_gw = 0.f, pre_gb = 0.f, pre_sx = 0.f, pre_sy = 0.f;
+  floatx4 pre_g, pre_b;   // per-tap sums of W1 gamma / W1 beta, taps 0..3
+  float pre_g4, pre_b4;   // ... tap 4
+  auto prefetch = [&](auto kind_tag, int gi) {
+    constexpr int KIND = decltype(kind_tag)::value;
+    const int blk = gi >> 1;
+    pre_wcs = gload(ed.cs + (1 + gi) * 256 + col);
+    if constexpr (KIND == 2) {
+      pre_sx = gload(ed.fold + 3 * 256 * 16 + col * 2);
+      pre_sy = gload(ed.fold + 3 * 256 * 16 + col * 2 + 1);
+    } else if constexpr (KIND == 0) {
+      if (blk > 0) {
+        pre_gw = gload(ed.gn_w + (blk - 1) * 256 + col);
+        pre_gb = gload(ed.gn_b + (blk - 1) * 256 + col);
+        typedef const __attribute__((address_space(1))) floatx4* gf4;
+        const float* fb = ed.fold + ((size_t)(blk - 1) * 256 + col) * 16;
+        pre_g = *(gf4)fb;
+        pre_g4 = gload(fb + 4);
+        pre_b = *(gf4)(fb + 8);
+        pre_b4 = gload(fb + 12);
+      }
+    }
+  };
+
+  auto epilogue = [&](auto kind_tag, int gi) {
+    constexpr int KIND = decltype(kind_tag)::value;
+    XTS(tslot);
+    const int par = gi & 1, blk = gi >> 1;
+    const float wcs = pre_wcs;
+    if constexpr (KIND == 2) {
+      // proj(GN_3(x)) = rstd (P gamma x - mu S_gamma) + S_beta; rows past n_windows are not written
+      const float2 sp = {pre_sx, pre_sy};
+#pragma unroll
+      for (int t = 0; t < R; ++t) {
+        float mu, rstd;
+        gn_stats(3, t, mu, rstd);
+        const float sc = ldexpf(1.0f, ax.ex[par][1][t]) * wcs, off = -mu * sp.x;
+        const int win = win0 + t;
+        if (win < n_windows) {
+          float* o = enc_out + ((size_t)e * n_windows * VGE_T + (size_t)win * VGE_T) * VGE_D + col;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) o[crow(0, r) * VGE_D] = fmaf(rstd, fmaf(acc.c[t][0][r], sc, off), sp.y);
+        }
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < R; ++t) {
+        const float sc = ldexpf(1.0f, ax.ex[par][1][t]) * wcs;
+        floatx16& v = acc.c[t][0];
+        if constexpr (KIND == 0) {
+          // GELU(conv1(block input)); for blocks 1..3 the input is GN_{blk-1}(x), folded (file comment), and the
+          // residual becomes GN_{blk-1}(x) here
+          if (blk > 0) {
+            float mu, rstd;
+            gn_stats(blk - 1, t, mu, rstd);
+            const float gs = rstd * pre_gw;
+            const float gsh = fmaf(-mu, gs, pre_gb);
+            const int dil = 1 << blk;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              // the taps of this row inside the window: row + (tap - 2) dil in [0, 32)
+              const int row = crow(0, r);
+              const bool k0 = row >= 2 * dil, k1 = row >= dil, k3 = row < 32 - dil, k4 = row < 32 - 2 * dil;
+              const float cg = (((k0 ? pre_g.x : 0.f) + (k1 ? pre_g.y : 0.f)) + pre_g.z) + (k3 ? pre_g.w : 0.f) +
+                               (k4 ? pre_g4 : 0.f);
+              const float cb = (((k0 ? pre_b.x : 0.f) + (k1 ? pre_b.y : 0.f)) + pre_b.z) + (k3 ? pre_b.w : 0.f) +
+                               (k4 ? pre_b4 : 0.f);
+              res[t][r] = fmaf(res[t][r], gs, gsh);  // (x - mu) rstd gamma + beta, as conv_encoder_body
+              v[r] = fmaf(rstd, fmaf(-mu, cg, v[r] * sc), cb);
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) v[r] *= sc;  // (the stem output needs no correction)
+          }
+          gelu_tile(v);
+        } else {
+          // x = GELU(conv2(h) + residual): stored pre-GroupNorm, kept as the residual, partial statistics published
+#pragma unroll
+          for (int r = 0; r < 16; ++r) v[r] = fmaf(v[r], sc, res[t][r]);
+          gelu_tile(v);
+          res[t] = v;
+        }
+        __builtin_amdgcn_sched_barrier(0);  // one tile's temporaries at a time
+      }
+      if constexpr (KIND == 1) {
+        // per-wave GroupNorm partials of every window: mean, then M2 about it (two-pass, in registers)
+        float mw[R], q[R];
+#pragma unroll
+        for (int t = 0; t < R; ++t) {
+          float s = 0.f;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) s += res[t][r];
+          mw[t] = wave_sum_last(s);
+        }
+#pragma unroll
+        for (int t = 0; t < R; ++t) {
+          mw[t] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mw[t]), 63)) *
+                  (1.0f / 1024.0f);
+          float a = 0.f;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float d = res[t][r] - mw[t];
+            a = fmaf(d, d, a);
+          }
+          q[t] = a;
+        }
+#pragma unroll
+        for (int t = 0; t < R; ++t) q[t] = wave_sum_last(q[t]);
+        if (lane == 63) {
+#pragma unroll
+          for (int t = 0; t < R; ++t) {
+            ax.stats[blk & 1][t][wave][0] = mw[t];
+            ax.stats[blk & 1][t][wave][1] = q[t];
+          }
+        }
+      }
+      store_act([&](int t) -> const floatx16& { return acc.c[t][0]; }, (gi + 1) & 1);
+    }
+  };
+
+  auto stream = [&](int gi, int part) {
+    if (part == 0) {
+      acc.zero();
+    } else {  // channels of B: the accumulators move from A's exponent to B's (exact)
+#pragma unroll
+      for (int t = 0; t < R; ++t) {
+        const float f = ldexpf(1.0f, ax.ex[gi & 1][0][t] - ax.ex[gi & 1][1][t]);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc.c[t][0][r] *= f;
+      }
+    }
+    const bool proj = gi == 8;
+    const char* wb = reinterpret_cast<const char*>(proj ? ed.proj : ed.conv + (size_t)gi * 80 * (CHUNK_B / 2)) +
+                     (size_t)part * 8 * CHUNK_B;
+    if (X3S_PRIO) __builtin_amdgcn_s_setprio(1);
+    stream_part<R, ROWS>(acc, wb, proj ? 1 : 5, loff, xa + part * 8 * 32, i, proj ? 0 : 1 << (gi >> 1), proj ? 0 : 2);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  // The task sequence of a half (file comment) is the same code for both: B starts it one barrier later and A ends
+  // with one more, so B runs one phase behind.
+  using K0 = std::integral_constant<int, 0>;
+  using K1 = std::integral_constant<int, 1>;
+  using K2 = std::integral_constant<int, 2>;
+  [[maybe_unused]] int ph = 0;  // trace: this wave's phase index
+  auto phase_end = [&]() {
+    XTS(2 + 2 * ph);
+    lds_barrier();
+    XTS(3 + 2 * ph);
+    ++ph;
+    lane_setup();
+  };
+  XTS(1);
+  if (grp == 1) phase_end();
+  else lane_setup();
+  stem_epilogue();
+  phase_end();
+#pragma unroll 1
+  for (int blk = 0; blk < 4; ++blk) {
+    stream(2 * blk, 0);
+    phase_end();
+    prefetch(K0{}, 2 * blk);
+    stream(2 * blk, 1);
+    phase_end();
+    epilogue(K0{}, 2 * blk);
+    phase_end();
+    stream(2 * blk + 1, 0);
+    phase_end();
+    prefetch(K1{}, 2 * blk + 1);
+    stream(2 * blk + 1, 1);
+    phase_end();
+    epilogue(K1{}, 2 * blk + 1);
+    phase_end();
+  }
+  stream(8, 0);
+  phase_end();
+  prefetch(K2{}, 8);
+  stream(8, 1);
+  phase_end();
+  epilogue(K2{}, 8);
+  phase_end();
+  if (grp == 0) phase_end();
+}
+
+__global__ void __launch_bounds__(512, 1) conv_encoder_x3s_kernel(const float* __restrict__ feats,
+                                                                   const EncDescX3* __restrict__ encs, vge::ConvSched cs,
+                                                                   float* __restrict__ enc_out) {
+  extern __shared__ __attribute__((aligned(16))) char lds_raw[];
+  X3sAux& ax = *reinterpret_cast<X3sAux*>(lds_raw + X3S_AUX_OFF);
+  if (threadIdx.x < 2) ax.cnt[threadIdx.x] = 0;  // ordered before any exchange by the stem staging's barriers
+#ifdef VGE_TRACE
+  if (blockIdx.x < 64 && (threadIdx.x & 63) == 0)
+    g_x3s_trace[(blockIdx.x * 8 + (threadIdx.x >> 6)) * 128 + 120] = __builtin_amdgcn_s_memtime();
+#endif
+  int n_ex = 0;
+  const int n = cs.n_windows;
+  const int p_big = (n - 4 * (cs.qa + 1) + 1) / 2, p_small = (n - 4 * cs.qa + 1) / 2;  // pairs per encoder
+  for (int round = 0; round * cs.G < cs.n_units; ++round) {
+    const int u = round * cs.G + xcd_remap(blockIdx.x, cs.G);
+    if (u >= cs.n_units) break;  // uniform over the block
+    if (u < cs.Q) {
+      const int big = cs.qr * (cs.qa + 1);
+      const int e = u < big ? u / (cs.qa + 1) : cs.qr + (u - big) / cs.qa;
+      const int j = u < big ? u % (cs.qa + 1) : (u - big) % cs.qa;
+      conv_x3s_body<4>(feats, n, 4 * j, encs[e], e, enc_out, lds_raw, n_ex, round == X3S_TRACE_ROUND);
+    } else {
+      const int v = u - cs.Q;
+      const int big = cs.qr * p_big;
+      const int e = v < big ? v / p_big : cs.qr + (v - big) / p_small;
+      const int j = v < big ? v % p_big : (v - big) % p_small;
+      const int q_e = cs.qa + (e < cs.qr);
+      conv_x3s_body<2>(feats, n, 4 * q_e + 2 * j, encs[e], e, enc_out, lds_raw, n_ex, round == X3S_TRACE_ROUND);
+    }
+  }
+#ifdef VGE_TRACE
+  if (blockIdx.x < 64 && (threadIdx.x & 63) == 0)
+    g_x3s_trace[(blockIdx.x * 8 + (threadIdx.x >> 6)) * 128 + 121] = __builtin_amdgcn_s_memtime();
+#endif
+}
+
+}  // namespace
+
+namespace vge {
+
+hipError_t encoder_x3s_kernel_setup() {
+  return hipFuncSetAttribute((const void*)conv_encoder_x3s_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                             X3S_LDS_BYTES);
+}
+
+hipError_t launch_conv_encoders_x3s(const float* feats, int n_windows, const void* encs, int n_enc, float* enc_out,
+                                    hipStream_t s) {
+  if (n_windows < 1 || n_enc < 1) return hipSuccess;
+  const ConvSched cs = conv_quad_sched(n_windows, n_enc);
+  hipLaunchKernelGGL(conv_encoder_x3s_kernel, dim3(cs.G), dim3(512), X3S_LDS_BYTES, s, feats,
+                     reinterpret_cast<const EncDescX3*>(encs), cs, enc_out);
+  return hipGetLastError();
+}
+
+}  // namespace vge
+
+#ifdef VGE_TRACE
+extern "C" int vge_debug_x3s_trace(long long* host, int n) {
+  return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_x3s_trace), sizeof(long long) * (size_t)n);
+}
+#endif

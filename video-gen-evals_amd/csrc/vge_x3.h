@@ -4,6 +4,18 @@
 #pragma once
 #include "vge_common.h"
 
+namespace vge {
+// Persistent schedule of the quad / pair conv kernels.  Work units: Q quads (4 windows) then the pairs (2 windows)
+// covering the rest of each encoder's windows; encoder e takes q_e = qa + (e < qr) quads (windows [0, 4 q_e)) and the
+// pairs after them.  Grid = G blocks (one per CU); unit u runs on block u % G in round u / G, so with Q a multiple
+// of G every CU does the same number of quads and at most one pair.  Within a round the block index is remapped so
+// the 8 XCDs (blocks dealt round robin) take contiguous units, i.e. the same encoders' weights in their L2.
+struct ConvSched {
+  int n_windows, n_enc, G, Q, qa, qr, n_units;
+};
+ConvSched conv_quad_sched(int n_windows, int n_enc);  // vge_encoder_x3.hip (host)
+}  // namespace vge
+
 #ifndef VGE_ABL
 #define VGE_ABL 0  // timing-only ablation builds (tools/ablate.sh), a bit mask: 1 no MFMA, 2 no B loads after the
                    // prologue, 4 no A reads, 16 identity GELU; 0 = the product
@@ -147,6 +159,27 @@ __device__ __forceinline__ void run_stream(Acc<R, N>& acc, const void* gw, int n
     lds_barrier();
 #endif
   }
+}
+
+// One MovementConvEncoder's weights (model.py:21-58) as the x3 conv kernels read them.
+struct EncDescX3 {
+  const _Float16* stem;  // stem chunks; panel p (256 K) starts at chunk 16p, padded to STREAM_GROUP chunks
+  const _Float16* conv;  // 8 convs x 5 taps x 16 chunks
+  const _Float16* proj;  // 16 chunks
+  const float* gn_w;     // [4][256]
+  const float* gn_b;     // [4][256]
+  const float* cs;       // [10][256] weight column scales: stem, conv 0..7, proj
+  // staggered split kernel only (vge_encoder_x3s.hip), else null: the GroupNorm-folded corrections of blocks 1..3's
+  // conv1, [3 blocks][256 cols][16] = per-tap sums over input channels of W1 gamma (taps 0..4), then of W1 beta (at 8..12),
+  // then the proj's [256][2] (sums of P gamma, P beta)
+  const float* fold;
+  int in_col, d_in, n_stem_panels, pad;
+  float gn_gmax[4], gn_bmax[4];  // max |gamma|, max |beta| of each GroupNorm (split-exponent bounds)
+};
+
+__device__ __forceinline__ int xcd_remap(int b, int nblk) {
+  const int q8 = nblk >> 3, r8 = nblk & 7, x8 = b & 7;
+  return (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (b >> 3);
 }
 
 }  // namespace
