@@ -55,7 +55,7 @@ namespace {
 #define X3S_TRACE_ROUND 0  // VGE_TRACE builds stamp the units of this round of the persistent schedule
 #endif
 #ifndef X3S_GELU
-#define X3S_GELU 0  // 0: gelu2_many (exact-erf pieces), 1: gelu2_fast (one exp2)
+#define X3S_GELU 1  // 1: gelu_fast_s (one exp2; f32 rounding-level error, see DESIGN), 0: gelu_many_s (exact-erf pieces)
 #endif
 #ifndef X3S_PRIO
 #define X3S_PRIO 1  // s_setprio 1 for the streaming half
@@ -399,6 +399,19 @@ __device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, i
         }
       }
     } else {
+      float cg[16], cb[16];  // K0, blocks 1..3: this lane's rows' corrections (the taps of the row inside the window)
+      if constexpr (KIND == 0) {
+        if (blk > 0) {
+          const int dil = 1 << blk;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = crow(0, r);  // row + (tap - 2) dil in [0, 32)
+            const bool k0 = row >= 2 * dil, k1 = row >= dil, k3 = row < 32 - dil, k4 = row < 32 - 2 * dil;
+            cg[r] = (((k0 ? pre_g.x : 0.f) + (k1 ? pre_g.y : 0.f)) + pre_g.z) + (k3 ? pre_g.w : 0.f) + (k4 ? pre_g4 : 0.f);
+            cb[r] = (((k0 ? pre_b.x : 0.f) + (k1 ? pre_b.y : 0.f)) + pre_b.z) + (k3 ? pre_b.w : 0.f) + (k4 ? pre_b4 : 0.f);
+          }
+        }
+      }
 #pragma unroll
       for (int t = 0; t < R; ++t) {
         const float sc = ldexpf(1.0f, ax.ex[par][1][t]) * wcs;
@@ -411,18 +424,10 @@ __device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, i
             gn_stats(blk - 1, t, mu, rstd);
             const float gs = rstd * pre_gw;
             const float gsh = fmaf(-mu, gs, pre_gb);
-            const int dil = 1 << blk;
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-              // the taps of this row inside the window: row + (tap - 2) dil in [0, 32)
-              const int row = crow(0, r);
-              const bool k0 = row >= 2 * dil, k1 = row >= dil, k3 = row < 32 - dil, k4 = row < 32 - 2 * dil;
-              const float cg = (((k0 ? pre_g.x : 0.f) + (k1 ? pre_g.y : 0.f)) + pre_g.z) + (k3 ? pre_g.w : 0.f) +
-                               (k4 ? pre_g4 : 0.f);
-              const float cb = (((k0 ? pre_b.x : 0.f) + (k1 ? pre_b.y : 0.f)) + pre_b.z) + (k3 ? pre_b.w : 0.f) +
-                               (k4 ? pre_b4 : 0.f);
               res[t][r] = fmaf(res[t][r], gs, gsh);  // (x - mu) rstd gamma + beta, as conv_encoder_body
-              v[r] = fmaf(rstd, fmaf(-mu, cg, v[r] * sc), cb);
+              v[r] = fmaf(rstd, fmaf(-mu, cg[r], v[r] * sc), cb[r]);
             }
           } else {
 #pragma unroll
