@@ -48,15 +48,18 @@ typedef enum {
 /* Encoder compute modes.  VGE_F32: exact f32 MFMA (v_mfma_f32_16x16x4_f32, bitwise an fmaf chain).
  * VGE_F32X3: f32-class split precision -- every GEMM operand carried as fp16 hi + fp16 lo*2^11 and
  * each product formed as hi*hi + 2^-11 (hi*lo + lo*hi) on v_mfma_f32_32x32x16_f16 with f32
- * accumulation (relative error ~2^-21 per product; AC/TC within ~1e-7 of the f32 mode). */
+ * accumulation (relative error ~2^-21 per product; AC/TC within ~1e-7 of the f32 mode).  Its conv encoders
+ * run staggered (vge_encoder_x3s.hip): each block's GroupNorm is folded into the next GEMM's weights and
+ * epilogue, and GELU is a one-exp2 form within ~1 f32 ulp at |x| <= 6 (f32 rounding-level, as the reference's
+ * own erf-based GELU); env VGE_X3S=0 keeps the unstaggered kernel and unfolded weights. */
 typedef enum { VGE_F32 = 0, VGE_F32X3 = 1, VGE_F16 = 2 } vge_dtype;
 /* VGE_F16: the throughput mode (BASELINE configs 2 / 5 "bf16" / "fp16 MFMA path"): the ten
  * MovementConvEncoders (85% of the FLOPs) take every GEMM operand as a single fp16 (the hi planes of the
  * VGE_F32X3 image, same power-of-two scaling), one v_mfma_f32_32x32x16_f16 per product, f32 accumulation
  * and f32 epilogues (GELU, GroupNorm); the transformer keeps the 3xfp16 split, because it carries most of
  * the fp16 error for ~10% of the FLOPs (env VGE_F16_MIX: bit 1 = transformer split [default 2], bit 0 =
- * stem split).  Measured AC/TC within 3e-5 of the reference on the golden set (tests/test_gpu_parity.py);
- * its deviation is reported by bench.py. */
+ * stem split).  Measured AC/TC within 3e-5 of the reference on the golden set (tests/test_gpu_parity.py),
+ * asserted at 1e-4 on the bench and config-5 workloads (tests/test_bench_parity.py); bench.py reports it. */
 
 #define VGE_FEAT_DIM 2596
 #define VGE_RAW_DIM 1370

@@ -48,10 +48,15 @@ _oracle.cache = {}
 
 
 @pytest.mark.parametrize("n", [256, 600])
-@pytest.mark.parametrize("compute", ["f32x3", "f32"])
-def test_bench_workload_vs_oracle(n, compute):
+@pytest.mark.parametrize("compute", ["f32x3", "f32x3-unstaggered", "f32"])
+def test_bench_workload_vs_oracle(n, compute, monkeypatch):
+    """f32x3 runs the staggered conv kernel (vge_encoder_x3s.hip, GroupNorm folded forward); f32x3-unstaggered the
+    quad / pair kernel it replaced (VGE_X3S=0, weights unfolded); f32 the exact-f32 MFMA kernels."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    if compute == "f32x3-unstaggered":
+        monkeypatch.setenv("VGE_X3S", "0")
+        compute = "f32x3"
     from vge import ops
     from vge.data import pack_frame_store
     o = _oracle(n)
@@ -93,7 +98,8 @@ def test_f16_throughput_mode_vs_oracle(n):
     e_ac = (ac.cpu() - o["ac"]).abs().max().item()
     e_tc = (tc.cpu() - o["tc"]).abs().max().item()
     print(f"f16 n={n}: seq {e_seq:.2e} ac {e_ac:.2e} tc {e_tc:.2e}")
-    assert e_seq < 2e-2 and e_ac < 1e-2 and e_tc < 1e-2, (e_seq, e_ac, e_tc)
+    # the north star's 1e-4 on the scores (measured ~2e-5, include/vge.h); embeddings ~1e-5
+    assert e_seq < 2e-4 and e_ac < 1e-4 and e_tc < 1e-4, (e_seq, e_ac, e_tc)
     s2, _, _ = enc.encode(feats[:64].contiguous(), frame_embed=False, tc=True)
     assert torch.equal(s2, seq[:64])
 
@@ -123,7 +129,7 @@ def test_f16_unit_kernel_matches_quad_kernel(n, monkeypatch):
     e_seq = (s_u.cpu() - o["seq"][:n]).abs().max().item()
     print(f"n={n}: unit vs quad seq {d_seq:.2e} frame {d_fe:.2e} tc {d_tc:.2e}; unit vs oracle seq {e_seq:.2e}")
     assert d_seq < 1e-4 and d_fe < 1e-4 and d_tc < 1e-4, (d_seq, d_fe, d_tc)
-    assert e_seq < 2e-2
+    assert e_seq < 2e-4
     if n >= 64:  # deterministic per window whatever unit it lands in
         s2, _, _ = unit.encode(feats[:64].contiguous(), frame_embed=False, tc=True)
         assert torch.equal(s2, s_u[:64])
@@ -214,3 +220,61 @@ def test_featurize_pipelined_on_a_side_stream_matches_serial():
                 ready.record(side)
     torch.cuda.synchronize()
     assert torch.equal(piped, serial)
+
+
+@pytest.mark.parametrize("compute,mix", [("f32x3", None), ("f16", "0"), ("f16", "2")])
+def test_config5_chunk_schedule_vs_oracle(compute, mix, monkeypatch):
+    """Config 5's own path (bench.py --workload cfg5): 64-frame clips of 5 windows each (starts 0, 8, 16, 24, 32,
+    utils.py:888-911), featurised and encoded in chunks of 4,096 windows -- here 1,000 clips = 5,000 windows, a full
+    chunk (the unit kernel's 27-round schedule in f16) and a 904-window tail -- then per-video AC / TC as eval.py takes
+    them (AC from the mean of a video's window embeddings, TC the float64 mean of its windows' terms, eval.py:209-257).
+    Compared with the oracle on 64 clips spread over the first chunk, the chunk boundary (clip 819's windows straddle
+    it) and the tail, in the f32-class mode and in the fp16 modes (VGE_F16_MIX=0: config 5's all-fp16 bench setting;
+    2: the default), at the north star's 1e-4."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    if mix is not None:
+        monkeypatch.setenv("VGE_F16_MIX", mix)
+    import bench
+    from oracle.encoder import OracleEncoder
+    from oracle.featurize import featurize_window
+    from vge import ops, synth
+    from vge.data import pack_frame_store
+    V, T, CH = 1000, 64, 4096
+    starts = list(range(0, T - 32 + 1, 8))
+    clips = [bench.make_clips(synth.SEED_GEN, k, 1, T)[0] for k in range(V)]
+    o = _oracle(256)  # stats (mean / std from the real clips), centroids, weights
+    store = ops.DeviceFrameStore.from_host(pack_frame_store(clips, [f"g{k}" for k in range(V)], ["X"] * V), DEV)
+    win = torch.tensor([[v, s0] for v in range(V) for s0 in starts], dtype=torch.int32, device=DEV)
+    NW = win.shape[0]
+    mean, std = torch.from_numpy(o["mean"]).to(DEV), torch.from_numpy(o["std"]).to(DEV)
+    enc = ops.Encoder(o["sd"], device=DEV, compute=compute)
+    enc.reserve(CH)
+    seq = torch.empty((NW, 256), device=DEV)
+    tcw = torch.empty((NW,), device=DEV)
+    feats = torch.empty((CH, 32, ops.FEAT_DIM), device=DEV)
+    for b0 in range(0, NW, CH):
+        b1 = min(NW, b0 + CH)
+        ops.featurize(store, win[b0:b1], mean, std, out=feats[: b1 - b0])
+        enc.encode(feats[: b1 - b0], frame_embed=False, tc=True, seq_out=seq[b0:b1], tc_out=tcw[b0:b1])
+    vcls = torch.tensor([k % 10 for k in range(V)], dtype=torch.int32, device=DEV)
+    first = torch.arange(0, NW + 1, len(starts), dtype=torch.int32, device=DEV)
+    ac, tc = ops.score_videos(seq, tcw, first, vcls, o["cent"].to(DEV))
+    sample = list(range(0, 16)) + list(range(812, 828)) + list(range(900, 916)) + list(range(984, 1000))
+    ref_feats = np.stack([(featurize_window(clips[k]["pose"], clips[k]["global_orient"], clips[k]["betas"],
+                                            clips[k]["vit"], clips[k]["keypoints"], s0, None) - o["mean"])
+                          / (o["std"] + np.float32(1e-6)) for k in sample for s0 in starts]).astype(np.float32)
+    rs, rf, _ = OracleEncoder(o["sd"], synth.DIMS_RAW, synth.DIMS_DIFF).forward(torch.from_numpy(ref_feats))
+    f = rf[:, 1:]
+    rtc = (f[:, 1:] - f[:, :-1]).norm(dim=-1).mean(dim=1).double().view(len(sample), len(starts)).mean(dim=1)
+    z = torch.nn.functional.normalize(rs.view(len(sample), len(starts), -1).mean(dim=1), dim=-1)
+    rac = (z - o["cent"][torch.tensor([k % 10 for k in sample])]).norm(dim=-1)
+    idx = torch.tensor(sample)
+    e_ac = (ac.cpu()[idx] - rac).abs().max().item()
+    e_tc = (tc.cpu()[idx] - rtc).abs().max().item()
+    rows = torch.tensor([k * len(starts) + j for k in sample for j in range(len(starts))])
+    e_seq = (seq.cpu()[rows] - rs).abs().max().item()
+    print(f"cfg5 {compute} mix={mix}: seq {e_seq:.2e} ac {e_ac:.2e} tc {e_tc:.2e} over {len(sample)} clips")
+    assert torch.isfinite(ac).all() and torch.isfinite(tc).all()
+    assert e_ac < 1e-4 and e_tc < 1e-4, (e_ac, e_tc)
+    assert e_seq < (2e-5 if compute == "f32x3" else 2e-4), e_seq

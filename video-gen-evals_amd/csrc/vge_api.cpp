@@ -229,8 +229,15 @@ struct vge_encoder {
   // quad / pair kernel); its table for batch units_B lives in d_units (sized by vge_encoder_reserve, built on the
   // device by vge_encode when the batch size changes)
   int f16w = 6;
+  // Up to kUnitTables tables are kept (one slot of units_cap entries each, least recently used replaced): config 5
+  // alternates a full chunk and its tail, and each table is built once.
+  static constexpr int kUnitTables = 4;
   int* d_units = nullptr;
-  int units_B = 0, units_G = 0, units_R = 0;
+  size_t units_cap = 0;  // entries per slot (>= R * G for any batch <= cap; checked per build)
+  struct UnitTable { int B = 0, G = 0, R = 0; unsigned long long used = 0; };
+  UnitTable tables[kUnitTables];
+  unsigned long long units_clock = 0;
+  int units_last = -1;  // slot of the last vge_encode (test hook vge_debug_encoder_units)
   hipEvent_t conv_done = nullptr;  // recorded after the conv stage of every vge_encode (vge_encoder_wait_conv)
   vge::FuseParamsHost fuse{};
   const void* Wov = nullptr;      // packed (f32 chunks or fp16 chunks)
@@ -779,8 +786,15 @@ int vge_encoder_reserve(vge_encoder* enc, int B) {
   enc->h = p;
   if (enc->d_units) (void)hipFree(enc->d_units);
   enc->d_units = nullptr;
-  enc->units_B = 0;
-  he = hipMalloc(&enc->d_units, ((size_t)10 * B + 1024) * sizeof(int));  // >= R * G for any batch <= B
+  for (auto& t : enc->tables) t = vge_encoder::UnitTable{};
+  enc->units_last = -1;
+  {  // the largest R * G over batches <= B (R * G <= 10 B + CUs - 1, conv_f16w_plan)
+    int G = 0, R = 0, U = 0;
+    enc->units_cap = (size_t)10 * B + 1024;
+    if (vge::conv_f16w_plan(B, 10, enc->f16w > 0 ? enc->f16w : 6, G, R, U))
+      enc->units_cap = std::max(enc->units_cap, (size_t)G * R);
+  }
+  he = hipMalloc(&enc->d_units, enc->units_cap * vge_encoder::kUnitTables * sizeof(int));
   if (he != hipSuccess) return fail(VGE_ERR_NOMEM, std::string("vge_encoder_reserve: ") + hipGetErrorString(he));
   enc->cap = B;
   return VGE_OK;
@@ -849,9 +863,10 @@ extern "C" int vge_debug_encoder_images(const vge_encoder* enc, const void** hbu
 // vge_debug_conv_schedule).
 extern "C" int vge_debug_encoder_units(const vge_encoder* enc, const void** table, int* G, int* R) {
   if (!enc || !table || !G || !R) return fail(VGE_ERR_ARG, "vge_debug_encoder_units: null argument");
-  *table = enc->d_units;
-  *G = enc->units_G;
-  *R = enc->units_R;
+  const int k = enc->units_last;
+  *table = k >= 0 ? enc->d_units + (size_t)k * enc->units_cap : nullptr;
+  *G = k >= 0 ? enc->tables[k].G : 0;
+  *R = k >= 0 ? enc->tables[k].R : 0;
   return VGE_OK;
 }
 
@@ -894,16 +909,25 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
   };
   HIPCHK(mark(0));
   if (x3 && !split && !(enc->f16_mix & 1) && enc->f16w > 0) {
-    if (B != enc->units_B) {  // new batch size: the unit table, built on the device (stream-ordered, no host copy)
+    // the unit table of this batch size: cached, else built on the device (stream-ordered, no host copy) into the
+    // least recently used slot
+    int k = -1;
+    for (int j = 0; j < vge_encoder::kUnitTables; ++j)
+      if (enc->tables[j].B == B) k = j;
+    if (k < 0) {
       int G = 0, R = 0, U = 0;
       if (!vge::conv_f16w_plan(B, 10, enc->f16w, G, R, U)) return fail(VGE_ERR_ARG, "vge_encode: batch too large");
-      HIPCHK(vge::launch_conv_f16w_table(B, 10, G, R, U, enc->d_units, s));
-      enc->units_B = B;
-      enc->units_G = G;
-      enc->units_R = R;
+      if ((size_t)G * R > enc->units_cap) return fail(VGE_ERR_WORKSPACE, "vge_encode: unit table exceeds its slot");
+      k = 0;
+      for (int j = 1; j < vge_encoder::kUnitTables; ++j)
+        if (enc->tables[j].used < enc->tables[k].used) k = j;
+      HIPCHK(vge::launch_conv_f16w_table(B, 10, G, R, U, enc->d_units + (size_t)k * enc->units_cap, s));
+      enc->tables[k] = vge_encoder::UnitTable{B, G, R, 0};
     }
-    HIPCHK(vge::launch_conv_encoders_f16w(feats, B, enc->d_encs, enc->enc_out, enc->d_units, enc->units_G,
-                                          enc->units_R, s));
+    enc->tables[k].used = ++enc->units_clock;
+    enc->units_last = k;
+    HIPCHK(vge::launch_conv_encoders_f16w(feats, B, enc->d_encs, enc->enc_out, enc->d_units + (size_t)k * enc->units_cap,
+                                          enc->tables[k].G, enc->tables[k].R, s));
   } else if (x3 && enc->x3s) {
     HIPCHK(vge::launch_conv_encoders_x3s(feats, B, enc->d_encs, 10, enc->enc_out, s));
   } else if (x3) {

@@ -1382,30 +1382,39 @@ bool conv_f16w_plan(int n_windows, int n_enc, int wmax, int& G, int& R, int& U) 
 }  // namespace vge
 namespace {
 // Device twin of conv_f16w_schedule's table (so vge_encode builds it without host round trips: capture-safe): the
-// same units (encoder e cut into u_e nearly equal runs), the same stable order (size descending, then encoder-major)
-// as a counting pass per size, the same snake dealing.  One thread: it runs only when the batch size changes.
-__global__ void conv_f16w_table_kernel(int n_windows, int n_enc, int G, int R, int U, int* __restrict__ table) {
+// same units (encoder e cut into u_e nearly equal runs of q_e = n / u_e or q_e + 1 windows), the same stable order
+// (size descending, then encoder-major, then run index), the same snake dealing.  One thread per unit computes its
+// rank in closed form: of the first j runs of encoder e, floor(j n / u_e) - j q_e have q_e + 1 windows.
+__global__ void __launch_bounds__(1024) conv_f16w_table_kernel(int n_windows, int n_enc, int G, int R, int U,
+                                                               int* __restrict__ table) {
   for (int i = threadIdx.x; i < G * R; i += blockDim.x) table[i] = -1;
   __syncthreads();
-  if (threadIdx.x != 0) return;
-  int k = 0;
-  for (int sz = F16W_MAX; sz >= 1; --sz)
-    for (int e = 0; e < n_enc; ++e) {
-      const int ue = min(n_windows, U / n_enc + (e < U % n_enc));
-      for (int j = 0; j < ue; ++j) {
-        const int a = (int)((long long)j * n_windows / ue), b = (int)((long long)(j + 1) * n_windows / ue);
-        if (b - a != sz) continue;
-        const int r = k / G, q = k % G, pos = (r & 1) ? G - 1 - q : q;
-        table[r * G + pos] = e | (sz << 4) | (a << 8);
-        ++k;
-      }
+  auto ue_of = [&](int e) { return min(n_windows, U / n_enc + (e < U % n_enc)); };
+  auto count = [&](int e, int sz) {  // runs of encoder e with sz windows
+    const int ue = ue_of(e), q = n_windows / ue, big = n_windows - q * ue;
+    return sz == q + 1 ? big : (sz == q ? ue - big : 0);
+  };
+  for (int e = 0; e < n_enc; ++e) {
+    const int ue = ue_of(e), q = n_windows / ue;
+    for (int j = threadIdx.x; j < ue; j += blockDim.x) {
+      const int a = (int)((long long)j * n_windows / ue), b = (int)((long long)(j + 1) * n_windows / ue);
+      const int sz = b - a;
+      int k = 0;
+      for (int s2 = F16W_MAX; s2 > sz; --s2)
+        for (int e2 = 0; e2 < n_enc; ++e2) k += count(e2, s2);
+      for (int e2 = 0; e2 < e; ++e2) k += count(e2, sz);
+      const int bigs = a - j * q;  // runs of q + 1 windows before run j
+      k += sz == q + 1 ? bigs : j - bigs;
+      const int r = k / G, p = k % G, pos = (r & 1) ? G - 1 - p : p;
+      table[r * G + pos] = e | (sz << 4) | (a << 8);
     }
+  }
 }
 }  // namespace
 namespace vge {
 
 hipError_t launch_conv_f16w_table(int n_windows, int n_enc, int G, int R, int U, int* d_table, hipStream_t s) {
-  hipLaunchKernelGGL(conv_f16w_table_kernel, dim3(1), dim3(256), 0, s, n_windows, n_enc, G, R, U, d_table);
+  hipLaunchKernelGGL(conv_f16w_table_kernel, dim3(1), dim3(1024), 0, s, n_windows, n_enc, G, R, U, d_table);
   return hipGetLastError();
 }
 

@@ -149,12 +149,15 @@ def run_eval_distributed(generated_meshes_dir: str, real_meshes_dir: str, model_
                          real_kp_dir: str, clip_len: int = 32, stride: int = 8,
                          out_json: Optional[str] = "video_scores.json", device="cuda", compute: str = "f32x3",
                          timings: Optional[dict] = None, human_scores_path: Optional[str] = None,
-                         save_features: Optional[str] = None):
+                         save_features: Optional[str] = None, stats_cache: Optional[str] = None):
     """vge.eval.run_eval sharded over the ranks of the initialised process group.  Returns the merged
     {video: {ac, tc}} dict on rank 0 (None elsewhere); rank 0 writes out_json, the Spearman correlations
     against `human_scores_path` (eval.py:456-464) and, with `save_features`, window_features.pt
     (eval.py:424, windows of all ranks in the single-process order: the shards are contiguous blocks of the
-    sorted generated list)."""
+    sorted generated list).  stats_cache: the real set's stats + centroid artifact (vge/stats_cache.py); when every
+    rank reads a matching one the real set is skipped: no stats or centroid exchange, only int32 flag gathers (the
+    cache-hit agreement and agree()'s error flags) before the score gather; otherwise the full flow runs and rank 0
+    writes the artifact after the exchanges."""
     from . import eval as VE
     from .data import NpzVideoDataset, create_dataset_from_generated_meshes
     rank, ws = world()
@@ -166,6 +169,10 @@ def run_eval_distributed(generated_meshes_dir: str, real_meshes_dir: str, model_
     gen_items = sorted(gen.items, key=lambda it: it.path)
     mine = NpzVideoDataset("", items=shard(gen_items, rank, ws))
     overlap = os.environ.get("VGE_FLOW_OVERLAP", "1") != "0"  # 0: every phase in order (A/B timing)
+    model_sha = None
+    if stats_cache:
+        from .stats_cache import model_digest
+        model_sha = model_digest(model_path)
     pool = ThreadPoolExecutor(max_workers=2)
     gen_fs = pool.submit(VE.load_frame_store, mine.items, keypoint_dir, True) if mine.items and overlap else None
     if overlap and isinstance(model_path, (str, os.PathLike)):  # the checkpoint read overlaps the real set's phases
@@ -173,13 +180,26 @@ def run_eval_distributed(generated_meshes_dir: str, real_meshes_dir: str, model_
     try:
         return _run_eval_phases(real_meshes_dir, model_path, keypoint_dir, real_kp_dir, clip_len, stride, out_json,
                                 device, compute, timings, rank, ws, t0, mine, gen_fs, human_scores_path,
-                                save_features)
+                                save_features, stats_cache, model_sha)
     finally:
         pool.shutdown(wait=True)
 
 
+def all_agree(flag: bool) -> bool:
+    """True iff `flag` holds on every rank (one int32 all-gather)."""
+    if not in_group():
+        return flag
+    _, ws = world()
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32)
+    t = t.to(_collective_device(t))
+    parts = [torch.empty_like(t) for _ in range(ws)]
+    dist.all_gather(parts, t)
+    return all(int(p.item()) == 1 for p in parts)
+
+
 def _run_eval_phases(real_meshes_dir, model_path, keypoint_dir, real_kp_dir, clip_len, stride, out_json, device,
-                     compute, timings, rank, ws, t0, mine, gen_fs, human_scores_path, save_features):
+                     compute, timings, rank, ws, t0, mine, gen_fs, human_scores_path, save_features, stats_cache=None,
+                     model_sha=None):
     """Three rank-local phases, each closed by agree() before its exchange, so an error on one rank (a missing
     keypoints.npy, an unreadable checkpoint) makes every rank raise instead of leaving peers in a collective."""
     from . import eval as VE
@@ -187,9 +207,84 @@ def _run_eval_phases(real_meshes_dir, model_path, keypoint_dir, real_kp_dir, cli
     from .data import ACTION_CLASSES, NpzVideoDataset, load_clip, train_test_split
     real_ds = NpzVideoDataset(real_meshes_dir, filter_classes=ACTION_CLASSES)
     train_ds, _ = train_test_split(real_ds, train_ratio=0.8, seed=1337)
-    my_train = shard(train_ds.items, rank, ws)
     label_dict = {cls: i for i, cls in enumerate(sorted({it.cls for it in real_ds.items}))}
 
+    from . import stats_cache as SC
+    fp = hit = None
+    if stats_cache:
+        fp = SC.fingerprint(train_ds.items, real_kp_dir, model_sha, compute, clip_len, stride)
+        hit = SC.load(stats_cache, fp)
+        if hit is not None and hit["classes"] != sorted(label_dict):
+            hit = None
+        if not all_agree(hit is not None):  # a miss on any rank: every rank runs the full flow
+            hit = None
+
+    if hit is not None:
+        # cached: stats and centroids from the exchanged sufficient statistics; no real set, no exchange
+        stats = VE.stats_from_sums(hit["stats_sums"], hit["stats_counts"], device)
+        dims_raw, dims_diff = VE.infer_dims_from_stats(stats)
+
+        def load_only():
+            mp = model_path.result() if isinstance(model_path, Future) else model_path
+            return VE.load_model(mp, dims_raw, dims_diff, device=device, compute=compute)
+
+        t1 = time.perf_counter()
+        model = guarded("checkpoint", load_only)
+        centroids = ops.centroid_finalize(torch.from_numpy(hit["cent_sums"]).to(device),
+                                          torch.from_numpy(hit["cent_counts"]).to(device))
+        t2 = time.perf_counter()
+    else:
+        model, stats, centroids, t1, t2 = _real_set_phases(VE, ops, real_meshes_dir, model_path, real_kp_dir, clip_len,
+                                                           stride, device, compute, rank, ws, train_ds, label_dict,
+                                                           load_clip, stats_cache, fp)
+
+    # phase 3: this rank's generated videos -> (ac, tc); no collective until the gather to rank 0
+    def local_scores():
+        combined, feats_host = {}, None
+        if mine.items:
+            fs = gen_fs.result() if gen_fs is not None else VE.load_frame_store(mine.items, keypoint_dir, True)
+            store = ops.DeviceFrameStore.from_host(fs, device)
+            feats = VE.extract_window_features(model, mine, keypoint_dir, stats, clip_len, stride, device,
+                                               store=store, frame_embed=bool(save_features))
+            ac = VE.compute_action_consistency_scores(feats, centroids, label_dict)
+            tc = VE.compute_temporal_coherence_scores(feats, centroids, label_dict)
+            combined = VE.combine_scores(ac, tc)
+            if save_features:
+                feats_host = {"seq_embeds": feats["seq_embeds"].cpu(), "frame_embeds": feats["frame_embeds"].cpu(),
+                              "cls_names": list(feats["cls_names"]), "vid_names": list(feats["vid_names"])}
+        if torch.cuda.is_available() and str(device).startswith("cuda"):
+            torch.cuda.synchronize(device)
+        return combined, feats_host
+
+    combined, feats_host = guarded("generated-set scoring", local_scores)
+    t3 = time.perf_counter()
+    parts = gather_to_rank0(combined)
+    fparts = gather_to_rank0(feats_host) if save_features else None
+    if timings is not None:
+        timings.update(stats_s=t1 - t0, centroids_s=t2 - t1, gen_s=t3 - t2, rank=rank, world=ws,
+                       stats_cache="off" if not stats_cache else ("hit" if hit is not None else "miss"))
+    if rank != 0:
+        return None
+    merged = merge_scores(parts)
+    if out_json:
+        with open(out_json, "w") as f:
+            json.dump(merged, f, indent=2)
+    if save_features:
+        save_window_features(fparts, save_features)
+    if human_scores_path and os.path.exists(human_scores_path):
+        for key in ("ac", "tc"):
+            sc = {v: e[key] for v, e in merged.items() if key in e}
+            corr, p, m = VE.compute_spearman_correlation(sc, human_scores_path, key)
+            if corr is not None:
+                print(f"{key.upper()} Spearman: {corr:.4f} (p={p:.4e}, matched {len(m)})")
+    return merged
+
+
+def _real_set_phases(VE, ops, real_meshes_dir, model_path, real_kp_dir, clip_len, stride, device, compute, rank, ws,
+                     train_ds, label_dict, load_clip, stats_cache=None, fp=None):
+    """Phases 1-2 of the flow: the real-train shard's stats and centroid sufficient statistics, each exchanged after
+    agree(); rank 0 writes the stats cache (when asked) from the exchanged sums."""
+    my_train = shard(train_ds.items, rank, ws)
     # phase 1: this rank's real-train shard -> float64 stats sufficient statistics
     def local_stats():
         sums = torch.zeros((2, ops.FEAT_DIM), device=device, dtype=torch.float64)
@@ -229,47 +324,10 @@ def _run_eval_phases(real_meshes_dir, model_path, keypoint_dir, real_kp_dir, cli
     csum, ccnt = centroid_reduce_fn(captured["s"], captured["c"])
     centroids = ops.centroid_finalize(csum, ccnt)
     t2 = time.perf_counter()
-
-    # phase 3: this rank's generated videos -> (ac, tc); no collective until the gather to rank 0
-    def local_scores():
-        combined, feats_host = {}, None
-        if mine.items:
-            fs = gen_fs.result() if gen_fs is not None else VE.load_frame_store(mine.items, keypoint_dir, True)
-            store = ops.DeviceFrameStore.from_host(fs, device)
-            feats = VE.extract_window_features(model, mine, keypoint_dir, stats, clip_len, stride, device,
-                                               store=store, frame_embed=bool(save_features))
-            ac = VE.compute_action_consistency_scores(feats, centroids, label_dict)
-            tc = VE.compute_temporal_coherence_scores(feats, centroids, label_dict)
-            combined = VE.combine_scores(ac, tc)
-            if save_features:
-                feats_host = {"seq_embeds": feats["seq_embeds"].cpu(), "frame_embeds": feats["frame_embeds"].cpu(),
-                              "cls_names": list(feats["cls_names"]), "vid_names": list(feats["vid_names"])}
-        if torch.cuda.is_available() and str(device).startswith("cuda"):
-            torch.cuda.synchronize(device)
-        return combined, feats_host
-
-    combined, feats_host = guarded("generated-set scoring", local_scores)
-    t3 = time.perf_counter()
-    parts = gather_to_rank0(combined)
-    fparts = gather_to_rank0(feats_host) if save_features else None
-    if timings is not None:
-        timings.update(stats_s=t1 - t0, centroids_s=t2 - t1, gen_s=t3 - t2, rank=rank, world=ws)
-    if rank != 0:
-        return None
-    merged = merge_scores(parts)
-    if out_json:
-        with open(out_json, "w") as f:
-            json.dump(merged, f, indent=2)
-    if save_features:
-        save_window_features(fparts, save_features)
-    if human_scores_path and os.path.exists(human_scores_path):
-        for key in ("ac", "tc"):
-            sc = {v: e[key] for v, e in merged.items() if key in e}
-            corr, p, m = VE.compute_spearman_correlation(sc, human_scores_path, key)
-            if corr is not None:
-                print(f"{key.upper()} Spearman: {corr:.4f} (p={p:.4e}, matched {len(m)})")
-    return merged
-
+    if stats_cache and rank == 0:
+        from . import stats_cache as SC
+        SC.save(stats_cache, fp, s.cpu().numpy(), c, csum.cpu().numpy(), ccnt.cpu().numpy(), sorted(label_dict))
+    return model, stats, centroids, t1, t2
 
 def save_window_features(parts: List[Optional[dict]], path: str) -> None:
     """window_features.pt (eval.py:197-204 layout) from the per-rank feature dicts, concatenated in rank order."""

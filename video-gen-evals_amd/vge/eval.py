@@ -284,27 +284,63 @@ def compute_spearman_correlation(model_scores: dict, human_scores_path: str, hum
     return corr, p, matched
 
 
+def stats_from_sums(sums, counts, device) -> ModalityStatsGPU:
+    """ModalityStats from (exchanged or cached) sufficient statistics: vge_stats_finalize on the device."""
+    sums = torch.as_tensor(sums, dtype=torch.float64).to(device)
+    counts = np.asarray(counts, np.int64)
+    mean, std = ops.stats_finalize(sums, counts)
+    return ModalityStatsGPU(mean, std, sums, counts)
+
+
 def run_eval(generated_meshes_dir: str, real_meshes_dir: str, model_path, keypoint_dir: str, real_kp_dir: str,
              human_scores_path: Optional[str] = None, clip_len: int = 32, stride: int = 8,
              out_json: Optional[str] = "video_scores.json", device="cuda", timings: Optional[dict] = None,
-             compute: str = "f32x3", save_features: Optional[str] = None):
+             compute: str = "f32x3", save_features: Optional[str] = None, stats_cache: Optional[str] = None):
     """eval.py __main__ (350-466) on one GPU; returns the combined {video: {ac, tc}} dict.  save_features: the
-    window_features.pt of eval.py:439-443 (off by default: it copies every frame embedding to the host)."""
+    window_features.pt of eval.py:439-443 (off by default: it copies every frame embedding to the host).
+    stats_cache: path of the real set's stats + centroid artifact (vge/stats_cache.py): read when its fingerprint
+    matches (the real set is then neither decoded nor encoded), else computed and written."""
+    from . import stats_cache as SC
     t0 = time.perf_counter()
     real_ds = NpzVideoDataset(real_meshes_dir, filter_classes=ACTION_CLASSES)
     train_ds, _ = train_test_split(real_ds, train_ratio=0.8, seed=1337)
-    real_store = ops.DeviceFrameStore.from_host(load_frame_store(train_ds.items, real_kp_dir, require_kp=False), device)
-    stats = compute_stats_from_npz(train_ds.items, real_kp_dir, device=device, store=real_store)
-    dims_raw, dims_diff = infer_dims_from_stats(stats)
-    model = load_model(model_path, dims_raw, dims_diff, device=device, compute=compute)
-    t1 = time.perf_counter()
     label_dict = {cls: i for i, cls in enumerate(sorted({it.cls for it in real_ds.items}))}
-    # centroids need every real-train keypoint file (WindowDataset raises otherwise)
-    for i, it in enumerate(train_ds.items):
-        if real_store.host_videos[i, 3] == 0:
-            load_clip(it, real_kp_dir, require_kp=True)  # raises FileNotFoundError like utils.py:416-417
-    centroids, label_dict, _ = build_real_centroids(model, real_meshes_dir, real_kp_dir, stats, clip_len, stride, device,
-                                                    train_items=train_ds.items, label_dict=label_dict, store=real_store)
+    fp = hit = None
+    if stats_cache:
+        fp = SC.fingerprint(train_ds.items, real_kp_dir, SC.model_digest(model_path), compute, clip_len, stride)
+        hit = SC.load(stats_cache, fp)
+        if hit is not None and hit["classes"] != sorted(label_dict):
+            hit = None
+    if hit is not None:
+        stats = stats_from_sums(hit["stats_sums"], hit["stats_counts"], device)
+        dims_raw, dims_diff = infer_dims_from_stats(stats)
+        model = load_model(model_path, dims_raw, dims_diff, device=device, compute=compute)
+        t1 = time.perf_counter()
+        centroids = ops.centroid_finalize(torch.from_numpy(hit["cent_sums"]).to(device),
+                                          torch.from_numpy(hit["cent_counts"]).to(device))
+    else:
+        real_store = ops.DeviceFrameStore.from_host(load_frame_store(train_ds.items, real_kp_dir, require_kp=False),
+                                                    device)
+        stats = compute_stats_from_npz(train_ds.items, real_kp_dir, device=device, store=real_store)
+        dims_raw, dims_diff = infer_dims_from_stats(stats)
+        model = load_model(model_path, dims_raw, dims_diff, device=device, compute=compute)
+        t1 = time.perf_counter()
+        # centroids need every real-train keypoint file (WindowDataset raises otherwise)
+        for i, it in enumerate(train_ds.items):
+            if real_store.host_videos[i, 3] == 0:
+                load_clip(it, real_kp_dir, require_kp=True)  # raises FileNotFoundError like utils.py:416-417
+        cap = {}
+
+        def capture(s_, c_):
+            cap["s"], cap["c"] = s_, c_
+            return s_, c_
+
+        centroids, label_dict, _ = build_real_centroids(model, real_meshes_dir, real_kp_dir, stats, clip_len, stride,
+                                                        device, train_items=train_ds.items, label_dict=label_dict,
+                                                        store=real_store, reduce_fn=capture)
+        if stats_cache:
+            SC.save(stats_cache, fp, stats.sums.cpu().numpy(), stats.counts, cap["s"].cpu().numpy(),
+                    cap["c"].cpu().numpy(), sorted(label_dict))
     t2 = time.perf_counter()
     dataset = create_dataset_from_generated_meshes(generated_meshes_dir)
     feats = extract_window_features(model, dataset, keypoint_dir, stats, clip_len, stride, device,
@@ -323,7 +359,8 @@ def run_eval(generated_meshes_dir: str, real_meshes_dir: str, model_path, keypoi
             if corr is not None:
                 print(f"{key.upper()} Spearman: {corr:.4f} (p={p:.4e}, matched {len(m)})")
     if timings is not None:
-        timings.update(stats_s=t1 - t0, centroids_s=t2 - t1, gen_s=t3 - t2, n_windows=len(feats["vid_names"]))
+        timings.update(stats_s=t1 - t0, centroids_s=t2 - t1, gen_s=t3 - t2, n_windows=len(feats["vid_names"]),
+                       stats_cache="off" if not stats_cache else ("hit" if hit is not None else "miss"))
     return combined
 
 
@@ -343,6 +380,8 @@ def main(argv=None):
     ap.add_argument("--clip-len", type=int, default=32)
     ap.add_argument("--stride", type=int, default=8)
     ap.add_argument("--compute", default="f32x3", choices=["f32x3", "f32", "f16"])
+    ap.add_argument("--stats-cache", default=None,
+                    help="real-set stats + centroid artifact (.npz): reused when its fingerprint matches, else written")
     a = ap.parse_args(argv)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
@@ -355,12 +394,13 @@ def main(argv=None):
             res = run_eval_distributed(a.generated_meshes, a.real_meshes, a.model, a.keypoints, a.real_keypoints,
                                        a.clip_len, a.stride, out_json=a.out, device=f"cuda:{local}",
                                        compute=a.compute, human_scores_path=a.human_scores,
-                                       save_features=a.save_features)
+                                       save_features=a.save_features, stats_cache=a.stats_cache)
         finally:
             dist.destroy_process_group()
     else:
         res = run_eval(a.generated_meshes, a.real_meshes, a.model, a.keypoints, a.real_keypoints, a.human_scores,
-                       a.clip_len, a.stride, out_json=a.out, compute=a.compute, save_features=a.save_features)
+                       a.clip_len, a.stride, out_json=a.out, compute=a.compute, save_features=a.save_features,
+                       stats_cache=a.stats_cache)
     if res is not None:
         print(f"Saved AC/TC scores for {len(res)} videos to {a.out}")
     return 0

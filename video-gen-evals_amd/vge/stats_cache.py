@@ -1,0 +1,97 @@
+"""The real set's ModalityStats + class-centroid artifact (SURVEY.md section 7 hard part 4, 8(e) option 2).
+
+eval.py recomputes, on every run, the per-dimension statistics of the real-train videos (utils.py:595-801) and the
+real-class centroids (eval.py:260-286, utils.py:1018-1045) before it scores anything.  Both are functions of the
+real-train set, the checkpoint, the compute mode and the window grid only, so they are kept here as their
+SUFFICIENT statistics, after the cross-rank exchange:
+
+    stats_sums    float64 [2, 2596]   column sums of x and x^2 (vge_stats_accumulate)
+    stats_counts  int64   [2]          mesh frames, keypoint frames
+    cent_sums     float32 [C, 256]     per-class sums of seq embeddings (vge_centroid_accumulate)
+    cent_counts   float32 [C]
+    classes       the sorted real class list (label = index)
+
+Finalising them (vge_stats_finalize, vge_centroid_finalize) on the device gives bit-identical mean / std /
+centroids to a fresh run, so a cached run's scores equal a fresh run's bit for bit.  The file is an .npz written
+with numpy (allow_pickle=False both ways) plus a JSON fingerprint; any mismatch of the fingerprint (a real file's
+size / mtime, the checkpoint's SHA-256, compute mode, clip length, stride, format) is a miss and the caller
+recomputes and rewrites it.  Writes are atomic (temporary file + os.replace).
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+from typing import Dict, Optional, Sequence
+
+import numpy as np
+
+from .data import VideoItem, keypoint_path
+
+FORMAT = 1
+
+
+def _file_sig(path: str) -> list:
+    try:
+        st = os.stat(path)
+        return [os.path.abspath(path), int(st.st_size), int(st.st_mtime_ns)]
+    except OSError:
+        return [os.path.abspath(path), -1, -1]
+
+
+def model_digest(model_path) -> str:
+    """SHA-256 of the checkpoint file, or of a state dict's arrays (names, shapes, bytes) in sorted order."""
+    h = hashlib.sha256()
+    if isinstance(model_path, (str, os.PathLike)):
+        with open(model_path, "rb") as f:
+            for blk in iter(lambda: f.read(1 << 22), b""):
+                h.update(blk)
+        return h.hexdigest()
+    sd = model_path[0] if isinstance(model_path, tuple) else model_path
+    for k in sorted(sd):
+        a = np.ascontiguousarray(np.asarray(sd[k], dtype=np.float32))
+        h.update(k.encode())
+        h.update(str(a.shape).encode())
+        h.update(a.tobytes())
+    return h.hexdigest()
+
+
+def fingerprint(train_items: Sequence[VideoItem], real_kp_dir: Optional[str], model_sha: str, compute: str,
+                clip_len: int, stride: int) -> Dict:
+    files = []
+    for it in sorted(train_items, key=lambda x: x.path):
+        files.append(_file_sig(it.path))
+        if real_kp_dir:
+            files.append(_file_sig(keypoint_path(real_kp_dir, it.cls, os.path.splitext(it.name)[0])))
+    return {"format": FORMAT, "model_sha256": model_sha, "compute": compute, "clip_len": int(clip_len),
+            "stride": int(stride), "real_files": files}
+
+
+def save(path: str, fp: Dict, stats_sums, stats_counts, cent_sums, cent_counts, classes: Sequence[str]) -> None:
+    """Write the artifact (host copies of the exchanged sufficient statistics) atomically."""
+    tmp = f"{path}.tmp.{os.getpid()}"
+    with open(tmp, "wb") as f:
+        np.savez(f, fingerprint=np.frombuffer(json.dumps(fp, sort_keys=True).encode(), np.uint8),
+                 classes=np.frombuffer(json.dumps(list(classes)).encode(), np.uint8),
+                 stats_sums=np.asarray(stats_sums, np.float64), stats_counts=np.asarray(stats_counts, np.int64),
+                 cent_sums=np.asarray(cent_sums, np.float32), cent_counts=np.asarray(cent_counts, np.float32))
+    os.replace(tmp, path)
+
+
+def load(path: Optional[str], fp: Dict) -> Optional[Dict]:
+    """The artifact's arrays if `path` exists and its fingerprint equals `fp`, else None (a miss)."""
+    if not path or not os.path.exists(path):
+        return None
+    try:
+        with np.load(path, allow_pickle=False) as z:
+            got = json.loads(bytes(z["fingerprint"]).decode())
+            if got != json.loads(json.dumps(fp, sort_keys=True)):
+                return None
+            out = {k: np.array(z[k]) for k in ("stats_sums", "stats_counts", "cent_sums", "cent_counts")}
+            out["classes"] = json.loads(bytes(z["classes"]).decode())
+    except (OSError, ValueError, KeyError):
+        return None
+    if out["stats_sums"].shape != (2, 2596) or out["stats_counts"].shape != (2,) or \
+            out["cent_sums"].shape != (len(out["classes"]), 256) or out["cent_counts"].shape != (len(out["classes"]),):
+        return None
+    return out
