@@ -188,8 +188,8 @@ int vge_score_videos(const float* seq_embed, const float* tc_window, const int32
 
 /* ---------------------------------------------------------------------------------------------
  * Real-class centroids.  Replaces build_train_centroids_subset (utils.py:1018-1045):
- * sums.index_add_(0, y, z); counts.index_add_ -- a deterministic segmented reduction (segments of 256
- * windows summed in window order, then the segment partials in segment order: the same bits for any
+ * sums.index_add_(0, y, z); counts.index_add_ -- a deterministic segmented reduction (segments of 512
+ * windows, CENT_SEG in vge_score.hip, summed in window order, then the segment partials in segment order: the same bits for any
  * device or launch, within a few ulps of a sequential index_add_); d <= 256; class ids outside [0, C)
  * are ignored.  finalize = normalize(sums / counts.clamp_min(1)).
  * sums [C,d] / counts [C] (device float) are ACCUMULATED INTO and are the RCCL all-gather payload.

@@ -172,8 +172,12 @@ def vitdet_geometry(box):
 
 def _gauss_nearest(img: np.ndarray, sigma: float) -> np.ndarray:
     """skimage.filters.gaussian(img, sigma, channel_axis=2, preserve_range=True): separable, mode 'nearest',
-    truncate 4 (scipy.ndimage.gaussian_filter1d's radius int(4 sigma + 0.5)); float32 here."""
-    r = min(8, int(4.0 * sigma + 0.5))
+    truncate 4 (scipy.ndimage.gaussian_filter1d's radius int(4 sigma + 0.5), uncapped up to the kernel's
+    MAX_RADIUS 32); float32 here.  Shares the device kernel's two documented deviations (vge_hmr_front.hip header):
+    the blurred patch is rounded to uint8, and bilinear weights are float rather than cv2's fixed point."""
+    r = int(4.0 * sigma + 0.5)
+    if r > 32:
+        raise ValueError(f"gaussian radius {r} > 32 (box too large for the crop kernel)")
     t = np.exp(-0.5 * np.arange(r + 1) ** 2 / sigma ** 2)
     t = (t / (t[0] + 2 * t[1:].sum())).astype(np.float32)
     x = img.astype(np.float32)

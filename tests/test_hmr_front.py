@@ -43,6 +43,7 @@ def test_vitdet_geometry_by_hand():
 @pytest.mark.parametrize("size,boxes", [
     (256, [[60, 40, 140, 230], [0, 0, 256, 256], [-30, 100, 80, 300], [120.5, 10.25, 131.75, 40.5]]),
     (512, [[10, 10, 500, 480], [200, 100, 320, 450], [0, 0, 512, 300]]),
+    (256, [[-400, -400, 660, 660], [-60, -300, 300, 560]]),  # radii 12 (> the old cap of 8) and 6
 ])
 def test_crop_matches_oracle(size, boxes):
     if not torch.cuda.is_available():
@@ -60,6 +61,8 @@ def test_crop_matches_oracle(size, boxes):
         assert d <= (1 if blurred else 0), (i, b, d, blurred)
     with pytest.raises(Exception, match="box"):
         crop_persons(torch.from_numpy(frames).to(DEV), np.array([[10, 10, 10, 50]], np.float32))
+    with pytest.raises(Exception, match="too large"):  # radius 44 > 32: refused, not truncated
+        crop_persons(torch.from_numpy(frames).to(DEV), np.array([[-1500, -1500, 2000, 2000]], np.float32))
 
 
 @gpu

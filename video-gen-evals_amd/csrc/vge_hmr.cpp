@@ -406,7 +406,10 @@ int vge_hmr_crop(const uint8_t* frames, int n_frames, int H, int W, const float*
     if (!(b[2] > b[0]) || !(b[3] > b[1]) || !std::isfinite(b[0] + b[1] + b[2] + b[3]))
       return fail(VGE_ERR_ARG, "vge_hmr_crop: empty or non-finite box");
   }
-  HIPCHK(vge::launch_hmr_crop(frames, H, W, boxes, frame_of, n_crops, crops, S(stream)));
+  const hipError_t e = vge::launch_hmr_crop(frames, H, W, boxes, frame_of, n_crops, crops, S(stream));
+  if (e == hipErrorInvalidValue)  // the only argument check inside: the anti-alias radius
+    return fail(VGE_ERR_ARG, "vge_hmr_crop: box too large (anti-alias Gaussian radius > 32)");
+  HIPCHK(e);
   return VGE_OK;
 }
 

@@ -9,6 +9,12 @@
 // gen_trans_from_patch_cv), bilinear over the frame (the blurred frame's 4 taps are computed in place from the
 // separable Gaussian), rounded to uint8 like warpAffine on a uint8 image.  Restated in float with contraction off,
 // so the host oracle (oracle/hmr.py vitdet_crop) reproduces every byte of the unblurred path.
+// Known deviations from ViTDetDataset, shared by the oracle (so its byte test cannot see them; parity unpinned):
+//  * the blurred path rounds the patch to uint8 (the reference warps the float64 blurred frame and never
+//    quantises it: <= 0.5 grey level per channel before the mean / std normalisation);
+//  * bilinear weights are float, not cv2's 1/32-subpixel fixed-point INTER_LINEAR weights (<= 1 grey level).
+// The Gaussian radius is scipy's int(4 sigma + 0.5) uncapped up to MAX_RADIUS (boxes up to ~8.6k px); a larger
+// box is refused with hipErrorInvalidValue rather than blurred with a truncated kernel.
 // HBM-bound: reads ~4 x 3 B of frame per output pixel (L2-resident rows), writes 196,608 B per crop.
 #include "vge_common.h"
 
@@ -21,10 +27,11 @@ struct CropInst {
   int frame;
   float cx, cy, k;  // source centre, source pixels per output pixel
   int radius;       // Gaussian half width (0: no blur)
-  float w[9];       // normalised Gaussian taps w[0..radius] (symmetric)
+  float w[33];      // normalised Gaussian taps w[0..radius] (symmetric)
 };
 
 constexpr int CROP = 256;
+constexpr int MAX_RADIUS = 32;
 
 __global__ void __launch_bounds__(256) hmr_crop_kernel(const uint8_t* __restrict__ frames, int H, int W,
                                                        const CropInst* __restrict__ inst, int n,
@@ -93,8 +100,9 @@ hipError_t launch_hmr_crop(const uint8_t* frames, int H, int W, const float* box
     const double df = bbox / CROP / 2.0;
     if (df > 1.1) {
       const double sigma = (df - 1.0) / 2.0;
-      c.radius = std::min(8, (int)(4.0 * sigma + 0.5));
-      double sum = 0.0, t[9];
+      c.radius = (int)(4.0 * sigma + 0.5);
+      if (c.radius > MAX_RADIUS) return hipErrorInvalidValue;
+      double sum = 0.0, t[MAX_RADIUS + 1];
       for (int j = 0; j <= c.radius; ++j) {
         t[j] = std::exp(-0.5 * j * j / (sigma * sigma));
         sum += j == 0 ? t[j] : 2.0 * t[j];
