@@ -16,6 +16,9 @@
  *   - Feature-column order is the reference's feats layout (utils.py:496-514):
  *       raw  = vit[1024] | global_orient[9] | pose[207] | betas[10] | kp2d[120]      (1370)
  *       diff = vit[1024] | global_orient[3] | pose[69]  | betas[10] | kp2d[120]      (1226)
+ *     or, when the reference runs without keypoints (keypoint_dir None: no kp2d columns, 4 modalities),
+ *       raw  = vit[1024] | global_orient[9] | pose[207] | betas[10]                   (1250)
+ *       diff = vit[1024] | global_orient[3] | pose[69]  | betas[10]                   (1106)
  */
 #ifndef VGE_H
 #define VGE_H
@@ -40,9 +43,9 @@ typedef enum {
   VGE_ERR_WORKSPACE = 6,      /* vge_encoder_reserve() was not called for this many windows */
   VGE_ERR_UNSUPPORTED = 7     /* a model shape the kernels are not built for (vge_encoder_create): d_model != 256,
                                  time_heads != 8, clip_len != 32, or a modality set / input dims other than the
-                                 reference's five (e.g. the keypoint-less layout utils.py:496-514 builds when
-                                 keypoint_dir is None).  load_model (eval.py:136-165) reads these from the
-                                 checkpoint; time_layers is free (any >= 1). */
+                                 reference's five or its keypoint-less four (clip / dino modalities, other vit or
+                                 pose widths).  load_model (eval.py:136-165) reads these from the checkpoint;
+                                 time_layers is free (any >= 1). */
 } vge_status;
 
 /* Encoder compute modes.  VGE_F32: exact f32 MFMA (v_mfma_f32_16x16x4_f32, bitwise an fmaf chain).
@@ -63,13 +66,21 @@ typedef enum { VGE_F32 = 0, VGE_F32X3 = 1, VGE_F16 = 2 } vge_dtype;
 
 #define VGE_FEAT_DIM 2596
 #define VGE_RAW_DIM 1370
+#define VGE_FEAT_DIM_NOKP 2356 /* keypoint-less layout (keypoint_dir None) */
+#define VGE_RAW_DIM_NOKP 1250
+
+/* Feature layouts: which columns WindowDataset._try_one concatenates (utils.py:496-514).  The reference picks it by
+ * whether keypoint_dir is set; infer_dims_from_stats (eval.py:104-133) then gives the model 5 or 4 modalities. */
+typedef enum { VGE_LAYOUT_KP = 0, VGE_LAYOUT_NOKP = 1 } vge_layout;
+int vge_layout_feat_dim(vge_layout layout); /* 2596 / 2356, 0 for an unknown layout */
 #define VGE_CLIP_LEN 32
 #define VGE_D_MODEL 256
 
 /* Model shape (infer_dims_from_stats, eval.py:104-133; HumanActionScorer, model.py:102-148).
  * The kernels are built for the reference configuration: 5 modalities in the order
- * vit, global, pose, beta, kp2d with dims {1024,9,207,10,120} / {1024,3,69,10,120},
- * d_model 256, 4 post-norm layers, 8 heads, FFN 1024, clip_len 32. */
+ * vit, global, pose, beta, kp2d with dims {1024,9,207,10,120} / {1024,3,69,10,120}, or the first 4 of them
+ * (keypoint-less layout: 8 conv encoders, a 4-way fusion, feats rows of 2356), d_model 256, post-norm
+ * layers, 8 heads, FFN 1024, clip_len 32. */
 typedef struct {
   int n_modalities;
   int dims_raw[8];
@@ -113,9 +124,13 @@ typedef struct {
  *   windows : device int32 [n_windows,2] = {video index, start frame}
  *   mean,std: device float [2596] (ModalityStats in feats column order)
  *   feats   : device float [n_windows,32,2596]
+ * vge_featurize_layout: the same for either layout; VGE_LAYOUT_NOKP (keypoint_dir None) reads no keypoints and
+ *   takes mean/std [2356] and feats [n_windows,32,2356] in that layout's column order.
  */
 int vge_featurize(const vge_frame_store* store, const int32_t* windows, int n_windows,
                   const float* mean, const float* std, float* feats, vge_stream_t stream);
+int vge_featurize_layout(const vge_frame_store* store, const int32_t* windows, int n_windows, const float* mean,
+                         const float* std, vge_layout layout, float* feats, vge_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * ModalityStats.  Replaces compute_stats_from_npz (utils.py:595-801) with _update_sum_sum2
@@ -129,12 +144,16 @@ int vge_featurize(const vge_frame_store* store, const int32_t* windows, int n_wi
  *               chunks of as many 32-frame tiles as fit (this call may synchronise the stream)
  * vge_stats_finalize turns (sums, counts) into float32 mean/std (std = sqrt(max(var,0)+1e-6),
  * utils.py:746-750).  Sums are the RCCL exchange payload when the real set is sharded.
+ * vge_stats_finalize_layout writes mean/std in a layout's column order (VGE_LAYOUT_NOKP: [2356], the kp2d
+ * columns dropped -- the reference's keypoint-less ModalityStats); the sums are always [2,2596].
  */
 size_t vge_stats_workspace_bytes(int chunk_tiles);
 int vge_stats_accumulate(const vge_frame_store* store, const int32_t* host_videos, const int32_t* host_video_sel,
                          int n_sel, double* sums, int64_t* counts, void* workspace, size_t workspace_bytes,
                          vge_stream_t stream);
 int vge_stats_finalize(const double* sums, const int64_t* counts, float* mean, float* std, vge_stream_t stream);
+int vge_stats_finalize_layout(const double* sums, const int64_t* counts, vge_layout layout, float* mean, float* std,
+                              vge_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Encoder.  Replaces load_model (eval.py:136-165) + HumanActionScorer.forward (model.py:162-193).
@@ -142,7 +161,8 @@ int vge_stats_finalize(const double* sums, const int64_t* counts, float* mean, f
  * weights into the library's MFMA panel layout in HBM (the handle owns them).
  * reserve: allocates the activation workspace for up to max_windows windows (outside timed
  * regions; compute calls never allocate).
- * encode: feats device [B,T,2596] -> seq_embed device [B,256] (L2-normalised CLS),
+ * encode: feats device [B,T,D] -> seq_embed device [B,256] (L2-normalised CLS), D = vge_encoder_feat_dim
+ *   (2596, or 2356 for a 4-modality keypoint-less model),
  *   frame_embed device [B,T+1,256] or NULL, tc_window device [B] (per-window temporal coherence,
  *   eval.py:216-224) or NULL.
  */
@@ -150,6 +170,7 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
                        vge_encoder** out);
 int vge_encoder_reserve(vge_encoder* enc, int max_windows);
 int vge_encoder_destroy(vge_encoder* enc);
+int vge_encoder_feat_dim(const vge_encoder* enc); /* feats row width the encoder reads: 2596 or 2356 (0: null) */
 int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_embed, float* frame_embed,
                float* tc_window, vge_stream_t stream);
 /* Pipelining hook (no reference counterpart; the reference featurises batch k+1 in DataLoader workers while batch k

@@ -48,3 +48,32 @@ def golden_ops():
 def golden_state_dict():
     from vge import synth
     return synth.make_state_dict(synth.DIMS_RAW, synth.DIMS_DIFF)
+
+
+# ---- the keypoint-less flow (keypoint_dir None: 4 modalities, feats rows of 2356)
+
+@pytest.fixture(scope="session")
+def golden_dataset_nokp(tmp_path_factory):
+    from tests.golden.dataset_spec import build_golden_dataset
+    root = tmp_path_factory.mktemp("golden_ds_nokp")
+    paths, ckpt, digest = build_golden_dataset(str(root), layout="nokp")
+    flow = np.load(GOLDEN / "golden_flow_nokp.npz")
+    assert bytes(flow["dataset_digest"]).hex() == digest, "synthetic generator drifted from the golden fixtures"
+    return paths, ckpt
+
+
+@pytest.fixture(scope="session")
+def golden_flow_nokp():
+    return dict(np.load(GOLDEN / "golden_flow_nokp.npz"))
+
+
+@pytest.fixture(scope="session")
+def golden_meta_nokp():
+    with open(GOLDEN / "golden_scores_nokp.json") as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def golden_state_dict_nokp():
+    from tests.golden.dataset_spec import golden_state_dict
+    return golden_state_dict("nokp")

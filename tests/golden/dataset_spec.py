@@ -20,8 +20,20 @@ GOLDEN_SPEC = {
 }
 
 
-def build_golden_dataset(root: str):
-    """Write dataset + checkpoint under `root`; returns (paths, checkpoint_path, sha256 hexdigest)."""
+NOKP_MODS = ("vit", "global", "pose", "beta")  # the keypoint-less model (keypoint_dir None, utils.py:496-514)
+
+
+def golden_state_dict(layout: str = "kp"):
+    """The golden checkpoint's weights: 5 modalities, or the keypoint-less 4 (same generator, no kp2d)."""
+    if layout == "kp":
+        return synth.make_state_dict(synth.DIMS_RAW, synth.DIMS_DIFF)
+    return synth.make_state_dict({m: synth.DIMS_RAW[m] for m in NOKP_MODS},
+                                 {m: synth.DIMS_DIFF[m] for m in NOKP_MODS})
+
+
+def build_golden_dataset(root: str, layout: str = "kp"):
+    """Write dataset + checkpoint under `root`; returns (paths, checkpoint_path, sha256 hexdigest).  layout "nokp":
+    the same dataset with the 4-modality checkpoint (model_nokp.pt) of the keypoint-less flow."""
     paths = synth.write_dataset(root, n_real_per_class=GOLDEN_SPEC["n_real_per_class"],
                                 n_gen=GOLDEN_SPEC["n_gen"], T_real=GOLDEN_SPEC["T_real"],
                                 T_gen=GOLDEN_SPEC["T_gen"], kp_short_every=GOLDEN_SPEC["kp_short_every"])
@@ -32,8 +44,8 @@ def build_golden_dataset(root: str):
     kd = Path(paths["generated_kps"]) / stem
     kd.mkdir(parents=True, exist_ok=True)
     np.save(kd / "keypoints.npy", clip.keypoints)
-    sd = synth.make_state_dict(synth.DIMS_RAW, synth.DIMS_DIFF)
-    ckpt = os.path.join(root, "model.pt")
+    sd = golden_state_dict(layout)
+    ckpt = os.path.join(root, "model.pt" if layout == "kp" else "model_nokp.pt")
     synth.save_checkpoint(ckpt, sd)
     h = hashlib.sha256()
     for sub in ("real", "real_kp", "generated_meshes", "generated_kps"):

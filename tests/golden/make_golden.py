@@ -11,6 +11,10 @@ synthetic dataset and weights of vge.synth, and stores inputs/outputs as small f
   golden_flow.npz     ModalityStats, feats of 3 windows, seq_embed of every generated window,
                       frame_embeds of 4 windows, centroids + counts, label order
   golden_scores.json  video_scores.json of the eval.py flow + Spearman on TAG_final_human_scores names
+  golden_flow_nokp.npz / golden_scores_nokp.json
+                      the same flow without keypoints (keypoint_dir None for the real and generated sets: the
+                      4-modality layout, raw 1250 | diff 1106, and a 4-modality checkpoint)
+                      -- `python -B tests/golden/make_golden.py nokp` writes only these
 
 Nothing from the reference is copied; only arrays and numbers it produced.  This script never runs
 on the GPU box (the reference is not there); tests regenerate the same synthetic inputs from seeds.
@@ -181,5 +185,70 @@ def main():
     print("golden written to", HERE)
 
 
+def main_nokp():
+    """The eval.py flow with keypoint_dir=None everywhere (utils.py:406-425 skips the keypoint files; the stats hold
+    no keypoint entries, so infer_dims_from_stats gives 4 modalities)."""
+    sys.path.insert(0, REF)
+    import utils as U  # noqa
+    import eval as E  # noqa
+    torch.manual_seed(0)
+    with tempfile.TemporaryDirectory() as tmp:
+        paths, ckpt, digest = build_golden_dataset(tmp, layout="nokp")
+        real_ds = U.NpzVideoDataset(paths["real"], filter_classes=E.ACTION_CLASSES)
+        train_ds, _ = U.train_test_split(real_ds, train_ratio=0.8, seed=1337)
+        stats = U.compute_stats_from_npz(train_ds.items, keypoint_dir=None)
+        dims_raw, dims_diff = E.infer_dims_from_stats(stats)
+        assert list(dims_raw) == ["vit", "global", "pose", "beta"], dims_raw
+        model = E.load_model(ckpt, dims_raw, dims_diff)
+        centroids, label_dict = E.build_real_centroids(model, paths["real"], None, stats, 32, 8)
+        loader = U.make_test_loader(train_ds, clip_len=32, stride=8, stats=stats, seed=1337, batch_size=64,
+                                    keypoint_dir=None, num_workers=0)
+        _, counts = U.build_train_centroids_subset(model, loader, label_dict, device="cpu")
+        dataset = E.create_dataset_from_generated_meshes(paths["generated_meshes"])
+        samples = U.sample_all_windows_npz(dataset, clip_len=32, stride=8)
+        wds = U.WindowDataset(samples=samples, clip_len=32, stats=stats, keypoint_dir=None)
+        dl = torch.utils.data.DataLoader(wds, batch_size=32, shuffle=False, num_workers=0,
+                                         collate_fn=U.safe_collate)
+        feats_all = torch.stack([wds[i][0] for i in range(len(wds))])
+        assert feats_all.shape[-1] == 2356, feats_all.shape
+        features = E.extract_window_features(model, dl)
+        ac = E.compute_action_consistency_scores(features, centroids, label_dict)
+        tc = E.compute_temporal_coherence_scores(features)
+        combined = {}
+        for v in sorted(set(ac) | set(tc)):
+            e = {}
+            if v in ac:
+                e["ac"] = ac[v]
+            if v in tc:
+                e["tc"] = tc[v]
+            combined[v] = e
+        mods = ["vit", "gori", "pose", "beta"]
+        flow = {
+            "stats_mean": np.concatenate([getattr(stats, f"{m}_raw_mean").numpy() for m in mods]
+                                         + [getattr(stats, f"{m}_diff_mean").numpy() for m in mods]),
+            "stats_std": np.concatenate([getattr(stats, f"{m}_raw_std").numpy() for m in mods]
+                                        + [getattr(stats, f"{m}_diff_std").numpy() for m in mods]),
+            "centroids": centroids.numpy(), "counts": counts.numpy(),
+            "seq_embeds": features["seq_embeds"].numpy(),
+            "frame_embeds_first4": features["frame_embeds"][:4].numpy(),
+            "feat_windows": np.array(GOLDEN_SPEC["feat_windows"], np.int64),
+            "feats_sel": feats_all[GOLDEN_SPEC["feat_windows"]].numpy(),
+            "feats_absmean": feats_all.abs().mean(dim=(1, 2)).numpy(),
+            "dataset_digest": np.frombuffer(bytes.fromhex(digest), np.uint8),
+        }
+        assert stats.keypoints_raw_mean is None and flow["stats_mean"].shape == (2356,)
+        np.savez_compressed(HERE / "golden_flow_nokp.npz", **flow)
+        meta = {"label_dict": label_dict, "window_vids": features["vid_names"], "window_cls": features["cls_names"],
+                "n_train_real": len(train_ds), "train_real": [it.name for it in train_ds.items],
+                "video_scores": combined, "dims_raw": list(dims_raw.items()), "dims_diff": list(dims_diff.items())}
+        with open(HERE / "golden_scores_nokp.json", "w") as f:
+            json.dump(meta, f, indent=1, sort_keys=True)
+    print("keypoint-less golden written to", HERE)
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["nokp"]:
+        main_nokp()
+    else:
+        main()
+        main_nokp()

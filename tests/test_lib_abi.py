@@ -98,12 +98,14 @@ def test_gelu_fast_accuracy():
     assert np.abs(out - ref).max() < 5e-7
 
 
-@pytest.mark.parametrize("field,value", [("d_model", 128), ("time_heads", 4), ("n_modalities", 4), ("clip_len", 64)])
+@pytest.mark.parametrize("field,value", [("d_model", 128), ("time_heads", 4), ("n_modalities", 6), ("n_modalities", 3),
+                                         ("clip_len", 64)])
 def test_unsupported_model_shape_has_its_own_status(field, value):
     """load_model (eval.py:136-165) builds HumanActionScorer with d_model / time_layers / time_heads from the
-    checkpoint, and the keypoint-less layout drops kp2d (utils.py:496-514).  Shapes the kernels are not built for
-    are refused before any device work with VGE_ERR_UNSUPPORTED (UnsupportedModelError in Python), distinct from
-    argument errors; time_layers is free."""
+    checkpoint; the modality set is the five of the keypoint layout or the keypoint-less four (utils.py:496-514),
+    clip / dino modalities (6 / 7) are not built.  Shapes the kernels are not built for are refused before any
+    device work with VGE_ERR_UNSUPPORTED (UnsupportedModelError in Python), distinct from argument errors;
+    time_layers is free."""
     import ctypes as C
     from vge import lib as L
     from vge import ops
@@ -123,11 +125,12 @@ def test_unsupported_model_shape_has_its_own_status(field, value):
     assert so.vge_encoder_create(C.byref(dims), (L.TensorView * 1)(), 0, 1, C.byref(h)) == 1  # VGE_ERR_ARG
 
 
-def test_load_model_refuses_keypointless_dims():
+def test_load_model_refuses_clip_modality():
+    """The keypoint-less four are built (tests/test_nokp_layout.py); a CLIP-embedding modality is not."""
     from vge import eval as VE
     from vge.lib import UnsupportedModelError
-    raw = {"vit": 1024, "global": 9, "pose": 207, "beta": 10}
-    diff = {"vit": 1024, "global": 3, "pose": 69, "beta": 10}
+    raw = {"vit": 1024, "global": 9, "pose": 207, "beta": 10, "kp2d": 120, "clip": 512}
+    diff = {"vit": 1024, "global": 3, "pose": 69, "beta": 10, "kp2d": 120, "clip": 512}
     with pytest.raises(UnsupportedModelError):
         VE.load_model({}, raw, diff, device="cpu")
 

@@ -18,12 +18,12 @@
 namespace vge {
 // launchers (vge_featurize.hip / vge_encoder.hip / vge_score.hip)
 hipError_t launch_featurize_tiles(const float*, const float*, const float*, const float*, const float*, const int*,
-                                  const void*, const int*, int, const float*, const float*, float*, hipStream_t);
+                                  const void*, const int*, int, const float*, const float*, float*, int, hipStream_t);
 hipError_t launch_stats_colsum(const float*, const void*, int, int, int, double*, double*, hipStream_t);
-hipError_t launch_stats_finalize(const double*, long long, long long, float*, float*, hipStream_t);
+hipError_t launch_stats_finalize(const double*, long long, long long, float*, float*, int, hipStream_t);
 struct EncDescHost {
   const float* stem; const float* conv; const float* proj; const float* gn_w; const float* gn_b;
-  int in_col, d_in, n_stem_panels, pad;
+  int in_col, d_in, n_stem_panels, ld;
 };
 struct FuseParamsHost {
   const float* kv_w; const float* kv_b; const float* u;
@@ -40,7 +40,7 @@ hipError_t launch_pack_x3(const float* W, int N, int K_real, int ldk, int conv, 
 struct EncDescX3Host {
   const _Float16* stem; const _Float16* conv; const _Float16* proj; const float* gn_w; const float* gn_b;
   const float* cs; const float* fold;
-  int in_col, d_in, n_stem_panels, pad;
+  int in_col, d_in, n_stem_panels, ld;
   float gn_gmax[4], gn_bmax[4];  // max |gamma|, max |beta| per GroupNorm
 };
 struct GemmArgsX3Host {
@@ -216,6 +216,8 @@ void pack_linear_x3(Get W, int N, int K_real, std::vector<_Float16>& out, std::v
 struct vge_encoder {
   int mode = VGE_F32;
   int n_layers = 4;
+  int n_mod = 5, n_enc = 10;     // modalities (5, or 4 keypoint-less) and conv encoders (state + motion)
+  int feat_dim = VGE_FEAT_DIM;   // feats row width of this model's layout (2596 / 2356)
   // weights: f32 image (all modes: norms, biases, constants; f32-mode matrices) + fp16 hi/lo chunks (x3 mode)
   float* wbuf = nullptr;
   _Float16* hbuf = nullptr;
@@ -273,12 +275,22 @@ const char* vge_last_error(void) { return g_err.c_str(); }
 const char* vge_version(void) { return "vge 0.2 (gfx950: f32 MFMA + 3xfp16 split MFMA)"; }
 
 // ------------------------------------------------------------------ featurise
+int vge_featurize_layout(const vge_frame_store* st, const int32_t* windows, int n_windows, const float* mean,
+                         const float* std_, vge_layout layout, float* feats, vge_stream_t stream) {
+  if (!st || !windows || !feats || n_windows < 0 || !mean || !std_) return fail(VGE_ERR_ARG, "vge_featurize: null argument");
+  if (layout != VGE_LAYOUT_KP && layout != VGE_LAYOUT_NOKP) return fail(VGE_ERR_ARG, "vge_featurize: unknown layout");
+  HIPCHK(vge::launch_featurize_tiles(st->pose, st->gori, st->betas, st->vit, st->kp, st->videos, nullptr, windows,
+                                     n_windows, mean, std_, feats, layout == VGE_LAYOUT_KP, S(stream)));
+  return VGE_OK;
+}
+
 int vge_featurize(const vge_frame_store* st, const int32_t* windows, int n_windows, const float* mean, const float* std_,
                   float* feats, vge_stream_t stream) {
-  if (!st || !windows || !feats || n_windows < 0 || !mean || !std_) return fail(VGE_ERR_ARG, "vge_featurize: null argument");
-  HIPCHK(vge::launch_featurize_tiles(st->pose, st->gori, st->betas, st->vit, st->kp, st->videos, nullptr, windows,
-                                     n_windows, mean, std_, feats, S(stream)));
-  return VGE_OK;
+  return vge_featurize_layout(st, windows, n_windows, mean, std_, VGE_LAYOUT_KP, feats, stream);
+}
+
+int vge_layout_feat_dim(vge_layout layout) {
+  return layout == VGE_LAYOUT_KP ? VGE_FEAT_DIM : layout == VGE_LAYOUT_NOKP ? VGE_FEAT_DIM_NOKP : 0;
 }
 
 // ------------------------------------------------------------------ stats
@@ -310,7 +322,7 @@ int vge_stats_accumulate(const vge_frame_store* st, const int32_t* host_videos, 
     if (n == 0) return VGE_OK;
     HIPCHK(hipMemcpyAsync(d_tiles, tiles.data(), tiles.size() * 4, hipMemcpyHostToDevice, S(stream)));
     HIPCHK(vge::launch_featurize_tiles(st->pose, st->gori, st->betas, st->vit, st->kp, st->videos, d_tiles, nullptr, n,
-                                       nullptr, nullptr, d_feats, S(stream)));
+                                       nullptr, nullptr, d_feats, 1, S(stream)));
     const int nch = (n + kColChunk - 1) / kColChunk;
     HIPCHK(vge::launch_stats_colsum(d_feats, d_tiles, n, kColChunk, nch, d_part, sums, S(stream)));
     HIPCHK(hipStreamSynchronize(S(stream)));  // host tile buffer is reused
@@ -338,10 +350,16 @@ int vge_stats_accumulate(const vge_frame_store* st, const int32_t* host_videos, 
   return flush();
 }
 
-int vge_stats_finalize(const double* sums, const int64_t* counts, float* mean, float* std_, vge_stream_t stream) {
+int vge_stats_finalize_layout(const double* sums, const int64_t* counts, vge_layout layout, float* mean, float* std_,
+                              vge_stream_t stream) {
   if (!sums || !counts || !mean || !std_) return fail(VGE_ERR_ARG, "vge_stats_finalize: null argument");
-  HIPCHK(vge::launch_stats_finalize(sums, counts[0], counts[1], mean, std_, S(stream)));
+  if (layout != VGE_LAYOUT_KP && layout != VGE_LAYOUT_NOKP) return fail(VGE_ERR_ARG, "vge_stats_finalize: unknown layout");
+  HIPCHK(vge::launch_stats_finalize(sums, counts[0], counts[1], mean, std_, layout == VGE_LAYOUT_KP, S(stream)));
   return VGE_OK;
+}
+
+int vge_stats_finalize(const double* sums, const int64_t* counts, float* mean, float* std_, vge_stream_t stream) {
+  return vge_stats_finalize_layout(sums, counts, VGE_LAYOUT_KP, mean, std_, stream);
 }
 
 // ------------------------------------------------------------------ encoder
@@ -354,12 +372,15 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
   // VGE_F16 shares the 3xfp16 weight image (its kernels read the hi planes only)
   const bool x3 = compute == VGE_F32X3 || compute == VGE_F16;
   if (dims->time_layers < 1) return fail(VGE_ERR_ARG, "vge_encoder_create: time_layers must be >= 1");
-  if (dims->n_modalities != 5 || dims->d_model != 256 || dims->time_heads != 8 || dims->clip_len != 32)
+  // 5 modalities (keypoint_dir given) or the keypoint-less 4 (utils.py:496-514; infer_dims_from_stats, eval.py:104-133)
+  const int M = dims->n_modalities;
+  if ((M != 5 && M != 4) || dims->d_model != 256 || dims->time_heads != 8 || dims->clip_len != 32)
     return fail(VGE_ERR_UNSUPPORTED,
-                "vge_encoder_create: kernels are built for 5 modalities, d_model 256, 8 heads, clip 32 (got " +
+                "vge_encoder_create: kernels are built for 5 (or 4, keypoint-less) modalities, d_model 256, 8 heads, "
+                "clip 32 (got " +
                     std::to_string(dims->n_modalities) + " modalities, d_model " + std::to_string(dims->d_model) +
                     ", " + std::to_string(dims->time_heads) + " heads, clip " + std::to_string(dims->clip_len) + ")");
-  for (int m = 0; m < 5; ++m)
+  for (int m = 0; m < M; ++m)
     if (dims->dims_raw[m] != kDimsRaw[m] || dims->dims_diff[m] != kDimsDiff[m])
       return fail(VGE_ERR_UNSUPPORTED, std::string("vge_encoder_create: unsupported dims for modality ") + kMods[m]);
 
@@ -422,11 +443,13 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
   const bool x3s = compute == VGE_F32X3 && !(x3s_env && x3s_env[0] == '0');
   std::vector<std::vector<float>> folded;  // folded weight copies, alive until packed
   struct Off { Mat stem, conv, proj; size_t gnw, gnb, fold; int in_col, d_in, P; };
-  std::vector<Off> eoff(10);
-  int col_raw = 0, col_diff = VGE_RAW_DIM;
+  const int n_enc = 2 * M;
+  const int feat_dim = M == 5 ? VGE_FEAT_DIM : VGE_FEAT_DIM_NOKP;
+  std::vector<Off> eoff(n_enc);
+  int col_raw = 0, col_diff = M == 5 ? VGE_RAW_DIM : VGE_RAW_DIM_NOKP;
   for (int kind = 0; kind < 2; ++kind) {
-    for (int m = 0; m < 5; ++m) {
-      const int e = kind * 5 + m;
+    for (int m = 0; m < M; ++m) {
+      const int e = kind * M + m;
       const std::string pre = std::string(kind == 0 ? "state_enc." : "motion_enc.") + kMods[m];
       const int d_in = kind == 0 ? kDimsRaw[m] : kDimsDiff[m];
       Off& o = eoff[e];
@@ -503,8 +526,8 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
   const float* Wk = get("fusion.Wk.weight", {256, 256});
   const float* Wv = get("fusion.Wv.weight", {256, 256});
   const float* Wo = get("fusion.Wo.weight", {256, 256});
-  const float* ltemp = get("fusion.logit_temp", {5});
-  const float* lbias = get("fusion.logit_bias", {5});
+  const float* ltemp = get("fusion.logit_temp", {M});
+  const float* lbias = get("fusion.logit_bias", {M});
   const float* cls = get("cls", {1, 1, 256});
   auto pe_it = wm.find("pos_enc.pe");
   if (pe_it == wm.end() && err.empty()) err = "missing weight: pos_enc.pe";
@@ -610,6 +633,9 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
 
   vge_encoder* enc = new vge_encoder();
   enc->mode = compute;
+  enc->n_mod = M;
+  enc->n_enc = n_enc;
+  enc->feat_dim = feat_dim;
   if (compute == VGE_F16) {  // default: the transformer keeps the split (most of the f16 error, ~10% of the FLOPs)
     const char* mx = getenv("VGE_F16_MIX");
     enc->f16_mix = mx ? atoi(mx) : 2;
@@ -689,13 +715,13 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
   _Float16* hb = enc->hbuf;
   auto mat = [&](const Mat& m) -> const void* { return x3 ? (const void*)(hb + m.off) : (const void*)(wb + m.off); };
   if (x3) {
-    std::vector<vge::EncDescX3Host> descs(10);
-    for (int e = 0; e < 10; ++e)
+    std::vector<vge::EncDescX3Host> descs(n_enc);
+    for (int e = 0; e < n_enc; ++e)
     {
       descs[e] = vge::EncDescX3Host{hb + eoff[e].stem.off, hb + eoff[e].conv.off, hb + eoff[e].proj.off,
                                     wb + eoff[e].gnw, wb + eoff[e].gnb, wb + eoff[e].stem.cs,  // [10][256] scales
-                                    x3s ? wb + eoff[e].fold : nullptr, eoff[e].in_col, eoff[e].d_in, eoff[e].P, 0,
-                                    {}, {}};
+                                    x3s ? wb + eoff[e].fold : nullptr, eoff[e].in_col, eoff[e].d_in, eoff[e].P,
+                                    feat_dim, {}, {}};
       for (int b = 0; b < 4; ++b) {
         float gm = 0.f, bm = 0.f;
         for (int c = 0; c < 256; ++c) {
@@ -706,22 +732,23 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
         descs[e].gn_bmax[b] = bm;
       }
     }
-    he = hipMalloc(&enc->d_encs, sizeof(vge::EncDescX3Host) * 10);
-    if (he == hipSuccess) he = hipMemcpy(enc->d_encs, descs.data(), sizeof(vge::EncDescX3Host) * 10, hipMemcpyHostToDevice);
+    he = hipMalloc(&enc->d_encs, sizeof(vge::EncDescX3Host) * n_enc);
+    if (he == hipSuccess)
+      he = hipMemcpy(enc->d_encs, descs.data(), sizeof(vge::EncDescX3Host) * n_enc, hipMemcpyHostToDevice);
   } else {
-    std::vector<vge::EncDescHost> descs(10);
-    for (int e = 0; e < 10; ++e)
+    std::vector<vge::EncDescHost> descs(n_enc);
+    for (int e = 0; e < n_enc; ++e)
       descs[e] = vge::EncDescHost{wb + eoff[e].stem.off, wb + eoff[e].conv.off, wb + eoff[e].proj.off, wb + eoff[e].gnw,
-                                  wb + eoff[e].gnb, eoff[e].in_col, eoff[e].d_in, eoff[e].P, 0};
-    he = hipMalloc(&enc->d_encs, sizeof(vge::EncDescHost) * 10);
-    if (he == hipSuccess) he = hipMemcpy(enc->d_encs, descs.data(), sizeof(vge::EncDescHost) * 10, hipMemcpyHostToDevice);
+                                  wb + eoff[e].gnb, eoff[e].in_col, eoff[e].d_in, eoff[e].P, feat_dim};
+    he = hipMalloc(&enc->d_encs, sizeof(vge::EncDescHost) * n_enc);
+    if (he == hipSuccess) he = hipMemcpy(enc->d_encs, descs.data(), sizeof(vge::EncDescHost) * n_enc, hipMemcpyHostToDevice);
   }
   if (he != hipSuccess) return hipfail(he);
   enc->fuse.kv_w = wb + off_kvw;
   enc->fuse.kv_b = wb + off_kvb;
   enc->fuse.u = wb + off_u;
-  enc->fuse.n_mod = 5;
-  for (int m = 0; m < 5; ++m) {
+  enc->fuse.n_mod = M;
+  for (int m = 0; m < M; ++m) {
     const float x = ltemp[m];
     const float sp = x > 20.0f ? x : log1pf(expf(x));  // F.softplus (beta 1, threshold 20)
     enc->fuse.inv_tau[m] = 1.0f / (sp + 1e-3f);
@@ -788,10 +815,10 @@ int vge_encoder_reserve(vge_encoder* enc, int B) {
   enc->d_units = nullptr;
   for (auto& t : enc->tables) t = vge_encoder::UnitTable{};
   enc->units_last = -1;
-  {  // the largest R * G over batches <= B (R * G <= 10 B + CUs - 1, conv_f16w_plan)
+  {  // the largest R * G over batches <= B (R * G <= n_enc B + CUs - 1, conv_f16w_plan)
     int G = 0, R = 0, U = 0;
-    enc->units_cap = (size_t)10 * B + 1024;
-    if (vge::conv_f16w_plan(B, 10, enc->f16w > 0 ? enc->f16w : 6, G, R, U))
+    enc->units_cap = (size_t)enc->n_enc * B + 1024;
+    if (vge::conv_f16w_plan(B, enc->n_enc, enc->f16w > 0 ? enc->f16w : 6, G, R, U))
       enc->units_cap = std::max(enc->units_cap, (size_t)G * R);
   }
   he = hipMalloc(&enc->d_units, enc->units_cap * vge_encoder::kUnitTables * sizeof(int));
@@ -870,6 +897,8 @@ extern "C" int vge_debug_encoder_units(const vge_encoder* enc, const void** tabl
   return VGE_OK;
 }
 
+int vge_encoder_feat_dim(const vge_encoder* enc) { return enc ? enc->feat_dim : 0; }
+
 int vge_encoder_destroy(vge_encoder* enc) {
   if (!enc) return VGE_OK;
   for (hipEvent_t e : enc->prof_ev) (void)hipEventDestroy(e);
@@ -916,12 +945,12 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
       if (enc->tables[j].B == B) k = j;
     if (k < 0) {
       int G = 0, R = 0, U = 0;
-      if (!vge::conv_f16w_plan(B, 10, enc->f16w, G, R, U)) return fail(VGE_ERR_ARG, "vge_encode: batch too large");
+      if (!vge::conv_f16w_plan(B, enc->n_enc, enc->f16w, G, R, U)) return fail(VGE_ERR_ARG, "vge_encode: batch too large");
       if ((size_t)G * R > enc->units_cap) return fail(VGE_ERR_WORKSPACE, "vge_encode: unit table exceeds its slot");
       k = 0;
       for (int j = 1; j < vge_encoder::kUnitTables; ++j)
         if (enc->tables[j].used < enc->tables[k].used) k = j;
-      HIPCHK(vge::launch_conv_f16w_table(B, 10, G, R, U, enc->d_units + (size_t)k * enc->units_cap, s));
+      HIPCHK(vge::launch_conv_f16w_table(B, enc->n_enc, G, R, U, enc->d_units + (size_t)k * enc->units_cap, s));
       enc->tables[k] = vge_encoder::UnitTable{B, G, R, 0};
     }
     enc->tables[k].used = ++enc->units_clock;
@@ -929,11 +958,11 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
     HIPCHK(vge::launch_conv_encoders_f16w(feats, B, enc->d_encs, enc->enc_out, enc->d_units + (size_t)k * enc->units_cap,
                                           enc->tables[k].G, enc->tables[k].R, s));
   } else if (x3 && enc->x3s) {
-    HIPCHK(vge::launch_conv_encoders_x3s(feats, B, enc->d_encs, 10, enc->enc_out, s));
+    HIPCHK(vge::launch_conv_encoders_x3s(feats, B, enc->d_encs, enc->n_enc, enc->enc_out, s));
   } else if (x3) {
-    HIPCHK(vge::launch_conv_encoders_x3(feats, B, enc->d_encs, 10, enc->enc_out, split, enc->f16_mix & 1, s));
+    HIPCHK(vge::launch_conv_encoders_x3(feats, B, enc->d_encs, enc->n_enc, enc->enc_out, split, enc->f16_mix & 1, s));
   } else {
-    HIPCHK(vge::launch_conv_encoders(feats, B, enc->d_encs, 10, enc->enc_out, s));
+    HIPCHK(vge::launch_conv_encoders(feats, B, enc->d_encs, enc->n_enc, enc->enc_out, s));
   }
   if (ev && (enc->prof_mask & 2)) {  // the conv-end profiling event doubles as the conv-done event (one marker)
     HIPCHK(mark(1));

@@ -11,6 +11,7 @@ typedef float floatx2 __attribute__((ext_vector_type(2)));
 #define VGE_T 32             // clip_len
 #define VGE_TOK 33           // clip_len + CLS
 #define VGE_FD 2596          // feats row width
+#define VGE_FD_NOKP 2356     // feats row width of the keypoint-less layout (keypoint_dir None)
 #define VGE_LDX 260          // LDS row stride (floats) of a 256-wide activation panel: 16-B shift per
                              // row keeps ds_read_b128 fragment reads conflict-free (see vge_encoder.hip)
 

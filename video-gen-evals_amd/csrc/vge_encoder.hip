@@ -24,7 +24,6 @@
 namespace {
 
 constexpr int CHUNK_F = 4096;          // floats per weight chunk (16 KB)
-constexpr int NMOD = 5;                // vit, global, pose, beta, kp2d (infer_dims_from_stats order)
 constexpr int CHUNKS_PER_PANEL = 16;   // 64 K-steps / 4
 
 // ------------------------------------------------------------------ weight-chunk ring (2 x 16 KB in LDS)
@@ -92,7 +91,7 @@ struct EncDesc {
   int in_col;          // column offset of this encoder's input in feats
   int d_in;
   int n_stem_panels;
-  int pad;
+  int ld;              // feats row width (2596, or 2356 keypoint-less)
 };
 
 // ------------------------------------------------------------------ conv encoder chain
@@ -136,7 +135,7 @@ __global__ void __launch_bounds__(256, 1) conv_encoder_kernel(const float* __res
     for (int r = 0; r < 64; ++r) {
       const int w = pair * 2 + (r >> 5);
       float v = 0.f;
-      if (kcol < ed.d_in && w < n_windows) v = feats[((size_t)w * VGE_T + (r & 31)) * VGE_FD + ed.in_col + kcol];
+      if (kcol < ed.d_in && w < n_windows) v = feats[((size_t)w * VGE_T + (r & 31)) * ed.ld + ed.in_col + kcol];
       X[r * VGE_LDX + c] = v;
     }
     __syncthreads();
@@ -250,6 +249,9 @@ struct FuseParams {
   int has_motion[8];
 };
 
+// NMOD modalities in infer_dims_from_stats order: vit, global, pose, beta[, kp2d] (5, or 4 keypoint-less); enc_out
+// planes 0..NMOD-1 are the state encoders, NMOD..2 NMOD-1 the motion encoders
+template <int NMOD>
 __global__ void __launch_bounds__(256) fuse_kernel(const float* __restrict__ enc_out, int n_rows, FuseParams fp,
                                                    float* __restrict__ pooled) {
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -513,7 +515,7 @@ namespace vge {
 
 struct EncDescHost {
   const float* stem; const float* conv; const float* proj; const float* gn_w; const float* gn_b;
-  int in_col, d_in, n_stem_panels, pad;
+  int in_col, d_in, n_stem_panels, ld;
 };
 static_assert(sizeof(EncDescHost) == sizeof(EncDesc), "EncDesc layout");
 
@@ -553,7 +555,12 @@ hipError_t launch_conv_encoders(const float* feats, int n_windows, const void* e
 hipError_t launch_fuse(const float* enc_out, int n_rows, const FuseParamsHost& fp, float* pooled, hipStream_t s) {
   FuseParams p;
   memcpy(&p, &fp, sizeof(p));
-  hipLaunchKernelGGL(fuse_kernel, dim3((n_rows + 3) / 4), dim3(256), 0, s, enc_out, n_rows, p, pooled);
+  if (fp.n_mod == 4)
+    hipLaunchKernelGGL(fuse_kernel<4>, dim3((n_rows + 3) / 4), dim3(256), 0, s, enc_out, n_rows, p, pooled);
+  else if (fp.n_mod == 5)
+    hipLaunchKernelGGL(fuse_kernel<5>, dim3((n_rows + 3) / 4), dim3(256), 0, s, enc_out, n_rows, p, pooled);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

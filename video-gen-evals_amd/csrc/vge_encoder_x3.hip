@@ -215,7 +215,7 @@ __device__ __forceinline__ void conv_encoder_body(const float* __restrict__ feat
       for (int jr = 0; jr < 4; ++jr) {
         const int r = wave * RPW + g8 * 4 + jr;
         const int w = win0 + (r >> 5);
-        const float* src = feats + ((size_t)w * VGE_T + (r & 31)) * VGE_FD + ed.in_col + p * 256;
+        const float* src = feats + ((size_t)w * VGE_T + (r & 31)) * ed.ld + ed.in_col + p * 256;
 #pragma unroll
         for (int jc = 0; jc < 4; ++jc) {
           const int c = lane + 64 * jc;
@@ -568,7 +568,7 @@ __device__ __forceinline__ void conv_f16w_body(const float* __restrict__ feats, 
     for (int jr = 0; jr < RPW; ++jr) {
       const int r = wave * RPW + jr;
       const int w = win0 + (r >> 5);
-      const float* src = feats + ((size_t)w * VGE_T + (r & 31)) * VGE_FD + ed.in_col + p * 256;
+      const float* src = feats + ((size_t)w * VGE_T + (r & 31)) * ed.ld + ed.in_col + p * 256;
 #pragma unroll
       for (int jc = 0; jc < 4; ++jc) {
         const int c = lane + 64 * jc;
@@ -1237,7 +1237,7 @@ hipError_t launch_pack_x3(const float* W, int N, int K_real, int ldk, int conv, 
 struct EncDescX3Host {
   const _Float16* stem; const _Float16* conv; const _Float16* proj; const float* gn_w; const float* gn_b;
   const float* cs; const float* fold;
-  int in_col, d_in, n_stem_panels, pad;
+  int in_col, d_in, n_stem_panels, ld;
   float gn_gmax[4], gn_bmax[4];
 };
 static_assert(sizeof(EncDescX3Host) == sizeof(EncDescX3), "EncDescX3 layout");

@@ -60,7 +60,6 @@ namespace {
 #ifndef X3S_PRIO
 #define X3S_PRIO 1  // s_setprio 1 for the streaming half
 #endif
-constexpr int X3S_PF = 4;       // weight chunks in flight per wave
 constexpr int X3S_WMAX = 4;     // windows per unit (quads; pairs fill the remainder)
 // Activation rows in LDS interleave the planes: [hi 256 + 8 pad | lo 256 + 8 pad | 8 pad] fp16 = 1,072 B, so one row
 // base addresses both planes with immediate offsets (lo at +528 B) and the ds_read_b128 fragment reads of 32
@@ -158,7 +157,7 @@ template <int W>
 __device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, int n_windows, int win0,
                                               const EncDescX3& ed, int e, float* __restrict__ enc_out, char* lds_raw,
                                               int& n_ex, [[maybe_unused]] bool tr_on) {
-  constexpr int R = W, ROWS = 32 * W, XROWS = ROWS + 1;
+  constexpr int R = W, ROWS = 32 * W;
   _Float16* X = reinterpret_cast<_Float16*>(lds_raw);  // [XROWS][XR]: hi at +0, lo at +XLO bytes
   X3sAux& ax = *reinterpret_cast<X3sAux*>(lds_raw + X3S_AUX_OFF);
 
@@ -210,7 +209,7 @@ __device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, i
       for (int jr = 0; jr < 4; ++jr) {
         const int r = wave * RPW + g8 * 4 + jr;
         const int w = win0 + (r >> 5);
-        const float* src = feats + ((size_t)w * VGE_T + (r & 31)) * VGE_FD + ed.in_col + p * 256;
+        const float* src = feats + ((size_t)w * VGE_T + (r & 31)) * ed.ld + ed.in_col + p * 256;
 #pragma unroll
         for (int jc = 0; jc < 4; ++jc) {
           const int c = lane + 64 * jc;

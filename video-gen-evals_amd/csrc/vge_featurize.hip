@@ -2,7 +2,8 @@
 //
 // Replaces WindowDataset._try_one (utils.py:383-516) and compute_stats_from_npz (utils.py:595-801).
 // One 256-thread workgroup turns one 32-row tile of a video into 32 rows of the reference feats
-// layout [raw 1370 | diff 1226].  A tile is either a window (window mode: rows are the
+// layout [raw 1370 | diff 1226] (keypoint_dir given), or of the keypoint-less layout [raw 1250 | diff 1106]
+// (keypoint_dir None: the same columns without kp2d, the diff part 120 columns earlier, rows 2356 wide).  A tile is either a window (window mode: rows are the
 // _slice_or_pad'ed frames start..start+31, first row self-diffs) or 32 consecutive frames of a
 // full sequence (stats mode: diffs against the previous video frame, un-normalised output that
 // the column reducer sums in float64).
@@ -211,8 +212,8 @@ __device__ __forceinline__ RowSrc row_src(int mode, int start, int L, int t) {
 // (x - mean) * (1 / (std + 1e-6)) -- within an ulp of the division)
 __device__ __forceinline__ void featurize_vit(const float* __restrict__ vit, int foff, int L, int mode, int mesh_start,
                                               int mcount, const float* __restrict__ mean,
-                                              const float* __restrict__ stdv, float* __restrict__ out, int wave,
-                                              int lane) {
+                                              const float* __restrict__ stdv, float* __restrict__ out, int ld,
+                                              int cvd, int wave, int lane) {
   float mr[16], ir[16], md[16], id[16];
 #pragma unroll
   for (int k = 0; k < 4; ++k)
@@ -221,8 +222,8 @@ __device__ __forceinline__ void featurize_vit(const float* __restrict__ vit, int
       const int c = k * 256 + lane * 4 + q;
       mr[k * 4 + q] = mean ? mean[C_VIT_RAW + c] : 0.f;
       ir[k * 4 + q] = mean ? 1.0f / (stdv[C_VIT_RAW + c] + 1e-6f) : 1.f;
-      md[k * 4 + q] = mean ? mean[C_VIT_DIFF + c] : 0.f;
-      id[k * 4 + q] = mean ? 1.0f / (stdv[C_VIT_DIFF + c] + 1e-6f) : 1.f;
+      md[k * 4 + q] = mean ? mean[cvd + c] : 0.f;
+      id[k * 4 + q] = mean ? 1.0f / (stdv[cvd + c] + 1e-6f) : 1.f;
     }
   auto issue = [&](int f, floatx4 (&x)[4]) {
     const floatx4* p = reinterpret_cast<const floatx4*>(vit + (size_t)(foff + f) * 1024);
@@ -255,7 +256,7 @@ __device__ __forceinline__ void featurize_vit(const float* __restrict__ vit, int
     for (int k = 0; k < 4; ++k) xa[k] = xb[k];
     if (t + 1 < t1) issue(row_src(mode, mesh_start, L, t + 1).src, xb);  // in flight during this row
     finish(xa, vcur, raw);
-    float* orow = out + (size_t)t * VGE_FD;
+    float* orow = out + (size_t)t * ld;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       floatx4 o, d4;
@@ -267,8 +268,8 @@ __device__ __forceinline__ void featurize_vit(const float* __restrict__ vit, int
       }
       const int c = k * 256 + lane * 4;
       *reinterpret_cast<floatx4*>(orow + C_VIT_RAW + c) = o;
-      *reinterpret_cast<floatx2*>(orow + C_VIT_DIFF + c) = (floatx2){d4[0], d4[1]};
-      *reinterpret_cast<floatx2*>(orow + C_VIT_DIFF + c + 2) = (floatx2){d4[2], d4[3]};
+      *reinterpret_cast<floatx2*>(orow + cvd + c) = (floatx2){d4[0], d4[1]};
+      *reinterpret_cast<floatx2*>(orow + cvd + c + 2) = (floatx2){d4[2], d4[3]};
     }
 #pragma unroll
     for (int i = 0; i < 16; ++i) vprev[i] = vcur[i];
@@ -280,7 +281,8 @@ __global__ void __launch_bounds__(256) featurize_tiles_kernel(
     const float* __restrict__ pose, const float* __restrict__ gori, const float* __restrict__ betas,
     const float* __restrict__ vit, const float* __restrict__ kp, const int* __restrict__ videos,
     const TileDesc* __restrict__ tiles, const int* __restrict__ windows, const float* __restrict__ mean,
-    const float* __restrict__ stdv, float* __restrict__ feats) {
+    const float* __restrict__ stdv, float* __restrict__ feats, int ld, int dsh) {
+  // ld: feats row width (2596, or 2356 keypoint-less); dsh: how far the diff columns sit before the 2596 layout's
   __shared__ float pn[33][120];  // normalised keypoints: slot 0 = prev of row 0, slot t+1 = row t
   __shared__ float kR[32][4];    // per row: H = X_{t-1}^T X_t, then the Procrustes rotation R (row-major)
   TileDesc td;
@@ -296,12 +298,12 @@ __global__ void __launch_bounds__(256) featurize_tiles_kernel(
   const int mode = td.mode;
   const int mcount = (mode == 0) ? 32 : td.mesh_count;
   const int kcount = (mode == 0) ? (Lk > 0 ? 32 : 0) : td.kp_count;
-  float* out = feats + (size_t)td.out_row * VGE_FD;
+  float* out = feats + (size_t)td.out_row * ld;
 
   // three workgroups per tile: vit columns (3/4 of the bytes), rotations + betas, keypoints
   if (blockIdx.y == 0) {
 #if !(defined(VGE_ABL) && (VGE_ABL & 2048))
-    featurize_vit(vit, foff, L, mode, td.mesh_start, mcount, mean, stdv, out, wave, lane);
+    featurize_vit(vit, foff, L, mode, td.mesh_start, mcount, mean, stdv, out, ld, C_VIT_DIFF - dsh, wave, lane);
 #endif
     return;
   }
@@ -323,9 +325,9 @@ __global__ void __launch_bounds__(256) featurize_tiles_kernel(
       for (int i = 0; i < 9; ++i) { Rl[i] = R[i]; Rpl[i] = Rp[i]; }
       float w[3];
       rot_delta(Rpl, Rl, w);
-      float* orow = out + (size_t)t * VGE_FD;
+      float* orow = out + (size_t)t * ld;
       int craw = (j == 0) ? C_GORI_RAW : C_POSE_RAW + (j - 1) * 9;
-      int cdif = (j == 0) ? C_GORI_DIFF : C_POSE_DIFF + (j - 1) * 3;
+      int cdif = ((j == 0) ? C_GORI_DIFF : C_POSE_DIFF + (j - 1) * 3) - dsh;
   #pragma unroll
       for (int i = 0; i < 9; ++i) orow[craw + i] = znorm(Rl[i], mean, stdv, craw + i);
   #pragma unroll
@@ -339,13 +341,14 @@ __global__ void __launch_bounds__(256) featurize_tiles_kernel(
       RowSrc rs = row_src(mode, td.mesh_start, L, t);
       float b = betas[(size_t)(foff + rs.src) * 10 + i];
       float bp = betas[(size_t)(foff + rs.prv) * 10 + i];
-      float* orow = out + (size_t)t * VGE_FD;
+      float* orow = out + (size_t)t * ld;
       orow[C_BETA_RAW + i] = znorm(b, mean, stdv, C_BETA_RAW + i);
-      orow[C_BETA_DIFF + i] = znorm(b - bp, mean, stdv, C_BETA_DIFF + i);
+      orow[C_BETA_DIFF - dsh + i] = znorm(b - bp, mean, stdv, C_BETA_DIFF - dsh + i);
     }
 
     return;
   }
+  // (the keypoint-less layout launches no keypoint workgroups)
   // ---- (d1) keypoints: centre + Frobenius-normalise every needed frame (utils.py:191-196)
   for (int slot = wave; slot < 33; slot += 4) {
     int t = slot - 1;
@@ -376,7 +379,7 @@ __global__ void __launch_bounds__(256) featurize_tiles_kernel(
   // per wave), then the deltas
   for (int t = wave; t < kcount; t += 4) {
     RowSrc rs = row_src(mode, td.kp_start, Lk, t);
-    float* orow = out + (size_t)t * VGE_FD;
+    float* orow = out + (size_t)t * ld;
     for (int c = lane; c < 120; c += 64)
       orow[C_KP_RAW + c] = znorm(kp[(size_t)(koff + rs.src) * 120 + c], mean, stdv, C_KP_RAW + c);
     if (!rs.first) {
@@ -417,7 +420,7 @@ __global__ void __launch_bounds__(256) featurize_tiles_kernel(
   __syncthreads();
   for (int t = wave; t < kcount; t += 4) {
     RowSrc rs = row_src(mode, td.kp_start, Lk, t);
-    float* orow = out + (size_t)t * VGE_FD;
+    float* orow = out + (size_t)t * ld;
     float dx = 0.f, dy = 0.f;
     if (!rs.first && lane < 60) {
       const float x0 = pn[t][2 * lane], x1 = pn[t][2 * lane + 1];
@@ -477,17 +480,20 @@ __global__ void stats_reduce_kernel(const double* __restrict__ partial, int n_ch
   sums[VGE_FD + col] += s2;
 }
 
+// mean / std in the feats column order of a layout of width ld: 2596, or 2356 keypoint-less (the kp2d columns
+// dropped, the diff part 120 columns earlier; the sums are always in the 2596 order)
 __global__ void stats_finalize_kernel(const double* __restrict__ sums, long long n_mesh, long long n_kp,
-                                      float* __restrict__ mean, float* __restrict__ stdv) {
-  const int col = blockIdx.x * 256 + threadIdx.x;
-  if (col >= VGE_FD) return;
+                                      float* __restrict__ mean, float* __restrict__ stdv, int ld) {
+  const int oc = blockIdx.x * 256 + threadIdx.x;
+  if (oc >= ld) return;
+  const int col = (ld == VGE_FD || oc < C_KP_RAW) ? oc : oc + (C_VIT_DIFF - C_KP_RAW);
   const bool is_kp = (col >= C_KP_RAW && col < C_VIT_DIFF) || col >= C_KP_DIFF;
   double n = (double)max(1LL, is_kp ? n_kp : n_mesh);
   double m = sums[col] / n;
   double var = sums[VGE_FD + col] / n - m * m;
   double sd = sqrt(fmax(var, 0.0) + 1e-6);
-  mean[col] = (float)m;
-  stdv[col] = (float)sd;
+  mean[oc] = (float)m;
+  stdv[oc] = (float)sd;
 }
 
 }  // namespace
@@ -497,10 +503,12 @@ namespace vge {
 
 hipError_t launch_featurize_tiles(const float* pose, const float* gori, const float* betas, const float* vit,
                                   const float* kp, const int* videos, const void* tiles, const int* windows,
-                                  int n_tiles, const float* mean, const float* stdv, float* feats, hipStream_t s) {
+                                  int n_tiles, const float* mean, const float* stdv, float* feats, int with_kp,
+                                  hipStream_t s) {
   if (n_tiles <= 0) return hipSuccess;
-  hipLaunchKernelGGL(featurize_tiles_kernel, dim3(n_tiles, 3), dim3(256), 0, s, pose, gori, betas, vit, kp, videos,
-                     reinterpret_cast<const TileDesc*>(tiles), windows, mean, stdv, feats);
+  hipLaunchKernelGGL(featurize_tiles_kernel, dim3(n_tiles, with_kp ? 3 : 2), dim3(256), 0, s, pose, gori, betas, vit,
+                     kp, videos, reinterpret_cast<const TileDesc*>(tiles), windows, mean, stdv, feats,
+                     with_kp ? VGE_FD : VGE_FD_NOKP, with_kp ? 0 : C_VIT_DIFF - C_KP_RAW);
   return hipGetLastError();
 }
 
@@ -514,9 +522,10 @@ hipError_t launch_stats_colsum(const float* feats, const void* tiles, int n_tile
 }
 
 hipError_t launch_stats_finalize(const double* sums, long long n_mesh, long long n_kp, float* mean, float* stdv,
-                                 hipStream_t s) {
-  hipLaunchKernelGGL(stats_finalize_kernel, dim3((VGE_FD + 255) / 256), dim3(256), 0, s, sums, n_mesh, n_kp, mean,
-                     stdv);
+                                 int with_kp, hipStream_t s) {
+  const int ld = with_kp ? VGE_FD : VGE_FD_NOKP;
+  hipLaunchKernelGGL(stats_finalize_kernel, dim3((ld + 255) / 256), dim3(256), 0, s, sums, n_mesh, n_kp, mean, stdv,
+                     ld);
   return hipGetLastError();
 }
 

@@ -173,7 +173,7 @@ struct EncDescX3 {
   // conv1, [3 blocks][256 cols][16] = per-tap sums over input channels of W1 gamma (taps 0..4), then of W1 beta (at 8..12),
   // then the proj's [256][2] (sums of P gamma, P beta)
   const float* fold;
-  int in_col, d_in, n_stem_panels, pad;
+  int in_col, d_in, n_stem_panels, ld;  // ld: feats row width (2596, or 2356 keypoint-less)
   float gn_gmax[4], gn_bmax[4];  // max |gamma|, max |beta| of each GroupNorm (split-exponent bounds)
 };
 

@@ -174,7 +174,8 @@ def run_eval_distributed(generated_meshes_dir: str, real_meshes_dir: str, model_
         from .stats_cache import model_digest
         model_sha = model_digest(model_path)
     pool = ThreadPoolExecutor(max_workers=2)
-    gen_fs = pool.submit(VE.load_frame_store, mine.items, keypoint_dir, True) if mine.items and overlap else None
+    need_kp = keypoint_dir is not None
+    gen_fs = pool.submit(VE.load_frame_store, mine.items, keypoint_dir, need_kp) if mine.items and overlap else None
     if overlap and isinstance(model_path, (str, os.PathLike)):  # the checkpoint read overlaps the real set's phases
         model_path = pool.submit(VE._load_state_dict, model_path)
     try:
@@ -242,7 +243,8 @@ def _run_eval_phases(real_meshes_dir, model_path, keypoint_dir, real_kp_dir, cli
     def local_scores():
         combined, feats_host = {}, None
         if mine.items:
-            fs = gen_fs.result() if gen_fs is not None else VE.load_frame_store(mine.items, keypoint_dir, True)
+            fs = gen_fs.result() if gen_fs is not None else VE.load_frame_store(mine.items, keypoint_dir,
+                                                                                 keypoint_dir is not None)
             store = ops.DeviceFrameStore.from_host(fs, device)
             feats = VE.extract_window_features(model, mine, keypoint_dir, stats, clip_len, stride, device,
                                                store=store, frame_embed=bool(save_features))
@@ -297,8 +299,7 @@ def _real_set_phases(VE, ops, real_meshes_dir, model_path, real_kp_dir, clip_len
 
     real_store, sums, counts = guarded("real-set statistics", local_stats)
     s, c = stats_reduce_fn(sums, counts)
-    mean, std = ops.stats_finalize(s, c)
-    stats = VE.ModalityStatsGPU(mean, std, s, c)
+    stats = VE.stats_from_sums(s, c, device)
     dims_raw, dims_diff = VE.infer_dims_from_stats(stats)
 
     # phase 2: checkpoint -> encoder; this rank's real-train windows -> centroid sufficient statistics
@@ -311,7 +312,7 @@ def _real_set_phases(VE, ops, real_meshes_dir, model_path, real_kp_dir, clip_len
     def local_centroids():
         mp = model_path.result() if isinstance(model_path, Future) else model_path
         model = VE.load_model(mp, dims_raw, dims_diff, device=device, compute=compute)
-        if real_store is not None:
+        if real_store is not None and real_kp_dir is not None:
             for i, it in enumerate(my_train):
                 if real_store.host_videos[i, 3] == 0:
                     load_clip(it, real_kp_dir, require_kp=True)  # raises like utils.py:416-417

@@ -52,10 +52,18 @@ def load_frame_store_numpy(items: Sequence[VideoItem], keypoint_dir: Optional[st
 
 
 class ModalityStatsGPU:
-    """mean/std [2596] f32 on device (feats column order) + the float64 sufficient statistics."""
+    """mean/std f32 on device in feats column order ([2596], or [2356] for the keypoint-less layout) + the float64
+    sufficient statistics ([2,2596] sums, frame counts).  The layout follows compute_stats_from_npz: keypoint stats
+    exist iff some real-train keypoint frame was read (utils.py:753-755), and infer_dims_from_stats then gives the
+    model 5 or 4 modalities (eval.py:119-123)."""
 
-    def __init__(self, mean, std, sums, counts):
-        self.mean, self.std, self.sums, self.counts = mean, std, sums, counts
+    def __init__(self, mean, std, sums, counts, layout="kp"):
+        self.mean, self.std, self.sums, self.counts, self.layout = mean, std, sums, counts, layout
+
+
+def stats_layout(counts) -> str:
+    """'kp' iff keypoint frames were counted (the reference's n_kp_raw > 0), else the keypoint-less 'nokp'."""
+    return "kp" if int(counts[1]) > 0 else "nokp"
 
 
 def compute_stats_from_npz(train_items: Sequence[VideoItem], keypoint_dir: str, device="cuda",
@@ -70,8 +78,9 @@ def compute_stats_from_npz(train_items: Sequence[VideoItem], keypoint_dir: str, 
     ops.stats_accumulate(store, range(store.n_videos), sums, counts)
     if reduce_fn is not None:
         sums, counts = reduce_fn(sums, counts)
-    mean, std = ops.stats_finalize(sums, counts)
-    return ModalityStatsGPU(mean, std, sums, counts)
+    layout = stats_layout(counts)
+    mean, std = ops.stats_finalize(sums, counts, layout)
+    return ModalityStatsGPU(mean, std, sums, counts, layout)
 
 
 def _load_state_dict(model_path: str):
@@ -92,12 +101,19 @@ def _load_state_dict(model_path: str):
 
 
 def load_model(model_path, dims_map_raw=None, dims_map_diff=None, device="cuda", compute="f32x3") -> ops.Encoder:
-    """eval.py:136-165 -> a libvge encoder handle (weights repacked into HBM)."""
+    """eval.py:136-165 -> a libvge encoder handle (weights repacked into HBM).  dims: the five-modality layout or
+    its keypoint-less first four (infer_dims_from_stats); anything else is VGE_ERR_UNSUPPORTED."""
+    n_mod = 5
     if dims_map_raw is not None:
-        if tuple(dims_map_raw.values()) != ops.DIMS_RAW or tuple(dims_map_diff.values()) != ops.DIMS_DIFF:
+        n_mod = len(dims_map_raw)
+        ok = n_mod in (4, 5) and list(dims_map_raw) == list(ops.MODALITIES[:n_mod]) and \
+            list(dims_map_diff) == list(ops.MODALITIES[:n_mod]) and \
+            tuple(dims_map_raw.values()) == ops.DIMS_RAW[:n_mod] and tuple(dims_map_diff.values()) == ops.DIMS_DIFF[:n_mod]
+        if not ok:
             from .lib import UnsupportedModelError
             raise UnsupportedModelError(f"unsupported modality dims {dims_map_raw} / {dims_map_diff} (the kernels "
-                                        f"are built for the five-modality layout; VGE_ERR_UNSUPPORTED)")
+                                        f"are built for the five-modality layout and its keypoint-less four; "
+                                        f"VGE_ERR_UNSUPPORTED)")
     if isinstance(model_path, dict):
         sd, hp = model_path, {"d_model": 256, "time_layers": 4, "time_heads": 8}
     elif isinstance(model_path, tuple):  # (state_dict, hyper-parameters) as _load_state_dict returns them
@@ -105,11 +121,13 @@ def load_model(model_path, dims_map_raw=None, dims_map_diff=None, device="cuda",
     else:
         sd, hp = _load_state_dict(model_path)
     return ops.Encoder(sd, time_layers=int(hp["time_layers"]), time_heads=int(hp["time_heads"]),
-                       d_model=int(hp["d_model"]), device=device, compute=compute)
+                       d_model=int(hp["d_model"]), device=device, compute=compute, n_modalities=n_mod)
 
 
 def infer_dims_from_stats(stats) -> Tuple[Dict[str, int], Dict[str, int]]:
-    return dict(zip(ops.MODALITIES, ops.DIMS_RAW)), dict(zip(ops.MODALITIES, ops.DIMS_DIFF))
+    """eval.py:104-133: vit, global, pose, beta, plus kp2d when the stats hold keypoint statistics."""
+    n = ops.N_MODALITIES[getattr(stats, "layout", "kp")]
+    return dict(zip(ops.MODALITIES[:n], ops.DIMS_RAW[:n])), dict(zip(ops.MODALITIES[:n], ops.DIMS_DIFF[:n]))
 
 
 # ----------------------------------------------------------------------------- windows -> embeddings
@@ -124,14 +142,17 @@ def encode_windows(model: ops.Encoder, store: ops.DeviceFrameStore, windows: tor
     """featurise + encode windows in batches; returns (seq [N,256], frame [N,33,256] | None, tc [N])."""
     n = int(windows.shape[0])
     dev = windows.device
+    if model.layout != stats.layout:
+        raise ValueError(f"model takes the {model.layout!r} feature layout but the stats are {stats.layout!r} "
+                         f"(the reference would fail on the feature width)")
     seq = torch.empty((n, ops.D_MODEL), device=dev)
     tcw = torch.empty((n,), device=dev)
     fe = torch.empty((n, 33, ops.D_MODEL), device=dev) if frame_embed else None
     model.reserve(min(batch, max(n, 1)))
-    feats = torch.empty((min(batch, max(n, 1)), 32, ops.FEAT_DIM), device=dev)
+    feats = torch.empty((min(batch, max(n, 1)), 32, model.feat_dim), device=dev)
     for b0 in range(0, n, batch):
         b1 = min(n, b0 + batch)
-        f = ops.featurize(store, windows[b0:b1], stats.mean, stats.std, out=feats[: b1 - b0])
+        f = ops.featurize(store, windows[b0:b1], stats.mean, stats.std, out=feats[: b1 - b0], layout=stats.layout)
         s, fr, t = model.encode(f, frame_embed=frame_embed, tc=True)
         seq[b0:b1] = s
         tcw[b0:b1] = t
@@ -155,7 +176,8 @@ def build_real_centroids(model: ops.Encoder, real_meshes_dir: str, real_kp_dir: 
     if len(train_items):
         samples = enumerate_test_windows(NpzVideoDataset("", items=list(train_items)), clip_len, stride)
         if store is None:
-            store = ops.DeviceFrameStore.from_host(load_frame_store(train_items, real_kp_dir, require_kp=True), device)
+            store = ops.DeviceFrameStore.from_host(load_frame_store(train_items, real_kp_dir,
+                                                                    require_kp=real_kp_dir is not None), device)
         idx = {it.path: i for i, it in enumerate(train_items)}
         win = _window_tensor(samples, idx, device)
         seq, _, _ = encode_windows(model, store, win, stats)
@@ -174,7 +196,8 @@ def extract_window_features(model: ops.Encoder, dataset: NpzVideoDataset, keypoi
     (frame embeddings are then produced too)."""
     samples = sample_all_windows_npz(dataset, clip_len, stride)
     if store is None:
-        store = ops.DeviceFrameStore.from_host(load_frame_store(dataset.items, keypoint_dir, require_kp=True), device)
+        store = ops.DeviceFrameStore.from_host(load_frame_store(dataset.items, keypoint_dir,
+                                                                require_kp=keypoint_dir is not None), device)
     idx = {it.path: i for i, it in enumerate(dataset.items)}
     win = _window_tensor(samples, idx, device)
     seq, fe, tcw = encode_windows(model, store, win, stats, frame_embed=frame_embed or bool(save_path))
@@ -288,8 +311,9 @@ def stats_from_sums(sums, counts, device) -> ModalityStatsGPU:
     """ModalityStats from (exchanged or cached) sufficient statistics: vge_stats_finalize on the device."""
     sums = torch.as_tensor(sums, dtype=torch.float64).to(device)
     counts = np.asarray(counts, np.int64)
-    mean, std = ops.stats_finalize(sums, counts)
-    return ModalityStatsGPU(mean, std, sums, counts)
+    layout = stats_layout(counts)
+    mean, std = ops.stats_finalize(sums, counts, layout)
+    return ModalityStatsGPU(mean, std, sums, counts, layout)
 
 
 def run_eval(generated_meshes_dir: str, real_meshes_dir: str, model_path, keypoint_dir: str, real_kp_dir: str,
@@ -327,7 +351,7 @@ def run_eval(generated_meshes_dir: str, real_meshes_dir: str, model_path, keypoi
         t1 = time.perf_counter()
         # centroids need every real-train keypoint file (WindowDataset raises otherwise)
         for i, it in enumerate(train_ds.items):
-            if real_store.host_videos[i, 3] == 0:
+            if real_kp_dir is not None and real_store.host_videos[i, 3] == 0:
                 load_clip(it, real_kp_dir, require_kp=True)  # raises FileNotFoundError like utils.py:416-417
         cap = {}
 
@@ -372,8 +396,10 @@ def main(argv=None):
     ap.add_argument("--generated-meshes", required=True)
     ap.add_argument("--real-meshes", required=True)
     ap.add_argument("--model", required=True, help="checkpoint with model_state_dict (eval.py:136-165)")
-    ap.add_argument("--keypoints", required=True, help="generated keypoint dir (<stem>/keypoints.npy)")
-    ap.add_argument("--real-keypoints", required=True)
+    ap.add_argument("--keypoints", default=None,
+                    help="generated keypoint dir (<stem>/keypoints.npy); omit both keypoint dirs for the "
+                         "keypoint-less 4-modality layout (keypoint_dir None)")
+    ap.add_argument("--real-keypoints", default=None)
     ap.add_argument("--human-scores", default=None)
     ap.add_argument("--out", default="video_scores.json")
     ap.add_argument("--save-features", default=None, help="e.g. window_features.pt")

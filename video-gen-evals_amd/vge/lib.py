@@ -14,7 +14,8 @@ STATUS = {0: "VGE_OK", 1: "VGE_ERR_ARG", 2: "VGE_ERR_HIP", 3: "VGE_ERR_MISSING_W
           5: "VGE_ERR_NOMEM", 6: "VGE_ERR_WORKSPACE", 7: "VGE_ERR_UNSUPPORTED"}
 VGE_ERR_UNSUPPORTED = 7
 
-EXPORTS = ["vge_featurize", "vge_stats_workspace_bytes", "vge_stats_accumulate", "vge_stats_finalize",
+EXPORTS = ["vge_featurize", "vge_featurize_layout", "vge_layout_feat_dim", "vge_stats_finalize_layout",
+           "vge_encoder_feat_dim", "vge_stats_workspace_bytes", "vge_stats_accumulate", "vge_stats_finalize",
            "vge_encoder_create", "vge_encoder_reserve", "vge_encoder_destroy", "vge_encode", "vge_tc_windows",
            "vge_score_videos", "vge_centroid_accumulate", "vge_centroid_finalize", "vge_last_error", "vge_version",
            "vge_encoder_profile_begin", "vge_encoder_profile_read", "vge_encoder_profile_mask", "vge_encoder_wait_conv", "vge_ingest_probe",
@@ -74,6 +75,10 @@ def load() -> C.CDLL:
     vp, i32, i64p = C.c_void_p, C.c_int, C.POINTER(C.c_int64)
     sig = {
         "vge_featurize": [C.POINTER(FrameStoreC), vp, i32, vp, vp, vp, vp],
+        "vge_featurize_layout": [C.POINTER(FrameStoreC), vp, i32, vp, vp, i32, vp, vp],
+        "vge_layout_feat_dim": [i32],
+        "vge_stats_finalize_layout": [vp, i64p, i32, vp, vp, vp],
+        "vge_encoder_feat_dim": [vp],
         "vge_stats_workspace_bytes": [i32],
         "vge_stats_accumulate": [C.POINTER(FrameStoreC), vp, vp, i32, vp, i64p, vp, C.c_size_t, vp],
         "vge_stats_finalize": [vp, i64p, vp, vp, vp],

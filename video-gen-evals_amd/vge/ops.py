@@ -17,6 +17,16 @@ D_MODEL = 256
 MODALITIES = ("vit", "global", "pose", "beta", "kp2d")
 DIMS_RAW = (1024, 9, 207, 10, 120)
 DIMS_DIFF = (1024, 3, 69, 10, 120)
+# Feature layouts (utils.py:496-514): "kp" when the reference runs with a keypoint_dir (5 modalities, rows of 2596),
+# "nokp" when keypoint_dir is None (no kp2d columns: 4 modalities, rows of 2356)
+LAYOUTS = {"kp": 0, "nokp": 1}
+FEAT_DIMS = {"kp": 2596, "nokp": 2356}
+N_MODALITIES = {"kp": 5, "nokp": 4}
+
+
+def layout_of(keypoint_dir) -> str:
+    """The feats layout the reference builds for a keypoint directory (None -> keypoint-less)."""
+    return "kp" if keypoint_dir is not None else "nokp"
 
 
 def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
@@ -64,17 +74,22 @@ class DeviceFrameStore:
 
 
 def featurize(store: DeviceFrameStore, windows: torch.Tensor, mean: torch.Tensor, std: torch.Tensor,
-              out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """WindowDataset._try_one for a batch of windows -> feats [Nw,32,2596] (utils.py:383-516)."""
+              out: Optional[torch.Tensor] = None, layout: str = "kp") -> torch.Tensor:
+    """WindowDataset._try_one for a batch of windows -> feats [Nw,32,2596] (utils.py:383-516); layout "nokp"
+    (keypoint_dir None): feats [Nw,32,2356] and mean/std [2356] in that layout."""
     lib = L.load()
     n = int(windows.shape[0])
+    D = FEAT_DIMS[layout]
+    if mean.numel() != D or std.numel() != D:
+        raise L.VgeError(f"featurize: mean/std must have {D} entries for layout {layout!r}")
     if out is None:
-        out = torch.empty((n, 32, FEAT_DIM), device=windows.device, dtype=torch.float32)
+        out = torch.empty((n, 32, D), device=windows.device, dtype=torch.float32)
+    elif tuple(out.shape[1:]) != (32, D) or out.shape[0] < n:
+        raise L.VgeError(f"featurize: out must be [>= {n}, 32, {D}] for layout {layout!r}")
     if n:
-        hv = store.host_videos
         cv = store.cview()
-        L.check(lib.vge_featurize(C.byref(cv), _ptr(windows), n, _ptr(mean), _ptr(std), _ptr(out),
-                                  _stream(windows.device)), "vge_featurize")
+        L.check(lib.vge_featurize_layout(C.byref(cv), _ptr(windows), n, _ptr(mean), _ptr(std), LAYOUTS[layout],
+                                         _ptr(out), _stream(windows.device)), "vge_featurize")
     return out
 
 
@@ -93,12 +108,14 @@ def stats_accumulate(store: DeviceFrameStore, video_sel: Sequence[int], sums: to
     counts[0], counts[1] = cnt[0], cnt[1]
 
 
-def stats_finalize(sums: torch.Tensor, counts: np.ndarray) -> Tuple[torch.Tensor, torch.Tensor]:
+def stats_finalize(sums: torch.Tensor, counts: np.ndarray, layout: str = "kp") -> Tuple[torch.Tensor, torch.Tensor]:
+    """mean / std in the layout's feats column order (layout "nokp": [2356], the keypoint-less ModalityStats)."""
     lib = L.load()
-    mean = torch.empty(FEAT_DIM, device=sums.device, dtype=torch.float32)
+    mean = torch.empty(FEAT_DIMS[layout], device=sums.device, dtype=torch.float32)
     std = torch.empty_like(mean)
     cnt = (C.c_int64 * 2)(int(counts[0]), int(counts[1]))
-    L.check(lib.vge_stats_finalize(_ptr(sums), cnt, _ptr(mean), _ptr(std), _stream(sums.device)), "vge_stats_finalize")
+    L.check(lib.vge_stats_finalize_layout(_ptr(sums), cnt, LAYOUTS[layout], _ptr(mean), _ptr(std),
+                                          _stream(sums.device)), "vge_stats_finalize")
     return mean, std
 
 
@@ -109,15 +126,16 @@ class Encoder:
     """HumanActionScorer (model.py:102-193) as a libvge encoder handle owning repacked HBM weights.
 
     compute="f32x3" (default): split-precision 3xfp16 MFMA, f32-class results (~1e-7 from exact f32);
-    compute="f32": exact f32 MFMA."""
+    compute="f32": exact f32 MFMA.  n_modalities 5 (vit, global, pose, beta, kp2d; feats rows of 2596) or 4 (the
+    keypoint-less model, feats rows of 2356)."""
 
     def __init__(self, state_dict: Dict[str, np.ndarray], time_layers: int = 4, time_heads: int = 8,
-                 d_model: int = 256, device=None, compute: str = "f32x3"):
+                 d_model: int = 256, device=None, compute: str = "f32x3", n_modalities: int = 5):
         lib = L.load()
         self.device = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
         dims = L.Dims()
-        dims.n_modalities = 5
-        for i in range(5):
+        dims.n_modalities = n_modalities
+        for i in range(min(n_modalities, 5)):
             dims.dims_raw[i] = DIMS_RAW[i]
             dims.dims_diff[i] = DIMS_DIFF[i]
         dims.d_model, dims.time_layers, dims.time_heads, dims.clip_len = d_model, time_layers, time_heads, 32
@@ -139,6 +157,9 @@ class Encoder:
         self._h = h
         self._lib = lib
         self.capacity = 0
+        self.n_modalities = n_modalities
+        self.feat_dim = int(lib.vge_encoder_feat_dim(h))
+        self.layout = "kp" if self.feat_dim == FEAT_DIM else "nokp"
 
     def reserve(self, max_windows: int) -> None:
         if max_windows > self.capacity:
@@ -148,11 +169,11 @@ class Encoder:
 
     def encode(self, feats: torch.Tensor, frame_embed: bool = False, tc: bool = True,
                seq_out: Optional[torch.Tensor] = None, tc_out: Optional[torch.Tensor] = None):
-        """feats [B,32,2596] -> (seq_embed [B,256], frame_embeds [B,33,256] | None, tc_window [B] | None).
+        """feats [B,32,feat_dim] -> (seq_embed [B,256], frame_embeds [B,33,256] | None, tc_window [B] | None).
         seq_out / tc_out: optional contiguous float32 destinations ([B,256] / [B]) written in place."""
         B, T, D = feats.shape
-        if D != FEAT_DIM:
-            raise L.VgeError(f"feats last dim {D} != {FEAT_DIM}")
+        if D != self.feat_dim:
+            raise L.VgeError(f"feats last dim {D} != {self.feat_dim}")
         for t, shape in ((seq_out, (B, D_MODEL)), (tc_out, (B,))):
             if t is not None and (tuple(t.shape) != shape or t.dtype != torch.float32 or not t.is_contiguous()
                                   or t.device != feats.device):
