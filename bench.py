@@ -57,8 +57,8 @@ F32_MFMA_PEAK_TFLOPS = 157.3                # MI355X_MICROARCH.md: v_mfma_f32_* 
 # the 3xfp16 path issues 3 f16 MFMAs per f32 product, so its ceiling in algorithmic f32 FLOP/s is 1/3 of it
 F16_MFMA_PEAK_TFLOPS = 2516.6
 PEAK_BY_COMPUTE = {"f32": (F32_MFMA_PEAK_TFLOPS, "conv_encoder_kernel (10 MovementConvEncoders, exact f32 MFMA)"),
-                   "f32x3": (F16_MFMA_PEAK_TFLOPS / 3, "conv_encoder_x3_kernel (10 MovementConvEncoders, "
-                                                      "3xfp16 split MFMA, peak = dense F16 MFMA / 3)"),
+                   "f32x3": (F16_MFMA_PEAK_TFLOPS / 3, "conv_encoder_x3s_kernel (10 MovementConvEncoders, "
+                                                      "3xfp16 split MFMA, staggered halves, peak = dense F16 MFMA / 3)"),
                    "f16": (F16_MFMA_PEAK_TFLOPS, "conv_encoder_f16w_kernel (10 MovementConvEncoders on 1..6-window "
                                                  "units, single fp16 MFMA per product, peak = dense F16 MFMA)")}
 ARITH = {"f32": "f32 in, f32 accumulate (v_mfma_f32_16x16x4_f32)",
@@ -313,7 +313,7 @@ def main():
 def _kernel_sources_sha() -> str:
     import hashlib
     h = hashlib.sha256()
-    for f in ("vge_encoder_x3.hip", "vge_x3.h", "vge_common.h"):
+    for f in ("vge_encoder_x3.hip", "vge_encoder_x3s.hip", "vge_x3.h", "vge_common.h"):
         h.update((ROOT / "video-gen-evals_amd" / "csrc" / f).read_bytes())
     return h.hexdigest()[:16]
 

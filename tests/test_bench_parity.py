@@ -104,6 +104,41 @@ def test_f16_throughput_mode_vs_oracle(n):
     assert torch.equal(s2, seq[:64])
 
 
+@pytest.mark.parametrize("compute", ["f32x3", "f16"])
+@pytest.mark.parametrize("n", [1, 37, 256, 293])
+def test_transformer_two_windows_per_block_matches_one(n, compute):
+    """The fused transformer with two windows per workgroup (vge_transformer_x3.hip W = 2: every weight chunk a wave
+    streams feeds both windows' rows; automatic once the windows outnumber the CUs) against one window per workgroup,
+    forced through vge_debug_set_tx_windows, on the same feats (odd n: the last workgroup holds one window).  The
+    frame rows take the same products in the same order; the CLS rows run on an MFMA tile at W = 2 and on VALU dot
+    products at W = 1 (another summation order), so the two agree to f32 rounding, and both match the oracle."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vge import lib as L
+    from vge import ops
+    so = L.load()
+    o = _oracle(max(n, 256)) if n <= 256 else _oracle(n)
+    feats = torch.from_numpy(o["feats"][:n]).to(DEV)
+    enc = ops.Encoder(o["sd"], device=DEV, compute=compute)
+    enc.reserve(n)
+    out = {}
+    try:
+        for w in (1, 2):
+            so.vge_debug_set_tx_windows(w)
+            out[w] = enc.encode(feats, frame_embed=True, tc=True)
+            torch.cuda.synchronize()
+    finally:
+        so.vge_debug_set_tx_windows(0)
+    for a, b in zip(out[1], out[2]):
+        assert (a - b).abs().max().item() < 2e-6, (a - b).abs().max().item()
+    e_seq = (out[2][0].cpu() - o["seq"][:n]).abs().max().item()
+    e_fe = (out[2][1].cpu() - o["fe"][:n]).abs().max().item()
+    d = max((a - b).abs().max().item() for a, b in zip(out[1], out[2]))
+    print(f"{compute} n={n}: |W=2 - W=1| {d:.2e}; vs oracle seq {e_seq:.2e} frame {e_fe:.2e}")
+    tol = 2e-5 if compute == "f32x3" else 2e-4
+    assert e_seq < tol and e_fe < tol, (e_seq, e_fe)
+
+
 @pytest.mark.parametrize("n", [1, 37, 256, 293, 600])
 def test_f16_unit_kernel_matches_quad_kernel(n, monkeypatch):
     """The fp16 conv kernel on 1..6-window units from the host-built table (conv_encoder_f16w_kernel, the VGE_F16
@@ -135,24 +170,33 @@ def test_f16_unit_kernel_matches_quad_kernel(n, monkeypatch):
         assert torch.equal(s2, s_u[:64])
 
 
-def test_f16_unit_kernel_is_position_independent_at_4096_windows():
+@pytest.mark.parametrize("tx_w", [1, 2])
+def test_f16_unit_kernel_is_position_independent_at_4096_windows(tx_w):
     """Config 5's encode chunk (4,096 windows: 27 rounds of 5- and 6-window units) checked without the oracle, by a
     property that pins the schedule: every window's outputs depend only on that window (per-window exponents, the
     same chunk order), so encoding a 256-window slice alone (two rounds, quint / hex / quad units) must reproduce its
-    rows of the 4,096-window encode bit for bit, wherever the big schedule placed them."""
+    rows of the 4,096-window encode bit for bit, wherever the big schedule placed them.  The transformer's windows per
+    workgroup are fixed for both encodes (at 2 a window shares its workgroup, and the CLS tile, with a neighbour whose
+    rows do not enter its own; the automatic choice differs between 4,096 and 256 windows)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
+    from vge import lib as L
     from vge import ops, synth
+    so = L.load()
     sd = synth.make_state_dict(synth.DIMS_RAW, synth.DIMS_DIFF)
     g = torch.Generator(device=DEV).manual_seed(11)
     feats = torch.randn((4096, 32, ops.FEAT_DIM), device=DEV, generator=g)
     enc = ops.Encoder(sd, device=DEV, compute="f16")
     enc.reserve(4096)
-    seq, _, tcw = enc.encode(feats, frame_embed=False, tc=True)
-    assert torch.isfinite(seq).all() and torch.isfinite(tcw).all()
-    for lo in (0, 1000, 3840):
-        s2, _, t2 = enc.encode(feats[lo:lo + 256].contiguous(), frame_embed=False, tc=True)
-        assert torch.equal(s2, seq[lo:lo + 256]) and torch.equal(t2, tcw[lo:lo + 256]), lo
+    so.vge_debug_set_tx_windows(tx_w)
+    try:
+        seq, _, tcw = enc.encode(feats, frame_embed=False, tc=True)
+        assert torch.isfinite(seq).all() and torch.isfinite(tcw).all()
+        for lo in (0, 1000, 3841):
+            s2, _, t2 = enc.encode(feats[lo:lo + 255].contiguous(), frame_embed=False, tc=True)
+            assert torch.equal(s2, seq[lo:lo + 255]) and torch.equal(t2, tcw[lo:lo + 255]), lo
+    finally:
+        so.vge_debug_set_tx_windows(0)
 
 
 @pytest.mark.parametrize("n", [1, 37, 256, 293, 4096])

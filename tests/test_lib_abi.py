@@ -170,3 +170,55 @@ def test_conv_unit_schedule_covers_every_window_once(n_windows):
     assert per_cu.max() - per_cu.min() <= 6
     if n_windows == 256:
         assert (G.value, R.value) == (256, 2) and set(per_cu.tolist()) == {10}
+
+
+@pytest.mark.parametrize("heavy", [False, True])
+@pytest.mark.parametrize("n_enc", [10, 8])
+@pytest.mark.parametrize("n_windows", [1, 2, 3, 5, 37, 64, 255, 256, 293, 512, 600, 4096])
+def test_quad_schedule_covers_every_window_once(n_windows, n_enc, heavy):
+    """Quad / pair schedule of the split-precision conv kernels (conv_quad_sched + conv_unit, as the kernels decode it;
+    256 CUs assumed without a GPU): every (encoder, window) pair in exactly one unit, quads in the rounds before the
+    pairs, every CU within one quad of the others.  At the bench's 256 windows every XCD's run of 32 CUs works on ONE
+    encoder in each round (24 encoder weight streams per launch; vge_x3.h), and with the vit encoders marked heavy
+    (multi-panel stems) every CU runs exactly one vit unit, a pair."""
+    import collections
+    import ctypes as C
+
+    import numpy as np
+    from vge import lib as L
+    so = L.load()
+    cap = 3 * (10 * n_windows + 1024)
+    tab = np.zeros(cap, np.int32)
+    G = C.c_int()
+    hv = ({10: 0x21, 8: 0x11}[n_enc]) if heavy else 0  # state / motion vit (vge/eval.py modality order)
+    n = so.vge_debug_quad_schedule(n_windows, n_enc, hv, tab.ctypes.data_as(C.c_void_p), cap // 3, C.byref(G))
+    assert n > 0 and n % G.value == 0
+    tab = tab[:3 * n].reshape(n // G.value, G.value, 3)
+    seen = collections.Counter()
+    per_cu = np.zeros(G.value, np.int64)
+    for r in range(tab.shape[0]):
+        for p in range(G.value):
+            e, w0, w = tab[r, p]
+            if w < 0:
+                continue
+            assert w in (2, 4) and 0 <= e < n_enc and w0 % 2 == 0 and 0 <= w0 < n_windows
+            if w == 4:
+                assert w0 + 4 <= n_windows
+            for k in range(w0, min(w0 + w, n_windows)):  # a pair may be half past the end (odd n_windows)
+                seen[(e, k)] += 1
+            per_cu[p] += w
+    assert len(seen) == n_enc * n_windows and set(seen.values()) == {1}
+    assert per_cu.max() - per_cu.min() <= 4
+    if n_windows == 256:
+        streams = 0
+        for r in range(tab.shape[0]):
+            for x in range(8):
+                run = tab[r, x::8]  # blocks of XCD x (dealt round robin), in xcd_remap order
+                streams += len({int(e) for e, _, w in run if w > 0})
+        assert streams == {10: 24, 8: 16}[n_enc]
+        if heavy and n_enc == 10:
+            assert tab.shape[0] == 3
+            for p in range(G.value):
+                units = [tuple(tab[r, p]) for r in range(3)]
+                assert [w for _, _, w in units] == [4, 4, 2]
+                assert sum((hv >> e) & 1 for e, _, _ in units) == 1 and (hv >> units[2][0]) & 1

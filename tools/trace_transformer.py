@@ -25,12 +25,14 @@ from vge import lib, ops, synth  # noqa: E402
 ap = argparse.ArgumentParser()
 ap.add_argument("--windows", type=int, default=256)
 ap.add_argument("--compute", default="f32x3")
+ap.add_argument("--tx-w", type=int, default=0, help="windows per workgroup (vge_debug_set_tx_windows; 0 = automatic)")
 a = ap.parse_args()
 dev = torch.device("cuda", 0)
 sd = synth.make_state_dict(synth.DIMS_RAW, synth.DIMS_DIFF)
 enc = ops.Encoder(sd, device=dev, compute=a.compute)
 x = torch.randn(a.windows, 32, 2596, device=dev)
 enc.reserve(a.windows)
+lib.load().vge_debug_set_tx_windows(a.tx_w)
 for _ in range(3):
     enc.encode(x)
 torch.cuda.synchronize()

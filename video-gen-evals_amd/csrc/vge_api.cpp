@@ -48,9 +48,9 @@ struct GemmArgsX3Host {
   const float* bias; const float* res; int ldr; const float* ln_w; const float* ln_b; const float* pe; const float* cls;
   const float* cs;
 };
-hipError_t launch_conv_encoders_x3(const float*, int, const void*, int, float*, bool, bool, hipStream_t);
+hipError_t launch_conv_encoders_x3(const float*, int, const void*, int, unsigned, float*, bool, bool, hipStream_t);
 hipError_t encoder_x3s_kernel_setup();
-hipError_t launch_conv_encoders_x3s(const float*, int, const void*, int, float*, hipStream_t);
+hipError_t launch_conv_encoders_x3s(const float*, int, const void*, int, unsigned, float*, hipStream_t);
 bool conv_f16w_plan(int n_windows, int n_enc, int wmax, int& G, int& R, int& U);
 hipError_t launch_conv_f16w_table(int n_windows, int n_enc, int G, int R, int U, int* d_table, hipStream_t s);
 hipError_t launch_conv_encoders_f16w(const float*, int, const void*, float*, const int*, int, int, hipStream_t);
@@ -225,6 +225,7 @@ struct vge_encoder {
   void* d_encs = nullptr;         // EncDescHost[10] or EncDescX3Host[10]
   std::vector<vge::TxLayerX3Host> tx_layers;  // x3: the fused transformer kernel's layer table
   bool tx_fused = true;           // x3: one fused transformer launch (VGE_X3_UNFUSED=1: per-layer kernels)
+  unsigned stem_heavy = 0;        // bit e: encoder e's stem spans more than one 256-wide K panel (vit)
   bool x3s = false;               // VGE_F32X3: the staggered conv kernel on GroupNorm-folded weights (VGE_X3S=0: off)
   int f16_mix = 0;                // VGE_F16: stages kept in 3xfp16 (bit 0 stem, bit 1 transformer; VGE_F16_MIX)
   // VGE_F16 with the stem unsplit: the unit-table conv kernel with units of up to `f16w` windows (VGE_F16W; 0 = the
@@ -580,6 +581,17 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
 
   struct LOff { Mat in_w, out_w, l1_w, l2_w; size_t in_b, out_b, l1_b, l2_b, n1_w, n1_b, n2_w, n2_b; int e_x1, e_x2, e_h; };
   std::vector<LOff> loff(L);
+  // the fused transformer (x3 modes, <= 8 layers, unless VGE_X3_UNFUSED=1) reads in_proj's outputs in head order
+  // (vge_transformer_x3.hip): output block j, wave w, tile t <- the original block (q | k | v) and head half of
+  // kInPerm[j][t], rows 64 w + 32 half .. + 31; the per-layer kernels of the unfused path keep q | k | v
+  const char* uf_env = getenv("VGE_X3_UNFUSED");
+  const bool tx_fused = x3 && (!(uf_env && uf_env[0] == '1') || compute == VGE_F16) && L <= 8;
+  static const int kInPerm[3][2][2] = {{{0, 0}, {1, 0}}, {{2, 0}, {0, 1}}, {{1, 1}, {2, 1}}};  // {block, half}
+  auto in_perm_row = [](int nr) {
+    const int j = nr >> 8, c = nr & 255, w = c >> 6, t = (c >> 5) & 1, i = c & 31;
+    return kInPerm[j][t][0] * 256 + 64 * w + 32 * kInPerm[j][t][1] + i;
+  };
+  std::vector<std::vector<float>> in_perm;  // permuted in_proj copies, alive until packed
   for (int l = 0; l < L; ++l) {
     const std::string p = "temporal.layers." + std::to_string(l);
     const float* inw = get(p + ".self_attn.in_proj_weight", {768, 256});
@@ -596,6 +608,16 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
     const float* n2b = get(p + ".norm2.bias", {256});
     if (!err.empty()) return bail();
     LOff& o = loff[l];
+    if (tx_fused) {
+      in_perm.emplace_back((size_t)768 * 257);
+      float* pw = in_perm.back().data();
+      for (int nr = 0; nr < 768; ++nr) {
+        std::copy(inw + (size_t)in_perm_row(nr) * 256, inw + (size_t)in_perm_row(nr) * 256 + 256, pw + (size_t)nr * 256);
+        pw[768 * 256 + nr] = inb[in_perm_row(nr)];
+      }
+      inw = pw;
+      inb = pw + 768 * 256;
+    }
     o.in_w = pack_lin(inw, 768, 256, 256, 1);
     o.out_w = pack_lin(ow, 256, 256, 256, 1);
     o.l1_w = pack_lin(l1w, 1024, 256, 256, 1);
@@ -732,6 +754,8 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
         descs[e].gn_bmax[b] = bm;
       }
     }
+    for (int e = 0; e < n_enc; ++e)
+      if (eoff[e].P > 1) enc->stem_heavy |= 1u << e;
     he = hipMalloc(&enc->d_encs, sizeof(vge::EncDescX3Host) * n_enc);
     if (he == hipSuccess)
       he = hipMemcpy(enc->d_encs, descs.data(), sizeof(vge::EncDescX3Host) * n_enc, hipMemcpyHostToDevice);
@@ -768,9 +792,7 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
                                         csp(o.in_w), csp(o.out_w), csp(o.l1_w), csp(o.l2_w), o.e_x1, o.e_x2, o.e_h};
   }
   if (x3) {
-    const char* uf = getenv("VGE_X3_UNFUSED");
-    enc->tx_fused = !(uf && uf[0] == '1') || compute == VGE_F16;  // the f16 mode has the fused kernel only
-    if (L > 8) enc->tx_fused = false;  // the fused kernel takes up to 8 layers
+    enc->tx_fused = tx_fused;  // the f16 mode has the fused kernel only; it takes up to 8 layers
     std::vector<vge::TxLayerX3Host>& tl = enc->tx_layers;
     tl.resize(L);
     for (int l = 0; l < L; ++l) {
@@ -958,9 +980,9 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
     HIPCHK(vge::launch_conv_encoders_f16w(feats, B, enc->d_encs, enc->enc_out, enc->d_units + (size_t)k * enc->units_cap,
                                           enc->tables[k].G, enc->tables[k].R, s));
   } else if (x3 && enc->x3s) {
-    HIPCHK(vge::launch_conv_encoders_x3s(feats, B, enc->d_encs, enc->n_enc, enc->enc_out, s));
+    HIPCHK(vge::launch_conv_encoders_x3s(feats, B, enc->d_encs, enc->n_enc, enc->stem_heavy, enc->enc_out, s));
   } else if (x3) {
-    HIPCHK(vge::launch_conv_encoders_x3(feats, B, enc->d_encs, enc->n_enc, enc->enc_out, split, enc->f16_mix & 1, s));
+    HIPCHK(vge::launch_conv_encoders_x3(feats, B, enc->d_encs, enc->n_enc, enc->stem_heavy, enc->enc_out, split, enc->f16_mix & 1, s));
   } else {
     HIPCHK(vge::launch_conv_encoders(feats, B, enc->d_encs, enc->n_enc, enc->enc_out, s));
   }

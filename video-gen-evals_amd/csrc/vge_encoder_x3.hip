@@ -406,24 +406,15 @@ __global__ void __launch_bounds__(512, 1) conv_encoder_x3_kernel(const float* __
                                                                   float* __restrict__ enc_out) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   const int n = cs.n_windows;
-  const int p_big = (n - 4 * (cs.qa + 1) + 1) / 2, p_small = (n - 4 * cs.qa + 1) / 2;  // pairs per encoder
   for (int round = 0; round * cs.G < cs.n_units; ++round) {
     const int u = round * cs.G + xcd_remap(blockIdx.x, cs.G);
     if (u >= cs.n_units) break;  // uniform over the block
     if (round > 0) __syncthreads();  // the previous unit's LDS is free
-    if (u < cs.Q) {
-      const int big = cs.qr * (cs.qa + 1);
-      const int e = u < big ? u / (cs.qa + 1) : cs.qr + (u - big) / cs.qa;
-      const int j = u < big ? u % (cs.qa + 1) : (u - big) % cs.qa;
-      conv_encoder_body<4, 8, SP, SPS>(feats, n, 4 * j, encs[e], e, enc_out, lds_raw, round == VGE_TRACE_ROUND);
-    } else {
-      const int v = u - cs.Q;
-      const int big = cs.qr * p_big;
-      const int e = v < big ? v / p_big : cs.qr + (v - big) / p_small;
-      const int j = v < big ? v % p_big : (v - big) % p_small;
-      const int q_e = cs.qa + (e < cs.qr);
-      conv_encoder_body<2, 8, SP, SPS>(feats, n, 4 * q_e + 2 * j, encs[e], e, enc_out, lds_raw, round == VGE_TRACE_ROUND);
-    }
+    int e, w0;
+    if (conv_unit(cs, u, e, w0))
+      conv_encoder_body<4, 8, SP, SPS>(feats, n, w0, encs[e], e, enc_out, lds_raw, round == VGE_TRACE_ROUND);
+    else
+      conv_encoder_body<2, 8, SP, SPS>(feats, n, w0, encs[e], e, enc_out, lds_raw, round == VGE_TRACE_ROUND);
   }
 }
 
@@ -1274,29 +1265,65 @@ hipError_t encoder_x3_kernel_setup() {
 // units) persistent blocks and m = ceil(pair units / G) per block, Q = G * floor(m / 2) quads (as many as
 // fit) make every block run floor(m / 2) quads and at most one pair.
 // split: 3xfp16 (VGE_F32X3); otherwise single fp16 with the stem split (stem_split) or not
-ConvSched conv_quad_sched(int n_windows, int n_enc) {
+// Quads per encoder: any split of Q with q_e <= n / 4 gives the same pair count (sum of ceil((n - 4 q_e) / 2)), so
+// the split is chosen for the L2s and the balance.  When Q is a whole number K of XCD runs (G / 8 units; xcd_remap),
+// the K runs go to the encoders whose stem is one K panel first, as many as each takes (n / 4 quads), then to the
+// `heavy` ones (vit: a 4-panel stem), so every run of an XCD in a round is one encoder's and the heavy encoders'
+// windows end up in the pairs, spread over all CUs instead of as a longer quad on some.  256 windows x 10 encoders on
+// 256 CUs: the 8 light encoders take 64 quads each (two rounds), the two vit encoders 128 pairs each (the third
+// round); every CU runs two quads and one vit pair; 24 encoder weight streams per launch against ~41 with nearly equal
+// q_e.  Otherwise nearly equal q_e.
+ConvSched conv_quad_sched(int n_windows, int n_enc, unsigned heavy) {
   const int n_cu = conv_cu_count();
   const int pair_units = n_enc * ((n_windows + 1) / 2);
   const int G0 = std::min(n_cu, pair_units);
   const int m = (pair_units + G0 - 1) / G0;
   const int Q = std::min(G0 * (m / 2), n_enc * (n_windows / 4));
   ConvSched cs;
+  memset(&cs, 0, sizeof(cs));
   cs.n_windows = n_windows;
-  cs.n_enc = n_enc;
+  cs.n_enc = std::min(n_enc, CONV_MAX_ENC);
   cs.Q = Q;
-  cs.qa = Q / n_enc;
-  cs.qr = Q % n_enc;
-  int pairs = 0;
-  for (int e = 0; e < n_enc; ++e) pairs += (n_windows - 4 * (cs.qa + (e < cs.qr)) + 1) / 2;
-  cs.n_units = Q + pairs;
+  int q[CONV_MAX_ENC];
+  const int X = G0 % 8 == 0 ? G0 / 8 : 0, qmax = n_windows / 4;
+  static const bool align = [] {  // VGE_QUAD_ALIGN=0: nearly equal q_e always (A/B of the L2 alignment)
+    const char* v = getenv("VGE_QUAD_ALIGN");
+    return !(v && v[0] == '0');
+  }();
+  bool whole = align && X > 0 && Q % X == 0;
+  if (whole) {
+    int K = Q / X;
+    const int kmax = qmax / X;
+    for (int pass = 0; pass < 2; ++pass) {  // light encoders, then heavy: nearly equal runs within each class
+      int cls = 0;
+      for (int e = 0; e < cs.n_enc; ++e) cls += ((heavy >> e) & 1) == (unsigned)pass;
+      if (pass == 0) {
+        for (int e = 0; e < cs.n_enc; ++e) q[e] = 0;
+      }
+      if (cls == 0) continue;
+      const int take = std::min(K, cls * kmax);
+      int j = 0;
+      for (int e = 0; e < cs.n_enc; ++e)
+        if (((heavy >> e) & 1) == (unsigned)pass) q[e] = X * (take / cls + (j++ < take % cls));
+      K -= take;
+    }
+    whole = K == 0;
+  }
+  if (!whole)
+    for (int e = 0; e < cs.n_enc; ++e) q[e] = Q / cs.n_enc + (e < Q % cs.n_enc);
+  for (int e = 0; e < cs.n_enc; ++e) {
+    cs.qpre[e + 1] = cs.qpre[e] + q[e];
+    cs.ppre[e + 1] = cs.ppre[e] + (n_windows - 4 * q[e] + 1) / 2;
+  }
+  cs.n_units = Q + cs.ppre[cs.n_enc];
   cs.G = std::min(n_cu, cs.n_units);
   return cs;
 }
 
-hipError_t launch_conv_encoders_x3(const float* feats, int n_windows, const void* encs, int n_enc, float* enc_out,
-                                   bool split, bool stem_split, hipStream_t s) {
+hipError_t launch_conv_encoders_x3(const float* feats, int n_windows, const void* encs, int n_enc, unsigned heavy,
+                                   float* enc_out, bool split, bool stem_split, hipStream_t s) {
   if (n_windows < 1 || n_enc < 1) return hipSuccess;
-  const ConvSched cs = conv_quad_sched(n_windows, n_enc);
+  const ConvSched cs = conv_quad_sched(n_windows, n_enc, heavy);
   auto k = split ? conv_encoder_x3_kernel<true, true>
                  : (stem_split ? conv_encoder_x3_kernel<false, true> : conv_encoder_x3_kernel<false, false>);
   hipLaunchKernelGGL(k, dim3(cs.G), dim3(512), (conv_lds_bytes<4, 8>()), s, feats,
@@ -1463,6 +1490,27 @@ extern "C" int vge_debug_conv_schedule(int n_windows, int wmax, int* table, int 
   if (!vge::conv_f16w_schedule(n_windows, 10, wmax, t, *G, *R) || (int)t.size() > cap) return -1;
   std::copy(t.begin(), t.end(), table);
   return (int)t.size();
+}
+
+// Test hook (host only, tests/test_lib_abi.py): the quad / pair schedule of n_windows x n_enc, as the kernels read it
+// (conv_unit on xcd_remap'd positions): units[3 (round * G + block) + {0, 1, 2}] = encoder, first window, windows
+// (-1 for an idle slot); heavy: the multi-panel-stem encoder mask.  Returns the entry count (rounds x G) and G.
+extern "C" int vge_debug_quad_schedule(int n_windows, int n_enc, unsigned heavy, int* units, int cap, int* G) {
+  if (n_windows < 1 || n_enc < 1 || n_enc > vge::CONV_MAX_ENC) return -1;
+  const vge::ConvSched cs = vge::conv_quad_sched(n_windows, n_enc, heavy);
+  const int R = (cs.n_units + cs.G - 1) / cs.G;
+  if (R * cs.G > cap) return -1;
+  for (int r = 0; r < R; ++r)
+    for (int b = 0; b < cs.G; ++b) {
+      int* o = units + 3 * (r * cs.G + b);
+      const int u = r * cs.G + xcd_remap(b, cs.G);
+      int e = -1, w0 = -1;
+      o[2] = u < cs.n_units ? (conv_unit(cs, u, e, w0) ? 4 : 2) : -1;
+      o[0] = e;
+      o[1] = w0;
+    }
+  *G = cs.G;
+  return R * cs.G;
 }
 
 #ifdef VGE_TRACE

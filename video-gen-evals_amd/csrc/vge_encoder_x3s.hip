@@ -554,22 +554,17 @@ __global__ void __launch_bounds__(512, 1) conv_encoder_x3s_kernel(const float* _
 #endif
   int n_ex = 0;
   const int n = cs.n_windows;
-  const int p_big = (n - 4 * (cs.qa + 1) + 1) / 2, p_small = (n - 4 * cs.qa + 1) / 2;  // pairs per encoder
   for (int round = 0; round * cs.G < cs.n_units; ++round) {
     const int u = round * cs.G + xcd_remap(blockIdx.x, cs.G);
     if (u >= cs.n_units) break;  // uniform over the block
     if (u < cs.Q) {
-      const int big = cs.qr * (cs.qa + 1);
-      const int e = u < big ? u / (cs.qa + 1) : cs.qr + (u - big) / cs.qa;
-      const int j = u < big ? u % (cs.qa + 1) : (u - big) % cs.qa;
-      conv_x3s_body<4>(feats, n, 4 * j, encs[e], e, enc_out, lds_raw, n_ex, round == X3S_TRACE_ROUND);
+      int e, w0;
+      conv_unit(cs, u, e, w0);
+      conv_x3s_body<4>(feats, n, w0, encs[e], e, enc_out, lds_raw, n_ex, round == X3S_TRACE_ROUND);
     } else {
-      const int v = u - cs.Q;
-      const int big = cs.qr * p_big;
-      const int e = v < big ? v / p_big : cs.qr + (v - big) / p_small;
-      const int j = v < big ? v % p_big : (v - big) % p_small;
-      const int q_e = cs.qa + (e < cs.qr);
-      conv_x3s_body<2>(feats, n, 4 * q_e + 2 * j, encs[e], e, enc_out, lds_raw, n_ex, round == X3S_TRACE_ROUND);
+      int e, w0;
+      conv_unit(cs, u, e, w0);
+      conv_x3s_body<2>(feats, n, w0, encs[e], e, enc_out, lds_raw, n_ex, round == X3S_TRACE_ROUND);
     }
   }
 #ifdef VGE_TRACE
@@ -587,10 +582,10 @@ hipError_t encoder_x3s_kernel_setup() {
                              X3S_LDS_BYTES);
 }
 
-hipError_t launch_conv_encoders_x3s(const float* feats, int n_windows, const void* encs, int n_enc, float* enc_out,
-                                    hipStream_t s) {
+hipError_t launch_conv_encoders_x3s(const float* feats, int n_windows, const void* encs, int n_enc, unsigned heavy,
+                                    float* enc_out, hipStream_t s) {
   if (n_windows < 1 || n_enc < 1) return hipSuccess;
-  const ConvSched cs = conv_quad_sched(n_windows, n_enc);
+  const ConvSched cs = conv_quad_sched(n_windows, n_enc, heavy);
   hipLaunchKernelGGL(conv_encoder_x3s_kernel, dim3(cs.G), dim3(512), X3S_LDS_BYTES, s, feats,
                      reinterpret_cast<const EncDescX3*>(encs), cs, enc_out);
   return hipGetLastError();

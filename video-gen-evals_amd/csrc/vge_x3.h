@@ -6,14 +6,19 @@
 
 namespace vge {
 // Persistent schedule of the quad / pair conv kernels.  Work units: Q quads (4 windows) then the pairs (2 windows)
-// covering the rest of each encoder's windows; encoder e takes q_e = qa + (e < qr) quads (windows [0, 4 q_e)) and the
-// pairs after them.  Grid = G blocks (one per CU); unit u runs on block u % G in round u / G, so with Q a multiple
-// of G every CU does the same number of quads and at most one pair.  Within a round the block index is remapped so
-// the 8 XCDs (blocks dealt round robin) take contiguous units, i.e. the same encoders' weights in their L2.
+// covering the rest of each encoder's windows; encoder e takes q_e quads (windows [0, 4 q_e)) and the pairs after
+// them.  Grid = G blocks (one per CU); unit u runs on block u % G in round u / G, so with Q a multiple of G every CU
+// does the same number of quads and at most one pair.  Within a round the block index is remapped so the 8 XCDs
+// (blocks dealt round robin) take contiguous runs of G / 8 units, i.e. the same encoders' weights in their L2.
+// q_e: whole XCD runs where that tiles Q (conv_quad_sched: then every XCD streams ONE encoder per round, and the
+// encoders with multi-panel stems -- `heavy`, a bit mask -- take the pairs), else nearly equal.  qpre / ppre: prefix
+// sums of the quads / pairs per encoder.
+constexpr int CONV_MAX_ENC = 16;
 struct ConvSched {
-  int n_windows, n_enc, G, Q, qa, qr, n_units;
+  int n_windows, n_enc, G, Q, n_units;
+  int qpre[CONV_MAX_ENC + 1], ppre[CONV_MAX_ENC + 1];
 };
-ConvSched conv_quad_sched(int n_windows, int n_enc);  // vge_encoder_x3.hip (host)
+ConvSched conv_quad_sched(int n_windows, int n_enc, unsigned heavy = 0);  // vge_encoder_x3.hip (host)
 }  // namespace vge
 
 #ifndef VGE_ABL
@@ -177,9 +182,32 @@ struct EncDescX3 {
   float gn_gmax[4], gn_bmax[4];  // max |gamma|, max |beta| of each GroupNorm (split-exponent bounds)
 };
 
-__device__ __forceinline__ int xcd_remap(int b, int nblk) {
+__host__ __device__ __forceinline__ int xcd_remap(int b, int nblk) {
   const int q8 = nblk >> 3, r8 = nblk & 7, x8 = b & 7;
   return (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (b >> 3);
+}
+
+// Unit u of a ConvSched: encoder e, first window w0, quad (true) or pair.  Uniform over the block (scalar loop over
+// the <= 16 prefix sums in kernel-argument memory).
+__host__ __device__ __forceinline__ bool conv_unit(const vge::ConvSched& cs, int u, int& e, int& w0) {
+  const bool quad = u < cs.Q;
+  const int v = quad ? u : u - cs.Q;
+  const int* pre = quad ? cs.qpre : cs.ppre;
+  int ee = 0, lo = 0, qa = 0, qb = cs.qpre[1];
+  for (int k = 1; k < cs.n_enc; ++k)  // fixed trip count, no dynamic index into the argument block
+    if (v >= pre[k]) {
+      ee = k;
+      lo = pre[k];
+      qa = cs.qpre[k];
+      qb = cs.qpre[k + 1];
+    }
+  w0 = quad ? 4 * (v - lo) : 4 * (qb - qa) + 2 * (v - lo);
+  e = ee;
+#ifdef __HIP_DEVICE_COMPILE__
+  e = __builtin_amdgcn_readfirstlane(e);
+  w0 = __builtin_amdgcn_readfirstlane(w0);
+#endif
+  return quad;
 }
 
 }  // namespace
