@@ -1286,10 +1286,11 @@ ConvSched conv_quad_sched(int n_windows, int n_enc, unsigned heavy) {
   cs.Q = Q;
   int q[CONV_MAX_ENC];
   const int X = G0 % 8 == 0 ? G0 / 8 : 0, qmax = n_windows / 4;
-  static const bool align = [] {  // VGE_QUAD_ALIGN=0: nearly equal q_e always (A/B of the L2 alignment)
-    const char* v = getenv("VGE_QUAD_ALIGN");
-    return !(v && v[0] == '0');
+  static const int align = [] {  // VGE_QUAD_ALIGN=0: nearly equal q_e always; 1: whole runs, heavy stems not
+    const char* v = getenv("VGE_QUAD_ALIGN");  // preferred in the pairs (A/B of the L2 alignment and the stem split)
+    return v ? atoi(v) : 2;
   }();
+  if (align < 2) heavy = 0;
   bool whole = align && X > 0 && Q % X == 0;
   if (whole) {
     int K = Q / X;

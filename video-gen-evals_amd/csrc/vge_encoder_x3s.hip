@@ -198,49 +198,60 @@ __device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, i
   };
   XTS(0);
   acc.zero();
-  for (int p = 0; p < ed.n_stem_panels; ++p) {
-    const int kw = min(256, ed.d_in - p * 256);
-    int* ecur = ax.rexp[p & 1];
-    constexpr int RPW = 32 * W / 8;
+  // Every row of PG panels is loaded before any is used (one HBM round trip per PG panels: a pair's 4-panel vit stem
+  // loads two panels at a time; the loads of a panel group are all issued before its first weight stream, so no
+  // stream's counted vmcnt wait can stall on them), then each panel is split into LDS and streamed in turn.
+  constexpr int RPW = 32 * W / 8;  // rows per wave
+  constexpr int PG = W <= 2 ? 2 : 1;
+  for (int p0 = 0; p0 < ed.n_stem_panels; p0 += PG) {
+    float a[PG][RPW][4];
 #pragma unroll
-    for (int g8 = 0; g8 < RPW / 4; ++g8) {
-      float a[4][4];
+    for (int q = 0; q < PG; ++q) {
+      const int p = p0 + q;
+      const int kw = p < ed.n_stem_panels ? min(256, ed.d_in - p * 256) : 0;
 #pragma unroll
-      for (int jr = 0; jr < 4; ++jr) {
-        const int r = wave * RPW + g8 * 4 + jr;
+      for (int jr = 0; jr < RPW; ++jr) {
+        const int r = wave * RPW + jr;
         const int w = win0 + (r >> 5);
         const float* src = feats + ((size_t)w * VGE_T + (r & 31)) * ed.ld + ed.in_col + p * 256;
 #pragma unroll
         for (int jc = 0; jc < 4; ++jc) {
           const int c = lane + 64 * jc;
-          a[jr][jc] = (c < kw && w < n_windows) ? src[c] : 0.f;
+          a[q][jr][jc] = (c < kw && w < n_windows) ? gload(src + c) : 0.f;
         }
       }
+    }
 #pragma unroll
-      for (int jr = 0; jr < 4; ++jr) {
-        float m = fmaxf(fmaxf(fabsf(a[jr][0]), fabsf(a[jr][1])), fmaxf(fabsf(a[jr][2]), fabsf(a[jr][3])));
+    for (int q = 0; q < PG; ++q) {
+      const int p = p0 + q;
+      if (p >= ed.n_stem_panels) break;
+      const int kw = min(256, ed.d_in - p * 256);
+      int* ecur = ax.rexp[p & 1];
+#pragma unroll
+      for (int jr = 0; jr < RPW; ++jr) {
+        float m = fmaxf(fmaxf(fabsf(a[q][jr][0]), fabsf(a[q][jr][1])), fmaxf(fabsf(a[q][jr][2]), fabsf(a[q][jr][3])));
         m = wave_max_all(m);
         const int ex = fp16_range_exp(m);
-        const int r = wave * RPW + g8 * 4 + jr;
+        const int r = wave * RPW + jr;
         if (lane == 0) ecur[r] = ex;
 #pragma unroll
         for (int jc = 0; jc < 4; ++jc) {
           const int c = lane + 64 * jc;
-          split_store(X + r * XR + c, X + r * XR + XLO / 2 + c, ldexpf(a[jr][jc], -ex));
+          split_store(X + r * XR + c, X + r * XR + XLO / 2 + c, ldexpf(a[q][jr][jc], -ex));
         }
       }
-    }
-    __syncthreads();  // X and ecur complete
-    if (p > 0) {
-      const int* eprev = ax.rexp[(p - 1) & 1];
+      __syncthreads();  // X and ecur complete
+      if (p > 0) {
+        const int* eprev = ax.rexp[(p - 1) & 1];
 #pragma unroll
-      for (int t = 0; t < R; ++t)
+        for (int t = 0; t < R; ++t)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc.c[t][0][r] *= ldexpf(1.0f, eprev[crow(t, r)] - ecur[crow(t, r)]);
+          for (int r = 0; r < 16; ++r) acc.c[t][0][r] *= ldexpf(1.0f, eprev[crow(t, r)] - ecur[crow(t, r)]);
+      }
+      run_stream<CONV_PF, true>(acc, reinterpret_cast<const char*>(ed.stem) + (size_t)p * 16 * CHUNK_B,
+                                ((kw + 127) >> 7) * STREAM_GROUP, loff, afn_stem);
+      __syncthreads();  // every wave is done reading X
     }
-    run_stream<CONV_PF, true>(acc, reinterpret_cast<const char*>(ed.stem) + (size_t)p * 16 * CHUNK_B,
-                              ((kw + 127) >> 7) * STREAM_GROUP, loff, afn_stem);
-    __syncthreads();  // every wave is done reading X
   }
 
   // ---------------- the staggered chain
