@@ -72,7 +72,7 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
     from vge.data import ACTION_CLASSES, pack_frame_store
     from vge.dist import shard
     from vge.dwpose import RTMPOSE_L, YOLOX_L, DwposeExtractor, YoloxDetector
-    from vge.extract import single_person_mask
+    from vge.extract import SINGLE_PERSON_MIN_FRACTION, single_person_mask
     from vge.hmr import TOKENHMR, HmrExtractor, crop_persons
 
     C, T = args.clips, 32
@@ -110,91 +110,149 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
     ex = HmrExtractor(hsd, TOKENHMR, device=dev, max_frames=FC)
     del hsd
     dw = DwposeExtractor(synth.make_rtmpose_state_dict(RTMPOSE_L), RTMPOSE_L, device=dev, max_instances=2 * FC)
-    det = None if args.no_detector else YoloxDetector(synth.make_yolox_state_dict(YOLOX_L), YOLOX_L, device=dev,
-                                                      chunk=min(FC, 64))
+    det = None if args.no_detector else YoloxDetector(synth.make_gate_detector_state_dict(YOLOX_L), YOLOX_L,
+                                                      device=dev, chunk=min(FC, 64))
     no_box = np.zeros(FC, np.int32)
-    base = torch.from_numpy(synth.make_frames(1000 + rank, FC)).to(dev)
-    if F == FC:
-        frames = base
-    else:  # distinct frames for every pass, derived on the device from one pass's worth of generated frames
-        frames = torch.empty((F,) + tuple(base.shape[1:]), dtype=torch.uint8, device=dev)
-        for f0 in range(0, F, FC):
-            n = min(FC, F - f0)
-            frames[f0:f0 + n] = ((base[:n].to(torch.int16) + (f0 // FC) * 37) % 256).to(torch.uint8)
-        del base
+    Hf = Wf = 256
+    whole = np.tile(np.array([0, 0, Wf, Hf], np.float32), (FC, 1))
+    # the generated clips' frames: drawn from a pool of synthetic scenes by what the detector finds in each pool frame
+    # (setup, untimed), so that 9 clips in 10 pass the single-person gate (2-3 of their 32 frames with no or two
+    # persons) and 1 in 10 is rejected (12 such frames: 20 / 32 < 80 %).  The timed steps run the detector on every
+    # frame again and take every decision from its output.
+    gate_plan = {"accept_every": 10, "bad_frames_accepted": (2, 3), "bad_frames_rejected": 12}
+    if det is None:
+        frames = torch.from_numpy(synth.make_frame_pool(5000 + 997 * rank, min(F, 4096))).to(dev)
+        frames = frames[torch.arange(F, device=dev) % frames.shape[0]] if F > frames.shape[0] else frames
+    else:
+        P = 2048
+        pool = torch.from_numpy(synth.make_frame_pool(5000 + 997 * rank, P)).to(dev)
+        _, _, psc = det.detect(pool, with_scores=True)
+        good = np.flatnonzero(single_person_mask(psc.cpu().numpy()))
+        bad = np.setdiff1d(np.arange(P), good)
+        if good.size < 64 or bad.size < 64:
+            raise RuntimeError(f"e2e: the detector finds exactly one person in {good.size} of {P} pool frames; "
+                               "recalibrate vge.synth.GATE_OBJ_SHIFT (tools/yolox_gate_calib.py)")
+        rs = np.random.default_rng(11 + rank)
+        idx = np.empty(F, np.int64)
+        for c in range(C):
+            nb = (gate_plan["bad_frames_rejected"] if c % gate_plan["accept_every"] == gate_plan["accept_every"] - 1
+                  else gate_plan["bad_frames_accepted"][c % 2])
+            sel = np.concatenate([rs.choice(bad, nb), rs.choice(good, T - nb)])
+            idx[c * T:(c + 1) * T] = rs.permutation(sel)
+        frames = pool[torch.from_numpy(idx).to(dev)]
+        del pool
     gen_clips = make_clips(synth.SEED_GEN, rank * C, C, T)
     names = [synth.generated_name(rank * C + i) for i in range(C)]
     gstore = ops.DeviceFrameStore.from_host(pack_frame_store(gen_clips, names, ["X"] * C), dev)
     outs = {"pose": gstore.pose, "global_orient": gstore.gori, "betas": gstore.betas, "vit": gstore.vit}
-    windows = torch.tensor([[v, 0] for v in range(C)], dtype=torch.int32, device=dev)
-    first = torch.arange(C + 1, dtype=torch.int32, device=dev)
-    vcls = torch.tensor([label[ACTION_CLASSES[((rank * C + i) // 5) % 10]] for i in range(C)], dtype=torch.int32,
-                        device=dev)
+    vcls_all = np.array([label[ACTION_CLASSES[((rank * C + i) // 5) % 10]] for i in range(C)], np.int32)
     feats = torch.empty((C, T, ops.FEAT_DIM), device=dev)
     host_ac = torch.empty((C,), dtype=torch.float32, pin_memory=True)
     host_tc = torch.empty((C,), dtype=torch.float64, pin_memory=True)
+    # per step: the accepted videos' frame-store descriptors {frame_off, n_frames, kp_off, kp_frames} (the npz holds
+    # the kept frames only, keypoints.npy every frame: extract_mesh.py:35-43, process_video.py:71-84), windows, the
+    # per-video window ranges and classes -> one pinned host table, one copy
+    pin_tab = torch.empty((C * 4 + C * 2 + (C + 1) + C,), dtype=torch.int32, pin_memory=True)
+    dev_tab = torch.empty_like(pin_tab, device=dev)
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t_setup
 
-    assert tuple(gstore.kp.shape) == (F, 120)
+    assert tuple(gstore.kp.shape) == (F, 120) and tuple(frames.shape) == (F, Hf, Wf, 3)
     # the two extractors are independent until the frame store is complete: TokenHMR on one HIP stream, DWPose on
     # another (the detector's host round trip waits on its own stream only), so each fills the other's tails
     s_hmr, s_pose = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
     concurrent = not getattr(args, "serial_extract", False)
 
-    Hf, Wf = int(frames.shape[1]), int(frames.shape[2])
-    whole = np.tile(np.array([0, 0, Wf, Hf], np.float32), (FC, 1))
     pin_b = torch.empty((FC, 2, 4), dtype=torch.float32, pin_memory=True)
     pin_n = torch.empty((FC,), dtype=torch.int32, pin_memory=True)
     pin_s = torch.empty((FC, 2), dtype=torch.float32, pin_memory=True)
-    gate = {"frames": 0, "single_person": 0}
+    gate = {"frames": 0, "single_person": 0, "videos": 0, "accepted": 0, "hmr_frames": 0}
 
     def detect(fr):
         """the shared person detection -> host (the pose model's instance table and the TokenHMR gate / crop boxes
-        are built on the host, as the reference's numpy NMS output is)"""
+        are built on the host, as the reference's numpy NMS output is) -> (boxes, n_persons, single-person mask)"""
         n = int(fr.shape[0])
         if det is None:
-            return None, no_box[:n], whole[:n]
+            return None, no_box[:n], np.ones(n, bool)
         boxes, npers, scores = det.detect(fr, with_scores=True)
         pin_b[:n].copy_(boxes, non_blocking=True)
         pin_n[:n].copy_(npers, non_blocking=True)
         pin_s[:n].copy_(scores, non_blocking=True)
         torch.cuda.current_stream(dev).synchronize()
-        hb, hn = pin_b[:n].numpy(), pin_n[:n].numpy()
         keep = single_person_mask(pin_s[:n].numpy())
         gate["frames"] += n
         gate["single_person"] += int(keep.sum())
-        return hb, hn, np.where(keep[:, None], hb[:, 0], whole[:n])
+        return pin_b[:n].numpy(), pin_n[:n].numpy(), keep
 
-    def hmr(fr, hbox, f0):
-        crops = crop_persons(fr, hbox)
-        ex.extract(crops, out={k: v[f0:f0 + int(fr.shape[0])] for k, v in outs.items()})
+    def hmr(fr, hb, kept, off):
+        """TokenHMR on the kept frames of the pass's accepted videos, into rows off.. of the frame store"""
+        nk = int(kept.size)
+        if nk:
+            box = whole[:nk] if hb is None else hb[kept, 0]
+            crops = crop_persons(fr, box, kept)
+            ex.extract(crops, out={k: v[off:off + nk] for k, v in outs.items()})
+            gate["hmr_frames"] += nk
 
     def keypoints(fr, hb, hn, f0):
         dw.keypoints(fr, hb, hn, out=gstore.kp[f0:f0 + int(fr.shape[0])])
 
     def step():
+        tab = pin_tab.numpy()
+        vids = tab[:4 * C].reshape(C, 4)
+        acc = []
+        off = 0
         for f0 in range(0, F, FC):
             fr = frames[f0:f0 + FC]
-            hb, hn, hbox = detect(fr)
+            n = int(fr.shape[0])
+            hb, hn, keep = detect(fr)
+            # mesh_generator.py:101-117 per video: the frames with exactly one person; the video is rejected
+            # (process_video returns False, no npz) when they are fewer than 80 % of its frames
+            kept = []
+            for c in range(f0 // T, (f0 + n) // T):
+                valid = np.flatnonzero(keep[c * T - f0:(c + 1) * T - f0])
+                gate["videos"] += 1
+                if valid.size == 0 or valid.size < SINGLE_PERSON_MIN_FRACTION * T:
+                    continue
+                vids[len(acc)] = (off + sum(len(k) for k in kept), valid.size, c * T, T)
+                acc.append(c)
+                kept.append(valid + (c * T - f0))
+            kept = np.concatenate(kept) if kept else np.zeros(0, np.int64)
             if concurrent:
                 cur = torch.cuda.current_stream(dev)
                 s_hmr.wait_stream(cur)
                 s_pose.wait_stream(cur)
                 with torch.cuda.stream(s_hmr):
-                    hmr(fr, hbox, f0)
+                    hmr(fr, hb, kept, off)
                 with torch.cuda.stream(s_pose):
                     keypoints(fr, hb, hn, f0)
                 cur.wait_stream(s_hmr)
                 cur.wait_stream(s_pose)
             else:
-                hmr(fr, hbox, f0)
+                hmr(fr, hb, kept, off)
                 keypoints(fr, hb, hn, f0)
-        ops.featurize(gstore, windows, stats.mean, stats.std, out=feats)
-        seq, _, tcw = enc.encode(feats, frame_embed=False, tc=True)
-        ac, tc = ops.score_videos(seq, tcw, first, vcls, centroids)
-        host_ac.copy_(ac, non_blocking=True)
-        host_tc.copy_(tc, non_blocking=True)
+            off += int(kept.size)
+        nA = len(acc)
+        gate["accepted"] += nA
+        if nA == 0:
+            return
+        # eval.py:360-400 on the accepted videos (window start 0: T' <= 32 frames, _slice_or_pad pads)
+        win = tab[4 * C:4 * C + 2 * nA].reshape(nA, 2)
+        win[:, 0], win[:, 1] = np.arange(nA), 0
+        first = tab[6 * C:6 * C + nA + 1]
+        first[:] = np.arange(nA + 1)
+        vc = tab[7 * C + 1:7 * C + 1 + nA]
+        vc[:] = vcls_all[acc]
+        dev_tab.copy_(pin_tab, non_blocking=True)
+        gstore.videos[:nA].copy_(dev_tab[:4 * nA].view(nA, 4))
+        windows = dev_tab[4 * C:4 * C + 2 * nA].view(nA, 2)
+        ops.featurize(gstore, windows, stats.mean, stats.std, out=feats[:nA])
+        seq, _, tcw = enc.encode(feats[:nA], frame_embed=False, tc=True)
+        ac, tc = ops.score_videos(seq, tcw, dev_tab[6 * C:6 * C + nA + 1], dev_tab[7 * C + 1:7 * C + 1 + nA],
+                                  centroids)
+        host_ac[:nA].copy_(ac, non_blocking=True)
+        host_tc[:nA].copy_(tc, non_blocking=True)
+        if det is None:   # else the next step's first detection syncs the stream before the table is rewritten
+            torch.cuda.current_stream(dev).synchronize()
 
     for _ in range(args.warmup):
         step()
@@ -211,6 +269,7 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    hmr_frames0 = gate["hmr_frames"]
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -223,16 +282,22 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
     if world > 1:
         dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
     dt = float(dt_t.item())
+    gate_timed = dict(gate)
+    # every extract / keypoints / detect call of the profiled steps is recorded (at most one per pass each)
     if concurrent:
         ex.profile_begin(prof_steps * n_chunks)
         dw.profile_begin(prof_steps * n_chunks)
         if det is not None:
             det.profile_begin(prof_steps * n_chunks)
+    # TokenHMR frames of one step (the same every step: the clips and the detector are deterministic)
+    hmr_frames_step = (gate["hmr_frames"] - hmr_frames0) / args.steps
+    if concurrent:
         concurrent = False
         for _ in range(prof_steps):
             step()
         torch.cuda.synchronize()
         concurrent = True
+    prof_hmr_frames = hmr_frames_step * prof_steps
     st, ncalls, gemm_flops_per_frame = ex.profile_read()
     dst, dcalls, dw_flops = dw.profile_read()
     yst, ycalls, y_flops = det.profile_read() if det is not None else ({}, 0, 0.0)
@@ -241,7 +306,9 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
         return None
     n = max(ncalls, 1)
     gemm_ms = st["gemm"] / n
-    achieved = gemm_flops_per_frame * FC / (gemm_ms * 1e-3) / 1e12
+    # TokenHMR runs on the kept frames only, so a call's size varies: FLOPs of the recorded calls / their GEMM time
+    hmr_frames_per_call = prof_hmr_frames / n
+    achieved = gemm_flops_per_frame * prof_hmr_frames / (st["gemm"] * 1e-3) / 1e12 if st["gemm"] else 0.0
     out = {
         "metric": metric,
         "value": world * C * args.steps / dt,
@@ -254,7 +321,8 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16 (extractor: bf16 operands, f32 accumulate / residual stream) + f32x3 (scorer)",
-        "data": "synthetic 256x256 RGB frames (vge.synth.make_frames); random-init weights of the TokenHMR "
+        "data": "synthetic 256x256 RGB frames (vge.synth.make_frame_pool, drawn by the detector's findings at setup); "
+                "random-init weights of the TokenHMR "
                 "(ViT-H/16 + decoder), YOLOX-L, RTMPose-l whole-body and scorer architectures",
         "config": {"workload": "BASELINE config 3: TokenHMR + DWPose (YOLOX-L + RTMPose-l) extract -> featurise -> "
                                "encoder -> AC/TC, 32-frame 256x256 clips, full frames resident in HBM (one YOLOX-L "
@@ -266,18 +334,27 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
                                                 "fc2; dense bf16 MFMA peak)",
                      "achieved": achieved, "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / BF16_MFMA_PEAK_TFLOPS, "traffic": None,
-                     "flop_per_call": gemm_flops_per_frame * FC, "gemm_ms_per_call": gemm_ms},
+                     "flop_per_call": gemm_flops_per_frame * hmr_frames_per_call, "gemm_ms_per_call": gemm_ms,
+                     "frames_per_call": hmr_frames_per_call},
         "stage_ms": {**{f"hmr_{k}": v / n for k, v in st.items()},
                      **{f"dwpose_{k}": v / max(dcalls, 1) for k, v in dst.items()},
                      **{f"yolox_{k}": v / max(ycalls, 1) for k, v in yst.items()}},
         "yolox_gemm_tflops": (y_flops / (yst["gemm"] / ycalls * 1e-3) / 1e12) if ycalls else None,
         "dwpose_gemm_tflops": dw_flops / (dst["gemm"] / max(dcalls, 1) * 1e-3) / 1e12,
         "frames_per_s": world * F * args.steps / dt,
-        "front_end": {"detector": "YOLOX-L (stand-in for detectron2 Faster R-CNN X101-FPN)" if det is not None else None,
-                      "gate": "exactly one person box with score > 0.5 (mesh_generator.py:103-111)",
-                      "single_person_fraction": (gate["single_person"] / gate["frames"]) if gate["frames"] else None,
-                      "crop": "ViTDetDataset warp to 256x256 (vge_hmr_crop); gate-rejected frames take the whole "
-                              "frame, so every frame is extracted"},
+        "front_end": {"detector": ("YOLOX-L (stand-in for detectron2 Faster R-CNN X101-FPN; "
+                                   "vge.synth.make_gate_detector_state_dict)") if det is not None else None,
+                      "gate": "exactly one person box with score > 0.5 per frame, >= 80 % such frames per video, else "
+                              "the video is rejected (mesh_generator.py:101-117)",
+                      "single_person_fraction": (gate_timed["single_person"] / gate_timed["frames"])
+                      if gate_timed["frames"] else None,
+                      "videos_accepted_fraction": (gate_timed["accepted"] / gate_timed["videos"])
+                      if gate_timed["videos"] else None,
+                      "tokenhmr_frames_per_video": gate_timed["hmr_frames"] / max(gate_timed["videos"], 1),
+                      "clip_plan": gate_plan if det is not None else None,
+                      "crop": "ViTDetDataset warp to 256x256 (vge_hmr_crop) of the kept frames of accepted videos; "
+                              "TokenHMR on those only; DWPose on every frame (process_video.py); rejected videos "
+                              "are not scored (no npz)"},
         "extractors": ("concurrent (TokenHMR and DWPose on two HIP streams; stage_ms / roofline from hipEvents on "
                        "serial steps after the timed region)") if concurrent else "serial",
         "setup_s": setup_s,

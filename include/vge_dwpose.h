@@ -66,7 +66,8 @@ int vge_dwpose_keypoints(vge_dwpose* m, const uint8_t* frames, int n_frames, int
 
 /* Device time of the dense convolutions (implicit GEMMs) and of everything else over the next max_calls
  * keypoint calls: stage_ms[0] = conv / Linear GEMMs, [1] = depthwise + pooling + attention + prep, [2] = GAU token
- * mixing + decode; gemm_flops = algorithmic GEMM FLOPs of the last call. */
+ * mixing + decode; gemm_flops_per_call = algorithmic GEMM FLOPs of the recorded calls / n_calls (the last call's
+ * when none was recorded). */
 int vge_dwpose_profile_begin(vge_dwpose* m, int max_calls);
 int vge_dwpose_profile_read(vge_dwpose* m, double* stage_ms, int* n_calls, double* gemm_flops_per_call);
 
@@ -105,7 +106,8 @@ int vge_yolox_detect(vge_yolox* m, const uint8_t* frames, int n_frames, int H, i
  * X101-FPN, absent offline; this YOLOX-L is its stand-in: parity unpinned.) */
 int vge_yolox_detect_scored(vge_yolox* m, const uint8_t* frames, int n_frames, int H, int W, float* boxes,
                             int* n_persons, float* scores, float* cand, vge_stream_t stream);
-/* stage_ms[0] = convolutions (implicit GEMMs), [1] = letterbox / upsample / pooling / decode + NMS */
+/* stage_ms[0] = convolutions (implicit GEMMs), [1] = letterbox / upsample / pooling / decode + NMS, summed over the
+ * recorded calls; gemm_flops_per_call = their algorithmic GEMM FLOPs / n_calls (a pass's tail call is smaller). */
 int vge_yolox_profile_begin(vge_yolox* m, int max_calls);
 int vge_yolox_profile_read(vge_yolox* m, double* stage_ms, int* n_calls, double* gemm_flops_per_call);
 

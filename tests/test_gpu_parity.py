@@ -173,7 +173,9 @@ def test_cli_with_saved_features(vg, golden_dataset, golden_flow, golden_meta, t
 
 
 def test_featurize_edge_cases_vs_oracle(vg):
-    """Static / all-invisible / partly invisible keypoints, start past the end, single-frame clip."""
+    """Static / all-invisible / partly invisible keypoints, start past the end, single-frame clip, and an npz shorter
+    than its keypoints.npy (the single-person gate keeps 27 of 32 frames: mesh_generator.py:101-117 saves the kept
+    frames only, process_video.py every frame; _try_one slices / pads each array on its own)."""
     VE, ops = vg
     from oracle import featurize as OF
     from vge import synth
@@ -192,9 +194,12 @@ def test_featurize_edge_cases_vs_oracle(vg):
             kp[3] = -1.0                                  # one fully invisible frame
         clips.append({"pose": c.pose, "global_orient": c.global_orient, "betas": c.betas, "vit": c.vit,
                       "keypoints": kp})
-    st = pack_frame_store(clips, [f"c{i}" for i in range(5)], ["X"] * 5)
+    c = synth.make_clip(11, 5, 32)
+    clips.append({"pose": c.pose[:27], "global_orient": c.global_orient[:27], "betas": c.betas[:27], "vit": c.vit[:27],
+                  "keypoints": c.keypoints})
+    st = pack_frame_store(clips, [f"c{i}" for i in range(6)], ["X"] * 6)
     store = ops.DeviceFrameStore.from_host(st, DEV)
-    wins = [(0, 0), (0, 8), (1, 0), (2, 0), (3, 8), (3, 39), (3, 100), (4, 0)]
+    wins = [(0, 0), (0, 8), (1, 0), (2, 0), (3, 8), (3, 39), (3, 100), (4, 0), (5, 0)]
     w = torch.tensor(wins, dtype=torch.int32, device=DEV)
     mean = torch.zeros(2596, device=DEV)
     std = torch.full((2596,), 1.0 - 1e-6, device=DEV)

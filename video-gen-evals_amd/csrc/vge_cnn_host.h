@@ -281,6 +281,7 @@ struct Profiler {
   int max_calls = 0, calls = 0, per_call = 0;
   size_t pair = 0;
   bool on = false;
+  double flops = 0;  // algorithmic GEMM FLOPs of the recorded calls (calls differ in size: a pass's tail)
   ~Profiler() {
     for (auto e : ev) (void)hipEventDestroy(e);
   }
@@ -292,16 +293,18 @@ struct Profiler {
     for (auto& e : ev) VGE_HIPCHK(hipEventCreate(&e));
     max_calls = n_calls;
     calls = 0;
+    flops = 0;
     return VGE_OK;
   }
   void start_call() {
     on = calls < max_calls;
     pair = on ? (size_t)calls * per_call : 0;
   }
-  void end_call() {
-    if (on) ++calls;
+  void end_call(double call_flops) {
+    if (on) ++calls, flops += call_flops;
     on = false;
   }
+  double flops_per_call(double fallback) const { return calls ? flops / calls : fallback; }
   int beg(int k, hipStream_t s) {
     if (on && pair < (size_t)(calls + 1) * per_call) {
       kind[pair] = k;

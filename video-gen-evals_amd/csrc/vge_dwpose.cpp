@@ -75,7 +75,7 @@ struct vge_dwpose {
   std::vector<hipEvent_t> ev;
   std::vector<int> ev_kind;
   int prof_max = 0, prof_calls = 0, ev_per_call = 0;
-  double gemm_flops = 0;
+  double gemm_flops = 0, prof_flops = 0;  // prof_flops: summed over the recorded calls (instance counts differ)
   ~vge_dwpose() {
     for (auto e : ev) (void)hipEventDestroy(e);
     if (staged) (void)hipEventSynchronize(staged), (void)hipEventDestroy(staged);
@@ -346,6 +346,7 @@ int vge_dwpose_profile_begin(vge_dwpose* m, int max_calls) {
   for (auto& e : m->ev) HIPCHK(hipEventCreate(&e));
   m->prof_max = max_calls;
   m->prof_calls = 0;
+  m->prof_flops = 0;
   return VGE_OK;
 }
 
@@ -360,7 +361,7 @@ int vge_dwpose_profile_read(vge_dwpose* m, double* stage_ms, int* n_calls, doubl
     stage_ms[m->ev_kind[p]] += t;
   }
   *n_calls = m->prof_calls;
-  if (gemm_flops_per_call) *gemm_flops_per_call = m->gemm_flops;
+  if (gemm_flops_per_call) *gemm_flops_per_call = m->prof_calls ? m->prof_flops / m->prof_calls : m->gemm_flops;
   return VGE_OK;
 }
 
@@ -510,7 +511,7 @@ int vge_dwpose_keypoints(vge_dwpose* m, const uint8_t* frames, int F, int H, int
 #undef OTHER
 #undef CONV
 #undef RC
-  if (prof) ++m->prof_calls;
+  if (prof) ++m->prof_calls, m->prof_flops += m->gemm_flops;
   return VGE_OK;
 }
 

@@ -252,7 +252,7 @@ int vge_yolox_profile_begin(vge_yolox* m, int max_calls) {
 int vge_yolox_profile_read(vge_yolox* m, double* stage_ms, int* n_calls, double* gemm_flops_per_call) {
   if (!m || !stage_ms || !n_calls) return fail(VGE_ERR_ARG, "vge_yolox_profile_read: bad argument");
   int rc = m->prof.read(stage_ms, 2, n_calls);
-  if (gemm_flops_per_call) *gemm_flops_per_call = m->gemm_flops;
+  if (gemm_flops_per_call) *gemm_flops_per_call = m->prof.flops_per_call(m->gemm_flops);
   return rc;
 }
 
@@ -354,7 +354,7 @@ int vge_yolox_detect_scored(vge_yolox* m, const uint8_t* frames, int F, int H, i
 #undef CSP
 #undef CONV
 #undef RC
-  m->prof.end_call();
+  m->prof.end_call(m->gemm_flops);
   return VGE_OK;
 }
 

@@ -461,3 +461,31 @@ def make_yolox_state_dict(cfg, seed: int = SEED_WEIGHTS + 30, gain: float = 1.0)
         sd[f"head.obj_preds.{k}.weight"] = N((1, hc, 1, 1), 0.01 * np.sqrt(hc))
         sd[f"head.obj_preds.{k}.bias"] = N((1,), 0.5)
     return sd
+
+
+# The e2e bench's person detector (TokenHMR's single-person gate, mesh_generator.py:103-117, and DWPose's boxes).
+# With make_yolox_state_dict's weights every synthetic frame has several person boxes above 0.5, so the gate would
+# reject every video.  These weights differ from it in the prediction biases only: the person class probability is
+# saturated (score = objectness), one common shift of the objectness logits (the anchors' ranking, hence which boxes
+# NMS keeps, is unchanged) puts the 0.5 threshold between the first and the second kept box of as many pool frames
+# as possible, and box sizes are person-like (about GATE_BOX_STRIDES strides wide).  GATE_OBJ_SHIFT is measured on
+# make_frame_pool's frames by tools/yolox_gate_calib.py on the GPU (the detector runs in bf16 there).
+GATE_OBJ_SHIFT = 0.0
+GATE_BOX_STRIDES = 12.0
+
+
+def make_gate_detector_state_dict(cfg, obj_shift: float = None, box_strides: float = GATE_BOX_STRIDES):
+    sd = make_yolox_state_dict(cfg)
+    shift = GATE_OBJ_SHIFT if obj_shift is None else obj_shift
+    for k in range(3):
+        sd[f"head.cls_preds.{k}.bias"][0] = np.float32(30.0)
+        sd[f"head.obj_preds.{k}.bias"] = (sd[f"head.obj_preds.{k}.bias"] - np.float32(shift)).astype(np.float32)
+        sd[f"head.reg_preds.{k}.bias"][2:] += np.float32(np.log(box_strides))
+    return sd
+
+
+def make_frame_pool(seed: int, n_frames: int, per_scene: int = 4, h: int = 256, w: int = 256) -> np.ndarray:
+    """uint8 RGB frames [n_frames, h, w, 3] from n_frames / per_scene independent make_frames scenes: the pool the
+    e2e bench draws its clips' frames from, by what the detector finds in each."""
+    scenes = [make_frames(seed + i, per_scene, h, w) for i in range(-(-n_frames // per_scene))]
+    return np.concatenate(scenes, 0)[:n_frames]
