@@ -271,10 +271,13 @@ def main():
     cpu = None
     if args.workload == "score" and int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_seconds)  # before the GPU is initialised: its DataLoader workers are forked
+    if args.workload == "tag" and int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.no_cpu_baseline:
+        import bench_tag
+        cpu = bench_tag.cpu_baseline()
     world, rank, dev = setup_dist()
     if args.workload == "tag":
         import bench_tag
-        out = bench_tag.run(args, world, rank, dev, METRIC)
+        out = bench_tag.run(args, world, rank, dev, METRIC, cpu)
         if rank == 0:
             print(json.dumps(out))
         if world > 1:

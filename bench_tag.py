@@ -41,7 +41,32 @@ def _dataset(rank: int, world: int):
             "gen_kp": str(root / "generated_kps"), "ckpt": str(root / "model.pt")}
 
 
-def run(args, world, rank, dev, metric):
+def cpu_baseline(workers: int = 4):
+    """oracle/evalflow.run_eval (the CPU restatement of eval.py:350-466 in the reference's structure: DataLoader
+    batch_size 32 with `workers` worker processes featurising, the torch-fp32 encoder on the process's CPU share)
+    over the same on-disk set, one whole flow, timed on this host.  Runs before the GPU is initialised (forked
+    workers); writes the dataset first if it is missing."""
+    from oracle import evalflow
+    from vge import synth
+    p = _dataset(0, 1)
+    share = max(1, min(16, len(os.sched_getaffinity(0))))
+    torch.set_num_threads(share)
+    sd = synth.make_state_dict(synth.DIMS_RAW, synth.DIMS_DIFF)
+    tm = {}
+    t0 = time.perf_counter()
+    scores, _ = evalflow.run_eval(p["real"], p["real_kp"], p["gen"], p["gen_kp"], sd, synth.DIMS_RAW, synth.DIMS_DIFF,
+                                  workers=workers, timings=tm)
+    dt = time.perf_counter() - t0
+    return {"value": len(scores) / dt, "unit": "videos/s", "cores": share, "kind": "port",
+            "sample": f"one whole flow over the same {len(scores)} generated videos ({tm.get('n_windows')} windows) + "
+                      f"{N_REAL_PER_CLASS * 10} real videos: oracle/evalflow.run_eval (npz load, stats, centroids, "
+                      f"DataLoader(batch_size=32, num_workers={workers}) featurising, torch-fp32 encoder on {share} "
+                      f"threads, AC/TC), {dt:.1f} s wall: stats {tm.get('stats_s', 0):.1f} s, centroids "
+                      f"{tm.get('centroids_s', 0):.1f} s, generated windows {tm.get('gen_extract_s', 0):.1f} s, "
+                      f"metrics {tm.get('metrics_s', 0):.2f} s"}
+
+
+def run(args, world, rank, dev, metric, cpu=None):
     from vge.dist import run_eval_distributed
     t0 = time.perf_counter()
     p = _dataset(rank, world)
@@ -93,6 +118,6 @@ def run(args, world, rank, dev, metric):
                    "videos": N_GEN, "parallelism": f"video-sharded x{world}"},
         "stage_s_last_step_rank0": {k: v for k, v in tm.items() if k.endswith("_s")},
         "setup_s": setup_s,
-        "roofline": None,
-        "cpu_baseline": None,
+        "roofline": None,   # host-bound flow (npz inflate, checkpoint read): stage_s_last_step_rank0 has the split
+        "cpu_baseline": cpu,
     }

@@ -46,7 +46,11 @@ tasks = ["stem-epi"] + [f"{k}({g})" for g in range(9) for k in ("P1", "P2", "E")
 kc = float((t[:, 0, 121] - t[:, 0, 120]).mean())
 out = {"conv_ms": conv_ms, "kernel_cycles_block": kc, "clock_ghz": kc / (conv_ms * 1e6),
        "blocks": 64, "unit_cycles": float((t[:, :, 59] - t[:, :, 0]).max(axis=1).mean()),
-       "stem_cycles": float((t[:, :, 1] - t[:, :, 0]).mean()), "phases": []}
+       "stem_cycles": float((t[:, :, 1] - t[:, :, 0]).mean()),
+       # stem parts: first panel's feats loaded + split into LDS (through the barrier), its weight stream, the rest
+       "stem_load_split": float((t[:, :, 122] - t[:, :, 0]).mean()),
+       "stem_stream0": float((t[:, :, 123] - t[:, :, 122]).mean()),
+       "stem_rest": float((t[:, :, 1] - t[:, :, 123]).mean()), "phases": []}
 for p in range(29):
     start = t[:, :, 1] if p == 0 else t[:, :, 3 + 2 * (p - 1)]
     task = t[:, :, 2 + 2 * p] - start
@@ -68,7 +72,8 @@ for k, nm in enumerate(names):
     out["epilogues"][nm] = d
 print(json.dumps(out))
 print(f"conv {conv_ms:.4f} ms, kernel {kc:.0f} cycles per block -> {kc / (conv_ms * 1e6):.3f} GHz; unit "
-      f"{out['unit_cycles']:.0f} cycles, stem {out['stem_cycles']:.0f}")
+      f"{out['unit_cycles']:.0f} cycles, stem {out['stem_cycles']:.0f} (load+split {out['stem_load_split']:.0f}, "
+      f"stream {out['stem_stream0']:.0f}, rest {out['stem_rest']:.0f})")
 for nm, d in out["epilogues"].items():
     print(f"{nm:>5s}  A compute/exchange/store {d['A']}   B {d['B']}")
 for ph in out["phases"]:

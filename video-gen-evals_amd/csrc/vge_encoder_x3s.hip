@@ -241,6 +241,7 @@ __device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, i
         }
       }
       __syncthreads();  // X and ecur complete
+      if (p == 0) XTS(122);
       if (p > 0) {
         const int* eprev = ax.rexp[(p - 1) & 1];
 #pragma unroll
@@ -250,6 +251,7 @@ __device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, i
       }
       run_stream<CONV_PF, true>(acc, reinterpret_cast<const char*>(ed.stem) + (size_t)p * 16 * CHUNK_B,
                                 ((kw + 127) >> 7) * STREAM_GROUP, loff, afn_stem);
+      if (p == 0) XTS(123);
       __syncthreads();  // every wave is done reading X
     }
   }

@@ -62,24 +62,28 @@ constexpr int QH = 36;           // f32 row stride of a wave's one-head Q / K / 
 #endif
 constexpr int TX_PF = VGE_TX_PF;  // weight chunks in flight per wave (ring depth)
 constexpr int TX_NW = 4;         // waves
-constexpr int AP_BYTES = 2 * AROWS * XSB;            // hi / lo planes of one window's A operand
+template <bool SPA>
+constexpr int ap_bytes() { return (SPA ? 2 : 1) * AROWS * XSB; }  // hi (/ lo) planes of one window's A operand
 constexpr int HEAD_BYTES = 3 * TOK * QH * 4;         // one wave's Q, K, V of one head (f32)
 constexpr int F_BYTES = TOK * QS * 4;                // one window's final embeddings (f32)
 // U (the union): the 4 waves' head staging | W windows' FFN hidden planes | W windows' final embeddings
-template <int W>
+template <int W, bool SPA>
 constexpr int tx_u_bytes() {
-  constexpr int a = TX_NW * HEAD_BYTES, b = W * AP_BYTES, c = W * F_BYTES;
+  constexpr int a = TX_NW * HEAD_BYTES, b = W * ap_bytes<SPA>(), c = W * F_BYTES;
   return a > b ? (a > c ? a : c) : (b > c ? b : c);
 }
 template <int W>
 constexpr int tx_red_floats() {  // row partials x2, block maxima x2, tc
   return 2 * W * TOK * TX_NW + 2 * W * TX_NW + W * TX_NW;
 }
-template <int W>
+template <int W, bool SPA>
 constexpr int tx_lds_bytes() {
-  return W * AP_BYTES + tx_u_bytes<W>() + tx_red_floats<W>() * 4;
+  return W * ap_bytes<SPA>() + tx_u_bytes<W, SPA>() + tx_red_floats<W>() * 4;
 }
-static_assert(tx_lds_bytes<2>() <= 160 * 1024, "LDS");
+static_assert(tx_lds_bytes<2, true>() <= 160 * 1024, "LDS");
+// single fp16 (no lo planes), one window: two workgroups fit a CU's LDS, so one's epilogues can run beside the
+// other's weight stream (OCC = 2: 256 registers per wave)
+static_assert(2 * tx_lds_bytes<1, false>() <= 160 * 1024, "LDS, two single-fp16 workgroups per CU");
 
 // CLS rows: W = 1 on the VALU (v_dot2_f32_f16 over the same B fragments, same split products), so no MFMA work is
 // spent on a mostly empty tile; W = 2 as one extra MFMA tile holding both windows' CLS rows (rows 0, 1): two windows'
@@ -120,12 +124,13 @@ __device__ __forceinline__ float cls_dot(float c, half8 xh, half8 xl, half8 wh, 
 // more windows than CUs.  A wave's Q / K / V columns are exactly its own two heads (2 wave + {0, 1}), so Q and K
 // wait in registers for V and each head's attention stages only its own Q / K / V (14 KB per wave) in LDS: the
 // windows' A planes and hidden planes (70 KB each at W = 2) then fit beside it.
-template <bool SPA, bool SPW, int W>
-__global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
+template <bool SPA, bool SPW, int W, int OCC = 1>
+__global__ void __launch_bounds__(256, OCC) transformer_x3_kernel(TxArgsX3 ta) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
+  constexpr int AP_BYTES = ap_bytes<SPA>();
   char* Ap = lds;                                   // [W] A planes: hi rows [0, AROWS), lo at + AROWS * XSB
   char* U = lds + W * AP_BYTES;                     // head staging | [W] hidden planes | [W] embeddings
-  float* red = reinterpret_cast<float*>(U + tx_u_bytes<W>());  // [2][W][TOK][4] rows, [2][W][4] maxima, [W][4] tc
+  float* red = reinterpret_cast<float*>(U + tx_u_bytes<W, SPA>());  // [2][W][TOK][4] rows, [2][W][4] maxima, [W][4] tc
   // consecutive reductions alternate between two buffers, so none needs a trailing barrier: the writes of
   // reduction k + 2 come after reduction k + 1's barrier, which every read of reduction k precedes
   int rs_buf = 0, bm_buf = 0;
@@ -291,7 +296,7 @@ __global__ void __launch_bounds__(256, 1) transformer_x3_kernel(TxArgsX3 ta) {
 #pragma unroll
   for (int v = 0; v < W; ++v) {
     reinterpret_cast<_Float16*>(Ap + v * AP_BYTES)[tid] = (_Float16)0.0f;
-    reinterpret_cast<_Float16*>(Ap + v * AP_BYTES + AROWS * XSB)[tid] = (_Float16)0.0f;
+    if constexpr (SPA) reinterpret_cast<_Float16*>(Ap + v * AP_BYTES + AROWS * XSB)[tid] = (_Float16)0.0f;
   }
   int ax[W];  // the accumulators of the current segment hold (A_v * 2^-ax[v]) W
   {
@@ -888,13 +893,18 @@ struct TxArgsX3Host {
 };
 
 hipError_t transformer_x3_kernel_setup() {
-  const void* k1[3] = {(const void*)transformer_x3_kernel<true, true, 1>, (const void*)transformer_x3_kernel<true, false, 1>,
-                       (const void*)transformer_x3_kernel<false, false, 1>};
-  const void* k2[3] = {(const void*)transformer_x3_kernel<true, true, 2>, (const void*)transformer_x3_kernel<true, false, 2>,
-                       (const void*)transformer_x3_kernel<false, false, 2>};
-  for (int j = 0; j < 3; ++j) {
-    hipError_t e = hipFuncSetAttribute(k1[j], hipFuncAttributeMaxDynamicSharedMemorySize, tx_lds_bytes<1>());
-    if (e == hipSuccess) e = hipFuncSetAttribute(k2[j], hipFuncAttributeMaxDynamicSharedMemorySize, tx_lds_bytes<2>());
+  const struct {
+    const void* k;
+    int lds;
+  } ks[7] = {{(const void*)transformer_x3_kernel<true, true, 1>, tx_lds_bytes<1, true>()},
+             {(const void*)transformer_x3_kernel<true, false, 1>, tx_lds_bytes<1, true>()},
+             {(const void*)transformer_x3_kernel<false, false, 1>, tx_lds_bytes<1, false>()},
+             {(const void*)transformer_x3_kernel<false, false, 1, 2>, tx_lds_bytes<1, false>()},
+             {(const void*)transformer_x3_kernel<true, true, 2>, tx_lds_bytes<2, true>()},
+             {(const void*)transformer_x3_kernel<true, false, 2>, tx_lds_bytes<2, true>()},
+             {(const void*)transformer_x3_kernel<false, false, 2>, tx_lds_bytes<2, false>()}};
+  for (const auto& k : ks) {
+    const hipError_t e = hipFuncSetAttribute(k.k, hipFuncAttributeMaxDynamicSharedMemorySize, k.lds);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
@@ -906,6 +916,7 @@ hipError_t transformer_x3_kernel_setup() {
 // tools/gpu_tx_modes.sh) fp16 0.71 -> 0.62 ms at 1,024 windows and 2.76 -> 2.38 ms at 4,096; split 2.35 -> 2.29 ms
 // at 2,048 but 0.89 -> 1.10 ms at 600 (round tails).  VGE_TX_W=1|2 forces it.
 static int g_tx_w_forced = -1;  // -1: not read yet, 0: automatic, 1 | 2 (VGE_TX_W, vge_debug_set_tx_windows)
+static int g_tx_occ = -1;       // single fp16, one window per workgroup: workgroups per CU (VGE_TX_OCC=1|2, default 2)
 static int tx_windows_per_block(int n_windows, int mode) {
   static int n_cu = 0;
   if (n_cu == 0) {
@@ -939,14 +950,32 @@ hipError_t launch_transformer_x3(const TxArgsX3Host& a, int mode, hipStream_t s)
   t.frame = a.frame;
   t.tc = a.tc;
   memcpy(t.layers, a.layers, sizeof(TxLayerX3) * a.n_layers);
+  if (g_tx_occ < 0) {
+    const char* v = getenv("VGE_TX_OCC");
+    g_tx_occ = (v && v[0] == '1') ? 1 : 2;
+  }
   if (tx_windows_per_block(a.n_windows, mode) == 2) {
-    auto k = mode == 2 ? transformer_x3_kernel<true, true, 2>
-                       : (mode == 1 ? transformer_x3_kernel<true, false, 2> : transformer_x3_kernel<false, false, 2>);
-    hipLaunchKernelGGL(k, dim3((a.n_windows + 1) / 2), dim3(256), tx_lds_bytes<2>(), s, t);
+    if (mode == 2)
+      hipLaunchKernelGGL((transformer_x3_kernel<true, true, 2>), dim3((a.n_windows + 1) / 2), dim3(256),
+                         (tx_lds_bytes<2, true>()), s, t);
+    else if (mode == 1)
+      hipLaunchKernelGGL((transformer_x3_kernel<true, false, 2>), dim3((a.n_windows + 1) / 2), dim3(256),
+                         (tx_lds_bytes<2, true>()), s, t);
+    else
+      hipLaunchKernelGGL((transformer_x3_kernel<false, false, 2>), dim3((a.n_windows + 1) / 2), dim3(256),
+                         (tx_lds_bytes<2, false>()), s, t);
   } else {
-    auto k = mode == 2 ? transformer_x3_kernel<true, true, 1>
-                       : (mode == 1 ? transformer_x3_kernel<true, false, 1> : transformer_x3_kernel<false, false, 1>);
-    hipLaunchKernelGGL(k, dim3(a.n_windows), dim3(256), tx_lds_bytes<1>(), s, t);
+    if (mode == 2)
+      hipLaunchKernelGGL((transformer_x3_kernel<true, true, 1>), dim3(a.n_windows), dim3(256), (tx_lds_bytes<1, true>()), s, t);
+    else if (mode == 1)
+      hipLaunchKernelGGL((transformer_x3_kernel<true, false, 1>), dim3(a.n_windows), dim3(256), (tx_lds_bytes<1, true>()), s,
+                         t);
+    else if (g_tx_occ == 2)
+      hipLaunchKernelGGL((transformer_x3_kernel<false, false, 1, 2>), dim3(a.n_windows), dim3(256),
+                         (tx_lds_bytes<1, false>()), s, t);
+    else
+      hipLaunchKernelGGL((transformer_x3_kernel<false, false, 1>), dim3(a.n_windows), dim3(256),
+                         (tx_lds_bytes<1, false>()), s, t);
   }
   return hipGetLastError();
 }

@@ -468,19 +468,20 @@ def make_yolox_state_dict(cfg, seed: int = SEED_WEIGHTS + 30, gain: float = 1.0)
 # reject every video.  These weights differ from it in the prediction biases only: the person class probability is
 # saturated (score = objectness), one common shift of the objectness logits (the anchors' ranking, hence which boxes
 # NMS keeps, is unchanged) puts the 0.5 threshold between the first and the second kept box of as many pool frames
-# as possible, and box sizes are person-like (about GATE_BOX_STRIDES strides wide).  GATE_OBJ_SHIFT is measured on
-# make_frame_pool's frames by tools/yolox_gate_calib.py on the GPU (the detector runs in bf16 there).
-GATE_OBJ_SHIFT = 0.0
-GATE_BOX_STRIDES = 12.0
+# as possible, and box sizes are person-like (about GATE_BOX_STRIDES (w, h) strides).  GATE_OBJ_SHIFT is measured on
+# make_frame_pool's frames by tools/yolox_gate_calib.py on the GPU (the detector runs in bf16 there);
+# VGE_GATE_OBJ_SHIFT overrides it for a calibration run.
+GATE_OBJ_SHIFT = float(os.environ.get("VGE_GATE_OBJ_SHIFT", "3.668"))
+GATE_BOX_STRIDES = (6.0, 60.0)
 
 
-def make_gate_detector_state_dict(cfg, obj_shift: float = None, box_strides: float = GATE_BOX_STRIDES):
+def make_gate_detector_state_dict(cfg, obj_shift: float = None, box_strides=GATE_BOX_STRIDES):
     sd = make_yolox_state_dict(cfg)
     shift = GATE_OBJ_SHIFT if obj_shift is None else obj_shift
     for k in range(3):
         sd[f"head.cls_preds.{k}.bias"][0] = np.float32(30.0)
         sd[f"head.obj_preds.{k}.bias"] = (sd[f"head.obj_preds.{k}.bias"] - np.float32(shift)).astype(np.float32)
-        sd[f"head.reg_preds.{k}.bias"][2:] += np.float32(np.log(box_strides))
+        sd[f"head.reg_preds.{k}.bias"][2:] += np.log(np.asarray(box_strides, np.float32))
     return sd
 
 
