@@ -913,11 +913,14 @@ hipError_t transformer_x3_kernel_setup() {
 // Windows per workgroup (each weight chunk a wave streams then feeds two windows' rows at W = 2).  A W = 2 workgroup
 // takes 1.7x (single fp16) / 1.9x (3xfp16 split) the time of a W = 1 one (its epilogues are per window, and the
 // split's stream turns MFMA-bound), so W = 2 pays once every CU holds several windows: measured (stage times,
-// tools/gpu_tx_modes.sh) fp16 0.71 -> 0.62 ms at 1,024 windows and 2.76 -> 2.38 ms at 4,096; split 2.35 -> 2.29 ms
-// at 2,048 but 0.89 -> 1.10 ms at 600 (round tails).  VGE_TX_W=1|2 forces it.
+// tools/gpu_tx_modes.sh) split 2.35 -> 2.29 ms at 2,048 but 0.89 -> 1.10 ms at 600 (round tails).  Single fp16 keeps
+// one window per workgroup and runs two workgroups per CU once there are more windows than CUs (76 KB of LDS each,
+// so one's epilogues run beside the other's weight stream; tools/gpu_tx_occ.sh): 0.686 -> 0.50 ms at 1,024 windows
+// and 2.67 -> 1.94 ms at 4,096 (W = 2: 0.61 / 2.39); at 256 windows the dispatcher would pair workgroups on some CUs
+// and leave others idle (0.175 -> 0.18-0.19 ms).  VGE_TX_W=1|2 and VGE_TX_OCC=1|2 force either.
 static int g_tx_w_forced = -1;  // -1: not read yet, 0: automatic, 1 | 2 (VGE_TX_W, vge_debug_set_tx_windows)
-static int g_tx_occ = -1;       // single fp16, one window per workgroup: workgroups per CU (VGE_TX_OCC=1|2, default 2)
-static int tx_windows_per_block(int n_windows, int mode) {
+static int g_tx_occ = -1;       // single fp16, one window per workgroup: -1 not read yet, 0 automatic, 1 | 2 forced
+static int tx_n_cu() {
   static int n_cu = 0;
   if (n_cu == 0) {
     int dev = 0;
@@ -925,12 +928,24 @@ static int tx_windows_per_block(int n_windows, int mode) {
         hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu < 1)
       n_cu = 256;
   }
+  return n_cu;
+}
+static int tx_windows_per_block(int n_windows, int mode) {
   if (g_tx_w_forced < 0) {
     const char* v = getenv("VGE_TX_W");
     g_tx_w_forced = (v && (v[0] == '1' || v[0] == '2')) ? v[0] - '0' : 0;
   }
   if (g_tx_w_forced) return g_tx_w_forced;
-  return n_windows >= (mode == 2 ? 8 : 4) * n_cu ? 2 : 1;
+  if (mode == 0) return 1;
+  return n_windows >= (mode == 2 ? 8 : 4) * tx_n_cu() ? 2 : 1;
+}
+static int tx_blocks_per_cu(int n_windows) {  // single fp16, W = 1
+  if (g_tx_occ < 0) {
+    const char* v = getenv("VGE_TX_OCC");
+    g_tx_occ = (v && (v[0] == '1' || v[0] == '2')) ? v[0] - '0' : 0;
+  }
+  if (g_tx_occ) return g_tx_occ;
+  return n_windows > tx_n_cu() ? 2 : 1;
 }
 
 // mode: 0 single fp16, 1 activations split (fp16 weights), 2 3xfp16
@@ -950,10 +965,6 @@ hipError_t launch_transformer_x3(const TxArgsX3Host& a, int mode, hipStream_t s)
   t.frame = a.frame;
   t.tc = a.tc;
   memcpy(t.layers, a.layers, sizeof(TxLayerX3) * a.n_layers);
-  if (g_tx_occ < 0) {
-    const char* v = getenv("VGE_TX_OCC");
-    g_tx_occ = (v && v[0] == '1') ? 1 : 2;
-  }
   if (tx_windows_per_block(a.n_windows, mode) == 2) {
     if (mode == 2)
       hipLaunchKernelGGL((transformer_x3_kernel<true, true, 2>), dim3((a.n_windows + 1) / 2), dim3(256),
@@ -970,7 +981,7 @@ hipError_t launch_transformer_x3(const TxArgsX3Host& a, int mode, hipStream_t s)
     else if (mode == 1)
       hipLaunchKernelGGL((transformer_x3_kernel<true, false, 1>), dim3(a.n_windows), dim3(256), (tx_lds_bytes<1, true>()), s,
                          t);
-    else if (g_tx_occ == 2)
+    else if (tx_blocks_per_cu(a.n_windows) == 2)
       hipLaunchKernelGGL((transformer_x3_kernel<false, false, 1, 2>), dim3(a.n_windows), dim3(256),
                          (tx_lds_bytes<1, false>()), s, t);
     else

@@ -471,7 +471,7 @@ def make_yolox_state_dict(cfg, seed: int = SEED_WEIGHTS + 30, gain: float = 1.0)
 # as possible, and box sizes are person-like (about GATE_BOX_STRIDES (w, h) strides).  GATE_OBJ_SHIFT is measured on
 # make_frame_pool's frames by tools/yolox_gate_calib.py on the GPU (the detector runs in bf16 there);
 # VGE_GATE_OBJ_SHIFT overrides it for a calibration run.
-GATE_OBJ_SHIFT = float(os.environ.get("VGE_GATE_OBJ_SHIFT", "3.668"))
+GATE_OBJ_SHIFT = float(os.environ.get("VGE_GATE_OBJ_SHIFT", "3.911"))
 GATE_BOX_STRIDES = (6.0, 60.0)
 
 
