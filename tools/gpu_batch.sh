@@ -8,5 +8,5 @@ for step in "$@"; do
   bash $step
   rc=$?
   echo "=== rc=$rc"
-  if [ $rc -ge 124 ]; then echo "stopping after rc=$rc"; exit $rc; fi
+  if [ $rc -ge 124 ] && [ $rc -ne 126 ] && [ $rc -ne 127 ]; then echo "stopping after rc=$rc"; exit $rc; fi
 done

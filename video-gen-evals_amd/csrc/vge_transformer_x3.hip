@@ -89,8 +89,11 @@ static_assert(2 * tx_lds_bytes<1, false>() <= 160 * 1024, "LDS, two single-fp16 
 // spent on a mostly empty tile; W = 2 as one extra MFMA tile holding both windows' CLS rows (rows 0, 1): two windows'
 // dot products would cost the VALU ~2x the MFMA time of the tile (8-cycle v_dot2, measured: 700 k vs 400 k stream
 // cycles per window pair)
+#ifndef VGE_TX_CLSM1
+#define VGE_TX_CLSM1 0  // 1: the CLS row on an MFMA tile at W = 1 too
+#endif
 template <int W>
-constexpr bool tx_cls_mfma() { return W >= 2; }
+constexpr bool tx_cls_mfma() { return W >= 2 || VGE_TX_CLSM1; }
 template <int W>
 struct AFragT {  // one chunk's A operands of W windows: the 32 frame rows and the CLS row(s)
   static constexpr int NC = tx_cls_mfma<W>() ? 1 : W;
