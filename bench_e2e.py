@@ -72,7 +72,7 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
     from vge.data import ACTION_CLASSES, pack_frame_store
     from vge.dist import shard
     from vge.dwpose import RTMPOSE_L, YOLOX_L, DwposeExtractor, YoloxDetector
-    from vge.extract import SINGLE_PERSON_MIN_FRACTION, single_person_mask
+    from vge.extract import gate_videos, single_person_mask
     from vge.hmr import TOKENHMR, HmrExtractor, crop_persons
 
     C, T = args.clips, 32
@@ -207,16 +207,13 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
             hb, hn, keep = detect(fr)
             # mesh_generator.py:101-117 per video: the frames with exactly one person; the video is rejected
             # (process_video returns False, no npz) when they are fewer than 80 % of its frames
-            kept = []
-            for c in range(f0 // T, (f0 + n) // T):
-                valid = np.flatnonzero(keep[c * T - f0:(c + 1) * T - f0])
-                gate["videos"] += 1
-                if valid.size == 0 or valid.size < SINGLE_PERSON_MIN_FRACTION * T:
-                    continue
-                vids[len(acc)] = (off + sum(len(k) for k in kept), valid.size, c * T, T)
-                acc.append(c)
-                kept.append(valid + (c * T - f0))
-            kept = np.concatenate(kept) if kept else np.zeros(0, np.int64)
+            c0 = f0 // T
+            va, kept, desc = gate_videos(keep, T, off)
+            gate["videos"] += n // T
+            if va.size:
+                desc[:, 2] += f0   # keypoint rows of the batch's videos sit at their frame offsets
+                vids[len(acc):len(acc) + va.size] = desc
+                acc.extend((va + c0).tolist())
             if concurrent:
                 cur = torch.cuda.current_stream(dev)
                 s_hmr.wait_stream(cur)

@@ -49,6 +49,30 @@ def test_single_person_gate():
 
 
 @pytest.mark.gpu
+def test_gate_videos_compacts_kept_frames():
+    """vge.extract.gate_videos (the e2e bench's per-pass gate): accepted videos, their kept frames and frame-store
+    descriptors, video by video the same decision as single_person_frames (mesh_generator.py:101-117)."""
+    from vge.extract import gate_videos, single_person_frames
+    T = 10
+    rng = np.random.default_rng(3)
+    keep = np.ones(5 * T, bool)
+    keep[T + 2] = keep[T + 7] = False                    # video 1: 8 / 10 kept (accepted)
+    keep[2 * T:2 * T + 3] = False                        # video 2: 7 / 10 (rejected)
+    keep[3 * T:4 * T] = False                            # video 3: none (rejected)
+    keep[4 * T + 9] = False                              # video 4: 9 / 10
+    acc, kept, desc = gate_videos(keep, T, frame_off=100)
+    assert acc.tolist() == [0, 1, 4]
+    want = [v * T + f for v in (0, 1, 4) for f in single_person_frames(np.where(keep[v * T:(v + 1) * T], 1, 0))]
+    assert kept.tolist() == want
+    assert desc.tolist() == [[100, 10, 0, T], [110, 8, T, T], [118, 9, 4 * T, T]]
+    # every decision matches the per-video rule on random masks
+    for _ in range(20):
+        k = rng.random(6 * T) < 0.85
+        acc, kept, desc = gate_videos(k, T)
+        ref = [v for v in range(6) if single_person_frames(np.where(k[v * T:(v + 1) * T], 1, 0)) is not None]
+        assert acc.tolist() == ref and int(desc[:, 1].sum()) == kept.size
+
+
 def test_extract_video_round_trip(tmp_path):
     if not torch.cuda.is_available():
         pytest.skip("no GPU")

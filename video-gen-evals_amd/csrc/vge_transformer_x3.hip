@@ -90,7 +90,7 @@ static_assert(2 * tx_lds_bytes<1, false>() <= 160 * 1024, "LDS, two single-fp16 
 // dot products would cost the VALU ~2x the MFMA time of the tile (8-cycle v_dot2, measured: 700 k vs 400 k stream
 // cycles per window pair)
 #ifndef VGE_TX_CLSM1
-#define VGE_TX_CLSM1 0  // 1: the CLS row on an MFMA tile at W = 1 too
+#define VGE_TX_CLSM1 0  // 1: the CLS row on an MFMA tile at W = 1 too (measured: 0.303 -> 0.325 ms at 256 windows)
 #endif
 template <int W>
 constexpr bool tx_cls_mfma() { return W >= 2 || VGE_TX_CLSM1; }
@@ -100,24 +100,36 @@ struct AFragT {  // one chunk's A operands of W windows: the 32 frame rows and t
   half8 h[W], l[W], h0[NC], l0[NC];
 };
 
-// CLS row on the VALU: c += x . w over this lane's 8 k of the chunk, the same 3 products as the MFMAs
+// CLS row on the VALU: c += x . w over this lane's 8 k of the chunk, the same 3 products as the MFMAs, in TX_CLS_NC
+// independent partial sums (k pairs p -> sum p % NC): dependent v_dot2 chains of 12 / NC instead of 12, so the dots
+// of a chunk finish while its MFMAs run
+#ifndef VGE_TX_CLS_NC
+#define VGE_TX_CLS_NC 1
+#endif
+constexpr int TX_CLS_NC = VGE_TX_CLS_NC;
 template <bool SPA, bool SPW>
-__device__ __forceinline__ float cls_dot(float c, half8 xh, half8 xl, half8 wh, half8 wl) {
+__device__ __forceinline__ void cls_dot(float (&c)[TX_CLS_NC], half8 xh, half8 xl, half8 wh, half8 wl) {
 #pragma unroll
   for (int p = 0; p < 4; ++p) {
+    float& cp = c[p % TX_CLS_NC];
     const half2v a = {xh[2 * p], xh[2 * p + 1]};
     const half2v b = {wh[2 * p], wh[2 * p + 1]};
     if constexpr (SPA) {
       const half2v al = {xl[2 * p], xl[2 * p + 1]};
-      c = __builtin_amdgcn_fdot2(al, b, c, false);
+      cp = __builtin_amdgcn_fdot2(al, b, cp, false);
     }
     if constexpr (SPW) {
       const half2v bl = {wl[2 * p], wl[2 * p + 1]};
-      c = __builtin_amdgcn_fdot2(a, bl, c, false);
+      cp = __builtin_amdgcn_fdot2(a, bl, cp, false);
     }
-    c = __builtin_amdgcn_fdot2(a, b, c, false);
+    cp = __builtin_amdgcn_fdot2(a, b, cp, false);
   }
-  return c;
+}
+__device__ __forceinline__ float cls_total(const float (&c)[TX_CLS_NC]) {
+  float t = c[0];
+#pragma unroll
+  for (int k = 1; k < TX_CLS_NC; ++k) t += c[k];
+  return t;
 }
 
 // SPA / SPW: activations / weights carried as hi + lo fp16 planes.  Both: 3xfp16 (VGE_F32X3, hi*hi + hi*lo +
@@ -356,7 +368,7 @@ __global__ void __launch_bounds__(256, OCC) transformer_x3_kernel(TxArgsX3 ta) {
 
   Acc<1, 2> acc[W], acc2[W];  // acc: the segment's accumulators; acc2: the FFN2 sum across its K panels
   constexpr bool CLSM = tx_cls_mfma<W>();
-  float c0[W][2], c02[W][2];  // the CLS row's partial sums (this lane's half of the k) | the linear2 sum (CLSM)
+  float c0[W][2][TX_CLS_NC], c02[W][2];  // the CLS row's partial sums (this lane's half of the k) | the linear2 sum
   Acc<1, 2> accc;             // CLSM: the CLS tile (row v = window v's CLS row)
   accc.zero();
   float X[W][2][16], x0[W][2];  // the layer input / residual: token rows trow(r), CLS
@@ -364,7 +376,9 @@ __global__ void __launch_bounds__(256, OCC) transformer_x3_kernel(TxArgsX3 ta) {
   for (int v = 0; v < W; ++v) {
     acc[v].zero();
 #pragma unroll
-    for (int n = 0; n < 2; ++n) c0[v][n] = 0.f;
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int k = 0; k < TX_CLS_NC; ++k) c0[v][n][k] = 0.f;
   }
 
   // the token epilogue's constants, loaded before the first weight loads (see the epilogue parameters below)
@@ -460,7 +474,7 @@ __global__ void __launch_bounds__(256, OCC) transformer_x3_kernel(TxArgsX3 ta) {
           asm volatile("" ::"v"(f.h[v]), "v"(f.l[v]), "v"(bb.h[n]), "v"(bb.l[n]));
 #endif
 #if !(VGE_ABL & 64)
-          if constexpr (!CLSM) c0[v][n] = cls_dot<SPA, SPW>(c0[v][n], f.h0[v], f.l0[v], bb.h[n], bb.l[n]);
+          if constexpr (!CLSM) cls_dot<SPA, SPW>(c0[v][n], f.h0[v], f.l0[v], bb.h[n], bb.l[n]);
 #endif
         }
       if constexpr (CLSM) {
@@ -475,7 +489,9 @@ __global__ void __launch_bounds__(256, OCC) transformer_x3_kernel(TxArgsX3 ta) {
       } else {
         // the CLS dot products stay in their step (else they are sunk past the loop and the ring stays live)
 #pragma unroll
-        for (int v = 0; v < W; ++v) asm volatile("" : "+v"(c0[v][0]), "+v"(c0[v][1]));
+        for (int v = 0; v < W; ++v)
+#pragma unroll
+          for (int k = 0; k < TX_CLS_NC; ++k) asm volatile("" : "+v"(c0[v][0][k]), "+v"(c0[v][1][k]));
       }
       asm volatile("" ::: "memory");
       __builtin_amdgcn_sched_barrier(0);
@@ -494,8 +510,9 @@ __global__ void __launch_bounds__(256, OCC) transformer_x3_kernel(TxArgsX3 ta) {
         if constexpr (CLSM) {
           cl[v][n] = halves_sum(accc.c[0][n][v]);  // row v: register v of the h = 0 lanes (h = 1 holds row 4 + v = 0)
         } else {
-          cl[v][n] = halves_sum(c0[v][n]);
-          c0[v][n] = 0.f;
+          cl[v][n] = halves_sum(cls_total(c0[v][n]));
+#pragma unroll
+          for (int k = 0; k < TX_CLS_NC; ++k) c0[v][n][k] = 0.f;
         }
       }
     }
@@ -756,7 +773,7 @@ __global__ void __launch_bounds__(256, OCC) transformer_x3_kernel(TxArgsX3 ta) {
           acc[v] = acc2[v];
           if constexpr (!CLSM) {
 #pragma unroll
-            for (int n = 0; n < 2; ++n) c0[v][n] = (h == 0) ? c02[v][n] : 0.f;  // c02: both k halves, one carries it
+            for (int n = 0; n < 2; ++n) c0[v][n][0] = (h == 0) ? c02[v][n] : 0.f;  // c02: both k halves, one carries it
           }
         }
       }

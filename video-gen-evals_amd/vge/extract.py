@@ -61,6 +61,28 @@ def single_person_frames(person_counts: Sequence[int]) -> Optional[np.ndarray]:
     return valid
 
 
+def gate_videos(keep: np.ndarray, frames_per_video: int, frame_off: int = 0):
+    """mesh_generator.py:101-117 over a batch of equal-length videos laid out back to back: keep [n_videos * T] per-frame
+    single-person flags -> (accepted video indices, kept frame indices into the batch, descriptor rows
+    {frame_off, n_frames, kp_off, kp_frames} of the accepted videos' frame-store entries: the npz holds the kept frames
+    only (compacted from `frame_off` on, extract_mesh.py:35-43), keypoints.npy every frame (process_video.py))."""
+    keep = np.asarray(keep, bool)
+    T = int(frames_per_video)
+    nv = keep.size // T
+    acc, kept, desc = [], [], []
+    off = int(frame_off)
+    for v in range(nv):
+        valid = single_person_frames(np.where(keep[v * T:(v + 1) * T], 1, 0))
+        if valid is None:
+            continue
+        acc.append(v)
+        kept.append(valid + v * T)
+        desc.append((off, valid.size, v * T, T))
+        off += valid.size
+    kept_idx = np.concatenate(kept) if kept else np.zeros(0, np.int64)
+    return np.asarray(acc, np.int64), kept_idx, np.asarray(desc, np.int32).reshape(-1, 4)
+
+
 def single_person_mask(scores) -> np.ndarray:
     """mesh_generator.py:103-111 per frame: exactly one person box with score > 0.5.  `scores` [F, 2] are the scores
     of the first two boxes the detector's greedy NMS keeps (vge_yolox_detect_scored), so a frame has one such box
