@@ -61,13 +61,41 @@ namespace {
 #define X3S_PRIO 1  // s_setprio 1 for the streaming half
 #endif
 constexpr int X3S_WMAX = 4;     // windows per unit (quads; pairs fill the remainder)
+#ifndef X3S_SKIP
+#define X3S_SKIP 1  // 1: a row tile skips the taps that put all its frames outside the window (dilated convs)
+#endif
 // Activation rows in LDS interleave the planes: [hi 256 + 8 pad | lo 256 + 8 pad | 8 pad] fp16 = 1,072 B, so one row
-// base addresses both planes with immediate offsets (lo at +528 B) and the ds_read_b128 fragment reads of 32
-// consecutive rows stay conflict-free (row r starts at bank 12 r mod 64).
+// base addresses both planes with immediate offsets (lo at +528 B).  A unit's windows are 32-row blocks WSB bytes
+// apart, and an MFMA row tile is a row GROUP across the windows: tile t of a quad = frames 8t..8t+7 of all four
+// windows (MFMA row i = window i / 8, frame 8t + i % 8), of a pair = frames 16t..16t+15 of both.  A dilated tap that
+// puts all of a tile's frames outside the window then contributes exact zeros to the whole tile, and the tile skips
+// it: of a block's 5 taps x 4 tiles, dilation 8 keeps 14, dilation 4 keeps 18 (quads; pairs: 8 of 10 at dilation 8).
+// The quads' 128-B block padding keeps the ds_read_b128 lane groups, which mix rows of all four windows, on distinct
+// banks (pairs: none needed).
 constexpr int XR = 536;                         // fp16 per row
 constexpr int XRB = 2 * XR;                     // bytes per row
 constexpr int XLO = 528;                        // byte offset of the lo plane in a row
-constexpr int X3S_AUX_OFF = (32 * X3S_WMAX + 1) * XRB;  // fixed LDS offset of the auxiliary area
+template <int W>
+constexpr int x3s_g() { return 32 / W; }        // frames of each window in one row tile
+template <int W>
+constexpr int x3s_wsb() { return 32 * XRB + (W >= 4 ? 128 : 0); }  // bytes per window block
+template <int W>
+constexpr int x3s_zr() { return W * x3s_wsb<W>(); }  // byte offset of the all-zero row (out-of-window taps)
+// C-layout register r of a lane (h = lane / 32) holds row rho = (r & 3) + 8 (r >> 2) + 4 h of its tile: window
+// rho / G, frame G t + rho % G; the h part (4 h) never crosses a window, so a register's window is r's alone
+template <int W>
+__host__ __device__ constexpr int x3s_rwin(int r) { return ((r & 3) + 8 * (r >> 2)) / x3s_g<W>(); }
+template <int W>
+__host__ __device__ constexpr int x3s_rfr0(int t, int r) {  // frame without the lane's 4 h
+  return x3s_g<W>() * t + ((r & 3) + 8 * (r >> 2)) % x3s_g<W>();
+}
+// does row tile t (frames G t .. G t + G - 1) see any in-window frame through tap offset o
+template <int W>
+__device__ __forceinline__ bool x3s_tap_ok(int t, int o) {
+  constexpr int G = x3s_g<W>();
+  return !X3S_SKIP || (G * t + G - 1 + o >= 0 && G * t + o <= 31);
+}
+constexpr int X3S_AUX_OFF = (x3s_zr<X3S_WMAX>() + XRB + 15) / 16 * 16;  // fixed LDS offset of the auxiliary area
 
 struct X3sAux {
   int rexp[2][32 * X3S_WMAX];       // stem row exponents, by panel parity
@@ -85,15 +113,19 @@ static_assert(X3S_AUX_OFF % 16 == 0, "aux alignment");
 // other tiles' MFMAs).  Addresses are formed once per tap -- LDS row bases (the zero row for taps outside the window)
 // plus immediate chunk offsets, uniform weight pointers plus the lane's offset -- so the stream issues almost no VALU
 // work besides its MFMAs (its partner wave's epilogue shares the SIMD's issue slots).
-template <int R, int ROWS>
-__device__ __forceinline__ void stream_part(Acc<R, 1>& acc, const char* wb, int ntap, unsigned loff, const char* xa,
+template <int W>
+__device__ __forceinline__ void stream_part(Acc<W, 1>& acc, const char* wb, int ntap, unsigned loff, const char* xa,
                                             int i, int dil, int ctr) {
+  constexpr int R = W, G = x3s_g<W>();
   // chunks in flight: a pair's chunk is only 6 MFMAs (192 cycles) -- 3 chunks ahead would not cover the weight
   // stream's L2 latency while one wave per SIMD streams -- and it has the registers for 7
   constexpr int PF = R >= 4 ? 4 : 8;
+  const char* xw = xa + (i / G) * x3s_wsb<W>();  // this lane's MFMA row: its window's block ...
+  const int fi = i % G;                          // ... and its frame within the tile's group
+  const char* xz = xa + x3s_zr<W>();
   auto rowp = [&](int k, int t) -> const char* {
-    const int tt = i + (k - ctr) * dil;
-    return xa + ((unsigned)tt < 32u ? t * 32 + tt : ROWS) * XRB;
+    const int tt = G * t + fi + (k - ctr) * dil;
+    return (unsigned)tt < 32u ? xw + tt * XRB : xz;
   };
   // weights through a buffer resource: the chunk offset in an SGPR, the lane's offset (+ the lo plane) in VGPRs
   const __amdgpu_buffer_rsrc_t rs =
@@ -109,18 +141,26 @@ __device__ __forceinline__ void stream_part(Acc<R, 1>& acc, const char* wb, int 
   for (int j = 0; j < PF - 1; ++j) ldb(0, j, b[j]);
   half8 ah[R], al[R];
   const char* pt[R];
+  bool okc[R];  // tile t takes part in the current tap (uniform)
 #pragma unroll
   for (int t = 0; t < R; ++t) {
     pt[t] = rowp(0, t);
-    ah[t] = *reinterpret_cast<const half8*>(pt[t]);
-    al[t] = *reinterpret_cast<const half8*>(pt[t] + XLO);
+    okc[t] = x3s_tap_ok<W>(t, -ctr * dil);
+    if (okc[t]) {
+      ah[t] = *reinterpret_cast<const half8*>(pt[t]);
+      al[t] = *reinterpret_cast<const half8*>(pt[t] + XLO);
+    }
   }
   for (int k = 0; k < ntap; ++k) {
     const bool more = k + 1 < ntap;
     const int kn = more ? k + 1 : k;
     const char* pn[R];
+    bool okn[R];
 #pragma unroll
-    for (int t = 0; t < R; ++t) pn[t] = rowp(kn, t);
+    for (int t = 0; t < R; ++t) {
+      pn[t] = rowp(kn, t);
+      okn[t] = x3s_tap_ok<W>(t, (kn - ctr) * dil);
+    }
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
 #if !(VGE_ABL & 2)
@@ -130,21 +170,28 @@ __device__ __forceinline__ void stream_part(Acc<R, 1>& acc, const char* wb, int 
 #pragma unroll
       for (int t = 0; t < R; ++t) {
 #if !(VGE_ABL & 1)
-        acc.c[t][0] = mfma32(ah[t], b[j % PF].h[0], acc.c[t][0]);
-        acc.c[t][0] = mfma32(ah[t], b[j % PF].l[0], acc.c[t][0]);
-        acc.c[t][0] = mfma32(al[t], b[j % PF].h[0], acc.c[t][0]);
+        if (okc[t]) {
+          acc.c[t][0] = mfma32(ah[t], b[j % PF].h[0], acc.c[t][0]);
+          acc.c[t][0] = mfma32(ah[t], b[j % PF].l[0], acc.c[t][0]);
+          acc.c[t][0] = mfma32(al[t], b[j % PF].h[0], acc.c[t][0]);
+        }
 #endif
 #if !(VGE_ABL & 4)
-        const char* q = j < 7 ? pt[t] + (j + 1) * 32 : pn[t];
-        ah[t] = *reinterpret_cast<const half8*>(q);
-        al[t] = *reinterpret_cast<const half8*>(q + XLO);
+        if (j < 7 ? okc[t] : okn[t]) {
+          const char* q = j < 7 ? pt[t] + (j + 1) * 32 : pn[t];
+          ah[t] = *reinterpret_cast<const half8*>(q);
+          al[t] = *reinterpret_cast<const half8*>(q + XLO);
+        }
 #endif
         __builtin_amdgcn_sched_barrier(0);  // tile by tile: the next fragments reuse this tile's registers
       }
       asm volatile("" ::: "memory");
     }
 #pragma unroll
-    for (int t = 0; t < R; ++t) pt[t] = pn[t];
+    for (int t = 0; t < R; ++t) {
+      pt[t] = pn[t];
+      okc[t] = okn[t];
+    }
   }
 }
 
@@ -157,8 +204,9 @@ template <int W>
 __device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, int n_windows, int win0,
                                               const EncDescX3& ed, int e, float* __restrict__ enc_out, char* lds_raw,
                                               int& n_ex, [[maybe_unused]] bool tr_on) {
-  constexpr int R = W, ROWS = 32 * W;
-  _Float16* X = reinterpret_cast<_Float16*>(lds_raw);  // [XROWS][XR]: hi at +0, lo at +XLO bytes
+  constexpr int R = W, G = x3s_g<W>(), WSB = x3s_wsb<W>();
+  _Float16* X = reinterpret_cast<_Float16*>(lds_raw);  // W blocks of 32 rows of XR (hi at +0, lo at +XLO bytes), zero row
+  char* Xb = lds_raw;
   X3sAux& ax = *reinterpret_cast<X3sAux*>(lds_raw + X3S_AUX_OFF);
 
   const int tid = threadIdx.x;
@@ -180,18 +228,22 @@ __device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, i
     xa = reinterpret_cast<const char*>(X) + h * 16;        // its 8 k-values of a 16-K chunk column
   };
   lane_setup();
-  auto crow = [&](int t, int r) { return t * 32 + (r & 3) + 8 * (r >> 2) + 4 * h; };  // C-layout row
+  // logical row (window * 32 + frame) of C-layout register r of tile t (the rexp index)
+  auto crow = [&](int t, int r) { return x3s_rwin<W>(r) * 32 + x3s_rfr0<W>(t, r) + 4 * h; };
+  // LDS byte offset of that row, without the lane's 4 h rows (compile-time for static t, r)
+  auto cofs = [&](int t, int r) { return x3s_rwin<W>(r) * WSB + x3s_rfr0<W>(t, r) * XRB; };
 
   Acc<R, 1> acc;
   floatx16 res[R];
-  for (int c = tid; c < XR; c += 512) X[ROWS * XR + c] = (_Float16)0.0f;  // the zero row (out-of-window taps)
+  for (int c = tid; c < XR; c += 512)  // the zero row (out-of-window taps)
+    *reinterpret_cast<_Float16*>(Xb + x3s_zr<W>() + 2 * c) = (_Float16)0.0f;
 
   // ---------------- stem: Conv1d(d_in -> 256, k=1, no bias), both halves together (conv_encoder_body's staging:
   // per-row power-of-two exponents, K in 256-wide panels)
   auto afn_stem = [&](int c, AFrag<R>& f) {
 #pragma unroll
-    for (int t = 0; t < R; ++t) {
-      const char* q = xa + (t * 32 + i) * XRB + c * 32;
+    for (int t = 0; t < R; ++t) {  // MFMA row i of tile t: window i / G, frame G t + i % G
+      const char* q = xa + (i / G) * WSB + (G * t + i % G) * XRB + c * 32;
       f.h[t] = *reinterpret_cast<const half8*>(q);
       f.l[t] = *reinterpret_cast<const half8*>(q + XLO);
     }
@@ -232,12 +284,13 @@ __device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, i
         float m = fmaxf(fmaxf(fabsf(a[q][jr][0]), fabsf(a[q][jr][1])), fmaxf(fabsf(a[q][jr][2]), fabsf(a[q][jr][3])));
         m = wave_max_all(m);
         const int ex = fp16_range_exp(m);
-        const int r = wave * RPW + jr;
+        const int r = wave * RPW + jr;  // logical row: window r / 32, frame r % 32
         if (lane == 0) ecur[r] = ex;
+        _Float16* xr = reinterpret_cast<_Float16*>(Xb + (r >> 5) * WSB + (r & 31) * XRB);
 #pragma unroll
         for (int jc = 0; jc < 4; ++jc) {
           const int c = lane + 64 * jc;
-          split_store(X + r * XR + c, X + r * XR + XLO / 2 + c, ldexpf(a[q][jr][jc], -ex));
+          split_store(xr + c, xr + XLO / 2 + c, ldexpf(a[q][jr][jc], -ex));
         }
       }
       __syncthreads();  // X and ecur complete
@@ -281,41 +334,41 @@ __device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, i
       m[t] = fmaxf(fmaxf(ax.mx[par][grp][t][0], ax.mx[par][grp][t][1]),
                    fmaxf(ax.mx[par][grp][t][2], ax.mx[par][grp][t][3]));
   };
-  // Store this wave's columns of the next GEMM's input (v = the accumulators or the residuals), window t scaled by
-  // 2^-ex[t] with the group's largest |value| in [2^8, 2^9) (exact), and publish the exponents for parity `par`.  Two
-  // rows per packed conversion, row r of a tile at an immediate offset of ds_write_b16.
+  // Store this wave's columns of the next GEMM's input (v = the accumulators or the residuals), window v scaled by
+  // 2^-ex[v] with the group's largest |value| in [2^8, 2^9) (exact), and publish the exponents for parity `par`.  Row
+  // of register r of tile t at an immediate offset of ds_write_b16.
   [[maybe_unused]] int tslot = 64;  // trace: epilogue stamp base (64 + 4 * epilogue index)
   auto store_act = [&](auto get, int par) {
     XTS(tslot + 1);
     float m[R];
 #pragma unroll
-    for (int t = 0; t < R; ++t) {
-      const floatx16& v = get(t);
-      float a = fmaxf(fabsf(v[0]), fabsf(v[1])), b = fmaxf(fabsf(v[2]), fabsf(v[3]));
+    for (int v = 0; v < R; ++v) m[v] = 0.f;
 #pragma unroll
-      for (int r = 4; r < 16; r += 2) {
-        a = fmaxf(a, fabsf(v[r]));
-        b = fmaxf(b, fabsf(v[r + 1]));
-      }
-      m[t] = fmaxf(a, b);
+    for (int t = 0; t < R; ++t) {
+      const floatx16& x = get(t);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) m[x3s_rwin<W>(r)] = fmaxf(m[x3s_rwin<W>(r)], fabsf(x[r]));
     }
     group_max(m);
     XTS(tslot + 2);
+    float scv[R];
+#pragma unroll
+    for (int v = 0; v < R; ++v) {
+      const int ex = fp16_range_exp(m[v]);
+      if (wg == 0 && lane == 0) ax.ex[par][grp][v] = ex;
+      scv[v] = ldexpf(1.0f, -ex);
+    }
+    char* bh = Xb + (4 * h * XR + col) * 2;
 #pragma unroll
     for (int t = 0; t < R; ++t) {
-      const floatx16& v = get(t);
-      const int ex = fp16_range_exp(m[t]);
-      if (wg == 0 && lane == 0) ax.ex[par][grp][t] = ex;
-      const float sc = ldexpf(1.0f, -ex);
-      char* bh = reinterpret_cast<char*>(X) + ((t * 32 + 4 * h) * XR + col) * 2;
-      char* bl = bh + XLO;
+      const floatx16& x = get(t);
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        const float y = v[r] * sc;
+        const float y = x[r] * scv[x3s_rwin<W>(r)];
         const _Float16 hi = (_Float16)y;
-        const int off = ((r & 3) + 8 * (r >> 2)) * XRB;
+        const int off = cofs(t, r);
         *reinterpret_cast<_Float16*>(bh + off) = hi;
-        *reinterpret_cast<_Float16*>(bl + off) = (_Float16)(y - (float)hi);
+        *reinterpret_cast<_Float16*>(bh + XLO + off) = (_Float16)(y - (float)hi);
       }
     }
     XTS(tslot + 3);
@@ -395,63 +448,75 @@ __device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, i
     XTS(tslot);
     const int par = gi & 1, blk = gi >> 1;
     const float wcs = pre_wcs;
+    float scv[R];  // per window: the accumulators' exponent x the column scale
+#pragma unroll
+    for (int v = 0; v < R; ++v) scv[v] = ldexpf(1.0f, ax.ex[par][1][v]) * wcs;
     if constexpr (KIND == 2) {
       // proj(GN_3(x)) = rstd (P gamma x - mu S_gamma) + S_beta; rows past n_windows are not written
       const float2 sp = {pre_sx, pre_sy};
+      float* ob = enc_out + (size_t)e * n_windows * VGE_T * VGE_D + col;
 #pragma unroll
-      for (int t = 0; t < R; ++t) {
+      for (int v = 0; v < R; ++v) {  // window by window: its statistics live only while its rows are written
         float mu, rstd;
-        gn_stats(3, t, mu, rstd);
-        const float sc = ldexpf(1.0f, ax.ex[par][1][t]) * wcs, off = -mu * sp.x;
-        const int win = win0 + t;
+        gn_stats(3, v, mu, rstd);
+        const int win = win0 + v;
         if (win < n_windows) {
-          float* o = enc_out + ((size_t)e * n_windows * VGE_T + (size_t)win * VGE_T) * VGE_D + col;
 #pragma unroll
-          for (int r = 0; r < 16; ++r) o[crow(0, r) * VGE_D] = fmaf(rstd, fmaf(acc.c[t][0][r], sc, off), sp.y);
+          for (int t = 0; t < R; ++t)
+#pragma unroll
+            for (int r = 0; r < 16; ++r)
+              if (x3s_rwin<W>(r) == v)
+                ob[((size_t)win * VGE_T + x3s_rfr0<W>(t, r) + 4 * h) * VGE_D] =
+                    fmaf(rstd, fmaf(acc.c[t][0][r], scv[v], -mu * sp.x), sp.y);
         }
       }
     } else {
-      float cg[16], cb[16];  // K0, blocks 1..3: this lane's rows' corrections (the taps of the row inside the window)
+      // K0, blocks 1..3: the corrections of this lane's frames (the taps of the frame inside the window); a lane's
+      // frame depends on (t, r % (G / 2)) only: 16 values, as when a tile was one window
+      constexpr int GH = G / 2;
+      float cg[16], cb[16], gsv[R], gshv[R], muv[R], rstdv[R];
       if constexpr (KIND == 0) {
         if (blk > 0) {
           const int dil = 1 << blk;
 #pragma unroll
-          for (int r = 0; r < 16; ++r) {
-            const int row = crow(0, r);  // row + (tap - 2) dil in [0, 32)
+          for (int f = 0; f < 16; ++f) {
+            const int row = x3s_rfr0<W>(f / GH, f % GH) + 4 * h;  // row + (tap - 2) dil in [0, 32)
             const bool k0 = row >= 2 * dil, k1 = row >= dil, k3 = row < 32 - dil, k4 = row < 32 - 2 * dil;
-            cg[r] = (((k0 ? pre_g.x : 0.f) + (k1 ? pre_g.y : 0.f)) + pre_g.z) + (k3 ? pre_g.w : 0.f) + (k4 ? pre_g4 : 0.f);
-            cb[r] = (((k0 ? pre_b.x : 0.f) + (k1 ? pre_b.y : 0.f)) + pre_b.z) + (k3 ? pre_b.w : 0.f) + (k4 ? pre_b4 : 0.f);
+            cg[f] = (((k0 ? pre_g.x : 0.f) + (k1 ? pre_g.y : 0.f)) + pre_g.z) + (k3 ? pre_g.w : 0.f) + (k4 ? pre_g4 : 0.f);
+            cb[f] = (((k0 ? pre_b.x : 0.f) + (k1 ? pre_b.y : 0.f)) + pre_b.z) + (k3 ? pre_b.w : 0.f) + (k4 ? pre_b4 : 0.f);
+          }
+#pragma unroll
+          for (int v = 0; v < R; ++v) {
+            gn_stats(blk - 1, v, muv[v], rstdv[v]);
+            gsv[v] = rstdv[v] * pre_gw;
+            gshv[v] = fmaf(-muv[v], gsv[v], pre_gb);
           }
         }
       }
 #pragma unroll
       for (int t = 0; t < R; ++t) {
-        const float sc = ldexpf(1.0f, ax.ex[par][1][t]) * wcs;
-        floatx16& v = acc.c[t][0];
+        floatx16& x = acc.c[t][0];
         if constexpr (KIND == 0) {
           // GELU(conv1(block input)); for blocks 1..3 the input is GN_{blk-1}(x), folded (file comment), and the
           // residual becomes GN_{blk-1}(x) here
           if (blk > 0) {
-            float mu, rstd;
-            gn_stats(blk - 1, t, mu, rstd);
-            const float gs = rstd * pre_gw;
-            const float gsh = fmaf(-mu, gs, pre_gb);
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-              res[t][r] = fmaf(res[t][r], gs, gsh);  // (x - mu) rstd gamma + beta, as conv_encoder_body
-              v[r] = fmaf(rstd, fmaf(-mu, cg[r], v[r] * sc), cb[r]);
+              const int v = x3s_rwin<W>(r), f = t * GH + r % GH;
+              res[t][r] = fmaf(res[t][r], gsv[v], gshv[v]);  // (x - mu) rstd gamma + beta, as conv_encoder_body
+              x[r] = fmaf(rstdv[v], fmaf(-muv[v], cg[f], x[r] * scv[v]), cb[f]);
             }
           } else {
 #pragma unroll
-            for (int r = 0; r < 16; ++r) v[r] *= sc;  // (the stem output needs no correction)
+            for (int r = 0; r < 16; ++r) x[r] *= scv[x3s_rwin<W>(r)];  // (the stem output needs no correction)
           }
-          gelu_tile(v);
+          gelu_tile(x);
         } else {
           // x = GELU(conv2(h) + residual): stored pre-GroupNorm, kept as the residual, partial statistics published
 #pragma unroll
-          for (int r = 0; r < 16; ++r) v[r] = fmaf(v[r], sc, res[t][r]);
-          gelu_tile(v);
-          res[t] = v;
+          for (int r = 0; r < 16; ++r) x[r] = fmaf(x[r], scv[x3s_rwin<W>(r)], res[t][r]);
+          gelu_tile(x);
+          res[t] = x;
         }
         __builtin_amdgcn_sched_barrier(0);  // one tile's temporaries at a time
       }
@@ -459,31 +524,31 @@ __device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, i
         // per-wave GroupNorm partials of every window: mean, then M2 about it (two-pass, in registers)
         float mw[R], q[R];
 #pragma unroll
-        for (int t = 0; t < R; ++t) {
-          float s = 0.f;
+        for (int v = 0; v < R; ++v) mw[v] = q[v] = 0.f;
 #pragma unroll
-          for (int r = 0; r < 16; ++r) s += res[t][r];
-          mw[t] = wave_sum_last(s);
+        for (int t = 0; t < R; ++t)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) mw[x3s_rwin<W>(r)] += res[t][r];
+#pragma unroll
+        for (int v = 0; v < R; ++v) {
+          mw[v] = wave_sum_last(mw[v]);
+          mw[v] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mw[v]), 63)) *
+                  (1.0f / 1024.0f);
         }
 #pragma unroll
-        for (int t = 0; t < R; ++t) {
-          mw[t] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, mw[t]), 63)) *
-                  (1.0f / 1024.0f);
-          float a = 0.f;
+        for (int t = 0; t < R; ++t)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const float d = res[t][r] - mw[t];
-            a = fmaf(d, d, a);
+            const float d = res[t][r] - mw[x3s_rwin<W>(r)];
+            q[x3s_rwin<W>(r)] = fmaf(d, d, q[x3s_rwin<W>(r)]);
           }
-          q[t] = a;
-        }
 #pragma unroll
-        for (int t = 0; t < R; ++t) q[t] = wave_sum_last(q[t]);
+        for (int v = 0; v < R; ++v) q[v] = wave_sum_last(q[v]);
         if (lane == 63) {
 #pragma unroll
-          for (int t = 0; t < R; ++t) {
-            ax.stats[blk & 1][t][wave][0] = mw[t];
-            ax.stats[blk & 1][t][wave][1] = q[t];
+          for (int v = 0; v < R; ++v) {
+            ax.stats[blk & 1][v][wave][0] = mw[v];
+            ax.stats[blk & 1][v][wave][1] = q[v];
           }
         }
       }
@@ -494,19 +559,20 @@ __device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, i
   auto stream = [&](int gi, int part) {
     if (part == 0) {
       acc.zero();
-    } else {  // channels of B: the accumulators move from A's exponent to B's (exact)
+    } else {  // channels of B: the accumulators move from A's exponent to B's (exact), window by window
+      float f[R];
 #pragma unroll
-      for (int t = 0; t < R; ++t) {
-        const float f = ldexpf(1.0f, ax.ex[gi & 1][0][t] - ax.ex[gi & 1][1][t]);
+      for (int v = 0; v < R; ++v) f[v] = ldexpf(1.0f, ax.ex[gi & 1][0][v] - ax.ex[gi & 1][1][v]);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc.c[t][0][r] *= f;
-      }
+      for (int t = 0; t < R; ++t)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc.c[t][0][r] *= f[x3s_rwin<W>(r)];
     }
     const bool proj = gi == 8;
     const char* wb = reinterpret_cast<const char*>(proj ? ed.proj : ed.conv + (size_t)gi * 80 * (CHUNK_B / 2)) +
                      (size_t)part * 8 * CHUNK_B;
     if (X3S_PRIO) __builtin_amdgcn_s_setprio(1);
-    stream_part<R, ROWS>(acc, wb, proj ? 1 : 5, loff, xa + part * 8 * 32, i, proj ? 0 : 1 << (gi >> 1), proj ? 0 : 2);
+    stream_part<W>(acc, wb, proj ? 1 : 5, loff, xa + part * 8 * 32, i, proj ? 0 : 1 << (gi >> 1), proj ? 0 : 2);
     __builtin_amdgcn_s_setprio(0);
   };
 
