@@ -10,7 +10,9 @@ pre-extracted per-frame features (SMPL rotations, betas, 1024-d token, 120-d key
 HBM.  One step = featurise all windows (HIP) -> HumanActionScorer forward (MFMA) -> per-video AC + TC
 (HIP reductions) -> scores copied to pinned host memory; each chunk's featurise is issued on a side stream once the
 previous encode's conv stage has consumed the feats buffer (vge_encoder_wait_conv), so it overlaps that chunk's
-fusion + transformer (--serial-featurize: the plain serial order; every step's work stays inside the timed region).  ModalityStats and the real-class centroids
+fusion + transformer, and the per-video scores + host copies run on that side stream too, behind the next step's
+first featurise, with the encodes alternating between two output buffers (--pipeline side2, the default; --pipeline
+serial / --serial-featurize: the plain serial order; every step's work stays inside the timed region).  ModalityStats and the real-class centroids
 (the real set is sharded over ranks, sufficient statistics all-gathered over RCCL) are built once in
 the setup phase (`setup_s`).  Weak scaling: every rank scores its own 256 clips; no collective in the
 step.  Compute mode: `f32x3` (3xfp16 split-precision MFMA: f32-class results, the reference computes in fp32;
@@ -246,9 +248,16 @@ def main():
     ap.add_argument("--chunk-clips", type=int, default=32, help="e2e: clips per extraction pass (frames in HBM)")
     ap.add_argument("--no-throughput-mode", action="store_true",
                     help="score: skip the second (f16) run reported as throughput_mode beside the f32x3 headline")
-    ap.add_argument("--serial-featurize", action="store_true",
-                    help="score/cfg5: featurise each chunk on the encode stream right before it (default: the next "
-                         "chunk is featurised on a second stream beside the current chunk's fusion + transformer)")
+    ap.add_argument("--pipeline", default="side2", choices=["side2", "side", "tail", "serial"],
+                    help="score/cfg5 stream layout: side = the next chunk is featurised on a second stream beside the "
+                         "current chunk's fusion + transformer; side2 (default) = side, plus the per-video scores and "
+                         "their host copies on that second stream (two output buffers, alternate steps); tail = the "
+                         "transformer / outputs / scores run on a second stream (vge_encoder_set_tail_stream) while "
+                         "the encode stream featurises the next chunk and queues its conv stage, which then takes CUs "
+                         "as the transformer's workgroups finish (its hipEvents include that wait, so the conv "
+                         "roofline is not measured in this mode); serial = one stream, featurise right before each "
+                         "encode")
+    ap.add_argument("--serial-featurize", action="store_true", help="= --pipeline serial")
     ap.add_argument("--serial-extract", action="store_true",
                     help="e2e: run TokenHMR and DWPose one after the other on one stream (default: two streams)")
     ap.add_argument("--no-detector", action="store_true",
@@ -397,6 +406,9 @@ def run_score(args, world, rank, dev):
     feats = torch.empty((CH, CLIP_LEN, ops.FEAT_DIM), device=dev)
     seq = torch.empty((NW, 256), device=dev)
     tcw = torch.empty((NW,), device=dev)
+    # side2: scores run on the side stream while the next step's encodes write the other buffer pair
+    seq_b, tcw_b = [seq, torch.empty_like(seq)], [tcw, torch.empty_like(tcw)]
+    n_step = [0]
     host_ac = torch.empty((V,), dtype=torch.float32, pin_memory=True)
     host_tc = torch.empty((V,), dtype=torch.float64, pin_memory=True)
     n_chunks = (NW + CH - 1) // CH
@@ -428,27 +440,48 @@ def run_score(args, world, rank, dev):
             feat_ready.record(side)
         pending[0] = c
 
+    mode = "serial" if args.serial_featurize else args.pipeline
+    tail = torch.cuda.Stream(device=dev) if mode == "tail" else None
+    enc.set_tail_stream(tail)
+    tx_done = torch.cuda.Event()
+
     def step(i=None):
         ac = tc = None
         cur = torch.cuda.current_stream()
+        sq, tw = (seq_b[n_step[0] % 2], tcw_b[n_step[0] % 2]) if mode == "side2" else (seq, tcw)
+        n_step[0] += 1
         for c in range(n_chunks):
             b0, b1 = c * CH, min(NW, (c + 1) * CH)
-            if args.serial_featurize:
+            if mode == "serial" or (mode == "tail" and pending[0] != c):
                 featurize_chunk(c, cur)
-            else:
+            elif mode in ("side", "side2"):
                 if pending[0] != c:
                     launch_feat(c)
                 cur.wait_event(feat_ready)
-            enc.encode(feats[: b1 - b0], frame_embed=False, tc=True, seq_out=seq[b0:b1], tc_out=tcw[b0:b1])
-            if not args.serial_featurize:
+            enc.encode(feats[: b1 - b0], frame_embed=False, tc=True, seq_out=sq[b0:b1], tc_out=tw[b0:b1])
+            if mode in ("side", "side2"):
                 launch_feat((c + 1) % n_chunks)  # the next chunk, or the next step's first
-        ac, tc = ops.score_videos(seq, tcw, first, vcls, centroids)
-        host_ac.copy_(ac, non_blocking=True)
-        host_tc.copy_(tc, non_blocking=True)
+            if mode == "tail":
+                # the next chunk (or the next step's first) on the encode stream, beside this chunk's transformer
+                # on the tail stream; the next encode's conv stage follows it there
+                featurize_chunk((c + 1) % n_chunks, cur)
+                pending[0] = (c + 1) % n_chunks
+        if mode == "side2":
+            # after the last transformer, on the side stream behind the next step's first featurise: the next conv
+            # waits for that featurise (feat_ready), not for the scores; the step after next rewrites this buffer
+            # pair only after a later featurise on the same side stream, so after these scores
+            tx_done.record(cur)
+            side.wait_event(tx_done)
+        sst = tail if tail is not None else (side if mode == "side2" else cur)
+        with torch.cuda.stream(sst):
+            ac, tc = ops.score_videos(sq, tw, first, vcls, centroids)
+            host_ac.copy_(ac, non_blocking=True)
+            host_tc.copy_(tc, non_blocking=True)
         return ac, tc
 
     # precision evidence for the timed mode: the untimed first step's scores vs the oracle on a sample of clips
     ac_a, tc_a = step()
+    torch.cuda.synchronize()  # the scores may come from the tail stream
     precision = oracle_precision(gen_clips, stats.mean, stats.std, centroids, vcls, seq, ac_a, tc_a, starts,
                                  n=16 if cfg5 else V) if rank == 0 else None
     torch.cuda.synchronize()
@@ -531,7 +564,7 @@ def run_score(args, world, rank, dev):
                      "flop_per_launch": CONV_FLOP_PER_WINDOW * CH, "avg_launch_ms": conv_ms},
         "stage_ms": stage_out,
         "stage_ms_source": "conv_encoders: hipEvents in the timed steps; the other stages: 5 untimed steps after them",
-        "featurize": {"avg_ms": feat_ms, "bound": "hbm", "overlapped": not args.serial_featurize,
+        "featurize": {"avg_ms": feat_ms, "bound": "hbm", "overlapped": mode != "serial", "pipeline": mode,
                       "achieved_GBs": FEAT_BYTES_PER_WINDOW * CH / (feat_ms * 1e-3) / 1e9, "peak_GBs": HBM_PEAK_GBS},
         "encoder_tflops_2.0203GF_per_window": ENCODER_FLOP_PER_WINDOW * NW * args.steps / dt / 1e12,
         "setup_s": setup_s,

@@ -178,6 +178,12 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
  * encoder -- the last reader of its feats -- has finished, so the next batch's vge_featurize can overwrite feats on
  * `stream` while this batch's fusion / transformer still run. */
 int vge_encoder_wait_conv(vge_encoder* enc, vge_stream_t stream);
+/* Pipelining hook (no reference counterpart): subsequent vge_encode calls run the stages after the fusion (token
+ * GEMM, transformer, output normalisation / TC) on `tail` instead of their own stream (NULL: back to it).  The encode
+ * stream keeps the conv stage and the fusion, so the caller can featurise and encode the next batch there while this
+ * batch's transformer runs; seq_embed / frame_embed / tc_window are complete in `tail`'s order (read them there).
+ * The next vge_encode's fusion waits for the previous encode's tail stages, which read the buffer it overwrites. */
+int vge_encoder_set_tail_stream(vge_encoder* enc, vge_stream_t tail);
 
 /* Per-stage device time of vge_encode, measured with hipEvents recorded on the encode stream around
  * each stage (used by bench.py for the roofline line).  profile_begin pre-creates events for up to

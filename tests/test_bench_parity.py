@@ -266,6 +266,50 @@ def test_featurize_pipelined_on_a_side_stream_matches_serial():
     assert torch.equal(piped, serial)
 
 
+@pytest.mark.parametrize("compute", ["f32x3", "f16"])
+def test_tail_stream_pipeline_matches_serial(compute):
+    """bench.py's default pipeline (vge_encoder_set_tail_stream): each encode's transformer / outputs run on a tail
+    stream while the encode stream featurises the next chunk into the same feats buffer and starts its conv stage;
+    the next fusion waits for the previous tail (it overwrites the transformer's input).  Per-video scores are
+    computed on the tail stream.  Seq embeddings, TC terms and scores must equal the serial order bit for bit."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vge import ops
+    from vge.data import pack_frame_store
+    o = _oracle(256)
+    store = ops.DeviceFrameStore.from_host(pack_frame_store(o["clips"], [f"g{i}" for i in range(256)], ["X"] * 256), DEV)
+    mean, std = torch.from_numpy(o["mean"]).to(DEV), torch.from_numpy(o["std"]).to(DEV)
+    win = torch.tensor([[v, 0] for v in range(256)], dtype=torch.int32, device=DEV)
+    enc = ops.Encoder(o["sd"], device=DEV, compute=compute)
+    enc.reserve(64)
+    chunks = [(c * 64, (c + 1) * 64) for c in range(4)]
+    feats = torch.empty((64, 32, ops.FEAT_DIM), device=DEV)
+    first = torch.arange(257, dtype=torch.int32, device=DEV)
+    vcls = torch.zeros(256, dtype=torch.int32, device=DEV)
+    cent = torch.nn.functional.normalize(torch.randn(10, 256, device=DEV), dim=1)
+
+    def run(tail):
+        seq, tcw = torch.zeros((256, 256), device=DEV), torch.zeros(256, device=DEV)
+        cur = torch.cuda.current_stream()
+        enc.set_tail_stream(tail)
+        for rep in range(2):  # the second pass re-featurises while the first pass's last tail may still run
+            ops.featurize(store, win[0:64], mean, std, out=feats)
+            for c, (b0, b1) in enumerate(chunks):
+                enc.encode(feats, tc=True, seq_out=seq[b0:b1], tc_out=tcw[b0:b1])
+                if c + 1 < len(chunks):
+                    ops.featurize(store, win[chunks[c + 1][0]:chunks[c + 1][1]], mean, std, out=feats)
+        with torch.cuda.stream(tail if tail is not None else cur):
+            ac, tc = ops.score_videos(seq, tcw, first, vcls, cent)
+        enc.set_tail_stream(None)
+        torch.cuda.synchronize()
+        return seq.clone(), tcw.clone(), ac.clone(), tc.clone()
+
+    ref = run(None)
+    got = run(torch.cuda.Stream(device=DEV))
+    for a, b in zip(ref, got):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("compute,mix", [("f32x3", None), ("f16", "0"), ("f16", "2")])
 def test_config5_chunk_schedule_vs_oracle(compute, mix, monkeypatch):
     """Config 5's own path (bench.py --workload cfg5): 64-frame clips of 5 windows each (starts 0, 8, 16, 24, 32,

@@ -44,6 +44,8 @@ def test_error_path_without_gpu_work():
     assert so.vge_encoder_create(C.byref(dims), None, 0, 0, C.byref(h)) == 1
     assert so.vge_encoder_wait_conv(None, None) == 1
     assert b"vge_encoder_wait_conv" in so.vge_last_error()
+    assert so.vge_encoder_set_tail_stream(None, None) == 1
+    assert b"vge_encoder_set_tail_stream" in so.vge_last_error()
 
 
 def _hexf(s):

@@ -19,7 +19,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--frames", type=int, default=256)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--only", default="", help="one shape name (qkv/proj/fc1/fc2)")
-ap.add_argument("--waves", default="w8,w4,lib", help="variants to run")
+ap.add_argument("--waves", default="w8,w4,lib", help="variants to run (w8s: 8 waves on 16x16x32)")
 a = ap.parse_args()
 M = a.frames * 192
 shapes = {"qkv": (M, 3840, 1280, "bf16"), "proj": (M, 1280, 1280, "res_f32"), "fc1": (M, 5120, 1280, "gelu_bf16"),
@@ -39,7 +39,7 @@ for name, (m, n, k, epi) in shapes.items():
         for which in t:
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             if which != "lib":
-                so.vge_debug_set_gemm_waves(8 if which == "w8" else 4)
+                so.vge_debug_set_gemm_waves({"w8": 8, "w4": 4, "w8s": 16}[which])
             e0.record()
             if which != "lib":
                 H.gemm_bf16(A, W, epi, bias=bias, res=r, out=out)
@@ -48,6 +48,17 @@ for name, (m, n, k, epi) in shapes.items():
             e1.record()
             torch.cuda.synchronize()
             t[which].append(e0.elapsed_time(e1))
+    if "w8s" in t and "w8" in t:  # same operands through both MFMA shapes
+        outs = []
+        for nw in (8, 16):
+            so.vge_debug_set_gemm_waves(nw)
+            o = torch.empty_like(out)
+            H.gemm_bf16(A, W, epi, bias=bias, res=r, out=o)
+            outs.append(o.float())
+        torch.cuda.synchronize()
+        d = (outs[0] - outs[1]).abs()
+        res.setdefault("_check", {})[name] = {"max_abs_diff_w8_w8s": float(d.max()),
+                                              "max_abs_out": float(outs[0].abs().max())}
     fl = 2.0 * m * n * k
     res[name] = {"M": m, "N": n, "K": k, "epi": epi}
     for which, v in t.items():

@@ -242,6 +242,11 @@ struct vge_encoder {
   unsigned long long units_clock = 0;
   int units_last = -1;  // slot of the last vge_encode (test hook vge_debug_encoder_units)
   hipEvent_t conv_done = nullptr;  // recorded after the conv stage of every vge_encode (vge_encoder_wait_conv)
+  // vge_encoder_set_tail_stream: the stages after the fusion run on `tail`; fuse_done hands the fusion output over,
+  // tail_done (after the last tail stage) makes the next fusion wait before it overwrites `pooled`
+  hipStream_t tail = nullptr;
+  bool tail_set = false, tail_pending = false;
+  hipEvent_t fuse_done = nullptr, tail_done = nullptr;
   vge::FuseParamsHost fuse{};
   const void* Wov = nullptr;      // packed (f32 chunks or fp16 chunks)
   const float* Wov_cs = nullptr;  // x3: its column scales
@@ -856,6 +861,17 @@ int vge_encoder_profile_mask(vge_encoder* enc, int event_mask) {
   return VGE_OK;
 }
 
+int vge_encoder_set_tail_stream(vge_encoder* enc, vge_stream_t tail) {
+  if (!enc) return fail(VGE_ERR_ARG, "vge_encoder_set_tail_stream: null encoder");
+  if (!enc->fuse_done) {
+    HIPCHK(hipEventCreateWithFlags(&enc->fuse_done, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&enc->tail_done, hipEventDisableTiming));
+  }
+  enc->tail = S(tail);
+  enc->tail_set = tail != nullptr;
+  return VGE_OK;
+}
+
 int vge_encoder_wait_conv(vge_encoder* enc, vge_stream_t stream) {
   if (!enc) return fail(VGE_ERR_ARG, "vge_encoder_wait_conv: null encoder");
   if (enc->last_conv) HIPCHK(hipStreamWaitEvent(S(stream), enc->last_conv, 0));
@@ -929,6 +945,8 @@ int vge_encoder_destroy(vge_encoder* enc) {
   if (enc->wbuf) (void)hipFree(enc->wbuf);
   if (enc->d_units) (void)hipFree(enc->d_units);
   if (enc->conv_done) (void)hipEventDestroy(enc->conv_done);
+  if (enc->fuse_done) (void)hipEventDestroy(enc->fuse_done);
+  if (enc->tail_done) (void)hipEventDestroy(enc->tail_done);
   if (enc->hbuf) (void)hipFree(enc->hbuf);
   delete enc;
   return VGE_OK;
@@ -994,8 +1012,20 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
     enc->last_conv = enc->conv_done;
     HIPCHK(mark(1));
   }
+  // the fusion overwrites `pooled`, which the previous encode's token stage reads (on the tail stream, if one was set)
+  if (enc->tail_pending) HIPCHK(hipStreamWaitEvent(s, enc->tail_done, 0));
   HIPCHK(vge::launch_fuse(enc->enc_out, frames, enc->fuse, enc->pooled, s));
   HIPCHK(mark(2));
+  if (enc->tail_set) {  // the rest of this encode on the tail stream (mark / gemm follow `s`)
+    HIPCHK(hipEventRecord(enc->fuse_done, s));
+    HIPCHK(hipStreamWaitEvent(enc->tail, enc->fuse_done, 0));
+    s = enc->tail;
+  }
+  auto tail_end = [&]() -> hipError_t {
+    if (!enc->tail_set) return hipSuccess;
+    enc->tail_pending = true;
+    return hipEventRecord(enc->tail_done, s);
+  };
   if (x3 && enc->tx_fused) {  // tokens + all layers + outputs in one launch, one window per workgroup
     HIPCHK(mark(3));
     const vge::TxArgsX3Host ta{enc->pooled, B, enc->n_layers, (const _Float16*)enc->Wov, enc->Wov_cs, enc->cls, enc->pe,
@@ -1003,6 +1033,7 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
     HIPCHK(vge::launch_transformer_x3(ta, (split || (enc->f16_mix & 2)) ? 2 : ((enc->f16_mix & 4) ? 1 : 0), s));
     HIPCHK(mark(4));
     HIPCHK(mark(5));
+    HIPCHK(tail_end());
     return VGE_OK;
   }
   HIPCHK(gemm(vge::EPI_TOKENS, enc->pooled, 256, enc->Wov, enc->Wov_cs, enc->x, 256, frames, 256, 256, nullptr, nullptr,
@@ -1029,6 +1060,7 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
   HIPCHK(mark(4));
   HIPCHK(vge::launch_embed_tc(enc->x, B, seq_embed, frame_embed, tc_window, s));
   HIPCHK(mark(5));
+  HIPCHK(tail_end());
   return VGE_OK;
 }
 

@@ -79,8 +79,12 @@ __device__ __forceinline__ int gb_xcd_remap(int b, int nblk) {  // bijective: ea
 
 // NW = 8: waves 2 (M) x 4 (N), 128 x 64 per wave (2 waves per SIMD); NW = 4: waves 2 x 2, 128 x 128 per wave
 // (one wave per SIMD, 256 accumulator registers): 25 % fewer LDS fragment bytes per MFMA.
-template <int EPI, int NW>
+// SH = 1 (NW = 8 only): the same wave tile on v_mfma_f32_16x16x32_bf16 (8 x 4 tiles of 16 x 16, one MFMA per 32-k
+// stage and tile) -- same LDS fragment bytes and MFMA cycles per stage; the chip holds a higher clock on this shape
+// (MI355X_MICROARCH.md, DVFS give-back item 7).
+template <int EPI, int NW, int SH = 0>
 __global__ void __launch_bounds__(64 * NW, 1) gemm_bf16_kernel(GemmBf16Args g) {
+  static_assert(SH == 0 || NW == 8, "16x16x32 variant: 8 waves");
   constexpr int TN = NW == 8 ? 2 : 4;  // 32-column tiles per wave
   constexpr int LPS = 2 * (16 / NW);   // global_load_lds per thread per stage
   extern __shared__ __attribute__((aligned(16))) char lds[];
@@ -101,13 +105,21 @@ __global__ void __launch_bounds__(64 * NW, 1) gemm_bf16_kernel(GemmBf16Args g) {
   const int swz = (lane >> 2) & 3;           // ((row >> 2) & 3) of every fragment row this lane reads
   const int rowoff = (lane & 31) * 64;
 
-  floatx16 acc[4][TN];
+  floatx16 acc[SH ? 1 : 4][SH ? 1 : TN];
+  floatx4 acq[SH ? 8 : 1][SH ? 4 : 1];  // SH = 1: 16 x 16 tiles [row tile][column tile]
+  if constexpr (SH == 0) {
 #pragma unroll
-  for (int t = 0; t < 4; ++t)
+    for (int t = 0; t < 4; ++t)
 #pragma unroll
-    for (int u = 0; u < TN; ++u)
+      for (int u = 0; u < TN; ++u)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
+        for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
+  } else {
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acq[t][u] = (floatx4){0.f, 0.f, 0.f, 0.f};
+  }
 
   auto issue = [&](int st) {
     char* slot = lds + (st % GB_ST) * 2 * GB_TILE;
@@ -115,28 +127,49 @@ __global__ void __launch_bounds__(64 * NW, 1) gemm_bf16_kernel(GemmBf16Args g) {
     gb_stage<NW>(g.W, g.ldw, n0, st * GB_K, slot + GB_TILE, wave, lane);
   };
   struct Frag {
-    bf16x8 a[2][4], b[2][TN];
+    bf16x8 a[2][4], b[2][TN];  // SH = 0: [16-k step][32-row / 32-column tile]; SH = 1: a = 8 16-row tiles, b = 4
   };
   auto read = [&](int st, Frag& f) {  // this wave's fragments of stage st (both 16-k steps)
     const char* cur = lds + (st % GB_ST) * 2 * GB_TILE;
-    const char* As = cur + wm * 128 * 64 + rowoff;
-    const char* Bs = cur + GB_TILE + wn * (32 * TN) * 64 + rowoff;
+    if constexpr (SH == 0) {
+      const char* As = cur + wm * 128 * 64 + rowoff;
+      const char* Bs = cur + GB_TILE + wn * (32 * TN) * 64 + rowoff;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int co = ((2 * s + h) ^ swz) * 16;
+      for (int s = 0; s < 2; ++s) {
+        const int co = ((2 * s + h) ^ swz) * 16;
 #pragma unroll
-      for (int t = 0; t < 4; ++t) f.a[s][t] = *reinterpret_cast<const bf16x8*>(As + t * 32 * 64 + co);
+        for (int t = 0; t < 4; ++t) f.a[s][t] = *reinterpret_cast<const bf16x8*>(As + t * 32 * 64 + co);
 #pragma unroll
-      for (int u = 0; u < TN; ++u) f.b[s][u] = *reinterpret_cast<const bf16x8*>(Bs + u * 32 * 64 + co);
+        for (int u = 0; u < TN; ++u) f.b[s][u] = *reinterpret_cast<const bf16x8*>(Bs + u * 32 * 64 + co);
+      }
+    } else {
+      // 16x16x32 fragments: lane -> row (lane & 15) of a 16-row tile, k chunk lane >> 4 of the stage's 32
+      const int co = ((lane >> 4) ^ ((lane >> 2) & 3)) * 16, ro = (lane & 15) * 64;
+      const char* As = cur + wm * 128 * 64 + ro + co;
+      const char* Bs = cur + GB_TILE + wn * 64 * 64 + ro + co;
+#pragma unroll
+      for (int t = 0; t < 8; ++t) f.a[t >> 2][t & 3] = *reinterpret_cast<const bf16x8*>(As + t * 16 * 64);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) f.b[u >> 1][u & 1] = *reinterpret_cast<const bf16x8*>(Bs + u * 16 * 64);
     }
   };
-  auto mma = [&](const Frag& f, int s) {
+  auto mma = [&](const Frag& f, int s) {  // SH = 1: s = row tiles 4s..4s+3
+    if constexpr (SH == 0) {
 #pragma unroll
-    for (int t = 0; t < 4; ++t)
+      for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int u = 0; u < TN; ++u)
-        acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[s][t], f.b[s][u], acc[t][u], 0, 0, 0);
+        for (int u = 0; u < TN; ++u)
+          acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[s][t], f.b[s][u], acc[t][u], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t)
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          acq[4 * s + t][u] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[s][t], f.b[u >> 1][u & 1], acq[4 * s + t][u], 0, 0, 0);
+    }
   };
+  constexpr int MPS = SH ? 2 : 1;  // MFMAs per step relative to the 32x32x16 schedule
   // Step kt: stage kt's fragments are already in registers (read during step kt - 1).  Wait for stage kt + 1 and
   // barrier (it also retires every wave's reads of stage kt - 1's slot); then one straight-line block: stage
   // kt + 4's global_load_lds into that slot interleaved with the first 16-k MFMAs, stage kt + 1's fragment reads
@@ -160,12 +193,12 @@ __global__ void __launch_bounds__(64 * NW, 1) gemm_bf16_kernel(GemmBf16Args g) {
     mma(cur, 1);
 #pragma unroll
     for (int j = 0; j < LPS; ++j) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 8 / LPS, 0);  // MFMA
-      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);        // VMEM read (global_load_lds)
+      __builtin_amdgcn_sched_group_barrier(0x008, MPS * 8 / LPS, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);              // VMEM read (global_load_lds)
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);                   // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x008, MPS * 2, 0);             // MFMA
       __builtin_amdgcn_sched_group_barrier(0x100, (8 + 2 * TN) / 4, 0);    // DS read
     }
   };
@@ -195,13 +228,23 @@ __global__ void __launch_bounds__(64 * NW, 1) gemm_bf16_kernel(GemmBf16Args g) {
   if constexpr (EPI == GE_PE_F32) bb += *reinterpret_cast<const floatx4*>(g.pos + gcol);  // pos_embed[:, :1]
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
+    if constexpr (SH == 0) {
 #pragma unroll
-    for (int tt = 0; tt < 2; ++tt)
+      for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
-      for (int u = 0; u < TN; ++u)
+        for (int u = 0; u < TN; ++u)
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          my[(tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * WC + u * 32 + (lane & 31)] = acc[2 * half + tt][u][r];
+          for (int r = 0; r < 16; ++r)
+            my[(tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * WC + u * 32 + (lane & 31)] = acc[2 * half + tt][u][r];
+    } else {
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            my[(tt * 16 + 4 * (lane >> 4) + r) * WC + u * 16 + (lane & 15)] = acq[4 * half + tt][u][r];
+    }
 #pragma unroll 4
     for (int it = 0; it < 64 / RPI; ++it) {
       const int rl = it * RPI + lr;
@@ -564,11 +607,11 @@ struct GemmBf16 {
   int M, N, K;
 };
 
-template <int NW>
+template <int NW, int SH = 0>
 hipError_t gemm_setup_nw() {
-  const void* ks[5] = {(const void*)gemm_bf16_kernel<GE_BF16, NW>, (const void*)gemm_bf16_kernel<GE_GELU_BF16, NW>,
-                       (const void*)gemm_bf16_kernel<GE_RES_F32, NW>, (const void*)gemm_bf16_kernel<GE_PE_F32, NW>,
-                       (const void*)gemm_bf16_kernel<GE_F32, NW>};
+  const void* ks[5] = {(const void*)gemm_bf16_kernel<GE_BF16, NW, SH>, (const void*)gemm_bf16_kernel<GE_GELU_BF16, NW, SH>,
+                       (const void*)gemm_bf16_kernel<GE_RES_F32, NW, SH>, (const void*)gemm_bf16_kernel<GE_PE_F32, NW, SH>,
+                       (const void*)gemm_bf16_kernel<GE_F32, NW, SH>};
   for (auto k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, GB_LDS);
     if (e != hipSuccess) return e;
@@ -579,6 +622,7 @@ hipError_t gemm_setup_nw() {
 hipError_t vit_kernels_setup() {
   hipError_t e = gemm_setup_nw<8>();
   if (e == hipSuccess) e = gemm_setup_nw<4>();
+  if (e == hipSuccess) e = gemm_setup_nw<8, 1>();
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)vit_attn_kernel<80>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           AttnCfg<80>::LDS);
@@ -587,17 +631,17 @@ hipError_t vit_kernels_setup() {
                              AttnCfg<64>::LDS);
 }
 
-static int g_gemm_waves = 0;  // 8 or 4 (VGE_GEMM_WAVES), chosen once
+static int g_gemm_waves = 0;  // 8, 4 or 16 (= 8 waves on 16x16x32) (VGE_GEMM_WAVES), chosen once
 
-template <int NW>
+template <int NW, int SH = 0>
 void launch_gemm_nw(int epi, dim3 grid, const GemmBf16Args& g, hipStream_t s) {
   const dim3 blk(64 * NW);
   switch (epi) {
-    case GE_BF16: hipLaunchKernelGGL((gemm_bf16_kernel<GE_BF16, NW>), grid, blk, GB_LDS, s, g); break;
-    case GE_GELU_BF16: hipLaunchKernelGGL((gemm_bf16_kernel<GE_GELU_BF16, NW>), grid, blk, GB_LDS, s, g); break;
-    case GE_RES_F32: hipLaunchKernelGGL((gemm_bf16_kernel<GE_RES_F32, NW>), grid, blk, GB_LDS, s, g); break;
-    case GE_PE_F32: hipLaunchKernelGGL((gemm_bf16_kernel<GE_PE_F32, NW>), grid, blk, GB_LDS, s, g); break;
-    default: hipLaunchKernelGGL((gemm_bf16_kernel<GE_F32, NW>), grid, blk, GB_LDS, s, g); break;
+    case GE_BF16: hipLaunchKernelGGL((gemm_bf16_kernel<GE_BF16, NW, SH>), grid, blk, GB_LDS, s, g); break;
+    case GE_GELU_BF16: hipLaunchKernelGGL((gemm_bf16_kernel<GE_GELU_BF16, NW, SH>), grid, blk, GB_LDS, s, g); break;
+    case GE_RES_F32: hipLaunchKernelGGL((gemm_bf16_kernel<GE_RES_F32, NW, SH>), grid, blk, GB_LDS, s, g); break;
+    case GE_PE_F32: hipLaunchKernelGGL((gemm_bf16_kernel<GE_PE_F32, NW, SH>), grid, blk, GB_LDS, s, g); break;
+    default: hipLaunchKernelGGL((gemm_bf16_kernel<GE_F32, NW, SH>), grid, blk, GB_LDS, s, g); break;
   }
 }
 
@@ -616,18 +660,20 @@ hipError_t launch_gemm_bf16(int epi, const GemmBf16& a, hipStream_t s) {
     return hipErrorInvalidValue;
   if (g_gemm_waves == 0) {
     const char* e = getenv("VGE_GEMM_WAVES");
-    g_gemm_waves = (e && atoi(e) == 4) ? 4 : 8;
+    g_gemm_waves = (e && (atoi(e) == 4 || atoi(e) == 16)) ? atoi(e) : 8;
   }
   const dim3 grid((a.M / GB_M) * (a.N / GB_N));
   if (g_gemm_waves == 4)
     launch_gemm_nw<4>(epi, grid, g, s);
+  else if (g_gemm_waves == 16)
+    launch_gemm_nw<8, 1>(epi, grid, g, s);
   else
     launch_gemm_nw<8>(epi, grid, g, s);
   return hipGetLastError();
 }
 
 extern "C" int vge_debug_set_gemm_waves(int nw) {  // A/B timing (tools/gemm_bench.py)
-  g_gemm_waves = (nw == 4) ? 4 : 8;
+  g_gemm_waves = (nw == 4 || nw == 16) ? nw : 8;
   return 0;
 }
 

@@ -19,6 +19,7 @@ EXPORTS = ["vge_featurize", "vge_featurize_layout", "vge_layout_feat_dim", "vge_
            "vge_encoder_create", "vge_encoder_reserve", "vge_encoder_destroy", "vge_encode", "vge_tc_windows",
            "vge_score_videos", "vge_centroid_accumulate", "vge_centroid_finalize", "vge_last_error", "vge_version",
            "vge_encoder_profile_begin", "vge_encoder_profile_read", "vge_encoder_profile_mask", "vge_encoder_wait_conv", "vge_ingest_probe",
+           "vge_encoder_set_tail_stream",
            "vge_ingest_decode",
            "vge_ingest_default_threads",
            "vge_hmr_create", "vge_hmr_reserve", "vge_hmr_destroy", "vge_hmr_extract", "vge_hmr_profile_begin",
@@ -92,6 +93,7 @@ def load() -> C.CDLL:
         "vge_centroid_finalize": [vp, vp, i32, i32, vp, vp],
         "vge_encoder_profile_begin": [vp, i32],
         "vge_encoder_wait_conv": [vp, vp],
+        "vge_encoder_set_tail_stream": [vp, vp],
         "vge_encoder_profile_mask": [vp, i32],
         "vge_encoder_profile_read": [vp, C.POINTER(C.c_double), C.POINTER(C.c_int)],
         "vge_last_error": [],
