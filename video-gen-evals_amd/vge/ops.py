@@ -201,8 +201,9 @@ class Encoder:
         """Run the stages after the fusion (token GEMM, transformer, outputs / TC) of later encode() calls on `stream`
         (None: back on the encode stream) -- vge_encoder_set_tail_stream.  encode()'s outputs are then complete in
         `stream`'s order; the encode stream is free for the next batch's featurise and conv stage."""
-        L.check(self._lib.vge_encoder_set_tail_stream(self._h, stream.cuda_stream if stream is not None else None),
-                "vge_encoder_set_tail_stream")
+        with torch.cuda.device(self.device):  # its events are created on the encoder's device
+            L.check(self._lib.vge_encoder_set_tail_stream(self._h, stream.cuda_stream if stream is not None else None),
+                    "vge_encoder_set_tail_stream")
 
     STAGES = ("conv_encoders", "fusion_pool", "token_gemm", "transformer", "outputs_tc")
 
