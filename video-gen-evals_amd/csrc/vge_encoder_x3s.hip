@@ -61,12 +61,6 @@ namespace {
 #define X3S_PRIO 1  // s_setprio 1 for the streaming half
 #endif
 constexpr int X3S_WMAX = 4;     // windows per unit (quads; pairs fill the remainder)
-#ifndef X3S_PF_QUAD
-#define X3S_PF_QUAD 4  // weight chunks in flight per wave in a quad's conv streams
-#endif
-#ifndef X3S_PF_PAIR
-#define X3S_PF_PAIR 8  // ... in a pair's
-#endif
 #ifndef X3S_SKIP
 #define X3S_SKIP 1  // 1: a row tile skips the taps that put all its frames outside the window (dilated convs)
 #endif
@@ -125,8 +119,7 @@ __device__ __forceinline__ void stream_part(Acc<W, 1>& acc, const char* wb, int 
   constexpr int R = W, G = x3s_g<W>();
   // chunks in flight: a pair's chunk is only 6 MFMAs (192 cycles) -- 3 chunks ahead would not cover the weight
   // stream's L2 latency while one wave per SIMD streams -- and it has the registers for 7
-  constexpr int PF = R >= 4 ? X3S_PF_QUAD : X3S_PF_PAIR;
-  static_assert(8 % PF == 0, "ring slots restart at every tap: chunk j of a tap sits in slot j % PF");
+  constexpr int PF = R >= 4 ? 4 : 8;
   const char* xw = xa + (i / G) * x3s_wsb<W>();  // this lane's MFMA row: its window's block ...
   const int fi = i % G;                          // ... and its frame within the tile's group
   const char* xz = xa + x3s_zr<W>();
