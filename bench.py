@@ -523,6 +523,12 @@ def run_score(args, world, rank, dev):
                  for k, v in stage_ms.items()}
     feat_ms = sum(fe0[k].elapsed_time(fe1[k]) for k in range(n_fe[0])) / max(1, n_fe[0])
     assert np.isfinite(host_ac.numpy()).all() and np.isfinite(host_tc.numpy()).all()
+    # every step scores the same windows: the last step's host copies (after the extra steps, which alternate the
+    # side2 output buffers like the timed ones) must equal the first step's scores bit for bit
+    last_equals_first = bool(np.array_equal(host_ac.numpy(), ac_a.cpu().numpy()) and
+                             np.array_equal(host_tc.numpy(), tc_a.cpu().numpy()))
+    if not last_equals_first:
+        raise RuntimeError("bench: the last step's scores differ from the first step's")
     if rank != 0:
         return None
     conv_ms = stage_ms["conv_encoders"] / max(ncalls, 1)
@@ -553,7 +559,8 @@ def run_score(args, world, rank, dev):
         "precision": {"arith": ARITH[args.compute] if not (args.compute == "f16" and
                                                              os.environ.get("VGE_F16_MIX", "2") == "0") else
                       ARITH["f16"].replace("transformer: 3xfp16 split (VGE_F16 default)",
-                                           "transformer: fp16 too (VGE_F16_MIX=0)"), **precision},
+                                           "transformer: fp16 too (VGE_F16_MIX=0)"), **precision,
+                      "last_step_equals_first": last_equals_first},
         "data": "synthetic (deterministic generator vge.synth: quaternion-walk SMPL rotations, N(0,1) betas/tokens, "
                 "U[0,1] keypoints with 5% invisible; random-init weights of the reference architecture)",
         "config": {"workload": workload, "clips_per_gpu": V, "frames_per_clip": T, "windows_per_step_per_gpu": NW,
