@@ -172,3 +172,41 @@ def test_default_thread_count_ignores_torchrun_single_thread(monkeypatch):
     assert share == min(64, len(os.sched_getaffinity(0))) or share >= 1
     monkeypatch.setenv("LOCAL_WORLD_SIZE", "2")
     assert lib.vge_ingest_default_threads() == max(1, share // 2)
+
+
+def test_explicit_keypoint_layout(tmp_path):
+    """keypoint_path: "auto" is the reference's name sniffing (utils.py:410-417); "flat" / "per_class" override
+    it, so a flat keypoint dir with an arbitrary name resolves; the native and numpy readers agree under it."""
+    from vge import data
+    assert data.keypoint_path("/x/generated_kps", "PushUps", "v0") == "/x/generated_kps/v0/keypoints.npy"
+    assert data.keypoint_path("/x/kps", "PushUps", "v0") == "/x/kps/PushUps/v0/keypoints.npy"
+    assert data.keypoint_path("/x/kps", "PushUps", "v0", layout="flat") == "/x/kps/v0/keypoints.npy"
+    assert data.keypoint_path("/x/SAVE_GEN", "PushUps", "v0", layout="per_class") == \
+        "/x/SAVE_GEN/PushUps/v0/keypoints.npy"
+    with pytest.raises(ValueError):
+        data.keypoint_path("/x", "PushUps", "v0", layout="nested")
+    with pytest.raises(ValueError):
+        data.set_keypoint_layout("nested")
+
+    mesh_dir, kp_dir = tmp_path / "meshes", tmp_path / "my_kps"
+    mesh_dir.mkdir()
+    items = []
+    for i in range(2):
+        c = synth.make_clip(synth.SEED_GEN, i, 33)
+        p = mesh_dir / f"PushUps_{i}.npz"
+        np.savez(p, pose=c.pose, global_orient=c.global_orient, betas=c.betas, vit=c.vit)
+        (kp_dir / p.stem).mkdir(parents=True)
+        np.save(kp_dir / p.stem / "keypoints.npy", c.keypoints)
+        items.append(VideoItem(cls="PushUps", name=p.name, path=str(p), length=33, vit_dim=1024))
+    prev = data.get_keypoint_layout()
+    try:
+        data.set_keypoint_layout("flat")
+        a = ingest.load_frame_store_native(items, str(kp_dir), require_kp=True)
+        b = numpy_store(items, str(kp_dir), True)
+        assert_same(a, b)
+        assert int(a.videos[:, 3].sum()) == 66
+        data.set_keypoint_layout("auto")   # the reference's rule reads my_kps as per-class: keypoints absent
+        with pytest.raises(Exception):
+            numpy_store(items, str(kp_dir), True)
+    finally:
+        data.set_keypoint_layout(prev)

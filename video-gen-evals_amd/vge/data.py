@@ -10,6 +10,7 @@ Mirrors (same names, argument meaning and error behaviour):
   sample_all_windows_npz (generated set: T<32 -> one window at 0)                utils.py:888-911
   enumerate_test_windows (make_test_loader's sample list, length<=0 skipped)      utils.py:803-844
   keypoint_path (flat dir if its name has SAVE_GEN/SAVE_NEW/generated_kps)       utils.py:410-417
+    (or an explicit "flat" / "per_class" layout: set_keypoint_layout, VGE_KP_LAYOUT, --kp-layout)
 
 Frame store layout in HBM (one float32 array per modality, videos concatenated on the frame axis):
   pose [F,207]  global_orient [F,9]  betas [F,10]  vit [F,1024]  keypoints [Fk,120]
@@ -200,8 +201,37 @@ def enumerate_test_windows(ds: NpzVideoDataset, clip_len: int, stride: int,
     return samples
 
 
-def keypoint_path(keypoint_dir: str, cls_name: str, vid_stem: str) -> str:
-    if "SAVE_GEN" in keypoint_dir or "SAVE_NEW" in keypoint_dir or "generated_kps" in keypoint_dir:
+# Keypoint directory layout.  "auto" is the reference's name sniffing (utils.py:410-417: a directory whose path
+# contains SAVE_GEN / SAVE_NEW / generated_kps is flat, <dir>/<stem>/keypoints.npy, any other is per class,
+# <dir>/<Class>/<stem>/keypoints.npy); "flat" and "per_class" state the layout explicitly, so a directory whose
+# name does not follow that convention still resolves.  Set per process by set_keypoint_layout (the CLI's
+# --kp-layout) or the VGE_KP_LAYOUT environment variable.
+KP_LAYOUTS = ("auto", "flat", "per_class")
+_kp_layout = os.environ.get("VGE_KP_LAYOUT", "auto")
+if _kp_layout not in KP_LAYOUTS:
+    raise ValueError(f"VGE_KP_LAYOUT must be one of {KP_LAYOUTS}, got {_kp_layout!r}")
+
+
+def set_keypoint_layout(layout: str) -> None:
+    global _kp_layout
+    if layout not in KP_LAYOUTS:
+        raise ValueError(f"keypoint layout must be one of {KP_LAYOUTS}, got {layout!r}")
+    _kp_layout = layout
+
+
+def get_keypoint_layout() -> str:
+    return _kp_layout
+
+
+def keypoint_path(keypoint_dir: str, cls_name: str, vid_stem: str, layout: Optional[str] = None) -> str:
+    layout = _kp_layout if layout is None else layout
+    if layout not in KP_LAYOUTS:
+        raise ValueError(f"keypoint layout must be one of {KP_LAYOUTS}, got {layout!r}")
+    if layout == "auto":
+        flat = "SAVE_GEN" in keypoint_dir or "SAVE_NEW" in keypoint_dir or "generated_kps" in keypoint_dir
+    else:
+        flat = layout == "flat"
+    if flat:
         return os.path.join(keypoint_dir, vid_stem, "keypoints.npy")
     return os.path.join(keypoint_dir, cls_name, vid_stem, "keypoints.npy")
 

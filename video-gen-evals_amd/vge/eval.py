@@ -400,6 +400,10 @@ def main(argv=None):
                     help="generated keypoint dir (<stem>/keypoints.npy); omit both keypoint dirs for the "
                          "keypoint-less 4-modality layout (keypoint_dir None)")
     ap.add_argument("--real-keypoints", default=None)
+    ap.add_argument("--kp-layout", default=None, choices=["auto", "flat", "per_class"],
+                    help="keypoint dir layout: auto = the reference's name sniffing (utils.py:410-417), flat = "
+                         "<dir>/<stem>/keypoints.npy, per_class = <dir>/<Class>/<stem>/keypoints.npy "
+                         "(default: VGE_KP_LAYOUT or auto)")
     ap.add_argument("--human-scores", default=None)
     ap.add_argument("--out", default="video_scores.json")
     ap.add_argument("--save-features", default=None, help="e.g. window_features.pt")
@@ -409,6 +413,9 @@ def main(argv=None):
     ap.add_argument("--stats-cache", default=None,
                     help="real-set stats + centroid artifact (.npz): reused when its fingerprint matches, else written")
     a = ap.parse_args(argv)
+    if a.kp_layout is not None:
+        from .data import set_keypoint_layout
+        set_keypoint_layout(a.kp_layout)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
         import torch.distributed as dist
