@@ -340,3 +340,27 @@ def test_centroid_segmented_reduction_vs_index_add(vg, n, C):
     s2, c2 = s.to(DEV).clone(), c.to(DEV).clone()
     ops.centroid_accumulate(ds, dy, s2, c2)
     assert torch.equal(c2.cpu(), 2 * ref_c)
+
+
+def test_cli_explicit_keypoint_layouts(vg, golden_dataset, golden_meta, tmp_path):
+    """--kp-layout / --real-kp-layout: the golden keypoint dirs copied under names the reference's sniffing rule
+    (utils.py:410-417) would misread; with the layouts stated the scores equal the reference's."""
+    import json
+    import shutil
+    from vge import data
+    VE, ops = vg
+    paths, ckpt = golden_dataset
+    gen_kp, real_kp = tmp_path / "gen_keypoints", tmp_path / "real_keypoints"
+    shutil.copytree(paths["generated_kps"], gen_kp)
+    shutil.copytree(paths["real_kp"], real_kp)
+    out = tmp_path / "video_scores.json"
+    try:
+        assert VE.main(["--generated-meshes", paths["generated_meshes"], "--real-meshes", paths["real"],
+                        "--model", ckpt, "--keypoints", str(gen_kp), "--real-keypoints", str(real_kp),
+                        "--kp-layout", "flat", "--real-kp-layout", "per_class", "--out", str(out)]) == 0
+    finally:
+        data.clear_keypoint_layouts()
+    scores = json.loads(out.read_text())
+    ref = golden_meta["video_scores"]
+    assert sorted(scores) == sorted(ref)
+    assert max(abs(ref[v][k] - scores[v][k]) for v in ref for k in ref[v]) < 1e-4

@@ -198,15 +198,15 @@ def test_explicit_keypoint_layout(tmp_path):
         (kp_dir / p.stem).mkdir(parents=True)
         np.save(kp_dir / p.stem / "keypoints.npy", c.keypoints)
         items.append(VideoItem(cls="PushUps", name=p.name, path=str(p), length=33, vit_dim=1024))
-    prev = data.get_keypoint_layout()
     try:
-        data.set_keypoint_layout("flat")
+        data.set_keypoint_layout("flat", str(kp_dir) + "/")     # per directory (normalised path)
+        assert data.get_keypoint_layout(str(kp_dir)) == "flat" and data.get_keypoint_layout("/other") == "auto"
         a = ingest.load_frame_store_native(items, str(kp_dir), require_kp=True)
         b = numpy_store(items, str(kp_dir), True)
         assert_same(a, b)
         assert int(a.videos[:, 3].sum()) == 66
-        data.set_keypoint_layout("auto")   # the reference's rule reads my_kps as per-class: keypoints absent
+        data.clear_keypoint_layouts()   # the reference's rule reads my_kps as per-class: keypoints absent
         with pytest.raises(Exception):
             numpy_store(items, str(kp_dir), True)
     finally:
-        data.set_keypoint_layout(prev)
+        data.clear_keypoint_layouts()

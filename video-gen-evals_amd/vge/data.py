@@ -204,27 +204,41 @@ def enumerate_test_windows(ds: NpzVideoDataset, clip_len: int, stride: int,
 # Keypoint directory layout.  "auto" is the reference's name sniffing (utils.py:410-417: a directory whose path
 # contains SAVE_GEN / SAVE_NEW / generated_kps is flat, <dir>/<stem>/keypoints.npy, any other is per class,
 # <dir>/<Class>/<stem>/keypoints.npy); "flat" and "per_class" state the layout explicitly, so a directory whose
-# name does not follow that convention still resolves.  Set per process by set_keypoint_layout (the CLI's
-# --kp-layout) or the VGE_KP_LAYOUT environment variable.
+# name does not follow that convention still resolves.  Set per process (all directories) or per directory by
+# set_keypoint_layout (the CLI's --kp-layout / --real-kp-layout), or for all directories by VGE_KP_LAYOUT.
 KP_LAYOUTS = ("auto", "flat", "per_class")
 _kp_layout = os.environ.get("VGE_KP_LAYOUT", "auto")
 if _kp_layout not in KP_LAYOUTS:
     raise ValueError(f"VGE_KP_LAYOUT must be one of {KP_LAYOUTS}, got {_kp_layout!r}")
+_kp_layout_by_dir: Dict[str, str] = {}
 
 
-def set_keypoint_layout(layout: str) -> None:
+def set_keypoint_layout(layout: str, keypoint_dir: Optional[str] = None) -> None:
+    """Layout for one keypoint directory, or (keypoint_dir None) the default for every directory without one."""
     global _kp_layout
     if layout not in KP_LAYOUTS:
         raise ValueError(f"keypoint layout must be one of {KP_LAYOUTS}, got {layout!r}")
-    _kp_layout = layout
+    if keypoint_dir is None:
+        _kp_layout = layout
+    else:
+        _kp_layout_by_dir[os.path.normpath(keypoint_dir)] = layout
 
 
-def get_keypoint_layout() -> str:
+def get_keypoint_layout(keypoint_dir: Optional[str] = None) -> str:
+    if keypoint_dir is not None:
+        return _kp_layout_by_dir.get(os.path.normpath(keypoint_dir), _kp_layout)
     return _kp_layout
 
 
+def clear_keypoint_layouts() -> None:
+    """Back to VGE_KP_LAYOUT (or auto) with no per-directory layouts."""
+    global _kp_layout
+    _kp_layout_by_dir.clear()
+    _kp_layout = os.environ.get("VGE_KP_LAYOUT", "auto")
+
+
 def keypoint_path(keypoint_dir: str, cls_name: str, vid_stem: str, layout: Optional[str] = None) -> str:
-    layout = _kp_layout if layout is None else layout
+    layout = get_keypoint_layout(keypoint_dir) if layout is None else layout
     if layout not in KP_LAYOUTS:
         raise ValueError(f"keypoint layout must be one of {KP_LAYOUTS}, got {layout!r}")
     if layout == "auto":

@@ -401,9 +401,11 @@ def main(argv=None):
                          "keypoint-less 4-modality layout (keypoint_dir None)")
     ap.add_argument("--real-keypoints", default=None)
     ap.add_argument("--kp-layout", default=None, choices=["auto", "flat", "per_class"],
-                    help="keypoint dir layout: auto = the reference's name sniffing (utils.py:410-417), flat = "
+                    help="layout of --keypoints: auto = the reference's name sniffing (utils.py:410-417), flat = "
                          "<dir>/<stem>/keypoints.npy, per_class = <dir>/<Class>/<stem>/keypoints.npy "
                          "(default: VGE_KP_LAYOUT or auto)")
+    ap.add_argument("--real-kp-layout", default=None, choices=["auto", "flat", "per_class"],
+                    help="layout of --real-keypoints (as --kp-layout)")
     ap.add_argument("--human-scores", default=None)
     ap.add_argument("--out", default="video_scores.json")
     ap.add_argument("--save-features", default=None, help="e.g. window_features.pt")
@@ -413,9 +415,12 @@ def main(argv=None):
     ap.add_argument("--stats-cache", default=None,
                     help="real-set stats + centroid artifact (.npz): reused when its fingerprint matches, else written")
     a = ap.parse_args(argv)
-    if a.kp_layout is not None:
-        from .data import set_keypoint_layout
-        set_keypoint_layout(a.kp_layout)
+    from .data import set_keypoint_layout
+    for layout, d in ((a.kp_layout, a.keypoints), (a.real_kp_layout, a.real_keypoints)):
+        if layout is not None:
+            if d is None:
+                ap.error("a keypoint layout was given without its keypoint directory")
+            set_keypoint_layout(layout, d)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1:
         import torch.distributed as dist
