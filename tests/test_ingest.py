@@ -210,3 +210,9 @@ def test_explicit_keypoint_layout(tmp_path):
             numpy_store(items, str(kp_dir), True)
     finally:
         data.clear_keypoint_layouts()
+
+
+def test_kp_layout_flag_needs_its_directory():
+    from vge import eval as VE
+    with pytest.raises(SystemExit):
+        VE.main(["--generated-meshes", "g", "--real-meshes", "r", "--model", "m.pt", "--kp-layout", "flat"])
