@@ -71,6 +71,12 @@ ARITH = {"f32": "f32 in, f32 accumulate (v_mfma_f32_16x16x4_f32)",
                 "and GroupNorm epilogues; transformer: 3xfp16 split (VGE_F16 default)"}
 HBM_PEAK_GBS = 8000.0
 FEAT_BYTES_PER_WINDOW = 32 * (1024 + 207 + 9 + 10 + 120) * 4 + 32 * 2596 * 4   # read + write
+# transformer_x3_kernel per 32-frame window: the token matrix (32 x 256 x 256) + 4 post-norm
+# layers of 33 tokens: in_proj 256->768, out_proj 256->256, FFN 256->1024->256, attention QK^T + PV (8 heads of 32)
+TX_FLOP_PER_WINDOW = 2 * 32 * 256 * 256 + 4 * (2 * 33 * (256 * 768 + 256 * 256 + 2 * 256 * 1024) + 2 * 2 * 33 * 33 * 256)
+TX_WEIGHT_BYTES = 12.85e6   # split weights streamed from L2 into each window's workgroup (3.21 M weights x 4 B)
+# fuse_kernel per window: the 10 encoder outputs read (f32) + the fused frame vectors written
+FUSE_BYTES_PER_WINDOW = 10 * 32 * 256 * 4 + 32 * 256 * 4
 
 
 def device_peaks() -> dict:
@@ -104,6 +110,8 @@ def make_clips(seed, start, n, T, kp_len=None):
 
 
 def setup_dist():
+    """One process per GPU (torchrun's env): rank r on GPU LOCAL_RANK over RCCL.  The world size reported in the line
+    is the process group's (dist.get_world_size()), not the --gpus argument."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -117,9 +125,22 @@ def setup_dist():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        world, rank = dist.get_world_size(), dist.get_rank()
     else:
         torch.cuda.set_device(0)
     return world, rank, torch.device("cuda", torch.cuda.current_device())
+
+
+def gather_rank_times(dt: float, videos: int, world: int, dev) -> list:
+    """[(seconds, videos)] of every rank in rank order (an all-gather over the bench's process group; RCCL takes
+    device tensors, gloo host ones)."""
+    if world == 1:
+        return [(dt, videos)]
+    on = dev if dist.get_backend() == "nccl" else "cpu"
+    mine = torch.tensor([dt, float(videos)], dtype=torch.float64, device=on)
+    got = [torch.empty_like(mine) for _ in range(dist.get_world_size())]
+    dist.all_gather(got, mine)
+    return [(float(g[0]), int(g[1])) for g in got]
 
 
 def allreduce_sum(t, world):
@@ -233,9 +254,53 @@ def oracle_precision(clips, mean, std, centroids, vcls, seq_gpu, ac_gpu, tc_gpu,
             "max_abs_seq_embed": float((seq - seq_gpu[: n * nw].cpu()).abs().max()), "north_star_tolerance": 1e-4}
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_command(args, env, argv, port=None):
+    """The rank launch for `--gpus N`: None when this process is itself the (only) rank -- N = 1, or under torchrun
+    (WORLD_SIZE set, which must then equal N) -- else the torch.distributed.run command that starts N ranks of this
+    script on 127.0.0.1 (one process per GPU; the children see WORLD_SIZE and run the benchmark)."""
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if args.gpus is not None and int(ws) != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={ws} (torchrun --nproc-per-node)")
+        return None
+    if args.gpus is None or args.gpus <= 1:
+        return None
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(port if port is not None else _free_port()),
+            str(Path(__file__).resolve()), *argv]
+
+
+def launch_ranks(args, cmd) -> int:
+    """Parent of a self-launched N-rank run: the CPU baseline first (this process never touches the GPU: it
+    is measured on the host before any rank starts, and handed to rank 0 in the environment), then torchrun as a
+    CHILD process (never exec: nothing here has initialised the GPU, but the ranks must be fresh processes anyway);
+    rank 0's JSON line goes straight to this process's stdout.  Returns the children's exit status."""
+    import subprocess
+    env = dict(os.environ)
+    if args.workload in ("score", "tag") and not args.no_cpu_baseline:
+        if args.workload == "score":
+            cpu = cpu_baseline(args.cpu_seconds)
+        else:
+            import bench_tag
+            cpu = bench_tag.cpu_baseline()
+        env["VGE_BENCH_CPU_BASELINE"] = json.dumps(cpu)
+    env.setdefault("OMP_NUM_THREADS", str(max(1, cpu_share() // args.gpus)))
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) of this node.  Without torchrun's WORLD_SIZE and N > 1, bench.py launches N ranks "
+                         "itself (torch.distributed.run as a child process, before any GPU call); under torchrun it "
+                         "must equal WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--clips", type=int, default=256, help="32-frame clips per GPU per step (config 2: 256)")
@@ -268,6 +333,9 @@ def main():
                          "features, the full sharded eval flow over 300 videos (bench_tag.py); cfg5: config 5, --clips "
                          "(default 10000) 64-frame clips sharded over the ranks, f16 MFMA path by default")
     args = ap.parse_args()
+    cmd = launch_command(args, os.environ, sys.argv[1:])
+    if cmd is not None:
+        sys.exit(launch_ranks(args, cmd))
     if args.compute is None:
         args.compute = "f16" if args.workload == "cfg5" else "f32x3"
     if args.workload == "cfg5" and args.compute == "f16":
@@ -277,10 +345,12 @@ def main():
     if args.workload == "cfg5" and args.clips == 256:
         args.clips = 10_000
 
-    cpu = None
-    if args.workload == "score" and int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.no_cpu_baseline:
+    cpu = json.loads(os.environ["VGE_BENCH_CPU_BASELINE"]) if os.environ.get("VGE_BENCH_CPU_BASELINE") else None
+    if cpu is None and args.workload == "score" and int(os.environ.get("WORLD_SIZE", "1")) == 1 and \
+            not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_seconds)  # before the GPU is initialised: its DataLoader workers are forked
-    if args.workload == "tag" and int(os.environ.get("WORLD_SIZE", "1")) == 1 and not args.no_cpu_baseline:
+    if cpu is None and args.workload == "tag" and int(os.environ.get("WORLD_SIZE", "1")) == 1 and \
+            not args.no_cpu_baseline:
         import bench_tag
         cpu = bench_tag.cpu_baseline()
     world, rank, dev = setup_dist()
@@ -320,6 +390,49 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def tx_peak(compute: str, pk: dict) -> float:
+    """The transformer's MFMA ceiling: it runs the 3xfp16 split in f32x3 and, by default, in f16 (VGE_F16_MIX bit 2);
+    activations-only split (bit 4): 2 MFMAs per product; VGE_F16_MIX=0: single fp16; exact f32 in f32."""
+    if compute == "f32":
+        return pk["f32"]
+    if compute == "f32x3":
+        return pk["f16"] / 3
+    mix = int(os.environ.get("VGE_F16_MIX", "2"))
+    return pk["f16"] / 3 if mix & 2 else (pk["f16"] / 2 if mix & 4 else pk["f16"])
+
+
+def stage_roofline(stage_ms: dict, feat_ms: float, score_ms: float, windows_per_encode: int, windows_per_step: int,
+                   videos: int, mfma_peak: float, tx_mfma_peak: float, steps: int, dt: float) -> dict:
+    """Every hot kernel of the step against its ceiling, from the same hipEvents as `stage_ms` (conv: the timed steps;
+    the others: the untimed steps after them).  MFMA kernels in algorithmic TFLOP/s against the compute mode's MFMA
+    ceiling; HBM kernels in algorithmic GB/s against HBM peak; the transformer also as its L2->CU weight stream (one
+    full image per window).  `whole_path`: the encoder's 2.0203 GFLOP per window at the measured windows/s."""
+    def mfma(flop, ms, peak=mfma_peak):
+        a = flop / (ms * 1e-3) / 1e12 if ms > 0 else None
+        return {"bound": "mfma", "achieved": a, "peak": peak, "unit": "TFLOP/s", "frac": a / peak if a else None,
+                "flop_per_launch": flop, "avg_launch_ms": ms}
+
+    def hbm(nbytes, ms):
+        a = nbytes / (ms * 1e-3) / 1e9 if ms > 0 else None
+        return {"bound": "hbm", "achieved": a, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": a / HBM_PEAK_GBS if a else None,
+                "bytes_per_launch": nbytes, "avg_launch_ms": ms}
+
+    W = windows_per_encode
+    tx = mfma(TX_FLOP_PER_WINDOW * W, stage_ms.get("transformer", 0.0), tx_mfma_peak)
+    tx["l2_weight_stream_GBs"] = TX_WEIGHT_BYTES * W / (tx["avg_launch_ms"] * 1e-3) / 1e9 if tx["avg_launch_ms"] else None
+    whole = ENCODER_FLOP_PER_WINDOW * windows_per_step * steps / dt / 1e12
+    return {
+        "conv_encoders": mfma(CONV_FLOP_PER_WINDOW * W, stage_ms.get("conv_encoders", 0.0)),
+        "transformer": tx,
+        "fusion_pool": hbm(FUSE_BYTES_PER_WINDOW * W, stage_ms.get("fusion_pool", 0.0)),
+        "featurize": hbm(FEAT_BYTES_PER_WINDOW * W, feat_ms),
+        # score_videos: per window its seq embedding + TC term, per video its centroid and two outputs
+        "score_videos": hbm(windows_per_step * (256 + 1) * 4 + videos * (256 * 4 + 4 + 8 + 4), score_ms),
+        "whole_path": {"achieved": whole, "peak": mfma_peak, "unit": "TFLOP/s", "frac": whole / mfma_peak,
+                       "flop_per_window": ENCODER_FLOP_PER_WINDOW},
+    }
 
 
 def _kernel_sources_sha() -> str:
@@ -445,7 +558,9 @@ def run_score(args, world, rank, dev):
     enc.set_tail_stream(tail)
     tx_done = torch.cuda.Event()
 
-    def step(i=None):
+    sc_ev = []  # (start, end) events around the per-video score launch of the untimed extra steps
+
+    def step(i=None, time_score=False):
         ac = tc = None
         cur = torch.cuda.current_stream()
         sq, tw = (seq_b[n_step[0] % 2], tcw_b[n_step[0] % 2]) if mode == "side2" else (seq, tcw)
@@ -474,7 +589,12 @@ def run_score(args, world, rank, dev):
             side.wait_event(tx_done)
         sst = tail if tail is not None else (side if mode == "side2" else cur)
         with torch.cuda.stream(sst):
+            if time_score:
+                sc_ev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+                sc_ev[-1][0].record(sst)
             ac, tc = ops.score_videos(sq, tw, first, vcls, centroids)
+            if time_score:
+                sc_ev[-1][1].record(sst)
             host_ac.copy_(ac, non_blocking=True)
             host_tc.copy_(tc, non_blocking=True)
         return ac, tc
@@ -506,18 +626,17 @@ def run_score(args, world, rank, dev):
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    dt_t = torch.tensor([dt], dtype=torch.float64, device=dev if dist.is_initialized() and
-                        dist.get_backend() == "nccl" else "cpu")
-    if world > 1:
-        dist.all_reduce(dt_t, op=dist.ReduceOp.MAX)
-    dt = float(dt_t.item())
+    # every rank's (wall time, videos): the line's time is the max over ranks, `value` all ranks' videos / that time
+    per_rank = gather_rank_times(dt, V, world, dev)
+    dt = max(t for t, _ in per_rank)
     stage_ms, ncalls = enc.profile_read()
     n_extra = 5
     enc.profile_mask(0x3F)
     enc.profile_begin(n_extra * n_chunks)
     for _ in range(n_extra):
-        step()
+        step(time_score=True)
     torch.cuda.synchronize()
+    score_ms = sum(a.elapsed_time(b) for a, b in sc_ev) / max(1, len(sc_ev))
     stage_x, ncalls_x = enc.profile_read()
     stage_out = {k: (v / max(ncalls, 1) if k == "conv_encoders" else stage_x[k] / max(ncalls_x, 1))
                  for k, v in stage_ms.items()}
@@ -536,7 +655,7 @@ def run_score(args, world, rank, dev):
     _, kname = PEAK_BY_COMPUTE[args.compute]
     pk = device_peaks()
     peak = {"f16": pk["f16"], "f32x3": pk["f16"] / 3, "f32": pk["f32"]}[args.compute]
-    total_videos = (args.clips if cfg5 else world * V) * args.steps
+    total_videos = sum(v for _, v in per_rank) * args.steps
     if cfg5:
         workload = (f"BASELINE config 5: {args.clips} synthetic 64-frame clips (5 windows each) sharded over "
                     f"{world} GPU(s), fusion-encoder fwd + AC/TC, pre-extracted features resident in HBM, "
@@ -549,6 +668,9 @@ def run_score(args, world, rank, dev):
         "value": total_videos / dt,
         "unit": "videos/s",
         "n_gpus": world,
+        "ranks_seen": len(per_rank),
+        "per_rank_videos_per_s": [v * args.steps / t for t, v in per_rank],
+        "backend": dist.get_backend() if dist.is_initialized() else None,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3,
@@ -570,6 +692,8 @@ def run_score(args, world, rank, dev):
                      "frac": achieved / peak, "traffic": pmc_traffic(args.compute, CH),
                      "flop_per_launch": CONV_FLOP_PER_WINDOW * CH, "avg_launch_ms": conv_ms},
         "stage_ms": stage_out,
+        "stage_roofline": stage_roofline(stage_out, feat_ms, score_ms, CH, NW, V, peak, tx_peak(args.compute, pk),
+                                         args.steps, dt),
         "stage_ms_source": "conv_encoders: hipEvents in the timed steps; the other stages: 5 untimed steps after them",
         "featurize": {"avg_ms": feat_ms, "bound": "hbm", "overlapped": mode != "serial", "pipeline": mode,
                       "achieved_GBs": FEAT_BYTES_PER_WINDOW * CH / (feat_ms * 1e-3) / 1e9, "peak_GBs": HBM_PEAK_GBS},

@@ -41,11 +41,15 @@ typedef enum {
   VGE_ERR_WEIGHT_SHAPE = 4,   /* a state_dict tensor has the wrong shape */
   VGE_ERR_NOMEM = 5,
   VGE_ERR_WORKSPACE = 6,      /* vge_encoder_reserve() was not called for this many windows */
-  VGE_ERR_UNSUPPORTED = 7     /* a model shape the kernels are not built for (vge_encoder_create): d_model != 256,
+  VGE_ERR_UNSUPPORTED = 7,    /* a model shape the kernels are not built for (vge_encoder_create): d_model != 256,
                                  time_heads != 8, clip_len != 32, or a modality set / input dims other than the
                                  reference's five or its keypoint-less four (clip / dino modalities, other vit or
                                  pose widths).  load_model (eval.py:136-165) reads these from the checkpoint;
                                  time_layers is free (any >= 1). */
+  VGE_ERR_DEVICE = 8          /* a kernel detected a broken invariant and raised the encoder's status word (the
+                                 staggered conv kernel's half-workgroup exchange wait ran out of its bound): the
+                                 outputs of that launch are wrong.  Reported by vge_encoder_status, by
+                                 vge_encoder_profile_read and by every later vge_encode until cleared. */
 } vge_status;
 
 /* Encoder compute modes.  VGE_F32: exact f32 MFMA (v_mfma_f32_16x16x4_f32, bitwise an fmaf chain).
@@ -194,6 +198,13 @@ int vge_encoder_set_tail_stream(vge_encoder* enc, vge_stream_t tail);
 #define VGE_N_STAGES 5
 int vge_encoder_profile_begin(vge_encoder* enc, int max_calls);
 int vge_encoder_profile_read(vge_encoder* enc, double* stage_ms, int* n_calls);
+
+/* The encoder's device status word: VGE_OK, or VGE_ERR_DEVICE once a completed launch raised it (the word is
+ * host-mapped: no synchronisation here -- synchronise the encode stream first to cover launches in flight).
+ * vge_encoder_clear_status resets it (tests).  No reference counterpart: the reference's torch ops cannot fail this
+ * way; this is the kernel-side guard that keeps a broken invariant from being a silent wrong score. */
+int vge_encoder_status(const vge_encoder* enc);
+int vge_encoder_clear_status(vge_encoder* enc);
 /* Which of the VGE_N_STAGES + 1 stage-boundary events profiled vge_encode calls record (bit k = event before stage k;
  * default all): each event is a queue marker, so a timed loop that only needs the conv stage records 0x3 and
  * profile_read reports the stages both of whose events were recorded (the others as 0). */

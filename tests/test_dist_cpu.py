@@ -223,3 +223,44 @@ def test_error_on_one_rank_raises_on_every_rank():
     got = dict(q.get() for _ in range(2))
     assert got[1].startswith("own:") and "Expected keypoints" in got[1]
     assert got[0].startswith("peer:") and "[1]" in got[0]
+
+
+def _digest_main(rank, ws, port, tmp, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from vge import dist as VD
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    try:
+        gen = os.path.join(tmp, "gen")
+        os.makedirs(gen, exist_ok=True)
+        ckpt = os.path.join(tmp, "model.pt")
+        if rank == 0:
+            open(ckpt + ".r0", "wb").write(b"x" * 64)
+        model = ckpt + ".r0" if rank == 0 else os.path.join(tmp, "missing.pt")  # rank 1 cannot read its checkpoint
+        try:
+            VD.run_eval_distributed(gen, os.path.join(tmp, "real"), model, None, None, out_json=None, device="cpu",
+                                    stats_cache=os.path.join(tmp, "stats.npz"))
+            q.put((rank, "ok"))
+        except VD.PeerRankFailed as e:
+            q.put((rank, f"peer:{e}"))
+        except OSError as e:
+            q.put((rank, f"own:{type(e).__name__}"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_unreadable_checkpoint_for_the_stats_cache_stops_every_rank(tmp_path):
+    """The stats-cache fingerprint reads the checkpoint before the first collective: a rank that cannot read it
+    raises, and its peer raises PeerRankFailed instead of waiting in the cache-hit all-gather."""
+    ctx = mp.get_context("spawn")
+    q = ctx.SimpleQueue()
+    port = _free_port()
+    procs = [ctx.Process(target=_digest_main, args=(r, 2, port, str(tmp_path), q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    got = dict(q.get() for _ in range(2))
+    assert got[1] == "own:FileNotFoundError", got
+    assert got[0].startswith("peer:") and "[1]" in got[0], got

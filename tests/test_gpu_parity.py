@@ -364,3 +364,34 @@ def test_cli_explicit_keypoint_layouts(vg, golden_dataset, golden_meta, tmp_path
     ref = golden_meta["video_scores"]
     assert sorted(scores) == sorted(ref)
     assert max(abs(ref[v][k] - scores[v][k]) for v in ref for k in ref[v]) < 1e-4
+
+
+def test_conv_exchange_timeout_raises_device_fault(vg, golden_state_dict):
+    """The staggered conv kernel's half-workgroup exchange wait is bounded; a wave that gives up raises the encoder's
+    status word, and the library reports VGE_ERR_DEVICE (DeviceFaultError) instead of returning its wrong embeddings
+    silently.  A spin bound of 0 forces the give-up on the real kernel; the bound restored and the word cleared, the
+    same encoder is correct again."""
+    VE, ops = vg
+    from vge import lib as L
+    so = L.load()
+    torch.manual_seed(3)
+    x = torch.randn(256, 32, 2596, device=DEV)
+    enc = VE.load_model(golden_state_dict, device=DEV, compute="f32x3")
+    good, _, _ = enc.encode(x)
+    torch.cuda.synchronize()
+    enc.status()
+    so.vge_debug_set_x3s_spin_limit(0)
+    try:
+        enc.encode(x)
+        torch.cuda.synchronize()
+    finally:
+        so.vge_debug_set_x3s_spin_limit(-1)
+    with pytest.raises(L.DeviceFaultError):
+        enc.status()
+    with pytest.raises(L.DeviceFaultError):  # later encodes refuse to run until the word is cleared
+        enc.encode(x)
+    enc.clear_status()
+    again, _, _ = enc.encode(x)
+    torch.cuda.synchronize()
+    enc.status()
+    assert torch.equal(good, again)

@@ -216,3 +216,24 @@ def test_kp_layout_flag_needs_its_directory():
     from vge import eval as VE
     with pytest.raises(SystemExit):
         VE.main(["--generated-meshes", "g", "--real-meshes", "r", "--model", "m.pt", "--kp-layout", "flat"])
+
+
+@pytest.mark.parametrize("flags", [["--keypoints", "k"], ["--real-keypoints", "rk"]])
+def test_one_keypoint_dir_without_the_other_is_a_usage_error(flags):
+    """Keypoints on one side only would featurise the generated set in a layout the real-set stats do not have; the
+    reference raises in both cases (feature width / keypoints_raw_mean None), the CLI refuses it up front."""
+    from vge import eval as VE
+    with pytest.raises(SystemExit):
+        VE.main(["--generated-meshes", "g", "--real-meshes", "r", "--model", "m.pt", *flags])
+
+
+@pytest.mark.parametrize("kp_dir,stats_layout", [(None, "kp"), ("some/kps", "nokp")])
+def test_feature_layout_must_match_the_stats(kp_dir, stats_layout):
+    """extract_window_features refuses a generated keypoint dir whose layout differs from the stats' (run_eval and
+    run_eval_distributed go through it) before anything is decoded or launched."""
+    from types import SimpleNamespace
+    from vge import eval as VE
+    from vge.data import NpzVideoDataset
+    stats = SimpleNamespace(layout=stats_layout)
+    with pytest.raises(ValueError, match="feature layout"):
+        VE.extract_window_features(None, NpzVideoDataset("", items=[]), kp_dir, stats, device="cpu")

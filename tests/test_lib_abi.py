@@ -46,6 +46,31 @@ def test_error_path_without_gpu_work():
     assert b"vge_encoder_wait_conv" in so.vge_last_error()
     assert so.vge_encoder_set_tail_stream(None, None) == 1
     assert b"vge_encoder_set_tail_stream" in so.vge_last_error()
+    assert so.vge_encoder_status(None) == 1 and b"vge_encoder_status" in so.vge_last_error()
+    assert so.vge_encoder_clear_status(None) == 1
+
+
+def test_device_status_is_plumbed_to_its_own_error():
+    """The conv kernel's status word (raised when its exchange wait runs out) reaches Python as DeviceFaultError:
+    the header declares VGE_ERR_DEVICE = 8, the binding maps that code to its own exception class, and the kernel's
+    spin-bound hook is exported (the GPU test forces the bound to 0 and checks the error)."""
+    import re as _re
+    from vge import lib as L
+    hdr = (REPO / "include" / "vge.h").read_text()
+    assert _re.search(r"VGE_ERR_DEVICE\s*=\s*8", hdr)
+    assert L.STATUS[8] == "VGE_ERR_DEVICE" and L.VGE_ERR_DEVICE == 8
+    so = L.load()
+    assert hasattr(so, "vge_debug_set_x3s_spin_limit")
+    prev = so.vge_debug_set_x3s_spin_limit(5)
+    assert so.vge_debug_set_x3s_spin_limit(-1) == 5
+    assert so.vge_debug_set_x3s_spin_limit(-1) == prev == (1 << 22)
+    orig = so.vge_last_error
+    try:
+        so.vge_last_error = lambda: b"status word set"
+        with pytest.raises(L.DeviceFaultError, match="VGE_ERR_DEVICE"):
+            L.check(L.VGE_ERR_DEVICE, "vge_encode")
+    finally:
+        so.vge_last_error = orig
 
 
 def _hexf(s):

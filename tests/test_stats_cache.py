@@ -50,6 +50,24 @@ def test_round_trip_and_misses(tmp_path):
     assert SC.load(str(tmp_path / "absent.npz"), fp) is None
     (tmp_path / "junk.npz").write_bytes(b"not an npz")
     assert SC.load(str(tmp_path / "junk.npz"), fp) is None
+    whole = open(path, "rb").read()                                                         # a partial copy
+    for cut in (len(whole) // 2, len(whole) - 30, 100):
+        (tmp_path / "cut.npz").write_bytes(whole[:cut])
+        assert SC.load(str(tmp_path / "cut.npz"), fp) is None
+
+
+def test_kernel_switches_are_in_the_fingerprint(tmp_path, monkeypatch):
+    """A cache written under one kernel selection / numerics switch (VGE_F16_MIX, VGE_X3S, ...) is a miss under
+    another; the library version is recorded too."""
+    items = _items(tmp_path)
+    monkeypatch.delenv("VGE_F16_MIX", raising=False)
+    fp = SC.fingerprint(items, None, "ab" * 32, "f16", 32, 8)
+    assert "version" in fp["kernels"] and fp["kernels"]["env"]["VGE_F16_MIX"] is None
+    path = str(tmp_path / "stats.npz")
+    SC.save(path, fp, *_arrays(), ["A", "B", "C", "D"])
+    assert SC.load(path, SC.fingerprint(items, None, "ab" * 32, "f16", 32, 8)) is not None
+    monkeypatch.setenv("VGE_F16_MIX", "0")
+    assert SC.load(path, SC.fingerprint(items, None, "ab" * 32, "f16", 32, 8)) is None
 
 
 def test_shape_mismatch_is_a_miss(tmp_path):

@@ -50,7 +50,7 @@ struct GemmArgsX3Host {
 };
 hipError_t launch_conv_encoders_x3(const float*, int, const void*, int, unsigned, float*, bool, bool, hipStream_t);
 hipError_t encoder_x3s_kernel_setup();
-hipError_t launch_conv_encoders_x3s(const float*, int, const void*, int, unsigned, float*, hipStream_t);
+hipError_t launch_conv_encoders_x3s(const float*, int, const void*, int, unsigned, float*, int*, hipStream_t);
 bool conv_f16w_plan(int n_windows, int n_enc, int wmax, int& G, int& R, int& U);
 hipError_t launch_conv_f16w_table(int n_windows, int n_enc, int G, int R, int U, int* d_table, hipStream_t s);
 hipError_t launch_conv_encoders_f16w(const float*, int, const void*, float*, const int*, int, int, hipStream_t);
@@ -242,6 +242,10 @@ struct vge_encoder {
   unsigned long long units_clock = 0;
   int units_last = -1;  // slot of the last vge_encode (test hook vge_debug_encoder_units)
   hipEvent_t conv_done = nullptr;  // recorded after the conv stage of every vge_encode (vge_encoder_wait_conv)
+  // device status word (host-mapped, coherent): a kernel that detects a broken invariant (the staggered conv kernel's
+  // exchange wait running out) stores 1; vge_encode / vge_encoder_profile_read / vge_encoder_status report it
+  int* status_h = nullptr;
+  int* status_d = nullptr;
   // vge_encoder_set_tail_stream: the stages after the fusion run on `tail`; fuse_done hands the fusion output over,
   // tail_done (after the last tail stage) makes the next fusion wait before it overwrites `pooled`
   hipStream_t tail = nullptr;
@@ -811,6 +815,12 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
   }
   he = hipEventCreateWithFlags(&enc->conv_done, hipEventDisableTiming);
   if (he != hipSuccess) return hipfail(he);
+  he = hipHostMalloc(reinterpret_cast<void**>(&enc->status_h), sizeof(int), hipHostMallocMapped | hipHostMallocCoherent);
+  if (he == hipSuccess) {
+    *enc->status_h = 0;
+    he = hipHostGetDevicePointer(reinterpret_cast<void**>(&enc->status_d), enc->status_h, 0);
+  }
+  if (he != hipSuccess) return hipfail(he);
   *out = enc;
   return VGE_OK;
 }
@@ -909,6 +919,23 @@ int vge_encoder_profile_read(vge_encoder* enc, double* stage_ms, int* n_calls) {
   }
   *n_calls = n;
   enc->prof_max = 0;
+  return vge_encoder_status(enc);  // the profiled launches are complete: any invariant they broke is visible now
+}
+
+static int device_fault(const vge_encoder* enc) {
+  return fail(VGE_ERR_DEVICE, "a conv encoder launch gave up waiting in its half-workgroup exchange (status word "
+                              "set): its outputs are wrong; the encoder stays in this state (vge_encoder_clear_status)");
+}
+
+int vge_encoder_status(const vge_encoder* enc) {
+  if (!enc) return fail(VGE_ERR_ARG, "vge_encoder_status: null encoder");
+  if (enc->status_h && __atomic_load_n(enc->status_h, __ATOMIC_ACQUIRE) != 0) return device_fault(enc);
+  return VGE_OK;
+}
+
+int vge_encoder_clear_status(vge_encoder* enc) {
+  if (!enc) return fail(VGE_ERR_ARG, "vge_encoder_clear_status: null encoder");
+  if (enc->status_h) __atomic_store_n(enc->status_h, 0, __ATOMIC_RELEASE);
   return VGE_OK;
 }
 
@@ -948,6 +975,7 @@ int vge_encoder_destroy(vge_encoder* enc) {
   if (enc->fuse_done) (void)hipEventDestroy(enc->fuse_done);
   if (enc->tail_done) (void)hipEventDestroy(enc->tail_done);
   if (enc->hbuf) (void)hipFree(enc->hbuf);
+  if (enc->status_h) (void)hipHostFree(enc->status_h);
   delete enc;
   return VGE_OK;
 }
@@ -958,6 +986,8 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
   if (T != 32) return fail(VGE_ERR_ARG, "vge_encode: clip_len must be 32");
   if (B <= 0) return VGE_OK;
   if (B > enc->cap) return fail(VGE_ERR_WORKSPACE, "vge_encode: call vge_encoder_reserve(B) first");
+  // an earlier launch that completed with its status word raised (no synchronisation: a host read of the word)
+  if (enc->status_h && __atomic_load_n(enc->status_h, __ATOMIC_ACQUIRE) != 0) return device_fault(enc);
   hipStream_t s = S(stream);
   const int frames = B * 32, M = B * 33;
   hipEvent_t* ev = nullptr;
@@ -998,7 +1028,8 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
     HIPCHK(vge::launch_conv_encoders_f16w(feats, B, enc->d_encs, enc->enc_out, enc->d_units + (size_t)k * enc->units_cap,
                                           enc->tables[k].G, enc->tables[k].R, s));
   } else if (x3 && enc->x3s) {
-    HIPCHK(vge::launch_conv_encoders_x3s(feats, B, enc->d_encs, enc->n_enc, enc->stem_heavy, enc->enc_out, s));
+    HIPCHK(vge::launch_conv_encoders_x3s(feats, B, enc->d_encs, enc->n_enc, enc->stem_heavy, enc->enc_out,
+                                         enc->status_d, s));
   } else if (x3) {
     HIPCHK(vge::launch_conv_encoders_x3(feats, B, enc->d_encs, enc->n_enc, enc->stem_heavy, enc->enc_out, split, enc->f16_mix & 1, s));
   } else {

@@ -61,6 +61,12 @@ namespace {
 #define X3S_PRIO 1  // s_setprio 1 for the streaming half
 #endif
 constexpr int X3S_WMAX = 4;     // windows per unit (quads; pairs fill the remainder)
+#ifndef X3S_PF_QUAD
+#define X3S_PF_QUAD 4  // weight chunks in flight per wave in a quad's conv streams
+#endif
+#ifndef X3S_PF_PAIR
+#define X3S_PF_PAIR 8  // ... in a pair's
+#endif
 #ifndef X3S_SKIP
 #define X3S_SKIP 1  // 1: a row tile skips the taps that put all its frames outside the window (dilated convs)
 #endif
@@ -119,7 +125,11 @@ __device__ __forceinline__ void stream_part(Acc<W, 1>& acc, const char* wb, int 
   constexpr int R = W, G = x3s_g<W>();
   // chunks in flight: a pair's chunk is only 6 MFMAs (192 cycles) -- 3 chunks ahead would not cover the weight
   // stream's L2 latency while one wave per SIMD streams -- and it has the registers for 7
-  constexpr int PF = R >= 4 ? 4 : 8;
+  constexpr int PF = R >= 4 ? X3S_PF_QUAD : X3S_PF_PAIR;
+  // the ring's slots restart at every tap (chunk j of a tap sits in slot j % PF, and the last steps of a tap load the
+  // next tap's first chunks into the slots they will be read from): a depth that does not divide a tap's 8 chunks
+  // reads the wrong chunk (measured: depths 3 / 6 / 12 gave wrong scores)
+  static_assert(8 % PF == 0, "ring depth must divide a tap's 8 chunks");
   const char* xw = xa + (i / G) * x3s_wsb<W>();  // this lane's MFMA row: its window's block ...
   const int fi = i % G;                          // ... and its frame within the tile's group
   const char* xz = xa + x3s_zr<W>();
@@ -203,7 +213,8 @@ __device__ __forceinline__ float gload(const float* p) {
 template <int W>
 __device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, int n_windows, int win0,
                                               const EncDescX3& ed, int e, float* __restrict__ enc_out, char* lds_raw,
-                                              int& n_ex, [[maybe_unused]] bool tr_on) {
+                                              int& n_ex, int* __restrict__ status, int spin_limit,
+                                              [[maybe_unused]] bool tr_on) {
   constexpr int R = W, G = x3s_g<W>(), WSB = x3s_wsb<W>();
   _Float16* X = reinterpret_cast<_Float16*>(lds_raw);  // W blocks of 32 rows of XR (hi at +0, lo at +XLO bytes), zero row
   char* Xb = lds_raw;
@@ -322,13 +333,19 @@ __device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, i
     }
     ++n_ex;
     if (lane == 63) __hip_atomic_fetch_add(&ax.cnt[grp], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-    // (bounded: a wave that never arrives would be a bug; the bound ends the wait -- with wrong results -- instead of
-    // hanging the device)
-    for (int spin = 0; spin < (1 << 22) &&
-                       __builtin_amdgcn_readfirstlane(__hip_atomic_load(&ax.cnt[grp], __ATOMIC_ACQUIRE,
-                                                                        __HIP_MEMORY_SCOPE_WORKGROUP)) < 4 * n_ex;
+    // Bounded: a wave that never arrives would be a bug.  The bound ends the wait instead of hanging the device, and a
+    // wave that gives up raises the encoder's status word (host-mapped; vge_encode / vge_encoder_profile_read /
+    // vge_encoder_status return VGE_ERR_DEVICE once it is set), so the wrong results it leaves are never silent.
+    int spin = 0;
+    for (; spin < spin_limit && __builtin_amdgcn_readfirstlane(__hip_atomic_load(
+                                    &ax.cnt[grp], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) < 4 * n_ex;
          ++spin)
       __builtin_amdgcn_s_sleep(1);
+    if (spin >= spin_limit &&
+        __builtin_amdgcn_readfirstlane(__hip_atomic_load(&ax.cnt[grp], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP)) <
+            4 * n_ex &&
+        lane == 0)
+      __hip_atomic_store(status, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 #pragma unroll
     for (int t = 0; t < R; ++t)
       m[t] = fmaxf(fmaxf(ax.mx[par][grp][t][0], ax.mx[par][grp][t][1]),
@@ -632,7 +649,8 @@ __device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, i
 
 __global__ void __launch_bounds__(512, 1) conv_encoder_x3s_kernel(const float* __restrict__ feats,
                                                                    const EncDescX3* __restrict__ encs, vge::ConvSched cs,
-                                                                   float* __restrict__ enc_out) {
+                                                                   float* __restrict__ enc_out, int* __restrict__ status,
+                                                                   int spin_limit) {
   extern __shared__ __attribute__((aligned(16))) char lds_raw[];
   X3sAux& ax = *reinterpret_cast<X3sAux*>(lds_raw + X3S_AUX_OFF);
   if (threadIdx.x < 2) ax.cnt[threadIdx.x] = 0;  // ordered before any exchange by the stem staging's barriers
@@ -648,11 +666,13 @@ __global__ void __launch_bounds__(512, 1) conv_encoder_x3s_kernel(const float* _
     if (u < cs.Q) {
       int e, w0;
       conv_unit(cs, u, e, w0);
-      conv_x3s_body<4>(feats, n, w0, encs[e], e, enc_out, lds_raw, n_ex, round == X3S_TRACE_ROUND);
+      conv_x3s_body<4>(feats, n, w0, encs[e], e, enc_out, lds_raw, n_ex, status, spin_limit,
+                       round == X3S_TRACE_ROUND);
     } else {
       int e, w0;
       conv_unit(cs, u, e, w0);
-      conv_x3s_body<2>(feats, n, w0, encs[e], e, enc_out, lds_raw, n_ex, round == X3S_TRACE_ROUND);
+      conv_x3s_body<2>(feats, n, w0, encs[e], e, enc_out, lds_raw, n_ex, status, spin_limit,
+                       round == X3S_TRACE_ROUND);
     }
   }
 #ifdef VGE_TRACE
@@ -670,16 +690,28 @@ hipError_t encoder_x3s_kernel_setup() {
                              X3S_LDS_BYTES);
 }
 
+// spin bound of the half-workgroup exchange (test hook vge_debug_set_x3s_spin_limit: 0 makes every wave that arrives
+// before its group's last one give up, which must surface as VGE_ERR_DEVICE)
+static int g_x3s_spin_limit = 1 << 22;
+
 hipError_t launch_conv_encoders_x3s(const float* feats, int n_windows, const void* encs, int n_enc, unsigned heavy,
-                                    float* enc_out, hipStream_t s) {
+                                    float* enc_out, int* status, hipStream_t s) {
   if (n_windows < 1 || n_enc < 1) return hipSuccess;
+  if (!status) return hipErrorInvalidValue;
   const ConvSched cs = conv_quad_sched(n_windows, n_enc, heavy);
   hipLaunchKernelGGL(conv_encoder_x3s_kernel, dim3(cs.G), dim3(512), X3S_LDS_BYTES, s, feats,
-                     reinterpret_cast<const EncDescX3*>(encs), cs, enc_out);
+                     reinterpret_cast<const EncDescX3*>(encs), cs, enc_out, status, g_x3s_spin_limit);
   return hipGetLastError();
 }
 
 }  // namespace vge
+
+// Test hook: the conv kernel's exchange spin bound (default 2^22 sleeps; < 0 restores it).  Returns the previous one.
+extern "C" int vge_debug_set_x3s_spin_limit(int n) {
+  const int prev = vge::g_x3s_spin_limit;
+  vge::g_x3s_spin_limit = n < 0 ? (1 << 22) : n;
+  return prev;
+}
 
 #ifdef VGE_TRACE
 extern "C" int vge_debug_x3s_trace(long long* host, int n) {

@@ -16,6 +16,7 @@ from __future__ import annotations
 import json
 import os
 import time
+import warnings
 from concurrent.futures import Future, ThreadPoolExecutor
 from typing import Dict, List, Optional, Sequence, Tuple
 
@@ -171,8 +172,10 @@ def run_eval_distributed(generated_meshes_dir: str, real_meshes_dir: str, model_
     overlap = os.environ.get("VGE_FLOW_OVERLAP", "1") != "0"  # 0: every phase in order (A/B timing)
     model_sha = None
     if stats_cache:
+        # the checkpoint digest runs before the first collective (the cache-hit agreement): an unreadable checkpoint on
+        # one rank must stop every rank, not leave the others in the all-gather
         from .stats_cache import model_digest
-        model_sha = model_digest(model_path)
+        model_sha = guarded("stats cache fingerprint", model_digest, model_path)
     pool = ThreadPoolExecutor(max_workers=2)
     need_kp = keypoint_dir is not None
     gen_fs = pool.submit(VE.load_frame_store, mine.items, keypoint_dir, need_kp) if mine.items and overlap else None
@@ -326,8 +329,13 @@ def _real_set_phases(VE, ops, real_meshes_dir, model_path, real_kp_dir, clip_len
     centroids = ops.centroid_finalize(csum, ccnt)
     t2 = time.perf_counter()
     if stats_cache and rank == 0:
+        # after the exchanges: a failed write (read-only dir, full disk) only costs the cache, so it is a warning here
+        # rather than an error the other ranks would wait for in the next agree()
         from . import stats_cache as SC
-        SC.save(stats_cache, fp, s.cpu().numpy(), c, csum.cpu().numpy(), ccnt.cpu().numpy(), sorted(label_dict))
+        try:
+            SC.save(stats_cache, fp, s.cpu().numpy(), c, csum.cpu().numpy(), ccnt.cpu().numpy(), sorted(label_dict))
+        except OSError as e:
+            warnings.warn(f"stats cache {stats_cache!r} not written: {e}")
     return model, stats, centroids, t1, t2
 
 def save_window_features(parts: List[Optional[dict]], path: str) -> None:

@@ -194,6 +194,11 @@ def extract_window_features(model: ops.Encoder, dataset: NpzVideoDataset, keypoi
     """eval.py:168-206 over all windows of `dataset` (sample_all_windows_npz order).  save_path: torch.save of
     {seq_embeds [Nw,256], frame_embeds [Nw,33,256], cls_names, vid_names} on the CPU like eval.py:197-204
     (frame embeddings are then produced too)."""
+    if ops.layout_of(keypoint_dir) != stats.layout:
+        # the reference fails here too: a keypoint-less WindowDataset's rows (2356) do not broadcast against kp stats
+        # (2596), and a keypoint dir with keypoint-less stats finds keypoints_raw_mean None (utils.py:406-425, 496-514)
+        raise ValueError(f"generated keypoint dir {keypoint_dir!r} gives the {ops.layout_of(keypoint_dir)!r} feature "
+                         f"layout but the real-set stats are {stats.layout!r}: pass both keypoint dirs or neither")
     samples = sample_all_windows_npz(dataset, clip_len, stride)
     if store is None:
         store = ops.DeviceFrameStore.from_host(load_frame_store(dataset.items, keypoint_dir,
@@ -415,6 +420,8 @@ def main(argv=None):
     ap.add_argument("--stats-cache", default=None,
                     help="real-set stats + centroid artifact (.npz): reused when its fingerprint matches, else written")
     a = ap.parse_args(argv)
+    if (a.keypoints is None) != (a.real_keypoints is None):
+        ap.error("--keypoints and --real-keypoints go together (both: the 5-modality layout; neither: keypoint-less)")
     from .data import set_keypoint_layout
     for layout, d in ((a.kp_layout, a.keypoints), (a.real_kp_layout, a.real_keypoints)):
         if layout is not None:

@@ -11,15 +11,16 @@ LIB_PATH = Path(os.environ.get("VGE_LIB", _HERE / "libvge.so"))
 
 VGE_OK = 0
 STATUS = {0: "VGE_OK", 1: "VGE_ERR_ARG", 2: "VGE_ERR_HIP", 3: "VGE_ERR_MISSING_WEIGHT", 4: "VGE_ERR_WEIGHT_SHAPE",
-          5: "VGE_ERR_NOMEM", 6: "VGE_ERR_WORKSPACE", 7: "VGE_ERR_UNSUPPORTED"}
+          5: "VGE_ERR_NOMEM", 6: "VGE_ERR_WORKSPACE", 7: "VGE_ERR_UNSUPPORTED", 8: "VGE_ERR_DEVICE"}
 VGE_ERR_UNSUPPORTED = 7
+VGE_ERR_DEVICE = 8
 
 EXPORTS = ["vge_featurize", "vge_featurize_layout", "vge_layout_feat_dim", "vge_stats_finalize_layout",
            "vge_encoder_feat_dim", "vge_stats_workspace_bytes", "vge_stats_accumulate", "vge_stats_finalize",
            "vge_encoder_create", "vge_encoder_reserve", "vge_encoder_destroy", "vge_encode", "vge_tc_windows",
            "vge_score_videos", "vge_centroid_accumulate", "vge_centroid_finalize", "vge_last_error", "vge_version",
            "vge_encoder_profile_begin", "vge_encoder_profile_read", "vge_encoder_profile_mask", "vge_encoder_wait_conv", "vge_ingest_probe",
-           "vge_encoder_set_tail_stream",
+           "vge_encoder_set_tail_stream", "vge_encoder_status", "vge_encoder_clear_status",
            "vge_ingest_decode",
            "vge_ingest_default_threads",
            "vge_hmr_create", "vge_hmr_reserve", "vge_hmr_destroy", "vge_hmr_extract", "vge_hmr_profile_begin",
@@ -38,6 +39,11 @@ class VgeError(RuntimeError):
 class UnsupportedModelError(VgeError):
     """VGE_ERR_UNSUPPORTED: a checkpoint whose d_model / time_heads / modality set the kernels are not built for
     (load_model, eval.py:136-165, would build such a HumanActionScorer; this library refuses it by name)."""
+
+
+class DeviceFaultError(VgeError):
+    """VGE_ERR_DEVICE: a kernel raised the encoder's status word (a broken invariant, e.g. the conv kernel's
+    half-workgroup exchange wait ran out): the results of that launch are wrong and must not be used."""
 
 
 class Dims(C.Structure):
@@ -96,6 +102,8 @@ def load() -> C.CDLL:
         "vge_encoder_set_tail_stream": [vp, vp],
         "vge_encoder_profile_mask": [vp, i32],
         "vge_encoder_profile_read": [vp, C.POINTER(C.c_double), C.POINTER(C.c_int)],
+        "vge_encoder_status": [vp],
+        "vge_encoder_clear_status": [vp],
         "vge_last_error": [],
         "vge_version": [],
         "vge_ingest_probe": [C.POINTER(C.c_char_p), C.POINTER(C.c_char_p), i32, i32, C.POINTER(ClipInfo)],
@@ -116,5 +124,5 @@ def load() -> C.CDLL:
 def check(status: int, what: str) -> None:
     if status != VGE_OK:
         msg = load().vge_last_error().decode(errors="replace")
-        cls = UnsupportedModelError if status == VGE_ERR_UNSUPPORTED else VgeError
+        cls = {VGE_ERR_UNSUPPORTED: UnsupportedModelError, VGE_ERR_DEVICE: DeviceFaultError}.get(status, VgeError)
         raise cls(f"{what} failed: {STATUS.get(status, status)}: {msg}")

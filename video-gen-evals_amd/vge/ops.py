@@ -155,6 +155,7 @@ class Encoder:
                     "vge_encoder_create")
         self.compute = compute
         self._h = h
+        self._tail = None  # set_tail_stream()
         self._lib = lib
         self.capacity = 0
         self.n_modalities = n_modalities
@@ -184,7 +185,26 @@ class Encoder:
         tcw = (tc_out if tc_out is not None else torch.empty((B,), device=feats.device, dtype=torch.float32)) if tc else None
         L.check(self._lib.vge_encode(self._h, _ptr(feats), B, T, _ptr(seq), _ptr(fe), _ptr(tcw), _stream(feats.device)),
                 "vge_encode")
+        if self._tail is not None:
+            # the outputs are written on the tail stream.  Those allocated here belong to the current stream in the
+            # caching allocator's books: record the tail stream on them (a dropped fe / tcw is not reused before the
+            # tail stream is done with it) and make the current stream wait for it, so they read as complete there.
+            # Caller-provided seq_out / tc_out (and no frame embeddings) keep the overlap: the caller orders them.
+            own = [t for t, given in ((seq, seq_out is not None), (fe, False), (tcw, tc_out is not None))
+                   if t is not None and not given]
+            for t in own:
+                t.record_stream(self._tail)
+            if own:
+                torch.cuda.current_stream(feats.device).wait_stream(self._tail)
         return seq, fe, tcw
+
+    def status(self) -> None:
+        """Raise DeviceFaultError if a completed launch raised the encoder's device status word (vge_encoder_status;
+        synchronise first to cover launches still in flight)."""
+        L.check(self._lib.vge_encoder_status(self._h), "vge_encoder_status")
+
+    def clear_status(self) -> None:
+        L.check(self._lib.vge_encoder_clear_status(self._h), "vge_encoder_clear_status")
 
     def profile_mask(self, event_mask: int) -> None:
         """Stage-boundary events recorded by profiled encodes (bit k = before stage k; 0x3 = the conv stage only)."""
@@ -204,6 +224,7 @@ class Encoder:
         with torch.cuda.device(self.device):  # its events are created on the encoder's device
             L.check(self._lib.vge_encoder_set_tail_stream(self._h, stream.cuda_stream if stream is not None else None),
                     "vge_encoder_set_tail_stream")
+        self._tail = stream
 
     STAGES = ("conv_encoders", "fusion_pool", "token_gemm", "transformer", "outputs_tc")
 

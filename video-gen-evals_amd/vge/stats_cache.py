@@ -22,6 +22,7 @@ from __future__ import annotations
 import hashlib
 import json
 import os
+import zipfile
 from typing import Dict, Optional, Sequence
 
 import numpy as np
@@ -64,7 +65,25 @@ def fingerprint(train_items: Sequence[VideoItem], real_kp_dir: Optional[str], mo
         if real_kp_dir:
             files.append(_file_sig(keypoint_path(real_kp_dir, it.cls, os.path.splitext(it.name)[0])))
     return {"format": FORMAT, "model_sha256": model_sha, "compute": compute, "clip_len": int(clip_len),
-            "stride": int(stride), "real_files": files}
+            "stride": int(stride), "real_files": files, "kernels": kernel_signature()}
+
+
+# environment switches that select kernels or change the f32x3 / f16 numerics of the encoder (vge_api.cpp and the
+# kernel launchers read them); a cache written under one setting is a miss under another
+KERNEL_ENV = ("VGE_X3S", "VGE_F16_MIX", "VGE_F16W", "VGE_X3_UNFUSED", "VGE_HOST_PACK", "VGE_TX_W", "VGE_TX_OCC",
+              "VGE_QUAD_ALIGN")
+
+
+def kernel_signature() -> Dict:
+    """The library build (vge_version and the loaded libvge.so's size / mtime) and the kernel-selecting env values."""
+    from . import lib as L
+    sig = {"env": {k: os.environ.get(k) for k in KERNEL_ENV}}
+    try:
+        sig["version"] = L.load().vge_version().decode(errors="replace")
+        sig["lib"] = _file_sig(str(L.LIB_PATH))[1:]
+    except Exception as e:  # no library: the flow fails later anyway; the fingerprint just cannot match a real one
+        sig["version"] = f"unavailable: {type(e).__name__}"
+    return sig
 
 
 def save(path: str, fp: Dict, stats_sums, stats_counts, cent_sums, cent_counts, classes: Sequence[str]) -> None:
@@ -89,7 +108,7 @@ def load(path: Optional[str], fp: Dict) -> Optional[Dict]:
                 return None
             out = {k: np.array(z[k]) for k in ("stats_sums", "stats_counts", "cent_sums", "cent_counts")}
             out["classes"] = json.loads(bytes(z["classes"]).decode())
-    except (OSError, ValueError, KeyError):
+    except (OSError, ValueError, KeyError, EOFError, zipfile.BadZipFile):  # unreadable / truncated / corrupt: a miss
         return None
     if out["stats_sums"].shape != (2, 2596) or out["stats_counts"].shape != (2,) or \
             out["cent_sums"].shape != (len(out["classes"]), 256) or out["cent_counts"].shape != (len(out["classes"]),):
