@@ -1,5 +1,5 @@
 #!/bin/bash
-# Per-phase traces of the fp16 unit conv kernel at 256 windows from VGE_TRACE builds (tools/build_variant.sh):
+# Per-phase traces of the fp16 unit conv kernel at 256 windows from VGE_TRACE builds (tools/build_variant_src.sh NAME vge_encoder_x3.hip "-DVGE_TRACE"):
 # bash tools/trace_f16w.sh trace trace1 ...  (build dirs under video-gen-evals_amd/csrc/build)
 cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
 for v in "$@"; do

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Per-phase timeline of conv_encoder_x3s_kernel (the staggered split conv kernel) from a VGE_TRACE build
-(tools/build_x3s_variant.sh trace_s "-DVGE_TRACE"; s_memtime stamps of every wave of blocks 0..63, first unit):
+(tools/build_variant_src.sh trace_s vge_encoder_x3s.hip "-DVGE_TRACE"; s_memtime stamps of every wave of blocks 0..63, first unit):
 
     VGE_LIB=.../build/trace_s/libvge.so python tools/trace_x3s.py [--windows 256]
 
