@@ -149,6 +149,7 @@ __device__ __forceinline__ void stream16(Acc16<W>& acc, const char* wb, int ntap
       ah[t] = *reinterpret_cast<const half8*>(pt[t]);
       al[t] = *reinterpret_cast<const half8*>(pt[t] + TXLO);
     }
+#pragma unroll 1
   for (int k = 0; k < ntap; ++k) {
     const bool more = k + 1 < ntap;
     const int kn = more ? k + 1 : k;
@@ -603,6 +604,8 @@ __device__ __forceinline__ void conv_x3t_body(const float* __restrict__ feats, i
   phase_end();
   using NoSkip = std::integral_constant<bool, false>;
   using Skip = std::integral_constant<bool, true>;
+  // blocks are compile-time (each block's straight-line code is its own: a runtime block loop keeps more values live
+  // across its back edge and spilled 96-226 scratch instructions against 7 this way)
   auto block = [&](auto skip_tag, auto blk_tag) {
     constexpr int blk = decltype(blk_tag)::value;
     stream(skip_tag, 2 * blk, 0);
