@@ -277,14 +277,29 @@ __device__ __forceinline__ void featurize_vit(const float* __restrict__ vit, int
 }
 
 // ---------------------------------------------------------------- the tile kernel
+// The mesh / keypoint frames a tile reads, as 33 slots: slot 0 = the previous frame of row 0, slot t + 1 = the frame
+// of row t (in both modes the previous frame of row t >= 1 is row t - 1's frame).  The rotation / beta and keypoint
+// workgroups stage their slots in LDS with every load of the tile in flight at once (one memory round trip), then
+// compute from LDS; issued row by row, a workgroup paid a round trip per row (latency-bound, ~1/3 of the kernel's
+// bytes taking as long as the vit part).
+constexpr int SLOTS = 33;
+constexpr int ROT_W = 9 + 207 + 10;  // a slot's global_orient | body_pose | betas
+constexpr int ROT_LOADS = (SLOTS * ROT_W + 255) / 256;
+constexpr int KP_LOADS = (SLOTS * 120 + 255) / 256;
+__device__ __forceinline__ int slot_frame(int mode, int start, int L, int slot) {
+  const RowSrc r = row_src(mode, start, L, slot == 0 ? 0 : slot - 1);
+  return slot == 0 ? r.prv : r.src;
+}
+
 __global__ void __launch_bounds__(256) featurize_tiles_kernel(
     const float* __restrict__ pose, const float* __restrict__ gori, const float* __restrict__ betas,
     const float* __restrict__ vit, const float* __restrict__ kp, const int* __restrict__ videos,
     const TileDesc* __restrict__ tiles, const int* __restrict__ windows, const float* __restrict__ mean,
     const float* __restrict__ stdv, float* __restrict__ feats, int ld, int dsh) {
   // ld: feats row width (2596, or 2356 keypoint-less); dsh: how far the diff columns sit before the 2596 layout's
-  __shared__ float pn[33][120];  // normalised keypoints: slot 0 = prev of row 0, slot t+1 = row t
-  __shared__ float kR[32][4];    // per row: H = X_{t-1}^T X_t, then the Procrustes rotation R (row-major)
+  __shared__ float stage[SLOTS * ROT_W];  // rotation workgroups: [slot][226]; keypoint workgroups: raw [slot][120]
+  __shared__ float pn[SLOTS][120];        // normalised keypoints of every slot
+  __shared__ float kR[32][4];             // per row: H = X_{t-1}^T X_t, then the Procrustes rotation R (row-major)
   TileDesc td;
   if (windows != nullptr) {  // window mode straight from the {video, start} list
     const int v = windows[2 * blockIdx.x], st = windows[2 * blockIdx.x + 1];
@@ -311,77 +326,99 @@ __global__ void __launch_bounds__(256) featurize_tiles_kernel(
   return;  // timing ablation: vit part only
 #endif
   if (blockIdx.y == 1) {  // rotations + betas
+    const int nslot = mcount + 1;
+    {
+      float v[ROT_LOADS];
+#pragma unroll
+      for (int k = 0; k < ROT_LOADS; ++k) {
+        const int it = tid + 256 * k;
+        const int sl = it / ROT_W, c = it - sl * ROT_W;
+        v[k] = 0.f;
+        if (sl < nslot) {
+          const size_t f = (size_t)(foff + slot_frame(mode, td.mesh_start, L, sl));
+          v[k] = c < 9 ? gori[f * 9 + c] : (c < 216 ? pose[f * 207 + (c - 9)] : betas[f * 10 + (c - 216)]);
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < ROT_LOADS; ++k)
+        if (tid + 256 * k < SLOTS * ROT_W) stage[tid + 256 * k] = v[k];
+    }
+    __syncthreads();
     // ---- (b) rotations: raw flattened rotmats + SO(3) log-map deltas (utils.py:165-174)
     for (int it = tid; it < 32 * 24; it += 256) {
-      int t = it / 24, j = it % 24;
+      const int t = it / 24, j = it % 24;
       if (t >= mcount) continue;
-      RowSrc rs = row_src(mode, td.mesh_start, L, t);
-      const float* base = (j == 0) ? gori : pose;
-      int stride = (j == 0) ? 9 : 207, off = (j == 0) ? 0 : (j - 1) * 9;
-      const float* R = base + (size_t)(foff + rs.src) * stride + off;
-      const float* Rp = base + (size_t)(foff + rs.prv) * stride + off;
+      const float* R = stage + (t + 1) * ROT_W + j * 9;   // (global_orient is slot column 0, joint j - 1 at 9 j)
+      const float* Rp = stage + t * ROT_W + j * 9;
       float Rl[9], Rpl[9];
-  #pragma unroll
+#pragma unroll
       for (int i = 0; i < 9; ++i) { Rl[i] = R[i]; Rpl[i] = Rp[i]; }
       float w[3];
       rot_delta(Rpl, Rl, w);
       float* orow = out + (size_t)t * ld;
       int craw = (j == 0) ? C_GORI_RAW : C_POSE_RAW + (j - 1) * 9;
       int cdif = ((j == 0) ? C_GORI_DIFF : C_POSE_DIFF + (j - 1) * 3) - dsh;
-  #pragma unroll
+#pragma unroll
       for (int i = 0; i < 9; ++i) orow[craw + i] = znorm(Rl[i], mean, stdv, craw + i);
-  #pragma unroll
+#pragma unroll
       for (int i = 0; i < 3; ++i) orow[cdif + i] = znorm(w[i], mean, stdv, cdif + i);
     }
 
     // ---- (c) betas raw + first difference (utils.py:161-163)
     for (int it = tid; it < 32 * 10; it += 256) {
-      int t = it / 10, i = it % 10;
+      const int t = it / 10, i = it % 10;
       if (t >= mcount) continue;
-      RowSrc rs = row_src(mode, td.mesh_start, L, t);
-      float b = betas[(size_t)(foff + rs.src) * 10 + i];
-      float bp = betas[(size_t)(foff + rs.prv) * 10 + i];
+      const float b = stage[(t + 1) * ROT_W + 216 + i];
+      const float bp = stage[t * ROT_W + 216 + i];
       float* orow = out + (size_t)t * ld;
       orow[C_BETA_RAW + i] = znorm(b, mean, stdv, C_BETA_RAW + i);
       orow[C_BETA_DIFF - dsh + i] = znorm(b - bp, mean, stdv, C_BETA_DIFF - dsh + i);
     }
-
     return;
   }
   // (the keypoint-less layout launches no keypoint workgroups)
-  // ---- (d1) keypoints: centre + Frobenius-normalise every needed frame (utils.py:191-196)
-  for (int slot = wave; slot < 33; slot += 4) {
-    int t = slot - 1;
-    bool need = (slot == 0) ? (kcount > 0) : (t < kcount);
-    if (!need) continue;  // wave-uniform
-    RowSrc rs = row_src(mode, td.kp_start, Lk, slot == 0 ? 0 : t);
-    int f = (slot == 0) ? rs.prv : rs.src;
+  if (kcount == 0) return;
+  {
+    const int nslot = kcount + 1;
+    float v[KP_LOADS];
+#pragma unroll
+    for (int k = 0; k < KP_LOADS; ++k) {
+      const int it = tid + 256 * k;
+      const int sl = it / 120, c = it - sl * 120;
+      v[k] = sl < nslot ? kp[(size_t)(koff + slot_frame(mode, td.kp_start, Lk, sl)) * 120 + c] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < KP_LOADS; ++k)
+      if (tid + 256 * k < SLOTS * 120) stage[tid + 256 * k] = v[k];
+  }
+  __syncthreads();
+  // ---- (d1) keypoints: centre + Frobenius-normalise every slot (utils.py:191-196)
+  for (int slot = wave; slot <= kcount; slot += 4) {
     float x = 0.f, y = 0.f;
     if (lane < 60) {
-      x = kp[(size_t)(koff + f) * 120 + 2 * lane];
-      y = kp[(size_t)(koff + f) * 120 + 2 * lane + 1];
+      x = stage[slot * 120 + 2 * lane];
+      y = stage[slot * 120 + 2 * lane + 1];
     }
-    float mx = wave_sum(lane < 60 ? x : 0.f) / 60.0f;
-    float my = wave_sum(lane < 60 ? y : 0.f) / 60.0f;
-    float cx = x - mx, cy = y - my;
-    float ss = wave_sum(lane < 60 ? (cx * cx + cy * cy) : 0.f);
-    float s = fmaxf(sqrtf(ss), 1e-6f);
+    // (wave_sum: the butterfly order the parity tests pinned; the Procrustes SVD is sensitive near rank 1)
+    const float mx = wave_sum(x) / 60.0f;
+    const float my = wave_sum(y) / 60.0f;
+    const float cx = x - mx, cy = y - my;
+    const float ss = wave_sum(lane < 60 ? (cx * cx + cy * cy) : 0.f);
+    const float sc = fmaxf(sqrtf(ss), 1e-6f);
     if (lane < 60) {
-      pn[slot][2 * lane] = cx / s;
-      pn[slot][2 * lane + 1] = cy / s;
+      pn[slot][2 * lane] = cx / sc;
+      pn[slot][2 * lane + 1] = cy / sc;
     }
   }
-
   __syncthreads();  // pn[] complete
 
   // ---- (d2) keypoints raw + Procrustes velocity (utils.py:177-217): H of every row by wave sums, then the
   // 2x2 SVDs of all rows in parallel on the lanes of wave 0 (one dependent LAPACK chain instead of eight
   // per wave), then the deltas
   for (int t = wave; t < kcount; t += 4) {
-    RowSrc rs = row_src(mode, td.kp_start, Lk, t);
+    const RowSrc rs = row_src(mode, td.kp_start, Lk, t);
     float* orow = out + (size_t)t * ld;
-    for (int c = lane; c < 120; c += 64)
-      orow[C_KP_RAW + c] = znorm(kp[(size_t)(koff + rs.src) * 120 + c], mean, stdv, C_KP_RAW + c);
+    for (int c = lane; c < 120; c += 64) orow[C_KP_RAW + c] = znorm(stage[(t + 1) * 120 + c], mean, stdv, C_KP_RAW + c);
     if (!rs.first) {
       float x0 = 0.f, x1 = 0.f, y0 = 0.f, y1 = 0.f;
       if (lane < 60) {
@@ -419,7 +456,7 @@ __global__ void __launch_bounds__(256) featurize_tiles_kernel(
   }
   __syncthreads();
   for (int t = wave; t < kcount; t += 4) {
-    RowSrc rs = row_src(mode, td.kp_start, Lk, t);
+    const RowSrc rs = row_src(mode, td.kp_start, Lk, t);
     float* orow = out + (size_t)t * ld;
     float dx = 0.f, dy = 0.f;
     if (!rs.first && lane < 60) {
