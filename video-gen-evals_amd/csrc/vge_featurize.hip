@@ -17,6 +17,10 @@
 
 #pragma clang fp contract(off)
 
+#ifndef FEAT_VIT_PF
+#define FEAT_VIT_PF 1  // vit rows in flight ahead of the one being finished (per wave)
+#endif
+
 namespace {
 
 struct TileDesc {     // 8 x int32
@@ -248,13 +252,25 @@ __device__ __forceinline__ void featurize_vit(const float* __restrict__ vit, int
   const int t1 = min(t0 + 8, mcount);
   float vprev[16], raw[16], vcur[16];
   floatx4 xa[4], xb[4];
+#if FEAT_VIT_PF >= 2
+  floatx4 xc[4];
+#endif
   issue(row_src(mode, mesh_start, L, t0).prv, xa);
   issue(row_src(mode, mesh_start, L, t0).src, xb);
+#if FEAT_VIT_PF >= 2
+  if (t0 + 1 < t1) issue(row_src(mode, mesh_start, L, t0 + 1).src, xc);
+#endif
   finish(xa, vprev, raw);
   for (int t = t0; t < t1; ++t) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) xa[k] = xb[k];
+#if FEAT_VIT_PF >= 2
+#pragma unroll
+    for (int k = 0; k < 4; ++k) xb[k] = xc[k];
+    if (t + 2 < t1) issue(row_src(mode, mesh_start, L, t + 2).src, xc);  // two rows in flight during this one
+#else
     if (t + 1 < t1) issue(row_src(mode, mesh_start, L, t + 1).src, xb);  // in flight during this row
+#endif
     finish(xa, vcur, raw);
     float* orow = out + (size_t)t * ld;
 #pragma unroll
