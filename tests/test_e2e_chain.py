@@ -76,7 +76,8 @@ def chain(golden_dataset, tmp_path_factory):
     # the on-disk hand-off the reference's scripts make: one npz per accepted video (its kept frames), keypoints.npy
     # for every video, in the generated-set layout eval.py reads (flat meshes, flat keypoint dirs)
     gen, gkp = root / "generated_meshes", root / "generated_kps"
-    classes = ["Soccer", "Bowling", "Punch", "Fencing", "Biking", "Drumming"]
+    from vge.data import ACTION_CLASSES
+    classes = ACTION_CLASSES[:C]           # the golden real set's classes: every accepted video gets an AC score
     stems = [f"vgen_{classes[c]}_{c:02d}" for c in range(C)]
     j = 0
     for c in acc:
