@@ -109,19 +109,22 @@ def _rank_main(rank, ws, port, paths, q):
         dist.destroy_process_group()
 
 
-def test_two_rank_gloo_flow_matches_single_process_golden(golden_dataset, golden_flow, golden_meta):
+@pytest.mark.parametrize("ws", [2, 8])
+def test_two_rank_gloo_flow_matches_single_process_golden(golden_dataset, golden_flow, golden_meta, ws):
+    """World sizes 2 and 8 (config 4's one rank per GPU of an 8-GPU node, rehearsed on gloo): the same merged stats,
+    centroids and scores as the single-process reference, every rank scoring its own contiguous shard."""
     paths, _ = golden_dataset
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, paths, q)) for r in range(2)]
+    procs = [ctx.Process(target=_rank_main, args=(r, ws, port, paths, q)) for r in range(ws)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(timeout=600)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     out = q.get()
-    assert out["n_parts"] == 2 and min(out["sizes"]) > 0          # both ranks scored videos
+    assert out["n_parts"] == ws and min(out["sizes"]) > 0         # every rank scored videos
     np.testing.assert_allclose(out["mean"], golden_flow["stats_mean"], rtol=1e-6, atol=1e-7)
     np.testing.assert_allclose(out["std"], golden_flow["stats_std"], rtol=1e-6, atol=1e-7)
     assert np.array_equal(out["counts"], golden_flow["counts"])

@@ -33,9 +33,10 @@ def _rank_main(rank, ws, port, paths, ckpt, out_json, q, overlap="1"):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("overlap", ["1", "0"])
-def test_two_rank_run_eval_matches_golden(golden_dataset, golden_meta, tmp_path, overlap):
-    """Both phase orders: background generated-set decode + checkpoint read (default) and eval.py's serial order."""
+@pytest.mark.parametrize("ws,overlap", [(2, "1"), (2, "0"), (8, "1")])
+def test_two_rank_run_eval_matches_golden(golden_dataset, golden_meta, tmp_path, ws, overlap):
+    """Both phase orders: background generated-set decode + checkpoint read (default) and eval.py's serial order; and
+    eight ranks (config 4's one rank per GPU of a node, here all on the box's one GPU over gloo)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     paths, ckpt = golden_dataset
@@ -43,14 +44,14 @@ def test_two_rank_run_eval_matches_golden(golden_dataset, golden_meta, tmp_path,
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, paths, ckpt, out, q, overlap)) for r in range(2)]
+    procs = [ctx.Process(target=_rank_main, args=(r, ws, port, paths, ckpt, out, q, overlap)) for r in range(ws)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(timeout=300)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
-    got = dict((r, res) for r, res, _ in (q.get(), q.get()))
-    assert got[1] is None
+    got = dict((r, res) for r, res, _ in (q.get() for _ in range(ws)))
+    assert all(got[r] is None for r in range(1, ws))
     merged = got[0]
     ref = golden_meta["video_scores"]
     assert sorted(merged) == sorted(ref)
