@@ -208,6 +208,7 @@ def cpu_baseline(seconds: float, clips_per_batch: int = 32, workers: int = 4):
     loader = torch.utils.data.DataLoader(_ClipWindows(clips, mean, std), batch_size=clips_per_batch, shuffle=False,
                                          num_workers=workers, multiprocessing_context="fork")
     n_done = 0
+    marks = []  # (seconds, clips) after every batch: the spread over the sample's quarters is reported
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         for feats, idx in loader:
@@ -216,11 +217,19 @@ def cpu_baseline(seconds: float, clips_per_batch: int = 32, workers: int = 4):
             evalflow.ac_scores(seq, [cls_all[i] for i in idx], [names[i] for i in idx], cents, label)
             evalflow.tc_scores(fe, [names[i] for i in idx])
             n_done += len(idx)
+            marks.append((time.perf_counter() - t0, n_done))
             if time.perf_counter() - t0 >= seconds:
                 break
     t_used = time.perf_counter() - t0
     del loader
+    quarters = []
+    for q in range(4):  # videos/s within each quarter of the sample (the first one includes the worker start-up)
+        lo, hi = q * t_used / 4, (q + 1) * t_used / 4
+        seg = [(t, n) for t, n in marks if lo <= t <= hi]
+        if len(seg) >= 2:
+            quarters.append((seg[-1][1] - seg[0][1]) / max(seg[-1][0] - seg[0][0], 1e-9))
     return {"value": n_done / t_used, "unit": "videos/s", "cores": share, "kind": "port",
+            "quarter_rates": [round(v, 1) for v in quarters],
             "sample": f"{n_done} synthetic 32-frame clips (in-memory features, no npz decode) through the reference's "
                       f"structure: DataLoader(batch_size={clips_per_batch}, num_workers={workers}) running the oracle "
                       f"featuriser (numpy) in worker processes, torch-fp32 oracle encoder on {share} threads (the "
@@ -304,7 +313,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--clips", type=int, default=256, help="32-frame clips per GPU per step (config 2: 256)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--compute", default=None, choices=["f32x3", "f32", "f16"],
                     help="f32x3: 3xfp16 split-precision MFMA (f32-class, default of score/tag/e2e); f32: exact f32 "

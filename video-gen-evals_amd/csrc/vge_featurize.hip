@@ -243,9 +243,11 @@ __device__ __forceinline__ void featurize_vit(const float* __restrict__ vit, int
         raw[k * 4 + q] = x[k][q];
         ss += x[k][q] * x[k][q];
       }
-    const float n = fmaxf(sqrtf(wave_sum(ss)), 1e-12f);
+    // x / max(||x||, 1e-12) as x * (1 / max(...)): one division per row instead of 16 per lane (the division
+    // sequences were a quarter of this part's VALU work); within an ulp of the quotient
+    const float inv = 1.0f / fmaxf(sqrtf(wave_sum(ss)), 1e-12f);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) v[i] = raw[i] / n;
+    for (int i = 0; i < 16; ++i) v[i] = raw[i] * inv;
   };
   const int t0 = wave * 8;
   if (t0 >= mcount) return;
