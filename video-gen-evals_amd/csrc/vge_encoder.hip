@@ -251,6 +251,12 @@ struct FuseParams {
 
 // NMOD modalities in infer_dims_from_stats order: vit, global, pose, beta[, kp2d] (5, or 4 keypoint-less); enc_out
 // planes 0..NMOD-1 are the state encoders, NMOD..2 NMOD-1 the motion encoders
+// wave sum broadcast to every lane by DPP row reductions + one readlane (VALU latency): the shuffle butterfly's
+// six LDS-latency steps per sum made a row's 25 dependent sums the fusion's long pole
+__device__ __forceinline__ float wave_sum_bc(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, wave_sum_last(x)), 63));
+}
+
 template <int NMOD>
 __global__ void __launch_bounds__(256) fuse_kernel(const float* __restrict__ enc_out, int n_rows, FuseParams fp,
                                                    float* __restrict__ pooled) {
@@ -271,18 +277,18 @@ __global__ void __launch_bounds__(256) fuse_kernel(const float* __restrict__ enc
       s = s + mo;
     }
     // F.layer_norm(s, (256,)) -- no affine
-    float mu = wave_sum(s[0] + s[1] + s[2] + s[3]) / 256.0f;
+    float mu = wave_sum_bc(s[0] + s[1] + s[2] + s[3]) / 256.0f;
     floatx4 d = s - mu;
-    float var = wave_sum(d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3]) / 256.0f;
+    float var = wave_sum_bc(d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3]) / 256.0f;
     float rstd = 1.0f / sqrtf(var + 1e-5f);
     s = d * rstd;
     // kv_ln (affine)
-    mu = wave_sum(s[0] + s[1] + s[2] + s[3]) / 256.0f;
+    mu = wave_sum_bc(s[0] + s[1] + s[2] + s[3]) / 256.0f;
     d = s - mu;
-    var = wave_sum(d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3]) / 256.0f;
+    var = wave_sum_bc(d[0] * d[0] + d[1] * d[1] + d[2] * d[2] + d[3] * d[3]) / 256.0f;
     rstd = 1.0f / sqrtf(var + 1e-5f);
     kv[m] = d * rstd * kw + kb;
-    const float qk = wave_sum(u[0] * kv[m][0] + u[1] * kv[m][1] + u[2] * kv[m][2] + u[3] * kv[m][3]);
+    const float qk = wave_sum_bc(u[0] * kv[m][0] + u[1] * kv[m][1] + u[2] * kv[m][2] + u[3] * kv[m][3]);
     logit[m] = (qk / 16.0f) * fp.inv_tau[m] + fp.bias[m];
   }
   float mx = logit[0];
