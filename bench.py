@@ -431,25 +431,61 @@ def stage_roofline(stage_ms: dict, feat_ms: float, score_ms: float, windows_per_
     W = windows_per_encode
     tx = mfma(TX_FLOP_PER_WINDOW * W, stage_ms.get("transformer", 0.0), tx_mfma_peak)
     tx["l2_weight_stream_GBs"] = TX_WEIGHT_BYTES * W / (tx["avg_launch_ms"] * 1e-3) / 1e9 if tx["avg_launch_ms"] else None
+    tx["traffic"] = pmc_kernel_traffic("transformer_x3_kernel", W)
     whole = ENCODER_FLOP_PER_WINDOW * windows_per_step * steps / dt / 1e12
+    fuse = hbm(FUSE_BYTES_PER_WINDOW * W, stage_ms.get("fusion_pool", 0.0))
+    fuse["traffic"] = pmc_kernel_traffic("fuse_kernel", W)
+    feat = hbm(FEAT_BYTES_PER_WINDOW * W, feat_ms)
+    feat["traffic"] = pmc_kernel_traffic("featurize_tiles_kernel", W)
+    # score_videos: per window its seq embedding + TC term, per video its centroid and two outputs
+    score = hbm(windows_per_step * (256 + 1) * 4 + videos * (256 * 4 + 4 + 8 + 4), score_ms)
+    score["traffic"] = pmc_kernel_traffic("score_videos_kernel", windows_per_step)
     return {
         "conv_encoders": mfma(CONV_FLOP_PER_WINDOW * W, stage_ms.get("conv_encoders", 0.0)),
         "transformer": tx,
-        "fusion_pool": hbm(FUSE_BYTES_PER_WINDOW * W, stage_ms.get("fusion_pool", 0.0)),
-        "featurize": hbm(FEAT_BYTES_PER_WINDOW * W, feat_ms),
-        # score_videos: per window its seq embedding + TC term, per video its centroid and two outputs
-        "score_videos": hbm(windows_per_step * (256 + 1) * 4 + videos * (256 * 4 + 4 + 8 + 4), score_ms),
+        "fusion_pool": fuse,
+        "featurize": feat,
+        "score_videos": score,
         "whole_path": {"achieved": whole, "peak": mfma_peak, "unit": "TFLOP/s", "frac": whole / mfma_peak,
                        "flop_per_window": ENCODER_FLOP_PER_WINDOW},
+        "traffic_source": "profiles/pmc_kernels.json (tools/pmc_kernels.py; null where the pass predates the kernel's "
+                          "sources)",
     }
 
 
-def _kernel_sources_sha() -> str:
+# the sources each measured kernel is compiled from: a committed PMC pass counts for a kernel only while these are
+# unchanged (its `source_sha`)
+KERNEL_SOURCES = {
+    "conv_encoders": ("vge_encoder_x3.hip", "vge_encoder_x3s.hip", "vge_x3.h", "vge_common.h"),
+    "transformer_x3_kernel": ("vge_transformer_x3.hip", "vge_x3.h", "vge_common.h"),
+    "featurize_tiles_kernel": ("vge_featurize.hip", "vge_common.h"),
+    "fuse_kernel": ("vge_encoder.hip", "vge_common.h"),
+    "score_videos_kernel": ("vge_score.hip", "vge_common.h"),
+}
+
+
+def sources_sha(files) -> str:
     import hashlib
     h = hashlib.sha256()
-    for f in ("vge_encoder_x3.hip", "vge_encoder_x3s.hip", "vge_x3.h", "vge_common.h"):
+    for f in files:
         h.update((ROOT / "video-gen-evals_amd" / "csrc" / f).read_bytes())
     return h.hexdigest()[:16]
+
+
+def _kernel_sources_sha() -> str:
+    return sources_sha(KERNEL_SOURCES["conv_encoders"])
+
+
+def pmc_kernel_traffic(kernel: str, windows: int):
+    """HBM bytes per launch of one of the step's other kernels from the committed PMC pass (profiles/pmc_kernels.json,
+    tools/pmc_kernels.py: FETCH_SIZE x 2 + WRITE_SIZE), scaled to `windows`, only if taken on this tree's sources."""
+    try:
+        e = json.loads((ROOT / "profiles" / "pmc_kernels.json").read_text())[kernel]
+        if e.get("source_sha") != sources_sha(KERNEL_SOURCES[kernel]):
+            return None
+        return e["hbm_bytes_per_launch"] / e["windows_per_launch"] * windows
+    except (OSError, KeyError, ValueError, ZeroDivisionError):
+        return None
 
 
 def pmc_traffic(compute: str, windows: int):
