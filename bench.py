@@ -603,9 +603,9 @@ def run_score(args, world, rank, dev):
     enc.set_tail_stream(tail)
     tx_done = torch.cuda.Event()
 
-    sc_ev = []  # (start, end) events around the per-video score launch of the untimed extra steps
+    sc_ev = []  # (start, end) events around standalone per-video score launches after the timed steps
 
-    def step(i=None, time_score=False):
+    def step(i=None):
         ac = tc = None
         cur = torch.cuda.current_stream()
         sq, tw = (seq_b[n_step[0] % 2], tcw_b[n_step[0] % 2]) if mode == "side2" else (seq, tcw)
@@ -634,12 +634,7 @@ def run_score(args, world, rank, dev):
             side.wait_event(tx_done)
         sst = tail if tail is not None else (side if mode == "side2" else cur)
         with torch.cuda.stream(sst):
-            if time_score:
-                sc_ev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
-                sc_ev[-1][0].record(sst)
             ac, tc = ops.score_videos(sq, tw, first, vcls, centroids)
-            if time_score:
-                sc_ev[-1][1].record(sst)
             host_ac.copy_(ac, non_blocking=True)
             host_tc.copy_(tc, non_blocking=True)
         return ac, tc
@@ -679,7 +674,16 @@ def run_score(args, world, rank, dev):
     enc.profile_mask(0x3F)
     enc.profile_begin(n_extra * n_chunks)
     for _ in range(n_extra):
-        step(time_score=True)
+        step()
+    torch.cuda.synchronize()
+    # the per-video score kernel alone (in the pipelined step it runs on the side stream, where its events would also
+    # span the next conv that holds every CU): 10 launches on the current stream, hipEvents around each
+    sq_last, tw_last = (seq_b[(n_step[0] - 1) % 2], tcw_b[(n_step[0] - 1) % 2]) if mode == "side2" else (seq, tcw)
+    for _ in range(10):
+        sc_ev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
+        sc_ev[-1][0].record()
+        ops.score_videos(sq_last, tw_last, first, vcls, centroids)
+        sc_ev[-1][1].record()
     torch.cuda.synchronize()
     score_ms = sum(a.elapsed_time(b) for a, b in sc_ev) / max(1, len(sc_ev))
     stage_x, ncalls_x = enc.profile_read()
@@ -739,7 +743,8 @@ def run_score(args, world, rank, dev):
         "stage_ms": stage_out,
         "stage_roofline": stage_roofline(stage_out, feat_ms, score_ms, CH, NW, V, peak, tx_peak(args.compute, pk),
                                          args.steps, dt),
-        "stage_ms_source": "conv_encoders: hipEvents in the timed steps; the other stages: 5 untimed steps after them",
+        "stage_ms_source": "conv_encoders: hipEvents in the timed steps; the other stages: 5 untimed steps after them; "
+                           "score_videos: 10 standalone launches after those",
         "featurize": {"avg_ms": feat_ms, "bound": "hbm", "overlapped": mode != "serial", "pipeline": mode,
                       "achieved_GBs": FEAT_BYTES_PER_WINDOW * CH / (feat_ms * 1e-3) / 1e9, "peak_GBs": HBM_PEAK_GBS},
         "encoder_tflops_2.0203GF_per_window": ENCODER_FLOP_PER_WINDOW * NW * args.steps / dt / 1e12,

@@ -48,17 +48,14 @@ _oracle.cache = {}
 
 
 @pytest.mark.parametrize("n", [256, 600])
-@pytest.mark.parametrize("compute", ["f32x3-x3t", "f32x3-x3s", "f32x3-unstaggered", "f32"])
+@pytest.mark.parametrize("compute", ["f32x3", "f32x3-unstaggered", "f32"])
 def test_bench_workload_vs_oracle(n, compute, monkeypatch):
-    """f32x3-x3t: the staggered conv kernel on the 16x16x32 MFMA shape (vge_encoder_x3t.hip, VGE_X3T=1); f32x3-x3s
-    the same schedule on 32x32x16 (vge_encoder_x3s.hip, VGE_X3T=0); both fold GroupNorm forward.  f32x3-unstaggered
-    the quad / pair kernel they replaced (VGE_X3S=0, weights unfolded); f32 the exact-f32 MFMA kernels."""
+    """f32x3 runs the staggered conv kernel (vge_encoder_x3s.hip, GroupNorm folded forward); f32x3-unstaggered the
+    quad / pair kernel it replaced (VGE_X3S=0, weights unfolded); f32 the exact-f32 MFMA kernels."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     if compute == "f32x3-unstaggered":
         monkeypatch.setenv("VGE_X3S", "0")
-    elif compute.startswith("f32x3-x3"):
-        monkeypatch.setenv("VGE_X3T", "1" if compute.endswith("t") else "0")
     compute = compute.split("-")[0]
     from vge import ops
     from vge.data import pack_frame_store

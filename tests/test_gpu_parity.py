@@ -252,14 +252,11 @@ def test_x3_large_weights_and_nonfinite(vg, golden_state_dict):
 
 
 @pytest.mark.parametrize("n", [37, 256, 293, 600])
-@pytest.mark.parametrize("x3t", ["1", "0"])
-def test_x3_quad_and_pair_blocks_vs_f32(vg, golden_state_dict, n, x3t, monkeypatch):
+def test_x3_quad_and_pair_blocks_vs_f32(vg, golden_state_dict, n):
     """Large batches run the conv chain in 4-window (quad) blocks with 2-window blocks filling the last round
     (37: pairs and a half-empty pair; 256: quads + a round of pairs; 293: quads + one half-empty pair; 600: quads
-    only), on both MFMA shapes of the staggered kernel (VGE_X3T).  Checked against the exact-f32 MFMA path (itself
-    pinned to the oracle above) on the same input."""
+    only).  Checked against the exact-f32 MFMA path (itself pinned to the oracle above) on the same input."""
     VE, ops = vg
-    monkeypatch.setenv("VGE_X3T", x3t)
     torch.manual_seed(n)
     x = torch.randn(n, 32, 2596, device=DEV)
     x[:, :, 40:48] *= 1e4   # a few large z-scores: per-row / per-window scaling at work

@@ -51,8 +51,7 @@ struct GemmArgsX3Host {
 hipError_t launch_conv_encoders_x3(const float*, int, const void*, int, unsigned, float*, bool, bool, hipStream_t);
 hipError_t encoder_x3s_kernel_setup();
 hipError_t launch_conv_encoders_x3s(const float*, int, const void*, int, unsigned, float*, int*, hipStream_t);
-hipError_t encoder_x3t_kernel_setup();
-hipError_t launch_conv_encoders_x3t(const float*, int, const void*, int, unsigned, float*, int*, hipStream_t);
+
 bool conv_f16w_plan(int n_windows, int n_enc, int wmax, int& G, int& R, int& U);
 hipError_t launch_conv_f16w_table(int n_windows, int n_enc, int G, int R, int U, int* d_table, hipStream_t s);
 hipError_t launch_conv_encoders_f16w(const float*, int, const void*, float*, const int*, int, int, hipStream_t);
@@ -111,9 +110,6 @@ int fail(int code, const std::string& msg) {
   } while (0)
 
 hipStream_t S(vge_stream_t s) { return reinterpret_cast<hipStream_t>(s); }
-
-// the f32x3 conv kernel on the 16x16x32 MFMA shape by default (env VGE_X3T=0|1 overrides)
-constexpr bool kX3tDefault = false;
 
 const char* kMods[5] = {"vit", "global", "pose", "beta", "kp2d"};
 const int kDimsRaw[5] = {1024, 9, 207, 10, 120};
@@ -232,7 +228,6 @@ struct vge_encoder {
   bool tx_fused = true;           // x3: one fused transformer launch (VGE_X3_UNFUSED=1: per-layer kernels)
   unsigned stem_heavy = 0;        // bit e: encoder e's stem spans more than one 256-wide K panel (vit)
   bool x3s = false;               // VGE_F32X3: the staggered conv kernel on GroupNorm-folded weights (VGE_X3S=0: off)
-  bool x3t = false;               // ... on the 16x16x32 MFMA shape (vge_encoder_x3t.hip; VGE_X3T=0: the 32x32x16 one)
   int f16_mix = 0;                // VGE_F16: stages kept in 3xfp16 (bit 0 stem, bit 1 transformer; VGE_F16_MIX)
   // VGE_F16 with the stem unsplit: the unit-table conv kernel with units of up to `f16w` windows (VGE_F16W; 0 = the
   // quad / pair kernel); its table for batch units_B lives in d_units (sized by vge_encoder_reserve, built on the
@@ -707,13 +702,9 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
       }
   }
   enc->x3s = x3s;
-  {
-    const char* v = getenv("VGE_X3T");
-    enc->x3t = x3s && (v ? v[0] == '1' : kX3tDefault);
-  }
   hipError_t he = x3 ? vge::encoder_x3_kernel_setup() : vge::encoder_kernel_setup();
   if (he == hipSuccess && x3s) he = vge::encoder_x3s_kernel_setup();
-  if (he == hipSuccess && enc->x3t) he = vge::encoder_x3t_kernel_setup();
+
   if (he == hipSuccess) he = hipMalloc(&enc->wbuf, pk.size() * sizeof(float));
   if (he == hipSuccess) he = hipMemcpy(enc->wbuf, pk.data(), pk.size() * sizeof(float), hipMemcpyHostToDevice);
   if (he == hipSuccess && x3) he = hipMalloc(&enc->hbuf, ph_n * sizeof(_Float16));
@@ -1038,9 +1029,6 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
     enc->units_last = k;
     HIPCHK(vge::launch_conv_encoders_f16w(feats, B, enc->d_encs, enc->enc_out, enc->d_units + (size_t)k * enc->units_cap,
                                           enc->tables[k].G, enc->tables[k].R, s));
-  } else if (x3 && enc->x3t) {
-    HIPCHK(vge::launch_conv_encoders_x3t(feats, B, enc->d_encs, enc->n_enc, enc->stem_heavy, enc->enc_out,
-                                         enc->status_d, s));
   } else if (x3 && enc->x3s) {
     HIPCHK(vge::launch_conv_encoders_x3s(feats, B, enc->d_encs, enc->n_enc, enc->stem_heavy, enc->enc_out,
                                          enc->status_d, s));

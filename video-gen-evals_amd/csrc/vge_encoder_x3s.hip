@@ -693,7 +693,6 @@ hipError_t encoder_x3s_kernel_setup() {
 // spin bound of the half-workgroup exchange (test hook vge_debug_set_x3s_spin_limit: 0 makes every wave that arrives
 // before its group's last one give up, which must surface as VGE_ERR_DEVICE)
 static int g_x3s_spin_limit = 1 << 22;
-int g_x3s_spin_limit_value() { return g_x3s_spin_limit; }  // (the 16x16x32 kernel, vge_encoder_x3t.hip, shares it)
 
 hipError_t launch_conv_encoders_x3s(const float* feats, int n_windows, const void* encs, int n_enc, unsigned heavy,
                                     float* enc_out, int* status, hipStream_t s) {

@@ -410,43 +410,73 @@ __global__ void __launch_bounds__(256) featurize_tiles_kernel(
       if (tid + 256 * k < SLOTS * 120) stage[tid + 256 * k] = v[k];
   }
   __syncthreads();
-  // ---- (d1) keypoints: centre + Frobenius-normalise every slot (utils.py:191-196)
-  for (int slot = wave; slot <= kcount; slot += 4) {
-    float x = 0.f, y = 0.f;
-    if (lane < 60) {
-      x = stage[slot * 120 + 2 * lane];
-      y = stage[slot * 120 + 2 * lane + 1];
+  // ---- (d1) keypoints: centre + Frobenius-normalise every slot (utils.py:191-196).  A wave's slots (wave, wave + 4,
+  // ...) are unrolled so their wave sums -- each a chain of six dependent lane shuffles -- run interleaved instead of
+  // one after another (the keypoint workgroup was the kernel's long pole)
+  {
+    constexpr int KS = (SLOTS + 3) / 4;
+    float x[KS], y[KS], cx[KS], cy[KS], mx[KS], my[KS], ss[KS];
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      const int slot = wave + 4 * k;
+      const bool ok = slot <= kcount && lane < 60;
+      x[k] = ok ? stage[slot * 120 + 2 * lane] : 0.f;
+      y[k] = ok ? stage[slot * 120 + 2 * lane + 1] : 0.f;
     }
     // (wave_sum: the butterfly order the parity tests pinned; the Procrustes SVD is sensitive near rank 1)
-    const float mx = wave_sum(x) / 60.0f;
-    const float my = wave_sum(y) / 60.0f;
-    const float cx = x - mx, cy = y - my;
-    const float ss = wave_sum(lane < 60 ? (cx * cx + cy * cy) : 0.f);
-    const float sc = fmaxf(sqrtf(ss), 1e-6f);
-    if (lane < 60) {
-      pn[slot][2 * lane] = cx / sc;
-      pn[slot][2 * lane + 1] = cy / sc;
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      mx[k] = wave_sum(x[k]) / 60.0f;
+      my[k] = wave_sum(y[k]) / 60.0f;
+    }
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      cx[k] = x[k] - mx[k];
+      cy[k] = y[k] - my[k];
+      ss[k] = wave_sum(lane < 60 ? (cx[k] * cx[k] + cy[k] * cy[k]) : 0.f);
+    }
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      const int slot = wave + 4 * k;
+      const float sc = fmaxf(sqrtf(ss[k]), 1e-6f);
+      if (slot <= kcount && lane < 60) {
+        pn[slot][2 * lane] = cx[k] / sc;
+        pn[slot][2 * lane + 1] = cy[k] / sc;
+      }
     }
   }
   __syncthreads();  // pn[] complete
 
-  // ---- (d2) keypoints raw + Procrustes velocity (utils.py:177-217): H of every row by wave sums, then the
-  // 2x2 SVDs of all rows in parallel on the lanes of wave 0 (one dependent LAPACK chain instead of eight
-  // per wave), then the deltas
-  for (int t = wave; t < kcount; t += 4) {
-    const RowSrc rs = row_src(mode, td.kp_start, Lk, t);
-    float* orow = out + (size_t)t * ld;
-    for (int c = lane; c < 120; c += 64) orow[C_KP_RAW + c] = znorm(stage[(t + 1) * 120 + c], mean, stdv, C_KP_RAW + c);
-    if (!rs.first) {
+  // ---- (d2) keypoints raw + Procrustes velocity (utils.py:177-217): H of every row by wave sums (a wave's 8 rows
+  // unrolled, 32 independent sums), then the 2x2 SVDs of all rows in parallel on the lanes of wave 0 (one dependent
+  // LAPACK chain instead of eight per wave), then the deltas
+  {
+    float h[8][4];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int t = wave + 4 * k;
+      const bool use = t < kcount && !row_src(mode, td.kp_start, Lk, t).first;  // (wave-uniform)
       float x0 = 0.f, x1 = 0.f, y0 = 0.f, y1 = 0.f;
-      if (lane < 60) {
+      if (use && lane < 60) {
         x0 = pn[t][2 * lane]; x1 = pn[t][2 * lane + 1];
         y0 = pn[t + 1][2 * lane]; y1 = pn[t + 1][2 * lane + 1];
       }
-      const float h00 = wave_sum(x0 * y0), h01 = wave_sum(x0 * y1);
-      const float h10 = wave_sum(x1 * y0), h11 = wave_sum(x1 * y1);
-      if (lane == 0) {
-        kR[t][0] = h00; kR[t][1] = h01; kR[t][2] = h10; kR[t][3] = h11;
+      h[k][0] = x0 * y0; h[k][1] = x0 * y1; h[k][2] = x1 * y0; h[k][3] = x1 * y1;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) h[k][q] = wave_sum(h[k][q]);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int t = wave + 4 * k;
+      if (t < kcount) {
+        float* orow = out + (size_t)t * ld;
+        for (int c = lane; c < 120; c += 64)
+          orow[C_KP_RAW + c] = znorm(stage[(t + 1) * 120 + c], mean, stdv, C_KP_RAW + c);
+        if (lane == 0 && !row_src(mode, td.kp_start, Lk, t).first) {
+          kR[t][0] = h[k][0]; kR[t][1] = h[k][1]; kR[t][2] = h[k][2]; kR[t][3] = h[k][3];
+        }
       }
     }
   }
