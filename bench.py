@@ -332,6 +332,8 @@ def main():
                          "roofline is not measured in this mode); serial = one stream, featurise right before each "
                          "encode")
     ap.add_argument("--serial-featurize", action="store_true", help="= --pipeline serial")
+    ap.add_argument("--event-every", type=int, default=1,
+                    help="record the conv stage's hipEvents on every k-th timed step (each event is a queue marker)")
     ap.add_argument("--serial-extract", action="store_true",
                     help="e2e: run TokenHMR and DWPose one after the other on one stream (default: two streams)")
     ap.add_argument("--no-detector", action="store_true",
@@ -567,6 +569,7 @@ def run_score(args, world, rank, dev):
     # side2: scores run on the side stream while the next step's encodes write the other buffer pair
     seq_b, tcw_b = [seq, torch.empty_like(seq)], [tcw, torch.empty_like(tcw)]
     n_step = [0]
+    n_timed = [0]  # timed steps started (the --event-every sampling)
     host_ac = torch.empty((V,), dtype=torch.float32, pin_memory=True)
     host_tc = torch.empty((V,), dtype=torch.float64, pin_memory=True)
     n_chunks = (NW + CH - 1) // CH
@@ -618,6 +621,8 @@ def run_score(args, world, rank, dev):
                 if pending[0] != c:
                     launch_feat(c)
                 cur.wait_event(feat_ready)
+            if timing[0]:  # the conv stage's two events on every --event-every-th step of the timed region
+                enc.profile_mask(0x3 if n_timed[0] % args.event_every == 0 else 0)
             enc.encode(feats[: b1 - b0], frame_embed=False, tc=True, seq_out=sq[b0:b1], tc_out=tw[b0:b1])
             if mode in ("side", "side2"):
                 launch_feat((c + 1) % n_chunks)  # the next chunk, or the next step's first
@@ -661,11 +666,13 @@ def run_score(args, world, rank, dev):
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(i)
+        n_timed[0] += 1
     torch.cuda.synchronize()
     timing[0] = False
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    enc.profile_mask(0x3)  # (profile_read finds the last recorded event from the mask)
     # every rank's (wall time, videos): the line's time is the max over ranks, `value` all ranks' videos / that time
     per_rank = gather_rank_times(dt, V, world, dev)
     dt = max(t for t, _ in per_rank)

@@ -207,7 +207,8 @@ int vge_encoder_status(const vge_encoder* enc);
 int vge_encoder_clear_status(vge_encoder* enc);
 /* Which of the VGE_N_STAGES + 1 stage-boundary events profiled vge_encode calls record (bit k = event before stage k;
  * default all): each event is a queue marker, so a timed loop that only needs the conv stage records 0x3 and
- * profile_read reports the stages both of whose events were recorded (the others as 0). */
+ * profile_read reports the stages both of whose events were recorded (the others as 0).  Mask 0: later calls are not
+ * profiled and take no slot (a caller can sample every k-th call inside a timed loop). */
 int vge_encoder_profile_mask(vge_encoder* enc, int event_mask);
 
 /* ---------------------------------------------------------------------------------------------

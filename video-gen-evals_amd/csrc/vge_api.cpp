@@ -993,7 +993,9 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
   hipStream_t s = S(stream);
   const int frames = B * 32, M = B * 33;
   hipEvent_t* ev = nullptr;
-  if (enc->prof_calls < enc->prof_max) ev = enc->prof_ev.data() + (size_t)(enc->prof_calls++) * (VGE_N_STAGES + 1);
+  // (mask 0: this call is not profiled and takes no slot -- callers sample every k-th call)
+  if (enc->prof_mask != 0 && enc->prof_calls < enc->prof_max)
+    ev = enc->prof_ev.data() + (size_t)(enc->prof_calls++) * (VGE_N_STAGES + 1);
   auto mark = [&](int k) -> hipError_t {
     return (ev && ((enc->prof_mask >> k) & 1)) ? hipEventRecord(ev[k], s) : hipSuccess;
   };
