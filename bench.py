@@ -22,7 +22,8 @@ mode (`f16`: VGE_F16, fp16 MFMA conv encoders) run on the same workload and repo
 
 Rank 0 prints ONE JSON line.  `roofline` is for the dominant kernel (the 10 MovementConvEncoders,
 MFMA-bound): achieved = its algorithmic FLOPs per launch (1.7622 GFLOP per window)
-/ its average duration from hipEvents recorded around it on its stream inside the timed steps; peak =
+/ its average duration from hipEvents recorded around it on its stream inside the timed steps (every --event-every-th
+step, default 5: each event is a queue marker); peak =
 the MFMA ceiling of the compute mode from rocminfo (CUs x max clock: f16 dense 4096 FLOP/clk/CU, 2516.6 TF on
 MI355X; 3xfp16 split: / 3 = 838.9 TF; exact f32 256 FLOP/clk/CU, 157.3 TF; `peak_source`).  `traffic` = HBM bytes per launch from the committed PMC pass
 (profiles/pmc_conv_encoder.json, FETCH_SIZE x2 + WRITE_SIZE per the guide), reported only when that pass
@@ -332,8 +333,10 @@ def main():
                          "roofline is not measured in this mode); serial = one stream, featurise right before each "
                          "encode")
     ap.add_argument("--serial-featurize", action="store_true", help="= --pipeline serial")
-    ap.add_argument("--event-every", type=int, default=1,
-                    help="record the conv stage's hipEvents on every k-th timed step (each event is a queue marker)")
+    ap.add_argument("--event-every", type=int, default=5,
+                    help="record the conv stage's (and featurise's) hipEvents on every k-th timed step, from the first: "
+                         "each event is a queue marker (measured: all steps 184.2k-185.4k videos/s, every 5th "
+                         "186.4k-186.5k, same box)")
     ap.add_argument("--serial-extract", action="store_true",
                     help="e2e: run TokenHMR and DWPose one after the other on one stream (default: two streams)")
     ap.add_argument("--no-detector", action="store_true",
@@ -583,7 +586,8 @@ def run_score(args, world, rank, dev):
 
     def featurize_chunk(c, stream):
         b0, b1 = c * CH, min(NW, (c + 1) * CH)
-        k = n_fe[0] if timing[0] else None
+        # (its events follow the conv's sampling: every --event-every-th timed step)
+        k = n_fe[0] if timing[0] and n_timed[0] % args.event_every == 0 else None
         if k is not None:
             fe0[k].record(stream)
         ops.featurize(gstore, windows[b0:b1], stats.mean, stats.std, out=feats[: b1 - b0])
