@@ -30,6 +30,24 @@ import torch
 import torch.distributed as dist
 
 BF16_MFMA_PEAK_TFLOPS = 2516.6
+# kernel sources whose PMC pass (tools/profile_e2e.sh -> tools/pmc_e2e.py -> profiles/pmc_e2e.json) gives `traffic`
+E2E_KERNEL_SOURCES = {"gemm_bf16_kernel": ["vge_vit.hip"],
+                      "yolox_conv": ["vge_cnn.hip", "vge_cnn_host.h", "vge_yolox.cpp"]}
+YOLOX_CHUNK = 256   # frames per detector pass (tools/yolox_prof.py --chunk: 637 vs 618 TFLOP/s at 64)
+
+
+def e2e_traffic(kernel: str, frames: float):
+    """HBM bytes (FETCH_SIZE x 2 + WRITE_SIZE) of `frames` frames through `kernel` from the committed PMC pass, only
+    while the kernel's sources hash to the pass's `source_sha`; else None."""
+    from pathlib import Path
+    from bench import sources_sha
+    try:
+        e = json.loads((Path(__file__).resolve().parent / "profiles" / "pmc_e2e.json").read_text())[kernel]
+        if e.get("source_sha") != sources_sha(E2E_KERNEL_SOURCES[kernel]):
+            return None
+        return e["hbm_bytes_per_frame"] * frames
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def cpu_baseline_e2e(seconds: float, detector: bool = True):
@@ -111,7 +129,7 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
     del hsd
     dw = DwposeExtractor(synth.make_rtmpose_state_dict(RTMPOSE_L), RTMPOSE_L, device=dev, max_instances=2 * FC)
     det = None if args.no_detector else YoloxDetector(synth.make_gate_detector_state_dict(YOLOX_L), YOLOX_L,
-                                                      device=dev, chunk=min(FC, 64))
+                                                      device=dev, chunk=min(FC, YOLOX_CHUNK))
     no_box = np.zeros(FC, np.int32)
     Hf = Wf = 256
     whole = np.tile(np.array([0, 0, Wf, Hf], np.float32), (FC, 1))
@@ -330,13 +348,18 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
         "roofline": {"bound": "mfma", "kernel": "gemm_bf16_kernel (ViT-H/16 backbone: patch-embed, qkv, proj, fc1, "
                                                 "fc2; dense bf16 MFMA peak)",
                      "achieved": achieved, "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / BF16_MFMA_PEAK_TFLOPS, "traffic": None,
+                     "frac": achieved / BF16_MFMA_PEAK_TFLOPS,
+                     "traffic": e2e_traffic("gemm_bf16_kernel", hmr_frames_per_call),
+                     "traffic_source": "profiles/pmc_e2e.json (tools/profile_e2e.sh: PMC of the same kernel on "
+                                       "tools/time_hmr.py, bytes per frame x frames per call)",
                      "flop_per_call": gemm_flops_per_frame * hmr_frames_per_call, "gemm_ms_per_call": gemm_ms,
                      "frames_per_call": hmr_frames_per_call},
         "stage_ms": {**{f"hmr_{k}": v / n for k, v in st.items()},
                      **{f"dwpose_{k}": v / max(dcalls, 1) for k, v in dst.items()},
                      **{f"yolox_{k}": v / max(ycalls, 1) for k, v in yst.items()}},
         "yolox_gemm_tflops": (y_flops / (yst["gemm"] / ycalls * 1e-3) / 1e12) if ycalls else None,
+        "yolox_traffic_per_call": e2e_traffic("yolox_conv", FC) if ycalls else None,
+        "yolox_chunk_frames": min(FC, YOLOX_CHUNK) if det is not None else None,
         "dwpose_gemm_tflops": dw_flops / (dst["gemm"] / max(dcalls, 1) * 1e-3) / 1e12,
         "frames_per_s": world * F * args.steps / dt,
         "front_end": {"detector": ("YOLOX-L (stand-in for detectron2 Faster R-CNN X101-FPN; "

@@ -174,22 +174,58 @@ def test_conv_persistent_matches_one_tile_per_workgroup(D, n, H, W, Cin, Cout, k
     lib.vge_debug_set_conv_persist.argtypes = [C.c_int]
     lib.vge_debug_set_conv_v1.argtypes = [C.c_int]
     lib.vge_debug_set_conv_tall.argtypes = [C.c_int]
+    lib.vge_debug_set_conv_variant.argtypes = [C.c_int]
     x = _bf((n, H, W, Cin), seed=7).to(DEV)
     w = _bf((Cout, Cin, k, k), (2.0 / (Cin * k * k)) ** 0.5, seed=8).to(DEV)
     b = (torch.randn(Cout, generator=torch.Generator().manual_seed(9)) * 0.1).to(DEV)
     outs = []
     try:
-        for v1, p, tall in ((0, 0, 0), (0, 1, 0), (1, 1, 0), (1, 1, 1)):  # every conv variant the tuner picks from
+        # every conv variant the tuner picks from; the last is the 512 x 128 persistent tile (variant 6)
+        for v1, p, tall, force in ((0, 0, 0, 0), (0, 1, 0, 0), (1, 1, 0, 0), (1, 1, 1, 0), (0, 1, 0, 6)):
             lib.vge_debug_set_conv_v1(v1)
             lib.vge_debug_set_conv_persist(p)
             lib.vge_debug_set_conv_tall(tall)
+            lib.vge_debug_set_conv_variant(force)
             outs.append(D.conv_bf16(x, w, b, stride=stride, pad=k // 2, act=act, out_f32=outf32))
             torch.cuda.synchronize()
     finally:
         lib.vge_debug_set_conv_persist(1)
         lib.vge_debug_set_conv_v1(0)
         lib.vge_debug_set_conv_tall(0)
+        lib.vge_debug_set_conv_variant(0)
     assert all(torch.equal(outs[0], o) for o in outs[1:])
+
+
+@gpu
+@pytest.mark.parametrize("n,H,W,Cin,Cout,k,res", [
+    (64, 80, 80, 128, 128, 3, "bf16"),      # YOLOX CSP bottleneck 3x3 with its identity
+    (5, 33, 47, 64, 128, 3, "bf16"),        # ragged M (tile tail)
+    (9, 21, 19, 128, 96, 1, "f32"),         # RTMCCBlock-style scaled f32 residual, Cout < 128
+])
+def test_conv_wide_tile_residual_matches_default(D, n, H, W, Cin, Cout, k, res):
+    """The 512 x 128 persistent tile (variant 6) with residual epilogues (bf16 identity after SiLU; f32 x per-column
+    scale) is bit-identical to the default kernel's."""
+    import ctypes as C
+    from vge import lib as Lb
+    lib = Lb.load()
+    lib.vge_debug_set_conv_variant.argtypes = [C.c_int]
+    x = _bf((n, H, W, Cin), seed=17).to(DEV)
+    w = _bf((Cout, Cin, k, k), (2.0 / (Cin * k * k)) ** 0.5, seed=18).to(DEV)
+    b = (torch.randn(Cout, generator=torch.Generator().manual_seed(19)) * 0.1).to(DEV)
+    if res == "bf16":
+        r, rs, act = _bf((n, H, W, Cout), seed=20).to(DEV), None, "silu"
+    else:
+        r = torch.randn((n, H, W, Cout), generator=torch.Generator().manual_seed(21)).to(DEV)
+        rs, act = (torch.rand(Cout, generator=torch.Generator().manual_seed(22)) + 0.5).to(DEV), "none"
+    outs = []
+    try:
+        for force in (0, 6):
+            lib.vge_debug_set_conv_variant(force)
+            outs.append(D.conv_bf16(x, w, b, stride=1, pad=k // 2, act=act, res=r, rscale=rs))
+            torch.cuda.synchronize()
+    finally:
+        lib.vge_debug_set_conv_variant(0)
+    assert torch.equal(outs[0], outs[1])
 
 
 @gpu

@@ -1,0 +1,24 @@
+#!/bin/bash
+# Config-3 extractor profiles on the GPU box (one rocprofv3 run per pass; no tracing domains with --pmc):
+#   hmr_{fetch,write}    PMC of the TokenHMR extractor alone (tools/time_hmr.py, full ViT-H/16, 256 frames x 3 calls)
+#   yolox_{trace,fetch,write}  kernel trace + stats and PMC of the detector on one e2e pass (tools/yolox_prof.py,
+#                        1,024 frames in 256-frame chunks, 2 profiled calls)
+# Summarise with tools/pmc_e2e.py TAG (-> profiles/pmc_e2e.json) and tools/yolox_prof_check.py.
+#   Usage (repo root, GPU box): bash tools/profile_e2e.sh TAG
+set -u
+TAG=$1
+R=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$R/gpurun_out; mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+run() {  # name, script args (as one string), extra rocprofv3 args...
+  local name=$1 cmd=$2; shift 2
+  timeout -k 10 300 rocprofv3 "$@" --output-format csv -d "$OUT/pe_${TAG}_$name" -o run -- python3 $cmd \
+    > "$OUT/pe_${TAG}_$name.log" 2>&1
+  local rc=$?; echo "[$name] rc=$rc"; return $rc
+}
+HMR="$R/tools/time_hmr.py --frames 256 --iters 2"
+YOLOX="$R/tools/yolox_prof.py --frames 1024 --calls 2 --chunk 256"
+run yolox_trace "$YOLOX" --kernel-trace --stats &&
+run yolox_fetch "$YOLOX" --pmc FETCH_SIZE --kernel-trace &&
+run yolox_write "$YOLOX" --pmc WRITE_SIZE --kernel-trace &&
+run hmr_fetch "$HMR" --pmc FETCH_SIZE --kernel-trace &&
+run hmr_write "$HMR" --pmc WRITE_SIZE --kernel-trace

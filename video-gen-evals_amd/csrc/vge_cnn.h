@@ -15,7 +15,8 @@ struct ConvLaunch {
   int act, out_f32, res_mode, tn;           // act 0 none / 1 SiLU / 2 sigmoid; res 0 / 1 bf16 / 2 f32 scaled
   int variant;                              // 0 default; 1 128-row kernel (tn <= 128); 2 256 x 256 tiles, one per
                                             // workgroup; 3 256 x 256 tiles on the persistent grid (res_mode 0 only);
-                                            // 5 256-row tiles with tn (64 / 128) columns
+                                            // 5 256-row tiles with tn (64 / 128) columns; 6 512 x 128 tiles on
+                                            // the persistent grid
 };
 
 struct WarpInst {  // warp_prep_kernel: source frame and affine map of one pose instance

@@ -230,15 +230,20 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
 // Epilogue through LDS (wave-private 64-row chunks re-read row-major, 4 columns per lane).
 constexpr int C2_M = 256, C2_ST = 5;
 
-template <int BN>
+// BM = 512 ("wide-M", BN 128 only): 8 waves of 128 x 64 as in the 256 x 256 tile, for layers with 128 output
+// channels; 40 KB stages, so the ring has 4 slots (all 160 KB of LDS) and two stages in flight instead of three
+template <int BN, int BM = C2_M>
 struct C2Cfg {
+  static_assert(BM == C2_M || (BM == 512 && BN == 128), "tile shapes");
   static constexpr int WM = BN == 256 ? 2 : 4, WN = 8 / WM;
-  static constexpr int WR = C2_M / WM, WC = BN / WN;          // wave tile
+  static constexpr int WR = BM / WM, WC = BN / WN;            // wave tile
   static constexpr int TM = WR / 32, TN = WC / 32;            // 32x32 MFMA tiles per wave
-  static constexpr int TA = C2_M * CV_K * 2, TB = BN * CV_K * 2, SLOT = TA + TB;
+  static constexpr int TA = BM * CV_K * 2, TB = BN * CV_K * 2, SLOT = TA + TB;
+  static constexpr int AJ = BM / 128;                         // A wave-instructions (16 rows each) per wave per stage
   static constexpr int BQ = BN / 128;                         // B wave-instructions per wave per stage
-  static constexpr int LPS = 2 + BQ;                          // global_load_lds per thread per stage
-  static constexpr int RING = C2_ST * SLOT, EPI = 8 * 64 * WC * 4;
+  static constexpr int LPS = AJ + BQ;                         // global_load_lds per thread per stage
+  static constexpr int ST = BM == C2_M ? C2_ST : 4;           // ring slots
+  static constexpr int RING = ST * SLOT, EPI = 8 * 64 * WC * 4;
   static constexpr int LDS = RING > EPI ? RING : EPI;
 };
 
@@ -448,16 +453,16 @@ __device__ __forceinline__ void quad_t4(float& v0, float& v1, float& v2, float& 
   v3 = o2 ? v3 : y;
 }
 
-template <int BN, int ACT, int OUT, int RES>
+template <int BN, int ACT, int OUT, int RES, int BM>
 __global__ void __launch_bounds__(512, 1) conv2p_bf16_kernel(ConvArgs a) {
-  using Cf = C2Cfg<BN>;
-  constexpr int TM = Cf::TM, TN = Cf::TN, LPS = Cf::LPS, BQ = Cf::BQ;
+  using Cf = C2Cfg<BN, BM>;
+  constexpr int TM = Cf::TM, TN = Cf::TN, LPS = Cf::LPS, BQ = Cf::BQ, AJ = Cf::AJ, ST = Cf::ST;
   constexpr int NST = TM * TN * 4;  // epilogue stores per thread
   extern __shared__ __attribute__((aligned(16))) char lds[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / Cf::WN, wn = wave % Cf::WN;
-  const int ntn = (a.Cout + BN - 1) / BN, ntiles = ((a.M + C2_M - 1) / C2_M) * ntn;
+  const int ntn = (a.Cout + BN - 1) / BN, ntiles = ((a.M + BM - 1) / BM) * ntn;
   const int G = gridDim.x, b = blockIdx.x;
   const int T = (ntiles - b + G - 1) / G;  // host: G <= ntiles, G % 8 == 0 unless G == ntiles
   const int nk = (a.Kp / CV_K + 1) & ~1, total = T * nk;  // even: an odd K gets one all-zero stage (zero page)
@@ -465,22 +470,22 @@ __global__ void __launch_bounds__(512, 1) conv2p_bf16_kernel(ConvArgs a) {
   const int lc = (lane & 3) ^ ((lane >> 4) & 3);
 
   // ---- issue side: gather state of the tile whose stages are being issued
-  int img_hw[2], ih0[2], iw0[2];
-  bool mval[2];
+  // per A row two registers: the pixel index of its (kh, kw) = (0, 0) tap, and (ih0 << 16) | (iw0 & 0xFFFF) (a row
+  // past M gets ih0 = -16384, which fails every tap's bounds check)
+  int pix0[AJ], hw0[AJ];
   const bf16* wrow[BQ];
   auto setup = [&](int i) {
     const int bid = xcd_remap(b + i * G, ntiles);
-    const int mt = bid / ntn, m0 = mt * C2_M, n0 = (bid - mt * ntn) * BN;
+    const int mt = bid / ntn, m0 = mt * BM, n0 = (bid - mt * ntn) * BN;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int m = m0 + 16 * (2 * wave + j) + (lane >> 2);
-      mval[j] = m < a.M;
+    for (int j = 0; j < AJ; ++j) {
+      const int m = m0 + 16 * (AJ * wave + j) + (lane >> 2);
       const int hw = a.Ho * a.Wo;
       const int img = m / hw, rem = m - img * hw;
       const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
-      img_hw[j] = img * a.H;
-      ih0[j] = oh * a.stride - a.pad;
-      iw0[j] = ow * a.stride - a.pad;
+      const int ih0 = m < a.M ? oh * a.stride - a.pad : -16384, iw0 = ow * a.stride - a.pad;
+      pix0[j] = (img * a.H + ih0) * a.W + iw0;
+      hw0[j] = (ih0 << 16) | (iw0 & 0xFFFF);
     }
 #pragma unroll
     for (int j = 0; j < BQ; ++j) wrow[j] = a.w + (size_t)(n0 + 16 * (BQ * wave + j) + (lane >> 2)) * a.Kp + lc * 8;
@@ -495,15 +500,16 @@ __global__ void __launch_bounds__(512, 1) conv2p_bf16_kernel(ConvArgs a) {
         setup(++is_t);
       }
     }
-    char* slot = lds + (is_g % C2_ST) * Cf::SLOT;
+    char* slot = lds + (is_g % ST) * Cf::SLOT;
     const int k = is_k * CV_K + lc * 8;
     const int tap = k >> a.cin_log2, ci = k & cmask;
     const int kh = (tap * a.kw_magic) >> 16, kw = tap - kh * a.KW;
+    const int toff = kh * a.W + kw;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int ih = ih0[j] + kh, iw = iw0[j] + kw;
-      const bool ok = mval[j] && tap < a.taps && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-      glds16(ok ? a.x + ((size_t)(img_hw[j] + ih) * a.W + iw) * a.ldx + ci : a.zero, slot + (2 * wave + j) * 1024);
+    for (int j = 0; j < AJ; ++j) {
+      const int ih = (hw0[j] >> 16) + kh, iw = (int)(short)hw0[j] + kw;
+      const bool ok = tap < a.taps && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      glds16(ok ? a.x + (size_t)(unsigned)(pix0[j] + toff) * a.ldx + ci : a.zero, slot + (AJ * wave + j) * 1024);
     }
     const bool kin = is_k * CV_K < a.Kp;
 #pragma unroll
@@ -516,7 +522,7 @@ __global__ void __launch_bounds__(512, 1) conv2p_bf16_kernel(ConvArgs a) {
     bf16x8 a[2][TM], b[2][TN];
   };
   auto read = [&](int g, Frag& f) {
-    const char* cur = lds + (g % C2_ST) * Cf::SLOT;
+    const char* cur = lds + (g % ST) * Cf::SLOT;
     const char* As = cur + wm * Cf::WR * 64 + rowoff;
     const char* Bs = cur + Cf::TA + wn * Cf::WC * 64 + rowoff;
 #pragma unroll
@@ -561,7 +567,7 @@ __global__ void __launch_bounds__(512, 1) conv2p_bf16_kernel(ConvArgs a) {
   auto tile_mn = [&](int i, int& m0, int& n0) {
     const int bid = xcd_remap(b + i * G, ntiles);
     const int mt = bid / ntn;
-    m0 = mt * C2_M;
+    m0 = mt * BM;
     n0 = (bid - mt * ntn) * BN;
   };
   // bias / rscale: asm loads, invisible to hipcc's waitcnt pass (which answers any load issued among LDS-DMA ring
@@ -592,7 +598,7 @@ __global__ void __launch_bounds__(512, 1) conv2p_bf16_kernel(ConvArgs a) {
     consts_wait();
     int m0, n0;
     tile_mn(i, m0, n0);
-    const int rows = min(C2_M, a.M - m0);
+    const int rows = min(BM, a.M - m0);
     const __amdgpu_buffer_rsrc_t ob = __builtin_amdgcn_make_buffer_rsrc(
         reinterpret_cast<char*>(a.out) + (size_t)m0 * a.ldo * OE, (short)0, (int)((size_t)rows * a.ldo * OE), 0x00020000);
     __amdgpu_buffer_rsrc_t rb = ob;
@@ -664,16 +670,18 @@ __global__ void __launch_bounds__(512, 1) conv2p_bf16_kernel(ConvArgs a) {
   // ring stages for three steps
   // mode 0: plain step; 1: the tile's second-to-last step, which loads its bias / rscale ahead of its ring loads;
   // 2: the last step, whose wait also retires them (and every store of the previous epilogue)
+  // ST slots: a step waits for stage g + 1 with ST - 3 later stages in flight and issues stage g + ST - 1; an
+  // epilogue's stores stay between the ring stages for ST - 2 steps
   auto body = [&](int g, int kk, int i, Frag& cur, Frag& nxt, int mode) {
     if (mode == 2)
       vmcnt_b<LPS>();
-    else if (i > 0 && kk < 3)
-      vmcnt_b<2 * LPS + NST>();
+    else if (i > 0 && kk < ST - 2)
+      vmcnt_b<(ST - 3) * LPS + NST>();
     else
-      vmcnt_b<2 * LPS>();
+      vmcnt_b<(ST - 3) * LPS>();
     lds_barrier_b();
     if (mode == 1) load_consts(i);
-    issue(g + 4);
+    issue(g + ST - 1);
     read(min(g + 1, total - 1), nxt);
     mma(cur, 0);
     mma(cur, 1);
@@ -693,8 +701,8 @@ __global__ void __launch_bounds__(512, 1) conv2p_bf16_kernel(ConvArgs a) {
     epilogue(i);
     zero();
   };
-  for (int st = 0; st < C2_ST - 1; ++st) issue(st);
-  vmcnt_b<3 * LPS>();  // stage 0 landed
+  for (int st = 0; st < ST - 1; ++st) issue(st);
+  vmcnt_b<(ST - 2) * LPS>();  // stage 0 landed
   lds_barrier_b();
   Frag f0, f1;
   read(0, f0);
@@ -1124,19 +1132,19 @@ static int persistent_grid(int ntiles) {  // one workgroup per CU, a multiple of
   return ntiles <= cus ? ntiles : cus;
 }
 
-template <int BN, int ACT, int OUT, int RES>
+template <int BN, int ACT, int OUT, int RES, int BM = C2_M>
 static hipError_t conv2p_go(const ConvArgs& a, hipStream_t s) {
-  constexpr int BYTES = C2Cfg<BN>::RING;
+  constexpr int BYTES = C2Cfg<BN, BM>::RING;
   static bool attr = false;
   if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv2p_bf16_kernel<BN, ACT, OUT, RES>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv2p_bf16_kernel<BN, ACT, OUT, RES, BM>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, BYTES);
     if (e != hipSuccess) return e;
     attr = true;
   }
-  const int ntiles = ((a.M + C2_M - 1) / C2_M) * ((a.Cout + BN - 1) / BN);
+  const int ntiles = ((a.M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
   const int grid = g_conv_persist == 2 ? ntiles : persistent_grid(ntiles);  // 2: A/B of the schedule alone
-  hipLaunchKernelGGL((conv2p_bf16_kernel<BN, ACT, OUT, RES>), dim3(grid), dim3(512), BYTES, s, a);
+  hipLaunchKernelGGL((conv2p_bf16_kernel<BN, ACT, OUT, RES, BM>), dim3(grid), dim3(512), BYTES, s, a);
   return hipGetLastError();
 }
 
@@ -1163,6 +1171,7 @@ static hipError_t conv2_go(const ConvArgs& a, hipStream_t s, int pmode) {
 }
 
 static int g_conv_v1 = -1;  // VGE_CONV_V1=1: every layer on the 128-row kernel (A/B timing)
+static int g_conv_force = 0;  // vge_debug_set_conv_variant(v): untuned launches (variant 0) take variant v (tests, A/B)
 static int g_conv_tall = 0;  // vge_debug_set_conv_tall(1): 256-row tiles for the 64 / 128-column layers (A/B timing)
 
 template <int TN, int ACT, int OUT, int RES, int BM>
@@ -1191,6 +1200,9 @@ static hipError_t conv_go(const ConvArgs& a, int grid, hipStream_t s, int pmode)
     return g_conv_v1 && pmode < 0 ? conv_go<128, ACT, OUT, RES>(a, grid, s, pmode) : conv2_go<256, ACT, OUT, RES>(a, s, pmode);
   } else if (pmode == 5) {  // 256-row ("tall") tiles
     return conv1_go<TN, ACT, OUT, RES, 256>(a, ((a.M + 255) / 256) * ((a.Cout + TN - 1) / TN), s);
+  } else if (pmode == 6) {  // 512 x 128 tiles on the persistent grid
+    if constexpr (TN == 128) return conv2p_go<128, ACT, OUT, RES, 512>(a, s);
+    return hipErrorInvalidValue;
   } else {
     return conv1_go<TN, ACT, OUT, RES, CV_M>(a, grid, s);
   }
@@ -1222,12 +1234,17 @@ hipError_t launch_conv_bf16(const ConvLaunch& c, hipStream_t s) {
   a.Cout = c.Cout;
   a.M = c.n_img * a.Ho * a.Wo;
   int tn = c.tn, pmode = -1;
-  if (c.variant == 1 || c.variant == 5) tn = tn > 128 ? 128 : tn;
-  if (c.variant == 5 || (c.variant == 0 && g_conv_tall && tn < 256)) pmode = 5;  // 256-row tiles, 64 / 128 columns
-  if (c.variant == 2 || c.variant == 3) {
+  const int variant = c.variant == 0 && g_conv_force > 0 ? g_conv_force : c.variant;
+  if (variant == 6) {  // 512 x 128 persistent tiles
+    tn = 128;
+    pmode = 6;
+  }
+  if (variant == 1 || variant == 5) tn = tn > 128 ? 128 : tn;
+  if (variant == 5 || (variant == 0 && g_conv_tall && tn < 256)) pmode = 5;  // 256-row tiles, 64 / 128 columns
+  if (variant == 2 || variant == 3) {
     if (c.Npad % 256) return hipErrorInvalidValue;
     tn = 256;
-    pmode = c.variant == 3 ? 1 : 0;
+    pmode = variant == 3 ? 1 : 0;
   }
   const int tn1 = tn > 128 ? 128 : tn;  // v1 grid (the tn 256 case runs conv2 with its own grid)
   const int grid = ((a.M + CV_M - 1) / CV_M) * ((c.Cout + tn1 - 1) / tn1);
@@ -1342,6 +1359,12 @@ extern "C" int vge_debug_set_conv_v1(int on) {  // A/B timing (tools/conv_bench.
 extern "C" int vge_debug_set_conv_tall(int on) {  // A/B timing (tools/conv_bench.py)
   vge::g_conv_tall = on ? 1 : 0;
   return 0;
+}
+
+extern "C" int vge_debug_set_conv_variant(int v) {  // tests / A/B: untuned launches take variant v (0 = default)
+  const int prev = vge::g_conv_force;
+  vge::g_conv_force = v;
+  return prev;
 }
 
 extern "C" int vge_debug_set_conv_persist(int mode) {  // A/B timing (tools/conv_bench.py): 0 off, 1 on, 2 one tile each

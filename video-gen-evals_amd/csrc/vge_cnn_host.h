@@ -162,7 +162,7 @@ inline bool fold_pair(WeightMap& wm, const std::string& p0, const std::string& p
 }
 
 // Per-layer kernel choice, measured on first use: the implicit-GEMM conv has bit-identical variants (128- or 256-row
-// tiles with 64 or 128 columns, 256 x 256 tiles one per workgroup, 256 x 256 tiles on the persistent grid) whose
+// tiles with 64 or 128 columns, 256 x 256 tiles one per workgroup, 256 x 256 or 512 x 128 tiles on the persistent grid) whose
 // ranking depends on K, Cout and the tile count (tools/conv_bench.py).  The first launch of each layer shape times
 // every applicable variant on the layer's own operands (one warm launch + 3 timed, hipEvents on its stream) and keeps
 // the fastest; layers whose output is also an input (in-place residual) are not re-run and take the default.
@@ -201,6 +201,7 @@ inline hipError_t conv_tuned_launch(ConvTuner& t, ConvLaunch& c, const std::arra
       cand.push_back(5000 + 64);
     }
     if (c.res_mode == 0 && c.Cout % 4 == 0) cand.push_back(3000 + 256);
+    if (c.Cout > 64 && c.Cout <= 128 && c.Cout % 4 == 0) cand.push_back(6000 + 128);  // 512 x 128 persistent
     int pick = -1;
     float best_ms = 0.f;
     for (int v : cand) {
