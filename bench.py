@@ -323,7 +323,7 @@ def main():
     ap.add_argument("--chunk-clips", type=int, default=32, help="e2e: clips per extraction pass (frames in HBM)")
     ap.add_argument("--no-throughput-mode", action="store_true",
                     help="score: skip the second (f16) run reported as throughput_mode beside the f32x3 headline")
-    ap.add_argument("--pipeline", default="side2", choices=["side2", "side", "tail", "serial"],
+    ap.add_argument("--pipeline", default="side2", choices=["side3", "side2", "side", "tail", "serial"],
                     help="score/cfg5 stream layout: side = the next chunk is featurised on a second stream beside the "
                          "current chunk's fusion + transformer; side2 (default) = side, plus the per-video scores and "
                          "their host copies on that second stream (two output buffers, alternate steps); tail = the "
@@ -331,7 +331,10 @@ def main():
                          "the encode stream featurises the next chunk and queues its conv stage, which then takes CUs "
                          "as the transformer's workgroups finish (its hipEvents include that wait, so the conv "
                          "roofline is not measured in this mode); serial = one stream, featurise right before each "
-                         "encode")
+                         "encode; side3 = side2 with each step's scores launched on the side stream after the NEXT "
+                         "step's conv (which follows this step's transformer on the encode stream), so no marker "
+                         "follows the transformer; the last step's scores are launched after the loop, inside the "
+                         "timed region")
     ap.add_argument("--serial-featurize", action="store_true", help="= --pipeline serial")
     ap.add_argument("--event-every", type=int, default=5,
                     help="record the conv stage's (and featurise's) hipEvents on every k-th timed step, from the first: "
@@ -595,12 +598,27 @@ def run_score(args, world, rank, dev):
             fe1[k].record(stream)
             n_fe[0] += 1
 
+    deferred = [None]  # side3: (seq, tc) buffers of the step whose scores are not launched yet
+
+    def launch_scores(stream, sq, tw):
+        with torch.cuda.stream(stream):
+            ac, tc = ops.score_videos(sq, tw, first, vcls, centroids)
+            host_ac.copy_(ac, non_blocking=True)
+            host_tc.copy_(tc, non_blocking=True)
+        return ac, tc
+
     def launch_feat(c):
         # featurise chunk c on the side stream once the last encode's conv stage (the last reader of feats) is done:
         # it runs beside that chunk's fusion + transformer (a featurise workgroup fits next to a transformer
         # workgroup on a CU: 16 KB of LDS and 141 registers per lane on top of 139 KB and 325)
         with torch.cuda.stream(side):
             enc.wait_conv(side)
+            if deferred[0] is not None:
+                # side3: the previous step's scores -- its transformer ran before this conv on the encode stream.  They
+                # precede this featurise, whose feat_ready gates the conv (and so the transformer) that next rewrites
+                # their buffer pair
+                launch_scores(side, *deferred[0])
+                deferred[0] = None
             featurize_chunk(c, side)
             feat_ready.record(side)
         pending[0] = c
@@ -612,29 +630,43 @@ def run_score(args, world, rank, dev):
 
     sc_ev = []  # (start, end) events around standalone per-video score launches after the timed steps
 
-    def step(i=None):
+    def drain():
+        """side3: launch the deferred scores now (after the last transformer: one marker)"""
+        if deferred[0] is None:
+            return None, None
+        cur = torch.cuda.current_stream()
+        tx_done.record(cur)
+        side.wait_event(tx_done)
+        out = launch_scores(side, *deferred[0])
+        deferred[0] = None
+        return out
+
+    def step(i=None, flush=False):
         ac = tc = None
         cur = torch.cuda.current_stream()
-        sq, tw = (seq_b[n_step[0] % 2], tcw_b[n_step[0] % 2]) if mode == "side2" else (seq, tcw)
+        sq, tw = (seq_b[n_step[0] % 2], tcw_b[n_step[0] % 2]) if mode in ("side2", "side3") else (seq, tcw)
         n_step[0] += 1
         for c in range(n_chunks):
             b0, b1 = c * CH, min(NW, (c + 1) * CH)
             if mode == "serial" or (mode == "tail" and pending[0] != c):
                 featurize_chunk(c, cur)
-            elif mode in ("side", "side2"):
+            elif mode in ("side", "side2", "side3"):
                 if pending[0] != c:
                     launch_feat(c)
                 cur.wait_event(feat_ready)
             if timing[0]:  # the conv stage's two events on every --event-every-th step of the timed region
                 enc.profile_mask(0x3 if n_timed[0] % args.event_every == 0 else 0)
             enc.encode(feats[: b1 - b0], frame_embed=False, tc=True, seq_out=sq[b0:b1], tc_out=tw[b0:b1])
-            if mode in ("side", "side2"):
+            if mode in ("side", "side2", "side3"):
                 launch_feat((c + 1) % n_chunks)  # the next chunk, or the next step's first
             if mode == "tail":
                 # the next chunk (or the next step's first) on the encode stream, beside this chunk's transformer
                 # on the tail stream; the next encode's conv stage follows it there
                 featurize_chunk((c + 1) % n_chunks, cur)
                 pending[0] = (c + 1) % n_chunks
+        if mode == "side3":
+            deferred[0] = (sq, tw)
+            return drain() if flush else (None, None)
         if mode == "side2":
             # after the last transformer, on the side stream behind the next step's first featurise: the next conv
             # waits for that featurise (feat_ready), not for the scores; the step after next rewrites this buffer
@@ -649,15 +681,15 @@ def run_score(args, world, rank, dev):
         return ac, tc
 
     # precision evidence for the timed mode: the untimed first step's scores vs the oracle on a sample of clips
-    ac_a, tc_a = step()
+    ac_a, tc_a = step(flush=True)
     torch.cuda.synchronize()  # the scores may come from the tail stream
     precision = oracle_precision(gen_clips, stats.mean, stats.std, centroids, vcls, seq, ac_a, tc_a, starts,
                                  n=16 if cfg5 else V) if rank == 0 else None
     torch.cuda.synchronize()
     setup_s = time.perf_counter() - t_setup
 
-    for _ in range(args.warmup):
-        step()
+    for k in range(args.warmup):
+        step(flush=k == args.warmup - 1)  # (side3: no deferred scores carried into the timed steps)
     torch.cuda.synchronize()
     # inside the timed steps only the conv stage's two events are recorded (each event is a queue marker: all six
     # stage markers measured -1.3 % videos/s); the other stages are timed on untimed steps afterwards
@@ -669,7 +701,7 @@ def run_score(args, world, rank, dev):
     timing[0] = True
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(i)
+        step(i, flush=i == args.steps - 1)  # side3: the last step's scores inside the timed region
         n_timed[0] += 1
     torch.cuda.synchronize()
     timing[0] = False
@@ -684,12 +716,12 @@ def run_score(args, world, rank, dev):
     n_extra = 5
     enc.profile_mask(0x3F)
     enc.profile_begin(n_extra * n_chunks)
-    for _ in range(n_extra):
-        step()
+    for k in range(n_extra):
+        step(flush=k == n_extra - 1)
     torch.cuda.synchronize()
     # the per-video score kernel alone (in the pipelined step it runs on the side stream, where its events would also
     # span the next conv that holds every CU): 10 launches on the current stream, hipEvents around each
-    sq_last, tw_last = (seq_b[(n_step[0] - 1) % 2], tcw_b[(n_step[0] - 1) % 2]) if mode == "side2" else (seq, tcw)
+    sq_last, tw_last = (seq_b[(n_step[0] - 1) % 2], tcw_b[(n_step[0] - 1) % 2]) if mode in ("side2", "side3") else (seq, tcw)
     for _ in range(10):
         sc_ev.append((torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)))
         sc_ev[-1][0].record()

@@ -266,6 +266,72 @@ def test_featurize_pipelined_on_a_side_stream_matches_serial():
     assert torch.equal(piped, serial)
 
 
+def test_deferred_scores_pipeline_matches_serial():
+    """bench.py --pipeline side3: step k's featurise runs on a side stream after step k-1's conv stage; step k-1's
+    per-video scores are launched on that side stream after step k's conv (which follows step k-1's transformer on the
+    encode stream), ahead of step k+1's featurise, whose readiness gates the encode that next rewrites their (seq, tc)
+    buffer pair.  Four steps over different window orders: every step's scores equal the serial order's bit for bit."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vge import ops
+    from vge.data import pack_frame_store
+    o = _oracle(256)
+    store = ops.DeviceFrameStore.from_host(pack_frame_store(o["clips"], [f"g{i}" for i in range(256)], ["X"] * 256), DEV)
+    mean, std = torch.from_numpy(o["mean"]).to(DEV), torch.from_numpy(o["std"]).to(DEV)
+    enc = ops.Encoder(o["sd"], device=DEV, compute="f32x3")
+    enc.reserve(256)
+    steps = 4
+    wins = [torch.tensor([[(v * (2 * k + 1) + 37 * k) % 256, 0] for v in range(256)], dtype=torch.int32, device=DEV)
+            for k in range(steps)]
+    first = torch.arange(0, 257, 2, dtype=torch.int32, device=DEV)      # 128 videos of 2 windows
+    vcls = (torch.arange(128, device=DEV) % 10).to(torch.int32)
+    cent = torch.nn.functional.normalize(torch.randn(10, 256, device=DEV, generator=torch.Generator(DEV).manual_seed(3)),
+                                         dim=1)
+    feats = torch.empty((256, 32, ops.FEAT_DIM), device=DEV)
+
+    ref = []
+    seq, tcw = torch.empty((256, 256), device=DEV), torch.empty(256, device=DEV)
+    for k in range(steps):
+        ops.featurize(store, wins[k], mean, std, out=feats)
+        enc.encode(feats, frame_embed=False, tc=True, seq_out=seq, tc_out=tcw)
+        ac, tc = ops.score_videos(seq, tcw, first, vcls, cent)
+        ref.append((ac.clone(), tc.clone()))
+
+    seq_b = [torch.empty((256, 256), device=DEV) for _ in range(2)]
+    tcw_b = [torch.empty(256, device=DEV) for _ in range(2)]
+    got = [None] * steps
+    side, ready, tx_done = torch.cuda.Stream(device=DEV), torch.cuda.Event(), torch.cuda.Event()
+    cur = torch.cuda.current_stream()
+    deferred = None
+
+    def scores(k, sq, tw):
+        with torch.cuda.stream(side):
+            ac, tc = ops.score_videos(sq, tw, first, vcls, cent)
+            got[k] = (ac, tc)
+
+    with torch.cuda.stream(side):
+        side.wait_stream(cur)
+        ops.featurize(store, wins[0], mean, std, out=feats)
+        ready.record(side)
+    for k in range(steps):
+        cur.wait_event(ready)
+        enc.encode(feats, frame_embed=False, tc=True, seq_out=seq_b[k % 2], tc_out=tcw_b[k % 2])
+        with torch.cuda.stream(side):
+            enc.wait_conv(side)
+            if deferred is not None:
+                scores(*deferred)
+            if k + 1 < steps:
+                ops.featurize(store, wins[k + 1], mean, std, out=feats)
+            ready.record(side)
+        deferred = (k, seq_b[k % 2], tcw_b[k % 2])
+    tx_done.record(cur)
+    side.wait_event(tx_done)
+    scores(*deferred)
+    torch.cuda.synchronize()
+    for k in range(steps):
+        assert torch.equal(got[k][0], ref[k][0]) and torch.equal(got[k][1], ref[k][1]), k
+
+
 @pytest.mark.parametrize("compute,bounds", [("f32x3", (0, 64, 128, 192, 256)), ("f16", (0, 64, 128, 192, 256)),
                                             ("f32x3", (0, 64, 72, 136, 200, 256))])
 def test_tail_stream_pipeline_matches_serial(compute, bounds):
