@@ -269,8 +269,8 @@ def test_featurize_pipelined_on_a_side_stream_matches_serial():
 def test_deferred_scores_pipeline_matches_serial():
     """bench.py --pipeline side3: step k's featurise runs on a side stream after step k-1's conv stage; step k-1's
     per-video scores are launched on that side stream after step k's conv (which follows step k-1's transformer on the
-    encode stream), ahead of step k+1's featurise, whose readiness gates the encode that next rewrites their (seq, tc)
-    buffer pair.  Four steps over different window orders: every step's scores equal the serial order's bit for bit."""
+    encode stream), ahead of step k+1's featurise, whose readiness event gates the encode that next rewrites their
+    (seq, tc) buffer pair.  Four steps over different window orders: every step's scores equal the serial order's bit for bit."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from vge import ops

@@ -56,6 +56,50 @@ __device__ __forceinline__ int xcd_remap(int b, int nblk) {  // bijective: each 
   return (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (b >> 3);
 }
 
+// Implicit-GEMM gather state of one A row (the tile rows a lane fetches): the address of the row's (kh, kw) = (0, 0)
+// tap plus this lane's 16-B chunk (lc8 = 8 lc channels), and (ih0 << 16) | (iw0 & 0xFFFF) (a row past M gets ih0 =
+// -16384, which fails every tap's bounds check).
+struct RowState {
+  const bf16* p;
+  int hw0;
+};
+__device__ __forceinline__ RowState row_state(const ConvArgs& a, int m, int lc8) {
+  const int hw = a.Ho * a.Wo;
+  const int img = m / hw, rem = m - img * hw;
+  const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
+  const int ih0 = m < a.M ? oh * a.stride - a.pad : -16384, iw0 = ow * a.stride - a.pad;
+  return {a.x + (long)((img * a.H + ih0) * a.W + iw0) * a.ldx + lc8, (ih0 << 16) | (iw0 & 0xFFFF)};
+}
+// The 32-k stage starting at k0 of NR rows into LDS (row j's 1 KB wave-instruction at dst(j)).  Cin >= 32: the stage
+// lies inside one tap, so the tap, its (kh, kw) and the channel base are uniform (scalar) and a row's source is its
+// base + one scalar offset; Cin 8 / 16: a lane's chunk may fall in the next tap (per-lane tap).  Taps outside the
+// image, past the kernel's taps, and rows past M read the zero page.
+template <int NR, typename Dst>
+__device__ __forceinline__ void gather_stage(const ConvArgs& a, const RowState (&rs)[NR], int k0, int lc8, Dst dst) {
+  if (a.cin_log2 >= 5) {
+    const int tap = k0 >> a.cin_log2;
+    const int kh = (tap * a.kw_magic) >> 16, kw = tap - kh * a.KW;
+    const long soff = (long)(kh * a.W + kw) * a.ldx + (k0 & ((1 << a.cin_log2) - 1));
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      const int ih = (rs[j].hw0 >> 16) + kh, iw = (int)(short)rs[j].hw0 + kw;
+      const bool ok = tap < a.taps && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      glds16(ok ? rs[j].p + soff : a.zero, dst(j));
+    }
+  } else {
+    const int k = k0 + lc8;
+    const int tap = k >> a.cin_log2, ci = k & ((1 << a.cin_log2) - 1);
+    const int kh = (tap * a.kw_magic) >> 16, kw = tap - kh * a.KW;
+    const long loff = (long)(kh * a.W + kw) * a.ldx + ci - lc8;
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      const int ih = (rs[j].hw0 >> 16) + kh, iw = (int)(short)rs[j].hw0 + kw;
+      const bool ok = tap < a.taps && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+      glds16(ok ? rs[j].p + loff : a.zero, dst(j));
+    }
+  }
+}
+
 __device__ __forceinline__ float silu(float v) { return v / (1.0f + __expf(-v)); }
 __device__ __forceinline__ float sigm(float v) { return 1.0f / (1.0f + __expf(-v)); }
 
@@ -79,40 +123,20 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
   const int mt = bid / ntn, nt = bid - mt * ntn;
   const int m0 = mt * BM, n0 = nt * TN;
   const int nk = a.Kp / CV_K;
-  const int cmask = (1 << a.cin_log2) - 1;
 
   // per-lane gather state of this lane's AJ A rows (row = 16 q + lane / 4, q = AJ wave + j)
   const int lc = (lane & 3) ^ ((lane >> 4) & 3);  // logical 16-B chunk this lane fetches (pre-swizzled)
-  int img_hw[AJ], ih0[AJ], iw0[AJ];
-  bool mval[AJ];
+  const int lc8 = lc * 8;
+  RowState rws[AJ];
 #pragma unroll
-  for (int j = 0; j < AJ; ++j) {
-    const int row = 16 * (AJ * wave + j) + (lane >> 2);
-    const int m = m0 + row;
-    mval[j] = m < a.M;
-    const int hw = a.Ho * a.Wo;
-    const int img = m / hw, rem = m - img * hw;
-    const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
-    img_hw[j] = img * a.H;
-    ih0[j] = oh * a.stride - a.pad;
-    iw0[j] = ow * a.stride - a.pad;
-  }
+  for (int j = 0; j < AJ; ++j) rws[j] = row_state(a, m0 + 16 * (AJ * wave + j) + (lane >> 2), lc8);
   const bf16* wrow[BQ];
 #pragma unroll
-  for (int j = 0; j < BQ; ++j) wrow[j] = a.w + (size_t)(n0 + 16 * (BQ * wave + j) + (lane >> 2)) * a.Kp + lc * 8;
+  for (int j = 0; j < BQ; ++j) wrow[j] = a.w + (size_t)(n0 + 16 * (BQ * wave + j) + (lane >> 2)) * a.Kp + lc8;
 
   auto issue = [&](int st) {
     char* slot = lds + (st % CV_ST) * SLOT;
-    const int k = st * CV_K + lc * 8;
-    const int tap = k >> a.cin_log2, ci = k & cmask;
-    const int kh = (tap * a.kw_magic) >> 16, kw = tap - kh * a.KW;
-#pragma unroll
-    for (int j = 0; j < AJ; ++j) {
-      const int ih = ih0[j] + kh, iw = iw0[j] + kw;
-      const bool ok = mval[j] && tap < a.taps && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-      const bf16* src = ok ? a.x + ((size_t)(img_hw[j] + ih) * a.W + iw) * a.ldx + ci : a.zero;
-      glds16(src, slot + (AJ * wave + j) * 1024);
-    }
+    gather_stage<AJ>(a, rws, st * CV_K, lc8, [&](int j) { return slot + (AJ * wave + j) * 1024; });
 #pragma unroll
     for (int j = 0; j < BQ; ++j) glds16(wrow[j] + st * CV_K, slot + TA + (BQ * wave + j) * 1024);
   };
@@ -260,36 +284,18 @@ __global__ void __launch_bounds__(512, 1) conv2_bf16_kernel(ConvArgs a) {
   const int mt = bid / ntn, nt = bid - mt * ntn;
   const int m0 = mt * C2_M, n0 = nt * BN;
   const int nk = a.Kp / CV_K;
-  const int cmask = (1 << a.cin_log2) - 1;
   const int lc = (lane & 3) ^ ((lane >> 4) & 3);
-  int img_hw[2], ih0[2], iw0[2];
-  bool mval[2];
+  const int lc8 = lc * 8;
+  RowState rws[2];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int m = m0 + 16 * (2 * wave + j) + (lane >> 2);
-    mval[j] = m < a.M;
-    const int hw = a.Ho * a.Wo;
-    const int img = m / hw, rem = m - img * hw;
-    const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
-    img_hw[j] = img * a.H;
-    ih0[j] = oh * a.stride - a.pad;
-    iw0[j] = ow * a.stride - a.pad;
-  }
+  for (int j = 0; j < 2; ++j) rws[j] = row_state(a, m0 + 16 * (2 * wave + j) + (lane >> 2), lc8);
   const bf16* wrow[BQ];
 #pragma unroll
-  for (int j = 0; j < BQ; ++j) wrow[j] = a.w + (size_t)(n0 + 16 * (BQ * wave + j) + (lane >> 2)) * a.Kp + lc * 8;
+  for (int j = 0; j < BQ; ++j) wrow[j] = a.w + (size_t)(n0 + 16 * (BQ * wave + j) + (lane >> 2)) * a.Kp + lc8;
 
   auto issue = [&](int st) {
     char* slot = lds + (st % C2_ST) * Cf::SLOT;
-    const int k = st * CV_K + lc * 8;
-    const int tap = k >> a.cin_log2, ci = k & cmask;
-    const int kh = (tap * a.kw_magic) >> 16, kw = tap - kh * a.KW;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int ih = ih0[j] + kh, iw = iw0[j] + kw;
-      const bool ok = mval[j] && tap < a.taps && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-      glds16(ok ? a.x + ((size_t)(img_hw[j] + ih) * a.W + iw) * a.ldx + ci : a.zero, slot + (2 * wave + j) * 1024);
-    }
+    gather_stage<2>(a, rws, st * CV_K, lc8, [&](int j) { return slot + (2 * wave + j) * 1024; });
 #pragma unroll
     for (int j = 0; j < BQ; ++j) glds16(wrow[j] + st * CV_K, slot + Cf::TA + (BQ * wave + j) * 1024);
   };
@@ -430,6 +436,17 @@ __global__ void __launch_bounds__(512, 1) conv2_bf16_kernel(ConvArgs a) {
 // consecutive columns) and stored straight to global memory, 8 B (bf16) / 16 B (f32) per lane.  vmcnt counts the
 // epilogue's stores in issue order between the ring stages, so the three steps after an epilogue allow NST more
 // outstanding operations.
+// Tile id -> (row panel, column panel): groups of C2_GM row panels walk the column panels with the row panel fastest,
+// so the ~32 consecutive ids an XCD runs at once cover ~8 row panels x ~4 column panels (A and W panels re-read from
+// the XCD's L2 instead of the fabric when Cout spans many column panels; the same order as gemm_bf16_kernel's)
+constexpr int C2_GM = 8;
+__device__ __forceinline__ void c2_tile(int bid, int ntn, int mtn, int& mt, int& nt) {
+  const int grp = bid / (C2_GM * ntn), rem = bid - grp * (C2_GM * ntn);
+  const int gm = min(C2_GM, mtn - grp * C2_GM);
+  mt = grp * C2_GM + rem % gm;
+  nt = rem / gm;
+}
+
 template <int CTRL>
 __device__ __forceinline__ float dppq(float v) {
   return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
@@ -466,27 +483,18 @@ __global__ void __launch_bounds__(512, 1) conv2p_bf16_kernel(ConvArgs a) {
   const int G = gridDim.x, b = blockIdx.x;
   const int T = (ntiles - b + G - 1) / G;  // host: G <= ntiles, G % 8 == 0 unless G == ntiles
   const int nk = (a.Kp / CV_K + 1) & ~1, total = T * nk;  // even: an odd K gets one all-zero stage (zero page)
-  const int cmask = (1 << a.cin_log2) - 1;
   const int lc = (lane & 3) ^ ((lane >> 4) & 3);
 
   // ---- issue side: gather state of the tile whose stages are being issued
-  // per A row two registers: the pixel index of its (kh, kw) = (0, 0) tap, and (ih0 << 16) | (iw0 & 0xFFFF) (a row
-  // past M gets ih0 = -16384, which fails every tap's bounds check)
-  int pix0[AJ], hw0[AJ];
+  const int lc8 = lc * 8;
+  RowState rws[AJ];
   const bf16* wrow[BQ];
   auto setup = [&](int i) {
-    const int bid = xcd_remap(b + i * G, ntiles);
-    const int mt = bid / ntn, m0 = mt * BM, n0 = (bid - mt * ntn) * BN;
+    int mt, nt;
+    c2_tile(xcd_remap(b + i * G, ntiles), ntn, ntiles / ntn, mt, nt);
+    const int m0 = mt * BM, n0 = nt * BN;
 #pragma unroll
-    for (int j = 0; j < AJ; ++j) {
-      const int m = m0 + 16 * (AJ * wave + j) + (lane >> 2);
-      const int hw = a.Ho * a.Wo;
-      const int img = m / hw, rem = m - img * hw;
-      const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
-      const int ih0 = m < a.M ? oh * a.stride - a.pad : -16384, iw0 = ow * a.stride - a.pad;
-      pix0[j] = (img * a.H + ih0) * a.W + iw0;
-      hw0[j] = (ih0 << 16) | (iw0 & 0xFFFF);
-    }
+    for (int j = 0; j < AJ; ++j) rws[j] = row_state(a, m0 + 16 * (AJ * wave + j) + (lane >> 2), lc8);
 #pragma unroll
     for (int j = 0; j < BQ; ++j) wrow[j] = a.w + (size_t)(n0 + 16 * (BQ * wave + j) + (lane >> 2)) * a.Kp + lc * 8;
   };
@@ -501,16 +509,7 @@ __global__ void __launch_bounds__(512, 1) conv2p_bf16_kernel(ConvArgs a) {
       }
     }
     char* slot = lds + (is_g % ST) * Cf::SLOT;
-    const int k = is_k * CV_K + lc * 8;
-    const int tap = k >> a.cin_log2, ci = k & cmask;
-    const int kh = (tap * a.kw_magic) >> 16, kw = tap - kh * a.KW;
-    const int toff = kh * a.W + kw;
-#pragma unroll
-    for (int j = 0; j < AJ; ++j) {
-      const int ih = (hw0[j] >> 16) + kh, iw = (int)(short)hw0[j] + kw;
-      const bool ok = tap < a.taps && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-      glds16(ok ? a.x + (size_t)(unsigned)(pix0[j] + toff) * a.ldx + ci : a.zero, slot + (AJ * wave + j) * 1024);
-    }
+    gather_stage<AJ>(a, rws, is_k * CV_K, lc8, [&](int j) { return slot + (AJ * wave + j) * 1024; });
     const bool kin = is_k * CV_K < a.Kp;
 #pragma unroll
     for (int j = 0; j < BQ; ++j) glds16(kin ? wrow[j] + is_k * CV_K : a.zero, slot + Cf::TA + (BQ * wave + j) * 1024);
@@ -565,10 +564,10 @@ __global__ void __launch_bounds__(512, 1) conv2p_bf16_kernel(ConvArgs a) {
   typedef typename std::conditional<RES == RES_F32S, uintx4_t, uintx2_t>::type RV;
   floatx4 bb[TN], rs[TN];
   auto tile_mn = [&](int i, int& m0, int& n0) {
-    const int bid = xcd_remap(b + i * G, ntiles);
-    const int mt = bid / ntn;
+    int mt, nt;
+    c2_tile(xcd_remap(b + i * G, ntiles), ntn, ntiles / ntn, mt, nt);
     m0 = mt * BM;
-    n0 = (bid - mt * ntn) * BN;
+    n0 = nt * BN;
   };
   // bias / rscale: asm loads, invisible to hipcc's waitcnt pass (which answers any load issued among LDS-DMA ring
   // loads and stores with vmcnt(0)); consts_wait retires them by count, naming the registers so nothing reads them
