@@ -74,29 +74,34 @@ __device__ __forceinline__ RowState row_state(const ConvArgs& a, int m, int lc8)
 // lies inside one tap, so the tap, its (kh, kw) and the channel base are uniform (scalar) and a row's source is its
 // base + one scalar offset; Cin 8 / 16: a lane's chunk may fall in the next tap (per-lane tap).  Taps outside the
 // image, past the kernel's taps, and rows past M read the zero page.
-template <int NR, typename Dst>
-__device__ __forceinline__ void gather_stage(const ConvArgs& a, const RowState (&rs)[NR], int k0, int lc8, Dst dst) {
+// The sources of the 32-k stage starting at k0 for NR rows: src[j] = row j's source or the zero page (taps outside
+// the image, past the kernel's taps, rows past M).  Cin >= 32: the stage lies inside one tap, so the tap, its (kh, kw)
+// and the channel base are uniform (scalar) and a row's source is its base + one scalar offset; Cin 8 / 16: a lane's
+// chunk may fall in the next tap (per-lane tap).  Kept in registers: callers compute them while their MFMAs run and
+// issue the loads at the top of the next step.
+template <int NR>
+__device__ __forceinline__ void gather_srcs(const ConvArgs& a, const RowState (&rs)[NR], int k0, int lc8,
+                                            const bf16* (&src)[NR]) {
+  int kh, kw, tap;
+  long off;
   if (a.cin_log2 >= 5) {
-    const int tap = k0 >> a.cin_log2;
-    const int kh = (tap * a.kw_magic) >> 16, kw = tap - kh * a.KW;
-    const long soff = (long)(kh * a.W + kw) * a.ldx + (k0 & ((1 << a.cin_log2) - 1));
-#pragma unroll
-    for (int j = 0; j < NR; ++j) {
-      const int ih = (rs[j].hw0 >> 16) + kh, iw = (int)(short)rs[j].hw0 + kw;
-      const bool ok = tap < a.taps && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-      glds16(ok ? rs[j].p + soff : a.zero, dst(j));
-    }
+    tap = k0 >> a.cin_log2;
+    kh = (tap * a.kw_magic) >> 16;
+    kw = tap - kh * a.KW;
+    off = (long)(kh * a.W + kw) * a.ldx + (k0 & ((1 << a.cin_log2) - 1));
   } else {
     const int k = k0 + lc8;
-    const int tap = k >> a.cin_log2, ci = k & ((1 << a.cin_log2) - 1);
-    const int kh = (tap * a.kw_magic) >> 16, kw = tap - kh * a.KW;
-    const long loff = (long)(kh * a.W + kw) * a.ldx + ci - lc8;
+    tap = k >> a.cin_log2;
+    kh = (tap * a.kw_magic) >> 16;
+    kw = tap - kh * a.KW;
+    off = (long)(kh * a.W + kw) * a.ldx + (k & ((1 << a.cin_log2) - 1)) - lc8;
+  }
 #pragma unroll
-    for (int j = 0; j < NR; ++j) {
-      const int ih = (rs[j].hw0 >> 16) + kh, iw = (int)(short)rs[j].hw0 + kw;
-      const bool ok = tap < a.taps && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
-      glds16(ok ? rs[j].p + loff : a.zero, dst(j));
-    }
+  for (int j = 0; j < NR; ++j) {
+    const int ih = (rs[j].hw0 >> 16) + kh, iw = (int)(short)rs[j].hw0 + kw;
+    const bool ok = tap < a.taps && (unsigned)ih < (unsigned)a.H && (unsigned)iw < (unsigned)a.W;
+    const unsigned long v = ok ? reinterpret_cast<unsigned long>(rs[j].p + off) : reinterpret_cast<unsigned long>(a.zero);
+    src[j] = reinterpret_cast<const bf16*>(v);
   }
 }
 
@@ -134,9 +139,14 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
 #pragma unroll
   for (int j = 0; j < BQ; ++j) wrow[j] = a.w + (size_t)(n0 + 16 * (BQ * wave + j) + (lane >> 2)) * a.Kp + lc8;
 
-  auto issue = [&](int st) {
+  // software-pipelined ring: prep(st) computes stage st's A sources (after a step's MFMAs are issued, so the VALU work
+  // runs beside them), fire(st) issues its loads at the top of the next step
+  const bf16* nsrc[AJ];
+  auto prep = [&](int st) { gather_srcs<AJ>(a, rws, st * CV_K, lc8, nsrc); };
+  auto fire = [&](int st) {
     char* slot = lds + (st % CV_ST) * SLOT;
-    gather_stage<AJ>(a, rws, st * CV_K, lc8, [&](int j) { return slot + (AJ * wave + j) * 1024; });
+#pragma unroll
+    for (int j = 0; j < AJ; ++j) glds16(nsrc[j], slot + (AJ * wave + j) * 1024);
 #pragma unroll
     for (int j = 0; j < BQ; ++j) glds16(wrow[j] + st * CV_K, slot + TA + (BQ * wave + j) * 1024);
   };
@@ -153,11 +163,15 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
   const int swz = (lane >> 2) & 3;
   const int rowoff = (lane & 31) * 64;
   constexpr int LPS = AJ + BQ;  // global_load_lds per thread per stage
-  for (int st = 0; st < CV_ST - 1; ++st) issue(min(st, nk - 1));
+  for (int st = 0; st < CV_ST - 1; ++st) {
+    prep(min(st, nk - 1));
+    fire(min(st, nk - 1));
+  }
+  prep(min(CV_ST - 1, nk - 1));
   for (int kt = 0; kt < nk; ++kt) {
     vmcnt_b<LPS>();     // stage kt landed (stage kt + 1 may still be in flight)
     lds_barrier_b();    // ... for every wave; every wave is done reading stage kt - 1's slot
-    issue(min(kt + CV_ST - 1, nk - 1));  // past the end: re-fetch the last stage into its own slot (same bytes)
+    fire(min(kt + CV_ST - 1, nk - 1));  // past the end: re-fetch the last stage into its own slot (same bytes)
     const char* cur = lds + (kt % CV_ST) * SLOT;
     const char* As = cur + wm * 64 * 64 + rowoff;
     const char* Bs = cur + TA + wn * (TN / NWV) * 64 + rowoff;
@@ -175,6 +189,7 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
         for (int u = 0; u < NB; ++u)
           acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[t], fb[u], acc[t][u], 0, 0, 0);
     }
+    prep(min(kt + CV_ST, nk - 1));
   }
 
   // epilogue through LDS in BM / 64 row quarters / halves (64 rows of f32 each), row-major re-read: 8 columns per
@@ -293,9 +308,13 @@ __global__ void __launch_bounds__(512, 1) conv2_bf16_kernel(ConvArgs a) {
 #pragma unroll
   for (int j = 0; j < BQ; ++j) wrow[j] = a.w + (size_t)(n0 + 16 * (BQ * wave + j) + (lane >> 2)) * a.Kp + lc8;
 
-  auto issue = [&](int st) {
+  // software-pipelined ring (as conv2p_bf16_kernel): prep after a step's MFMAs, fire at the top of the next step
+  const bf16* nsrc[2];
+  auto prep = [&](int st) { gather_srcs<2>(a, rws, st * CV_K, lc8, nsrc); };
+  auto fire = [&](int st) {
     char* slot = lds + (st % C2_ST) * Cf::SLOT;
-    gather_stage<2>(a, rws, st * CV_K, lc8, [&](int j) { return slot + (2 * wave + j) * 1024; });
+#pragma unroll
+    for (int j = 0; j < 2; ++j) glds16(nsrc[j], slot + (2 * wave + j) * 1024);
 #pragma unroll
     for (int j = 0; j < BQ; ++j) glds16(wrow[j] + st * CV_K, slot + Cf::TA + (BQ * wave + j) * 1024);
   };
@@ -334,10 +353,11 @@ __global__ void __launch_bounds__(512, 1) conv2_bf16_kernel(ConvArgs a) {
   auto step = [&](int kt, Frag& cur, Frag& nxt) {
     vmcnt_b<2 * LPS>();  // stage kt + 1 landed (kt + 2, kt + 3 in flight)
     lds_barrier_b();
-    issue(min(kt + 4, nk - 1));  // past the end: the last stage again, into its own slot (same bytes)
+    fire(min(kt + 4, nk - 1));  // past the end: the last stage again, into its own slot (same bytes)
     read(min(kt + 1, nk - 1), nxt);
     mma(cur, 0);
     mma(cur, 1);
+    prep(min(kt + 5, nk - 1));
 #pragma unroll
     for (int j = 0; j < LPS; ++j) {
       __builtin_amdgcn_sched_group_barrier(0x008, NM / LPS > 0 ? NM / LPS : 1, 0);  // MFMA
@@ -347,9 +367,14 @@ __global__ void __launch_bounds__(512, 1) conv2_bf16_kernel(ConvArgs a) {
     for (int j = 0; j < 4; ++j) {
       __builtin_amdgcn_sched_group_barrier(0x008, NM / 4 > 0 ? NM / 4 : 1, 0);      // MFMA
       __builtin_amdgcn_sched_group_barrier(0x100, (2 * (TM + TN) + 3) / 4, 0);     // DS read
+      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);                            // VALU (the next stage's sources)
     }
   };
-  for (int st = 0; st < C2_ST - 1; ++st) issue(min(st, nk - 1));
+  for (int st = 0; st < C2_ST - 1; ++st) {
+    prep(min(st, nk - 1));
+    fire(min(st, nk - 1));
+  }
+  prep(min(C2_ST - 1, nk - 1));
   vmcnt_b<3 * LPS>();  // stage 0 landed
   lds_barrier_b();
   Frag f0, f1;
@@ -498,9 +523,14 @@ __global__ void __launch_bounds__(512, 1) conv2p_bf16_kernel(ConvArgs a) {
 #pragma unroll
     for (int j = 0; j < BQ; ++j) wrow[j] = a.w + (size_t)(n0 + 16 * (BQ * wave + j) + (lane >> 2)) * a.Kp + lc * 8;
   };
-  int is_t = 0, is_k = -1, is_g = -1;  // last issued stage (tile, k-stage, global index)
+  int is_t = 0, is_k = -1, is_g = -1;  // last prepared stage (tile, k-stage, global index)
   setup(0);
-  auto issue = [&](int g) {  // g == is_g + 1, or past the end: re-fetch the last stage into its own slot (same bytes)
+  // The ring is software-pipelined: prep(g) moves the issue state to stage g and computes its A sources (VALU work,
+  // done right after a step's MFMAs are issued, so it runs beside them); fire() issues the prepared stage's loads at
+  // the top of the next step.  Past the end, prep keeps the last stage: it is re-fetched into its own slot (same
+  // bytes).
+  const bf16* nsrc[AJ];
+  auto prep = [&](int g) {  // g == is_g + 1, or past the end
     if (g < total) {
       is_g = g;
       if (++is_k == nk) {
@@ -508,8 +538,12 @@ __global__ void __launch_bounds__(512, 1) conv2p_bf16_kernel(ConvArgs a) {
         setup(++is_t);
       }
     }
+    gather_srcs<AJ>(a, rws, is_k * CV_K, lc8, nsrc);
+  };
+  auto fire = [&]() {
     char* slot = lds + (is_g % ST) * Cf::SLOT;
-    gather_stage<AJ>(a, rws, is_k * CV_K, lc8, [&](int j) { return slot + (AJ * wave + j) * 1024; });
+#pragma unroll
+    for (int j = 0; j < AJ; ++j) glds16(nsrc[j], slot + (AJ * wave + j) * 1024);
     const bool kin = is_k * CV_K < a.Kp;
 #pragma unroll
     for (int j = 0; j < BQ; ++j) glds16(kin ? wrow[j] + is_k * CV_K : a.zero, slot + Cf::TA + (BQ * wave + j) * 1024);
@@ -680,10 +714,11 @@ __global__ void __launch_bounds__(512, 1) conv2p_bf16_kernel(ConvArgs a) {
       vmcnt_b<(ST - 3) * LPS>();
     lds_barrier_b();
     if (mode == 1) load_consts(i);
-    issue(g + ST - 1);
+    fire();  // stage g + ST - 1
     read(min(g + 1, total - 1), nxt);
     mma(cur, 0);
     mma(cur, 1);
+    prep(g + ST);
 #pragma unroll
     for (int j = 0; j < LPS; ++j) {
       __builtin_amdgcn_sched_group_barrier(0x008, NM / LPS > 0 ? NM / LPS : 1, 0);  // MFMA
@@ -693,6 +728,7 @@ __global__ void __launch_bounds__(512, 1) conv2p_bf16_kernel(ConvArgs a) {
     for (int j = 0; j < 4; ++j) {
       __builtin_amdgcn_sched_group_barrier(0x008, NM / 4 > 0 ? NM / 4 : 1, 0);      // MFMA
       __builtin_amdgcn_sched_group_barrier(0x100, (2 * (TM + TN) + 3) / 4, 0);     // DS read
+      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);                            // VALU (the next stage's sources)
     }
   };
   auto last = [&](int g, int kk, int i, Frag& cur, Frag& nxt) {  // the tile's last stage + its epilogue
@@ -700,7 +736,11 @@ __global__ void __launch_bounds__(512, 1) conv2p_bf16_kernel(ConvArgs a) {
     epilogue(i);
     zero();
   };
-  for (int st = 0; st < ST - 1; ++st) issue(st);
+  for (int st = 0; st < ST - 1; ++st) {
+    prep(st);
+    fire();
+  }
+  prep(ST - 1);
   vmcnt_b<(ST - 2) * LPS>();  // stage 0 landed
   lds_barrier_b();
   Frag f0, f1;
