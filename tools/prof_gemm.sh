@@ -1,14 +1,14 @@
 #!/bin/bash
 # PMC passes over the extractor GEMM (tools/gemm_bench.py --only SHAPE, our kernel only), one rocprofv3 run per
-# counter group.  Usage (repo root, GPU box): bash tools/prof_gemm.sh TAG SHAPE
+# counter group.  Usage (repo root, GPU box): bash tools/prof_gemm.sh TAG SHAPE [WAVES]   (WAVES: w8 | w4 | w8s | lib)
 set -u
-TAG=$1; SHAPE=${2:-qkv}
+TAG=$1; SHAPE=${2:-qkv}; WAVES=${3:-w8}
 R=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$R/gpurun_out; mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 run() {
   local name=$1; shift
   timeout -k 10 120 rocprofv3 "$@" --output-format csv -d "$OUT/pg_${TAG}_$name" -o run -- python3 "$R/tools/gemm_bench.py" \
-    --only "$SHAPE" --waves w8 --rounds 3 > "$OUT/pg_${TAG}_$name.log" 2>&1
+    --only "$SHAPE" --waves "$WAVES" --rounds 3 > "$OUT/pg_${TAG}_$name.log" 2>&1
   local rc=$?; echo "[$name] rc=$rc"; return $rc
 }
 run trace --kernel-trace --stats &&

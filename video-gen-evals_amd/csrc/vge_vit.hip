@@ -226,6 +226,25 @@ __global__ void __launch_bounds__(64 * NW, 1) gemm_bf16_kernel(GemmBf16Args g) {
   floatx4 bb = {0.f, 0.f, 0.f, 0.f};
   if (g.bias) bb = *reinterpret_cast<const floatx4*>(g.bias + gcol);
   if constexpr (EPI == GE_PE_F32) bb += *reinterpret_cast<const floatx4*>(g.pos + gcol);  // pos_embed[:, :1]
+  // f32 epilogues read one row vector per output (residual or position embedding): every load of a half is issued
+  // before that half's LDS round trip, and the next half's while this one is written, so the epilogue pays about one
+  // memory latency instead of one per 4-iteration batch
+  constexpr int NIT = 64 / RPI;                          // row-major iterations per half
+  constexpr bool LD = EPI == GE_RES_F32 || EPI == GE_PE_F32;
+  constexpr int NPF = LD ? (NIT > 16 ? 16 : NIT) : 1;    // loads kept in flight (NW = 4: 16 of 32 per half)
+  auto grow_of = [&](int half, int it) { return m0 + wm * 128 + half * 64 + it * RPI + lr; };
+  auto rowload = [&](int half, int it) -> floatx4 {
+    const int grow = grow_of(half, it);
+    if constexpr (EPI == GE_RES_F32) return *reinterpret_cast<const floatx4*>(g.res + (grow * (int)g.ldr + gcol));
+    if constexpr (EPI == GE_PE_F32)  // tokens per frame = 192 (checked by the host)
+      return *reinterpret_cast<const floatx4*>(g.pos + ((1 + grow - (grow / 192) * 192) * g.N + gcol));
+    return floatx4{0.f, 0.f, 0.f, 0.f};
+  };
+  floatx4 rr[NPF];
+  if constexpr (LD) {
+#pragma unroll
+    for (int it = 0; it < NPF; ++it) rr[it] = rowload(0, it);
+  }
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     if constexpr (SH == 0) {
@@ -245,26 +264,25 @@ __global__ void __launch_bounds__(64 * NW, 1) gemm_bf16_kernel(GemmBf16Args g) {
           for (int r = 0; r < 4; ++r)
             my[(tt * 16 + 4 * (lane >> 4) + r) * WC + u * 16 + (lane & 15)] = acq[4 * half + tt][u][r];
     }
-#pragma unroll 4
-    for (int it = 0; it < 64 / RPI; ++it) {
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
       const int rl = it * RPI + lr;
-      const int grow = m0 + wm * 128 + half * 64 + rl;
+      const int grow = grow_of(half, it);
       floatx4 v = *reinterpret_cast<const floatx4*>(my + rl * WC + c4) + bb;
       const int o = grow * (int)g.ldo + gcol;
       if constexpr (EPI == GE_BF16 || EPI == GE_GELU_BF16) {
-        if constexpr (EPI == GE_GELU_BF16) {
-          floatx2 y[2] = {{v.x, v.y}, {v.z, v.w}};
-          gelu2_many(y);
+        if constexpr (EPI == GE_GELU_BF16) {  // bf16 output: the one-exp2 GELU (|error| < 4.8e-7) is exact at this
+          floatx2 y[2] = {{v.x, v.y}, {v.z, v.w}};  // precision and takes ~2/3 of gelu2_many's VALU slots
+          gelu2_fast(y);
           v = {y[0].x, y[0].y, y[1].x, y[1].y};
         }
         bf16x4 ob;
         ob[0] = (bf16)v.x; ob[1] = (bf16)v.y; ob[2] = (bf16)v.z; ob[3] = (bf16)v.w;
         *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(g.out) + o) = ob;
       } else {
-        if constexpr (EPI == GE_RES_F32) v += *reinterpret_cast<const floatx4*>(g.res + (grow * (int)g.ldr + gcol));
-        if constexpr (EPI == GE_PE_F32)  // tokens per frame = 192 (checked by the host)
-          v += *reinterpret_cast<const floatx4*>(g.pos + ((1 + grow - (grow / 192) * 192) * g.N + gcol));
+        v += (it < NPF) ? rr[it % NPF] : rowload(half, it);
         *reinterpret_cast<floatx4*>(reinterpret_cast<float*>(g.out) + o) = v;
+        if (it < NPF && half == 0) rr[it % NPF] = rowload(1, it);  // the next half's, in the freed register
       }
     }
   }
