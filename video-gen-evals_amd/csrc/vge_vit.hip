@@ -271,9 +271,9 @@ __global__ void __launch_bounds__(64 * NW, 1) gemm_bf16_kernel(GemmBf16Args g) {
       floatx4 v = *reinterpret_cast<const floatx4*>(my + rl * WC + c4) + bb;
       const int o = grow * (int)g.ldo + gcol;
       if constexpr (EPI == GE_BF16 || EPI == GE_GELU_BF16) {
-        if constexpr (EPI == GE_GELU_BF16) {  // bf16 output: the one-exp2 GELU (|error| < 4.8e-7) is exact at this
-          floatx2 y[2] = {{v.x, v.y}, {v.z, v.w}};  // precision and takes ~2/3 of gelu2_many's VALU slots
-          gelu2_fast(y);
+        if constexpr (EPI == GE_GELU_BF16) {  // exact-erf GELU: the one-exp2 form (|error| < 4.8e-7) flips enough
+          floatx2 y[2] = {{v.x, v.y}, {v.z, v.w}};  // bf16 roundings to move TokenHMR's global_orient past the e2e
+          gelu2_many(y);                              // chain's 1.5e-2 bound vs the bf16-point oracle (1.68e-2, r04 box)
           v = {y[0].x, y[0].y, y[1].x, y[1].y};
         }
         bf16x4 ob;
