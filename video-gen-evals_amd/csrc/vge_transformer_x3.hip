@@ -61,6 +61,7 @@ constexpr int QH = 36;           // f32 row stride of a wave's one-head Q / K / 
 #define VGE_TX_PF 4
 #endif
 constexpr int TX_PF = VGE_TX_PF;  // weight chunks in flight per wave (ring depth)
+static_assert(16 % TX_PF == 0, "ring slots restart per 16-chunk segment: the depth must divide 16");
 constexpr int TX_NW = 4;         // waves
 template <bool SPA>
 constexpr int ap_bytes() { return (SPA ? 2 : 1) * AROWS * XSB; }  // hi (/ lo) planes of one window's A operand
