@@ -660,8 +660,27 @@ __global__ void __launch_bounds__(512, 1) conv_encoder_x3s_kernel(const float* _
 #endif
   int n_ex = 0;
   const int n = cs.n_windows;
-  for (int round = 0; round * cs.G < cs.n_units; ++round) {
-    const int u = round * cs.G + xcd_remap(blockIdx.x, cs.G);
+  const int bp = xcd_remap(blockIdx.x, cs.G);
+  // Round order per block.  With three full rounds (256 windows: two quad rounds, then the vit pairs) block bp runs
+  // them starting at round bp % 3, so in every XCD a third of the CUs streams the L2-bound vit pairs beside the
+  // MFMA-bound quads at any time instead of all 32 at once in the last round (and the units' stem loads are spread
+  // the same way): 1.044-1.048 -> 1.031-1.035 ms, same box (profiles/ab_r04j_conv_round_order.log); each unit's
+  // results are unchanged.  VGE_X3S_ROT=0 restores the plain order; 1 / 2: only blocks with bit VGE_X3S_ROT_BIT of
+  // bp set start at that round.
+#ifndef VGE_X3S_ROT
+#define VGE_X3S_ROT 3
+#endif
+#ifndef VGE_X3S_ROT_BIT
+#define VGE_X3S_ROT_BIT 0
+#endif
+#if VGE_X3S_ROT == 3
+  const int rot = cs.n_units == 3 * cs.G ? bp % 3 : 0;
+#else
+  const int rot = (VGE_X3S_ROT && cs.n_units == 3 * cs.G && ((bp >> VGE_X3S_ROT_BIT) & 1)) ? VGE_X3S_ROT : 0;
+#endif
+  for (int k = 0; k * cs.G < cs.n_units; ++k) {
+    const int round = rot ? (k + rot) % 3 : k;
+    const int u = round * cs.G + bp;
     if (u >= cs.n_units) break;  // uniform over the block
     if (u < cs.Q) {
       int e, w0;
