@@ -661,20 +661,25 @@ __global__ void __launch_bounds__(512, 1) conv_encoder_x3s_kernel(const float* _
   int n_ex = 0;
   const int n = cs.n_windows;
   const int bp = xcd_remap(blockIdx.x, cs.G);
-  // Round order per block.  With three full rounds (256 windows: two quad rounds, then the vit pairs) block bp runs
-  // them starting at round bp % 3, so in every XCD a third of the CUs streams the L2-bound vit pairs beside the
-  // MFMA-bound quads at any time instead of all 32 at once in the last round (and the units' stem loads are spread
-  // the same way): 1.044-1.048 -> 1.031-1.035 ms, same box (profiles/ab_r04j_conv_round_order.log); each unit's
-  // results are unchanged.  VGE_X3S_ROT=0 restores the plain order; 1 / 2: only blocks with bit VGE_X3S_ROT_BIT of
-  // bp set start at that round.
+  // Round order per XCD.  With three full rounds (256 windows: two quad rounds, then the vit pairs) the blocks of
+  // XCD x start at round x % 3, so at any time about a third of the XCDs run the L2-bound vit pairs and their HBM stem
+  // loads while the rest run MFMA-bound quads, instead of every CU hitting the same kind of round at once; inside an
+  // XCD all CUs still stream one encoder in lockstep (its L2 shared).  Same box, interleaved
+  // (profiles/ab_r04j_conv_round_order*.log): plain order 1.019-1.023 ms and 374 MB of fabric fetches (FETCH_SIZE x 2)
+  // per launch, per XCD (this) 1.006-1.009 ms and 373 MB, per block (bp % 3: pairs beside quads inside every XCD)
+  // 1.000-1.002 ms but 914 MB (the XCD's CUs then stream different encoders and the L2 sharing is lost).  Each unit's
+  // results are unchanged.  VGE_X3S_ROT: 0 plain order, 3 per block, 4 per XCD; 1 / 2: blocks with bit
+  // VGE_X3S_ROT_BIT of bp set start at that round.
 #ifndef VGE_X3S_ROT
-#define VGE_X3S_ROT 3
+#define VGE_X3S_ROT 4
 #endif
 #ifndef VGE_X3S_ROT_BIT
 #define VGE_X3S_ROT_BIT 0
 #endif
 #if VGE_X3S_ROT == 3
   const int rot = cs.n_units == 3 * cs.G ? bp % 3 : 0;
+#elif VGE_X3S_ROT == 4
+  const int rot = (cs.n_units == 3 * cs.G && cs.G % 8 == 0) ? (bp / (cs.G / 8)) % 3 : 0;
 #else
   const int rot = (VGE_X3S_ROT && cs.n_units == 3 * cs.G && ((bp >> VGE_X3S_ROT_BIT) & 1)) ? VGE_X3S_ROT : 0;
 #endif
