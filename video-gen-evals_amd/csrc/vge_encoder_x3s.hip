@@ -661,14 +661,15 @@ __global__ void __launch_bounds__(512, 1) conv_encoder_x3s_kernel(const float* _
   int n_ex = 0;
   const int n = cs.n_windows;
   const int bp = xcd_remap(blockIdx.x, cs.G);
-  // Round order per XCD.  With three full rounds (256 windows: two quad rounds, then the vit pairs) the blocks of
-  // XCD x start at round x % 3, so at any time about a third of the XCDs run the L2-bound vit pairs and their HBM stem
-  // loads while the rest run MFMA-bound quads, instead of every CU hitting the same kind of round at once; inside an
-  // XCD all CUs still stream one encoder in lockstep (its L2 shared).  Same box, interleaved
+  // Round order per XCD.  The blocks of XCD x start at round x % R (R rounds; at 256 windows two quad rounds, then
+  // the vit pairs), so at any time about a third of the XCDs run the L2-bound vit pairs and their HBM stem loads
+  // while the rest run MFMA-bound quads, instead of every CU hitting the same kind of round at once; inside an XCD
+  // all CUs still stream one encoder in lockstep (its L2 shared).  A partial last round becomes a skipped slot in a
+  // rotated block's order.  600 windows: 2.433-2.442 -> 2.422-2.423 ms; 4,096: unchanged.  Same box, interleaved
   // (profiles/ab_r04j_conv_round_order*.log): plain order 1.019-1.023 ms and 374 MB of fabric fetches (FETCH_SIZE x 2)
   // per launch, per XCD (this) 1.006-1.009 ms and 373 MB, per block (bp % 3: pairs beside quads inside every XCD)
   // 1.000-1.002 ms but 914 MB (the XCD's CUs then stream different encoders and the L2 sharing is lost).  Each unit's
-  // results are unchanged.  VGE_X3S_ROT: 0 plain order, 3 per block, 4 per XCD; 1 / 2: blocks with bit
+  // results are unchanged.  VGE_X3S_ROT: 0 plain order, 3 per block (three full rounds), 4 per XCD; 1 / 2: blocks with bit
   // VGE_X3S_ROT_BIT of bp set start at that round.
 #ifndef VGE_X3S_ROT
 #define VGE_X3S_ROT 4
@@ -677,16 +678,17 @@ __global__ void __launch_bounds__(512, 1) conv_encoder_x3s_kernel(const float* _
 #define VGE_X3S_ROT_BIT 0
 #endif
 #if VGE_X3S_ROT == 3
-  const int rot = cs.n_units == 3 * cs.G ? bp % 3 : 0;
+  const int rot = cs.n_units == 3 * cs.G ? bp % 3 : 0;  // (three full rounds only)
 #elif VGE_X3S_ROT == 4
-  const int rot = (cs.n_units == 3 * cs.G && cs.G % 8 == 0) ? (bp / (cs.G / 8)) % 3 : 0;
+  const int rot = cs.G % 8 == 0 ? (bp / (cs.G / 8)) % ((cs.n_units + cs.G - 1) / cs.G) : 0;
 #else
   const int rot = (VGE_X3S_ROT && cs.n_units == 3 * cs.G && ((bp >> VGE_X3S_ROT_BIT) & 1)) ? VGE_X3S_ROT : 0;
 #endif
-  for (int k = 0; k * cs.G < cs.n_units; ++k) {
-    const int round = rot ? (k + rot) % 3 : k;
+  const int n_rounds = (cs.n_units + cs.G - 1) / cs.G;
+  for (int k = 0; k < n_rounds; ++k) {
+    const int round = rot ? (k + rot) % n_rounds : k;
     const int u = round * cs.G + bp;
-    if (u >= cs.n_units) break;  // uniform over the block
+    if (u >= cs.n_units) continue;  // uniform over the block (only the last round is partial)
     if (u < cs.Q) {
       int e, w0;
       conv_unit(cs, u, e, w0);
