@@ -616,8 +616,9 @@ def run_score(args, world, rank, dev):
 
     def launch_feat(c):
         # featurise chunk c on the side stream once the last encode's conv stage (the last reader of feats) is done:
-        # it runs beside that chunk's fusion + transformer (a featurise workgroup fits next to a transformer
-        # workgroup on a CU: 16 KB of LDS and 141 registers per lane on top of 139 KB and 325)
+        # it runs beside that chunk's fusion + transformer, on the CUs the transformer's workgroups leave free
+        # (every featurise workgroup reserves its kernel's static LDS, ~46 KB, which does not fit beside a transformer
+        # workgroup's 139 KB: the two share the chip, not a CU)
         with torch.cuda.stream(side):
             enc.wait_conv(side)
             if deferred[0] is not None:
@@ -715,6 +716,7 @@ def run_score(args, world, rank, dev):
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    enc.status()  # the device status word of every timed launch (a host read after the synchronize above)
     enc.profile_mask(0x3)  # (profile_read finds the last recorded event from the mask)
     # every rank's (wall time, videos): the line's time is the max over ranks, `value` all ranks' videos / that time
     per_rank = gather_rank_times(dt, V, world, dev)

@@ -1,0 +1,202 @@
+"""GPU parity of TokenHMR's gate detector (detectron2 Faster R-CNN X101-32x8d-FPN, modifications/mesh_generator.py:69-73,
+103-117) through the C ABI (include/vge_frcnn.h) against oracle/frcnn.py, at full width and the reference's 800-pixel
+input on four 256 x 256 frames (two chunks of the workspace).
+
+Every stage is checked on the GPU's own input to that stage, so a tolerance covers one stage's arithmetic:
+  resize        the PIL bilinear resample, byte for byte
+  backbone+FPN  P2..P6 vs the oracle run from the frames (bf16 storage points, 101 layers: relative L2 < 3e-2)
+  RPN head      logits / deltas from the GPU's P levels (one bf16 conv + f32 1x1)
+  proposals     top-k / decode / clip / batched NMS / merge from the GPU's logits: identical order and scores
+  ROIAlign      from the GPU's P levels and proposals: torchvision's float order, identical but for rare 1-ulp bf16
+  box head      fc1 / fc2 / predictor from the GPU's box features
+  inference     softmax / per-class decode / NMS / top 100 / postprocess from the GPU's head: identical instances
+  gate          the person count of mesh_generator.py:106-108, and the whole predictor end to end vs the oracle
+Parity vs detectron2's trained model is UNPINNED (code and weights absent offline; random weights of the reference's
+shapes, vge.synth.make_frcnn_state_dict).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+NF = 4
+
+
+@pytest.fixture(scope="module")
+def run():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from oracle.frcnn import OracleFrcnn
+    from vge import synth
+    from vge.frcnn import FRCNN_X101, FrcnnDetector
+    cfg = FRCNN_X101
+    sd = synth.make_frcnn_state_dict(cfg)
+    det = FrcnnDetector(sd, cfg, device=DEV, chunk=3)          # 4 frames = two chunks (tap / output offsets)
+    frames = synth.make_frame_pool(9100, NF)
+    fr = torch.from_numpy(frames).to(DEV)
+    taps = det.make_taps(NF, 256, 256)
+    out = det.detect(fr, taps=taps)
+    torch.cuda.synchronize()
+    host = lambda v: [x.cpu() for x in v] if isinstance(v, list) else v.cpu()  # noqa: E731
+    r = dict(cfg=cfg, sd=sd, frames=frames, out={k: host(v) for k, v in out.items()},
+             taps={k: host(v) for k, v in taps.items()}, shapes=det.shapes(256, 256),
+             oracle=OracleFrcnn(sd, cfg, bf16=True))
+    det.close()
+    return r
+
+
+@pytest.fixture(scope="module")
+def oracle_fwd(run):
+    """The oracle predictor from the frames themselves, on the first two frames."""
+    torch.set_num_threads(16)
+    res, aux = run["oracle"].detect(run["frames"][:2], taps=True)
+    return res, aux
+
+
+def _nchw(t):  # bf16 [F, h, w, C] -> float [F, C, h, w]
+    return t.float().permute(0, 3, 1, 2).contiguous()
+
+
+def test_resize_is_pil_bilinear(run):
+    from oracle.frcnn import resize_pil
+    nh, nw = run["shapes"]["resized"]
+    for f in range(NF):
+        np.testing.assert_array_equal(run["taps"]["resized"][f].numpy(), resize_pil(run["frames"][f], nh, nw))
+
+
+def test_backbone_fpn_vs_oracle(run, oracle_fwd):
+    _, aux = oracle_fwd
+    for l in range(5):
+        g, o = _nchw(run["taps"]["fpn"][l][:2]), aux["P"][l]
+        rel = float((g - o).norm() / o.norm())
+        mx = float((g - o).abs().max() / o.abs().max())
+        print(f"P{l + 2}: rel L2 {rel:.2e}, max |d| / max |ref| {mx:.2e}")
+        assert rel < 3e-2 and mx < 0.15, (l, rel, mx)
+
+
+def test_rpn_head_vs_oracle(run):
+    o = run["oracle"]
+    for l in range(5):
+        P = _nchw(run["taps"]["fpn"][l][:2])
+        lo, de = o.rpn_head(P)
+        g = run["taps"]["rpn"][l][:2]
+        h, w = g.shape[1:3]
+        gl = g[..., :3].reshape(2, -1)
+        gd = g[..., 3:15].reshape(2, h * w * 3, 4)
+        el, ed = float((gl - lo).abs().max()), float((gd - de).abs().max())
+        print(f"RPN P{l + 2}: logits max|d| {el:.2e} (max {float(lo.abs().max()):.2f}), deltas {ed:.2e}")
+        assert el < 3e-2 * max(1.0, float(lo.abs().max())) and ed < 3e-2 * max(0.1, float(de.abs().max()))
+
+
+def _gpu_head_inputs(run, f):
+    t = run["taps"]
+    logits = [t["rpn"][l][f, ..., :3].reshape(-1) for l in range(5)]
+    deltas = [t["rpn"][l][f, ..., 3:15].reshape(-1, 4) for l in range(5)]
+    return logits, deltas
+
+
+def test_proposals_vs_oracle_on_gpu_logits(run):
+    o, t = run["oracle"], run["taps"]
+    shapes = [tuple(s) for s in run["shapes"]["levels"]]
+    size = tuple(run["shapes"]["resized"])
+    for f in range(NF):
+        lo, de = _gpu_head_inputs(run, f)
+        pb, ps = o.proposals(lo, de, size, shapes)
+        n = int(t["n_proposals"][f])
+        gp = t["proposals"][f, :n]
+        assert n == pb.shape[0], (f, n, pb.shape[0])
+        assert torch.equal(gp[:, 4], ps), f"frame {f}: proposal order / scores differ"
+        err = float((gp[:, :4] - pb).abs().max())
+        print(f"frame {f}: {n} proposals, max |box d| {err:.2e}")
+        assert err < 2e-3
+
+
+def test_box_features_vs_oracle_on_gpu_levels(run):
+    o, t = run["oracle"], run["taps"]
+    for f in range(2):
+        n = int(t["n_proposals"][f])
+        pf = [_nchw(t["fpn"][l][f:f + 1])[0] for l in range(4)]
+        ref = o.box_features(pf, t["proposals"][f, :n, :4])                    # [n, 256, 7, 7] (bf16 values)
+        got = t["box_features"][f, :n].float().view(n, 7, 7, 256).permute(0, 3, 1, 2)
+        d = (got - ref).abs()
+        same = float((d == 0).float().mean())
+        ulp = float((d / ref.abs().clamp_min(1e-30)).max())
+        print(f"frame {f}: ROIAlign bins identical {same:.6f}, max rel diff {ulp:.2e}")
+        assert same > 0.999 and float((d - ref.abs() * 2 ** -7).max()) <= 1e-6
+
+
+def test_box_head_vs_oracle_on_gpu_features(run):
+    o, t, K = run["oracle"], run["taps"], run["cfg"].num_classes
+    for f in range(2):
+        n = int(t["n_proposals"][f])
+        cl, de = o.box_head(t["box_features"][f, :n].float().view(n, 7, 7, 256).permute(0, 3, 1, 2))
+        g = t["head"][f, :n]
+        ec, ed = float((g[:, :K + 1] - cl).abs().max()), float((g[:, K + 1:5 * K + 1] - de).abs().max())
+        print(f"frame {f}: cls logits max|d| {ec:.2e} (max {float(cl.abs().max()):.2f}), deltas {ed:.2e}")
+        assert ec < 3e-2 * max(1.0, float(cl.abs().max())) and ed < 3e-2 * max(0.1, float(de.abs().max()))
+
+
+def test_inference_and_postprocess_vs_oracle_on_gpu_head(run):
+    from oracle.frcnn import OracleFrcnn, gate_persons
+    o, t, out, K = run["oracle"], run["taps"], run["out"], run["cfg"].num_classes
+    size = tuple(run["shapes"]["resized"])
+    checked = 0
+    for f in range(NF):
+        n = int(t["n_proposals"][f])
+        cl, de = t["head"][f, :n, :K + 1], t["head"][f, :n, K + 1:5 * K + 1]
+        e = torch.exp(cl - cl.max(1, keepdim=True).values)
+        p = e / e.sum(1, keepdim=True)
+        if bool(((p[:, :K] - run["cfg"].score_thresh).abs() < 1e-5).any()):
+            print(f"frame {f}: a class probability within 1e-5 of the threshold: skipped")
+            continue
+        b, s, k = o.inference(cl, de, t["proposals"][f, :n, :4], size)
+        m = int(t["n_pre_dets"][f])
+        g = t["pre_dets"][f, :m]
+        assert m == b.shape[0], (f, m, b.shape[0])
+        assert torch.equal(g[:, 5].long(), k), f"frame {f}: classes / order differ"
+        np.testing.assert_allclose(g[:, 4].numpy(), s.numpy(), rtol=2e-6, atol=1e-7)
+        np.testing.assert_allclose(g[:, :4].numpy(), b.numpy(), rtol=1e-5, atol=2e-3)
+        fb, fs, fk = OracleFrcnn.postprocess(b, s, k, size, 256, 256)
+        nd = int(out["n_dets"][f])
+        assert nd == fb.shape[0]
+        np.testing.assert_allclose(out["dets"][f, :nd, :4].numpy(), fb.numpy(), rtol=1e-5, atol=1e-3)
+        assert torch.equal(out["dets"][f, :nd, 5].long(), fk)
+        assert int(out["n_person"][f]) == gate_persons({"classes": fk, "scores": fs})
+        pers = fk == 0
+        for j in range(min(2, int(pers.sum()))):
+            np.testing.assert_allclose(out["person"][f, j, :4].numpy(), fb[pers][j].numpy(), rtol=1e-5, atol=1e-3)
+        checked += 1
+        print(f"frame {f}: {m} instances, {int(out['n_person'][f])} persons > 0.5, classes {k[:8].tolist()}")
+    assert checked >= 2
+
+
+def test_predictor_end_to_end_vs_oracle(run, oracle_fwd):
+    """The whole predictor from the frames: the oracle's instances are found among the GPU's (same class, IoU > 0.9,
+    score within 0.05) and the gate's person count agrees unless an oracle person score is within 0.05 of 0.5."""
+    res, _ = oracle_fwd
+    out = run["out"]
+    from oracle.frcnn import gate_persons
+    for f, r in enumerate(res):
+        nd = int(out["n_dets"][f])
+        g = out["dets"][f, :nd]
+        top = min(20, len(r["scores"]))
+        hit = 0
+        for j in range(top):
+            bo = r["boxes"][j]
+            same = g[g[:, 5].long() == int(r["classes"][j])]
+            if same.shape[0] == 0:
+                continue
+            x1 = torch.maximum(same[:, 0], bo[0]); y1 = torch.maximum(same[:, 1], bo[1])
+            x2 = torch.minimum(same[:, 2], bo[2]); y2 = torch.minimum(same[:, 3], bo[3])
+            inter = (x2 - x1).clamp_min(0) * (y2 - y1).clamp_min(0)
+            iou = inter / ((same[:, 2] - same[:, 0]) * (same[:, 3] - same[:, 1]) + (bo[2] - bo[0]) * (bo[3] - bo[1]) - inter)
+            ok = (iou > 0.9) & ((same[:, 4] - r["scores"][j]).abs() < 0.05)
+            hit += int(bool(ok.any()))
+        print(f"frame {f}: {hit}/{top} oracle instances matched; persons gpu {int(out['n_person'][f])} "
+              f"oracle {gate_persons(r)}")
+        assert hit >= 0.8 * top
+        ps = r["scores"][r["classes"] == 0]
+        if not bool(((ps - 0.5).abs() < 0.05).any()):
+            assert int(out["n_person"][f]) == gate_persons(r)

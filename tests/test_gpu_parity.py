@@ -395,3 +395,22 @@ def test_conv_exchange_timeout_raises_device_fault(vg, golden_state_dict):
     torch.cuda.synchronize()
     enc.status()
     assert torch.equal(good, again)
+
+
+def test_device_fault_in_the_last_encode_stops_run_eval(vg, golden_dataset, tmp_path):
+    """a fault in the last (here: the only) encode of a flow has no later vge_encode to report it; the flow
+    checks the status word after its final synchronize, so run_eval raises DeviceFaultError instead of writing scores
+    computed from wrong embeddings.  The golden set is one batch (< 1024 windows) per phase."""
+    VE, _ = vg
+    from vge import lib as L
+    so = L.load()
+    paths, ckpt = golden_dataset
+    out = tmp_path / "scores.json"
+    so.vge_debug_set_x3s_spin_limit(0)
+    try:
+        with pytest.raises(L.DeviceFaultError):
+            VE.run_eval(paths["generated_meshes"], paths["real"], ckpt, paths["generated_kps"], paths["real_kp"],
+                        out_json=str(out), device=DEV, compute="f32x3")
+    finally:
+        so.vge_debug_set_x3s_spin_limit(-1)
+    assert not out.exists()

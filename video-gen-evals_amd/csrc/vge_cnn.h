@@ -12,7 +12,9 @@ struct ConvLaunch {
   const void* res; long ldr; const float* rscale;
   const void* zero;                         // >= 16 B of zeros in device memory
   int n_img, H, W, Cin, KH, KW, stride, pad, Kp, Cout, Npad;
-  int act, out_f32, res_mode, tn;           // act 0 none / 1 SiLU / 2 sigmoid; res 0 / 1 bf16 / 2 f32 scaled
+  int act, out_f32, res_mode, tn;           // act 0 none / 1 SiLU / 2 sigmoid / 3 ReLU; res 0 / 1 bf16 (after
+                                            // act) / 2 f32 scaled / 3 bf16 before act
+  int gslice;                               // grouped conv slices (vge_cnn.hip ConvArgs::gslice): Cin == tn
   int variant;                              // 0 default; 1 128-row kernel (tn <= 128); 2 256 x 256 tiles, one per
                                             // workgroup; 3 256 x 256 tiles on the persistent grid (res_mode 0 only);
                                             // 5 256-row tiles with tn (64 / 128) columns; 6 512 x 128 tiles on

@@ -35,9 +35,9 @@ typedef unsigned uintx4_t __attribute__((ext_vector_type(4)));
 
 constexpr int CV_M = 128, CV_K = 32, CV_ST = 3;
 
-enum { ACT_NONE = 0, ACT_SILU = 1, ACT_SIGMOID = 2 };
+enum { ACT_NONE = 0, ACT_SILU = 1, ACT_SIGMOID = 2, ACT_RELU = 3 };
 enum { OUT_BF16 = 0, OUT_F32 = 1 };
-enum { RES_NONE = 0, RES_BF16 = 1, RES_F32S = 2 };
+enum { RES_NONE = 0, RES_BF16 = 1, RES_F32S = 2, RES_BF16_PRE = 3 };  // _PRE: added before the activation
 
 struct ConvArgs {
   const bf16* x;       // NHWC input, pixel stride ldx elements (channel offset folded into the pointer)
@@ -49,6 +49,8 @@ struct ConvArgs {
   const bf16* zero;    // >= 16 B of zeros (the source of padding taps)
   long ldx, ldo, ldr;
   int H, W, cin_log2, Ho, Wo, KW, kw_magic, stride, pad, taps, Kp, Cout, M;
+  int gslice;          // grouped conv as block-diagonal slices: the tile of output columns n0.. reads input channels
+                       // n0 .. n0 + Cin - 1 (Cin = the tile width; weights [Cout][taps * Cin], zero off the groups)
 };
 
 __device__ __forceinline__ int xcd_remap(int b, int nblk) {  // bijective: each XCD takes a contiguous range
@@ -68,7 +70,10 @@ __device__ __forceinline__ RowState row_state(const ConvArgs& a, int m, int lc8)
   const int img = m / hw, rem = m - img * hw;
   const int oh = rem / a.Wo, ow = rem - oh * a.Wo;
   const int ih0 = m < a.M ? oh * a.stride - a.pad : -16384, iw0 = ow * a.stride - a.pad;
-  return {a.x + (long)((img * a.H + ih0) * a.W + iw0) * a.ldx + lc8, (ih0 << 16) | (iw0 & 0xFFFF)};
+  // 64-bit row offset (n_img * H * W may pass 2^31 elements); a row past M keeps the base pointer (its taps all fail
+  // the bounds check and read the zero page, so no out-of-range address is ever formed for it)
+  const long off = m < a.M ? ((long)img * a.H + ih0) * a.W + iw0 : 0;
+  return {a.x + off * a.ldx + lc8, (ih0 << 16) | (iw0 & 0xFFFF)};
 }
 // The 32-k stage starting at k0 of NR rows into LDS (row j's 1 KB wave-instruction at dst(j)).  Cin >= 32: the stage
 // lies inside one tap, so the tap, its (kh, kw) and the channel base are uniform (scalar) and a row's source is its
@@ -134,7 +139,10 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
   const int lc8 = lc * 8;
   RowState rws[AJ];
 #pragma unroll
-  for (int j = 0; j < AJ; ++j) rws[j] = row_state(a, m0 + 16 * (AJ * wave + j) + (lane >> 2), lc8);
+  for (int j = 0; j < AJ; ++j) {
+    rws[j] = row_state(a, m0 + 16 * (AJ * wave + j) + (lane >> 2), lc8);
+    if (a.gslice) rws[j].p += n0;  // grouped: this column tile's input channel slice
+  }
   const bf16* wrow[BQ];
 #pragma unroll
   for (int j = 0; j < BQ; ++j) wrow[j] = a.w + (size_t)(n0 + 16 * (BQ * wave + j) + (lane >> 2)) * a.Kp + lc8;
@@ -225,10 +233,16 @@ __global__ void __launch_bounds__(256) conv_bf16_kernel(ConvArgs a) {
       const floatx4 x0 = *reinterpret_cast<const floatx4*>(cs + rl * LDC + c8) + b0;
       const floatx4 x1 = *reinterpret_cast<const floatx4*>(cs + rl * LDC + c8 + 4) + b1;
       v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w; v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+      if constexpr (RES == RES_BF16_PRE) {
+        const bf16x8 r8 = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(a.res) + (size_t)m * a.ldr + col);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] += (float)r8[i];
+      }
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
         if constexpr (ACT == ACT_SILU) v[i] = silu(v[i]);
         if constexpr (ACT == ACT_SIGMOID) v[i] = sigm(v[i]);
+        if constexpr (ACT == ACT_RELU) v[i] = fmaxf(v[i], 0.f);
       }
       if constexpr (RES == RES_BF16) {
         const bf16x8 r8 = *reinterpret_cast<const bf16x8*>(reinterpret_cast<const bf16*>(a.res) + (size_t)m * a.ldr + col);
@@ -413,10 +427,17 @@ __global__ void __launch_bounds__(512, 1) conv2_bf16_kernel(ConvArgs a) {
       floatx4 v = *reinterpret_cast<const floatx4*>(my + rl * WC + c4) + bb;
       if (m >= a.M || gcol >= a.Cout) continue;
       float e[4] = {v.x, v.y, v.z, v.w};
+      if constexpr (RES == RES_BF16_PRE) {
+        typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+        const bf16x4_t r4 = *reinterpret_cast<const bf16x4_t*>(reinterpret_cast<const bf16*>(a.res) + (size_t)m * a.ldr + gcol);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) e[i] += (float)r4[i];
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         if constexpr (ACT == ACT_SILU) e[i] = silu(e[i]);
         if constexpr (ACT == ACT_SIGMOID) e[i] = sigm(e[i]);
+        if constexpr (ACT == ACT_RELU) e[i] = fmaxf(e[i], 0.f);
       }
       if constexpr (RES == RES_BF16) {
         typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
@@ -648,7 +669,8 @@ __global__ void __launch_bounds__(512, 1) conv2p_bf16_kernel(ConvArgs a) {
       const int t = blk / TN, u = blk % TN;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        if constexpr (RES == RES_BF16) d[q] = __builtin_amdgcn_raw_buffer_load_b64(rb, offs(t, u, q, a.ldr, RE), 0, 0);
+        if constexpr (RES == RES_BF16 || RES == RES_BF16_PRE)
+          d[q] = __builtin_amdgcn_raw_buffer_load_b64(rb, offs(t, u, q, a.ldr, RE), 0, 0);
         if constexpr (RES == RES_F32S) d[q] = __builtin_amdgcn_raw_buffer_load_b128(rb, offs(t, u, q, a.ldr, RE), 0, 0);
       }
     };
@@ -668,10 +690,16 @@ __global__ void __launch_bounds__(512, 1) conv2p_bf16_kernel(ConvArgs a) {
           e[1] += bb[u].y;
           e[2] += bb[u].z;
           e[3] += bb[u].w;
+          if constexpr (RES == RES_BF16_PRE) {
+            const bf16x4_t r4 = __builtin_bit_cast(bf16x4_t, rv[blk & 1][q]);
+#pragma unroll
+            for (int c = 0; c < 4; ++c) e[c] += (float)r4[c];
+          }
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
             if constexpr (ACT == ACT_SILU) e[c] = silu(e[c]);
             if constexpr (ACT == ACT_SIGMOID) e[c] = sigm(e[c]);
+            if constexpr (ACT == ACT_RELU) e[c] = fmaxf(e[c], 0.f);
           }
           if constexpr (RES == RES_BF16) {
             const bf16x4_t r4 = __builtin_bit_cast(bf16x4_t, rv[blk & 1][q]);
@@ -1272,8 +1300,13 @@ hipError_t launch_conv_bf16(const ConvLaunch& c, hipStream_t s) {
   a.Kp = c.Kp;
   a.Cout = c.Cout;
   a.M = c.n_img * a.Ho * a.Wo;
+  a.gslice = c.gslice;
   int tn = c.tn, pmode = -1;
-  const int variant = c.variant == 0 && g_conv_force > 0 ? g_conv_force : c.variant;
+  const int variant = c.variant == 0 && g_conv_force > 0 && !c.gslice ? g_conv_force : c.variant;
+  // grouped slices run on the 128- / 256-row kernel only, with the slice width as the column tile
+  if (c.gslice && (variant == 2 || variant == 3 || variant == 6 || (c.tn != 64 && c.tn != 128) || c.Cin != c.tn ||
+                   c.Cout % c.tn))
+    return hipErrorInvalidValue;
   if (variant == 6) {  // 512 x 128 persistent tiles
     tn = 128;
     pmode = 6;
@@ -1301,6 +1334,9 @@ hipError_t launch_conv_bf16(const ConvLaunch& c, hipStream_t s) {
   VGE_CONV_CASE(ACT_NONE, OUT_F32, RES_NONE)
   VGE_CONV_CASE(ACT_SILU, OUT_F32, RES_NONE)
   VGE_CONV_CASE(ACT_SIGMOID, OUT_F32, RES_NONE)
+  VGE_CONV_CASE(ACT_RELU, OUT_BF16, RES_NONE)       // Faster R-CNN: conv + FrozenBN + ReLU, RPN conv, box head fc
+  VGE_CONV_CASE(ACT_RELU, OUT_BF16, RES_BF16_PRE)   // bottleneck conv3: relu(conv + shortcut)
+  VGE_CONV_CASE(ACT_NONE, OUT_BF16, RES_BF16)       // FPN lateral + top-down sum
 #undef VGE_CONV_CASE
   return hipErrorInvalidValue;
 }

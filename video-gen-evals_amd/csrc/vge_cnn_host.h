@@ -201,7 +201,9 @@ inline hipError_t conv_tuned_launch(ConvTuner& t, ConvLaunch& c, const std::arra
       cand.push_back(5000 + 64);
     }
     if (c.res_mode == 0 && c.Cout % 4 == 0) cand.push_back(3000 + 256);
-    if (c.Cout > 64 && c.Cout <= 128 && c.Cout % 4 == 0) cand.push_back(6000 + 128);  // 512 x 128 persistent
+    // 512 x 128 persistent tile: residual-free layers only, like variant 3 (conv2_go keeps residual epilogues off the
+    // persistent kernels: its hand-counted vmcnt budget is reasoned for RES_NONE)
+    if (c.res_mode == 0 && c.Cout > 64 && c.Cout <= 128 && c.Cout % 4 == 0) cand.push_back(6000 + 128);
     int pick = -1;
     float best_ms = 0.f;
     for (int v : cand) {

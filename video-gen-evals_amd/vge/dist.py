@@ -259,6 +259,7 @@ def _run_eval_phases(real_meshes_dir, model_path, keypoint_dir, real_kp_dir, cli
                               "cls_names": list(feats["cls_names"]), "vid_names": list(feats["vid_names"])}
         if torch.cuda.is_available() and str(device).startswith("cuda"):
             torch.cuda.synchronize(device)
+            model.status()  # a device fault in this rank's last encode stops every rank (guarded) instead of scoring
         return combined, feats_host
 
     combined, feats_host = guarded("generated-set scoring", local_scores)

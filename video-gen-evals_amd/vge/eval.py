@@ -158,6 +158,10 @@ def encode_windows(model: ops.Encoder, store: ops.DeviceFrameStore, windows: tor
         tcw[b0:b1] = t
         if frame_embed:
             fe[b0:b1] = fr
+    # the conv kernel's device status word: a fault in the last (or only) batch has no later vge_encode to report it,
+    # so check it once every launch has completed, before the caller consumes these embeddings
+    torch.cuda.synchronize(dev)
+    model.status()
     return seq, fe, tcw
 
 

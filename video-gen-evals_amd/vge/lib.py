@@ -29,7 +29,9 @@ EXPORTS = ["vge_featurize", "vge_featurize_layout", "vge_layout_feat_dim", "vge_
            "vge_dwpose_profile_begin", "vge_dwpose_profile_read", "vge_op_conv_bf16",
            "vge_yolox_create", "vge_yolox_reserve", "vge_yolox_destroy", "vge_yolox_detect", "vge_yolox_detect_scored",
            "vge_hmr_crop",
-           "vge_yolox_profile_begin", "vge_yolox_profile_read"]
+           "vge_yolox_profile_begin", "vge_yolox_profile_read",
+           "vge_frcnn_create", "vge_frcnn_reserve", "vge_frcnn_destroy", "vge_frcnn_shapes", "vge_frcnn_detect",
+           "vge_frcnn_profile_begin", "vge_frcnn_profile_read"]
 
 
 class VgeError(RuntimeError):

@@ -490,3 +490,79 @@ def make_frame_pool(seed: int, n_frames: int, per_scene: int = 4, h: int = 256, 
     e2e bench draws its clips' frames from, by what the detector finds in each."""
     scenes = [make_frames(seed + i, per_scene, h, w) for i in range(-(-n_frames // per_scene))]
     return np.concatenate(scenes, 0)[:n_frames]
+
+
+def make_frcnn_state_dict(cfg, seed: int = SEED_WEIGHTS + 40, cls_gain: float = 4.0) -> Dict[str, np.ndarray]:
+    """Deterministic random weights for TokenHMR's gate detector, detectron2's Faster R-CNN X101-32x8d-FPN
+    (vge.frcnn.FrcnnConfig shapes, detectron2 state_dict keys).  The model-zoo weights are a download (none offline):
+    parity vs detectron2 is unpinned.  Convs He-initialised N(0, 2 / fan_in) with the bottleneck's last conv at 0.02 /
+    fan_in (the 23-block res4 stream stays O(1)), FPN convs 0.25 / 0.5 over fan_in, FrozenBN weight 1 + N(0, 0.1), bias / running mean N(0, 0.1),
+    running var U(0.5, 1.5); FPN / RPN / fc biases N(0, 0.1); objectness logits O(1) (no flat ties among the top-k);
+    box deltas ~0.1; cls_score N(0, cls_gain^2 / 1024) + N(0, 1) biases, so the softmax over 81 classes is peaked and
+    most proposals carry one or two classes above the 0.25 threshold (every class-aware path runs)."""
+    rng = np.random.default_rng(seed)
+    sd: Dict[str, np.ndarray] = {}
+
+    def N(shape, s):
+        return (rng.standard_normal(size=shape, dtype=np.float32) * np.float32(s)).astype(np.float32)
+
+    def conv_bn(name, cin, cout, k, groups=1, gain=2.0):
+        fan = (cin // groups) * k * k
+        sd[name + ".weight"] = N((cout, cin // groups, k, k), np.sqrt(gain / fan))
+        sd[name + ".norm.weight"] = (1.0 + N((cout,), 0.1)).astype(np.float32)
+        sd[name + ".norm.bias"] = N((cout,), 0.1)
+        sd[name + ".norm.running_mean"] = N((cout,), 0.1)
+        sd[name + ".norm.running_var"] = (0.5 + rng.random(size=(cout,), dtype=np.float32)).astype(np.float32)
+
+    def conv_b(name, cin, cout, k, gain=1.0, bias=0.1):
+        sd[name + ".weight"] = N((cout, cin, k, k), np.sqrt(gain / (cin * k * k)))
+        sd[name + ".bias"] = N((cout,), bias)
+
+    def linear(name, cin, cout, std, bias=0.1):
+        sd[name + ".weight"] = N((cout, cin), std)
+        sd[name + ".bias"] = N((cout,), bias)
+
+    bb = "backbone.bottom_up."
+    conv_bn(bb + "stem.conv1", 3, cfg.stem_ch, 7)
+    blocks = {50: (3, 4, 6, 3), 101: (3, 4, 23, 3), 152: (3, 8, 36, 3)}[cfg.depth]
+    cin, width, out = cfg.stem_ch, cfg.groups * cfg.width_per_group, cfg.res2_ch
+    for s, nb in enumerate(blocks):
+        for b in range(nb):
+            p = f"{bb}res{s + 2}.{b}"
+            if b == 0:
+                conv_bn(p + ".shortcut", cin, out, 1, gain=1.0)
+            conv_bn(p + ".conv1", cin if b == 0 else out, width, 1)
+            conv_bn(p + ".conv2", width, width, 3, groups=cfg.groups)
+            conv_bn(p + ".conv3", width, out, 1, gain=0.02)
+        cin, width, out = out, width * 2, out * 2
+    F = cfg.fpn_ch
+    for l in range(4):
+        conv_b(f"backbone.fpn_lateral{l + 2}", cfg.res2_ch << l, F, 1, gain=0.25)
+        conv_b(f"backbone.fpn_output{l + 2}", F, F, 3, gain=0.5)
+    conv_b("proposal_generator.rpn_head.conv", F, F, 3, gain=2.0)
+    conv_b("proposal_generator.rpn_head.objectness_logits", F, 3, 1, gain=1.0, bias=0.5)
+    conv_b("proposal_generator.rpn_head.anchor_deltas", F, 12, 1, gain=0.01, bias=0.0)
+    linear("roi_heads.box_head.fc1", F * cfg.pool * cfg.pool, cfg.fc_dim, np.sqrt(2.0 / (F * cfg.pool * cfg.pool)))
+    linear("roi_heads.box_head.fc2", cfg.fc_dim, cfg.fc_dim, np.sqrt(2.0 / cfg.fc_dim))
+    linear("roi_heads.box_predictor.cls_score", cfg.fc_dim, cfg.num_classes + 1, cls_gain / np.sqrt(cfg.fc_dim), 1.0)
+    linear("roi_heads.box_predictor.bbox_pred", cfg.fc_dim, 4 * cfg.num_classes, 0.1 / np.sqrt(cfg.fc_dim), 0.0)
+    return sd
+
+
+# The e2e bench's gate detector (mesh_generator.py:103-117 with the reference's Faster R-CNN).  With
+# make_frcnn_state_dict's weights most frames have several person instances above 0.5, so the gate would reject every
+# video.  These weights differ in the predictor's class biases only: classes 1..79 at -20 (never above 0.25), so a
+# proposal's person probability is sigmoid(person logit - background logit); one common background bias (the person
+# logits' ranking, hence which boxes the class-aware NMS keeps, is unchanged) puts the 0.5 threshold between the first
+# and second kept person instance of as many pool frames as possible.  GATE_FRCNN_BG is measured on make_frame_pool's
+# frames by tools/frcnn_gate_calib.py on the GPU; VGE_GATE_FRCNN_BG overrides it for a calibration run.
+GATE_FRCNN_BG = float(os.environ.get("VGE_GATE_FRCNN_BG", "0.0"))
+
+
+def make_gate_frcnn_state_dict(cfg, bg: float = None) -> Dict[str, np.ndarray]:
+    sd = make_frcnn_state_dict(cfg)
+    b = sd["roi_heads.box_predictor.cls_score.bias"]
+    b[0] = np.float32(0.0)
+    b[1:cfg.num_classes] = np.float32(-20.0)
+    b[cfg.num_classes] = np.float32(GATE_FRCNN_BG if bg is None else bg)
+    return sd
