@@ -5,14 +5,13 @@ fusion encoder (f32x3) -> AC/TC, per step `--clips` 32-frame clips per GPU.
 
 The reference pipeline is extract_mesh.py (TokenHMR per frame, modifications/mesh_generator.py:119-171) + DWPose
 (modifications/process_video.py) -> npz / keypoints.npy on disk -> eval.py.  Here the frames-to-scores path stays
-in HBM and both extractors start from the full frames.  One YOLOX-L person detection per frame (640x640 letterbox)
-serves both: DWPose runs as the reference's Wholebody does (RTMPose-l on persons 0 / 1, the whole frame when nobody
-is found -> keypoints.npy rows), and TokenHMR's front end (mesh_generator.py:101-145; YOLOX-L stands in for its
-detectron2 Faster R-CNN, absent offline) applies the single-person gate (exactly one person > 0.5) and crops every
-frame with ViTDetDataset's warp (vge_hmr_crop).  The gate's decision is computed and reported (`front_end`); a frame
-it rejects is still cropped (whole-frame box) and extracted, so the timed work is the every-frame-valid upper bound
-whatever the random-weight detector finds.  `--no-detector`: whole-frame boxes for both extractors.  Parity for the
-upstream models is unpinned.
+in HBM and both extractors start from the full frames, each with the reference's own person detector on every frame:
+TokenHMR's front end (mesh_generator.py:101-145) runs detectron2's Faster R-CNN X101-32x8d-FPN at 800 px (vge.frcnn),
+applies the single-person gate (exactly one person instance > 0.5 per frame, >= 80 % of a video's frames) and crops
+the kept frames with ViTDetDataset's warp (vge_hmr_crop); DWPose runs as the reference's Wholebody does (YOLOX-L
+persons, RTMPose-l on persons 0 / 1, the whole frame when nobody is found -> keypoints.npy rows).  The Faster R-CNN +
+TokenHMR chain runs on one HIP stream, YOLOX + DWPose on another.  `--no-detector`: neither detector (whole-frame
+boxes, every frame kept).  Parity for the upstream models is unpinned.
 
 Roofline: the backbone GEMM kernel (gemm_bf16_kernel, MFMA bound): achieved = algorithmic FLOPs of every backbone
 GEMM launch / their summed durations (hipEvents recorded around each launch on the extract stream inside the timed
@@ -23,6 +22,7 @@ from __future__ import annotations
 
 import json
 import os
+import sys
 import time
 
 import numpy as np
@@ -32,8 +32,10 @@ import torch.distributed as dist
 BF16_MFMA_PEAK_TFLOPS = 2516.6
 # kernel sources whose PMC pass (tools/profile_e2e.sh -> tools/pmc_e2e.py -> profiles/pmc_e2e.json) gives `traffic`
 E2E_KERNEL_SOURCES = {"gemm_bf16_kernel": ["vge_vit.hip"],
-                      "yolox_conv": ["vge_cnn.hip", "vge_cnn_host.h", "vge_yolox.cpp"]}
+                      "yolox_conv": ["vge_cnn.hip", "vge_cnn_host.h", "vge_yolox.cpp"],
+                      "frcnn_conv": ["vge_cnn.hip", "vge_cnn_host.h", "vge_frcnn.cpp"]}
 YOLOX_CHUNK = 256   # frames per detector pass (tools/yolox_prof.py --chunk: 637 vs 618 TFLOP/s at 64)
+FRCNN_CHUNK = 32    # frames per Faster R-CNN workspace chunk (~0.3 GB per 800 x 800 frame)
 
 
 def e2e_traffic(kernel: str, frames: float):
@@ -52,19 +54,22 @@ def e2e_traffic(kernel: str, frames: float):
 
 def cpu_baseline_e2e(seconds: float, detector: bool = True):
     from oracle.dwpose import OracleRtmpose
+    from oracle.frcnn import OracleFrcnn
     from oracle.hmr import OracleHmr
     from oracle.yolox import OracleYolox
     from vge import synth
     from vge.dwpose import RTMPOSE_L, YOLOX_L
+    from vge.frcnn import FRCNN_X101
     from vge.hmr import TOKENHMR
     threads = max(1, min(16, len(os.sched_getaffinity(0))))
     torch.set_num_threads(threads)
     o = OracleHmr(synth.make_hmr_state_dict(TOKENHMR), TOKENHMR, bf16=False)
     p = OracleRtmpose(synth.make_rtmpose_state_dict(RTMPOSE_L), RTMPOSE_L, bf16=False)
     y = OracleYolox(synth.make_yolox_state_dict(YOLOX_L), YOLOX_L, bf16=False) if detector else None
+    g = OracleFrcnn(synth.make_gate_frcnn_state_dict(FRCNN_X101), FRCNN_X101, bf16=False) if detector else None
     frames = synth.make_frames(99, 4)
     full = [[0.0, 0.0, 256.0, 256.0]] * frames.shape[0]
-    n, used_h, used_p = 0, 0.0, 0.0
+    n, used_h, used_p, used_g, ng = 0, 0.0, 0.0, 0.0, 0
     while used_h + used_p < seconds or n == 0:
         t0 = time.perf_counter()
         o.forward(frames)
@@ -75,13 +80,20 @@ def cpu_baseline_e2e(seconds: float, detector: bool = True):
         used_p += time.perf_counter() - t1
         used_h += t1 - t0
         n += frames.shape[0]
-    fps = n / (used_h + used_p)
+    if g is not None:   # the gate detector: one frame (several seconds of CPU work at 800 px), rate per frame
+        t0 = time.perf_counter()
+        g.detect(frames[:1])
+        used_g, ng = time.perf_counter() - t0, 1
+    spf = (used_h + used_p) / n + (used_g / ng if ng else 0.0)
+    fps = 1.0 / spf
     return {"value": fps / 32.0, "unit": "videos/s", "cores": threads, "kind": "port",
             "sample": f"{n} frames through oracle/hmr.py (fp32 torch ViT-H/16 + decoder head) and oracle/dwpose.py "
-                      f"({'fp32 torch YOLOX-L + ' if y is not None else ''}RTMPose-l whole-body), {threads} threads, "
-                      f"{used_h:.1f} + {used_p:.1f} s = "
-                      f"{fps:.3f} frames/s, / 32 frames per clip (the scoring stages, ~450 clips/s on the same host in "
-                      f"the config-2 baseline, are <0.1% of this and not added)"}
+                      f"({'fp32 torch YOLOX-L + ' if y is not None else ''}RTMPose-l whole-body) in "
+                      f"{used_h:.1f} + {used_p:.1f} s"
+                      + (f", {ng} frame through oracle/frcnn.py (fp32 torch Faster R-CNN X101-32x8d-FPN at 800 px) in "
+                         f"{used_g:.1f} s" if ng else "")
+                      + f", {threads} threads: {fps:.3f} frames/s, / 32 frames per clip (the scoring stages, ~450 "
+                        f"clips/s on the same host in the config-2 baseline, are <0.1% of this and not added)"}
 
 
 def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
@@ -90,7 +102,8 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
     from vge.data import ACTION_CLASSES, pack_frame_store
     from vge.dist import shard
     from vge.dwpose import RTMPOSE_L, YOLOX_L, DwposeExtractor, YoloxDetector
-    from vge.extract import gate_videos, single_person_mask
+    from vge.extract import gate_mask, gate_videos
+    from vge.frcnn import FRCNN_X101, FrcnnDetector
     from vge.hmr import TOKENHMR, HmrExtractor, crop_persons
 
     C, T = args.clips, 32
@@ -130,13 +143,15 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
     dw = DwposeExtractor(synth.make_rtmpose_state_dict(RTMPOSE_L), RTMPOSE_L, device=dev, max_instances=2 * FC)
     det = None if args.no_detector else YoloxDetector(synth.make_gate_detector_state_dict(YOLOX_L), YOLOX_L,
                                                       device=dev, chunk=min(FC, YOLOX_CHUNK))
+    gdet = None if args.no_detector else FrcnnDetector(synth.make_gate_frcnn_state_dict(FRCNN_X101), FRCNN_X101,
+                                                       device=dev, chunk=min(FC, FRCNN_CHUNK))
     no_box = np.zeros(FC, np.int32)
     Hf = Wf = 256
     whole = np.tile(np.array([0, 0, Wf, Hf], np.float32), (FC, 1))
-    # the generated clips' frames: drawn from a pool of synthetic scenes by what the detector finds in each pool frame
-    # (setup, untimed), so that 9 clips in 10 pass the single-person gate (2-3 of their 32 frames with no or two
-    # persons) and 1 in 10 is rejected (12 such frames: 20 / 32 < 80 %).  The timed steps run the detector on every
-    # frame again and take every decision from its output.
+    # the generated clips' frames: drawn from a pool of synthetic scenes by what the gate detector finds in each pool
+    # frame (setup, untimed), so that 9 clips in 10 pass the single-person gate (2-3 of their 32 frames with no or two
+    # persons) and 1 in 10 is rejected (12 such frames: 20 / 32 < 80 %).  The timed steps run the detectors on every
+    # frame again and take every decision from their output.
     gate_plan = {"accept_every": 10, "bad_frames_accepted": (2, 3), "bad_frames_rejected": 12}
     if det is None:
         frames = torch.from_numpy(synth.make_frame_pool(5000 + 997 * rank, min(F, 4096))).to(dev)
@@ -144,12 +159,11 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
     else:
         P = 2048
         pool = torch.from_numpy(synth.make_frame_pool(5000 + 997 * rank, P)).to(dev)
-        _, _, psc = det.detect(pool, with_scores=True)
-        good = np.flatnonzero(single_person_mask(psc.cpu().numpy()))
+        good = np.flatnonzero(gate_mask(gdet.detect(pool)["n_person"].cpu().numpy()))
         bad = np.setdiff1d(np.arange(P), good)
         if good.size < 64 or bad.size < 64:
-            raise RuntimeError(f"e2e: the detector finds exactly one person in {good.size} of {P} pool frames; "
-                               "recalibrate vge.synth.GATE_OBJ_SHIFT (tools/yolox_gate_calib.py)")
+            raise RuntimeError(f"e2e: the gate detector finds exactly one person in {good.size} of {P} pool frames; "
+                               "recalibrate vge.synth.GATE_FRCNN_BG (tools/frcnn_gate_calib.py)")
         rs = np.random.default_rng(11 + rank)
         idx = np.empty(F, np.int64)
         for c in range(C):
@@ -183,30 +197,48 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
 
     pin_b = torch.empty((FC, 2, 4), dtype=torch.float32, pin_memory=True)
     pin_n = torch.empty((FC,), dtype=torch.int32, pin_memory=True)
-    pin_s = torch.empty((FC, 2), dtype=torch.float32, pin_memory=True)
+    pin_gb = torch.empty((FC, 2, 5), dtype=torch.float32, pin_memory=True)
+    pin_gn = torch.empty((FC,), dtype=torch.int32, pin_memory=True)
+    gate_ready = torch.cuda.Event()
     gate = {"frames": 0, "single_person": 0, "videos": 0, "accepted": 0, "hmr_frames": 0}
 
-    def detect(fr):
-        """the shared person detection -> host (the pose model's instance table and the TokenHMR gate / crop boxes
-        are built on the host, as the reference's numpy NMS output is) -> (boxes, n_persons, single-person mask)"""
+    def detect_gate(fr):
+        """the Faster R-CNN on every frame, its person outputs to pinned host memory (the gate and the crop boxes are
+        decided on the host, as mesh_generator.py does with the predictor's instances)"""
         n = int(fr.shape[0])
-        if det is None:
-            return None, no_box[:n], np.ones(n, bool)
-        boxes, npers, scores = det.detect(fr, with_scores=True)
-        pin_b[:n].copy_(boxes, non_blocking=True)
-        pin_n[:n].copy_(npers, non_blocking=True)
-        pin_s[:n].copy_(scores, non_blocking=True)
-        torch.cuda.current_stream(dev).synchronize()
-        keep = single_person_mask(pin_s[:n].numpy())
+        if gdet is None:
+            return
+        g = gdet.detect(fr)
+        pin_gb[:n].copy_(g["person"], non_blocking=True)
+        pin_gn[:n].copy_(g["n_person"], non_blocking=True)
+        gate_ready.record()
+
+    def gate_result(n):
+        """-> (person boxes [n, 4] of the first class-0 instance, single-person mask) once the gate's copies landed"""
+        if gdet is None:
+            return None, np.ones(n, bool)
+        gate_ready.synchronize()
+        keep = gate_mask(pin_gn[:n].numpy())
         gate["frames"] += n
         gate["single_person"] += int(keep.sum())
-        return pin_b[:n].numpy(), pin_n[:n].numpy(), keep
+        return pin_gb[:n, 0, :4].numpy(), keep
 
-    def hmr(fr, hb, kept, off):
+    def detect_pose(fr):
+        """DWPose's YOLOX persons -> host (the pose model's instance table, as the reference's numpy NMS output)"""
+        n = int(fr.shape[0])
+        if det is None:
+            return None, no_box[:n]
+        boxes, npers = det.detect(fr)
+        pin_b[:n].copy_(boxes, non_blocking=True)
+        pin_n[:n].copy_(npers, non_blocking=True)
+        torch.cuda.current_stream(dev).synchronize()
+        return pin_b[:n].numpy(), pin_n[:n].numpy()
+
+    def hmr(fr, gb, kept, off):
         """TokenHMR on the kept frames of the pass's accepted videos, into rows off.. of the frame store"""
         nk = int(kept.size)
         if nk:
-            box = whole[:nk] if hb is None else hb[kept, 0]
+            box = whole[:nk] if gb is None else gb[kept]
             crops = crop_persons(fr, box, kept)
             ex.extract(crops, out={k: v[off:off + nk] for k, v in outs.items()})
             gate["hmr_frames"] += nk
@@ -214,15 +246,35 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
     def keypoints(fr, hb, hn, f0):
         dw.keypoints(fr, hb, hn, out=gstore.kp[f0:f0 + int(fr.shape[0])])
 
+    beat = [time.perf_counter()]
+
+    def heartbeat(msg):
+        """a progress line every ~20 s on stderr (a 1k-clip step runs for about a minute without other output)"""
+        now = time.perf_counter()
+        if now - beat[0] > 20.0:
+            beat[0] = now
+            print(f"[e2e] {msg}", file=sys.stderr, flush=True)
+
     def step():
         tab = pin_tab.numpy()
         vids = tab[:4 * C].reshape(C, 4)
         acc = []
         off = 0
+        cur = torch.cuda.current_stream(dev)
+        if concurrent:
+            s_hmr.wait_stream(cur)
+            s_pose.wait_stream(cur)
         for f0 in range(0, F, FC):
             fr = frames[f0:f0 + FC]
             n = int(fr.shape[0])
-            hb, hn, keep = detect(fr)
+            # Faster R-CNN on the TokenHMR stream while YOLOX + DWPose run on the other; the host waits for the gate
+            # only after DWPose is queued, so chunk i's TokenHMR overlaps chunk i + 1's YOLOX + DWPose
+            with torch.cuda.stream(s_hmr if concurrent else cur):
+                detect_gate(fr)
+            with torch.cuda.stream(s_pose if concurrent else cur):
+                hb, hn = detect_pose(fr)
+                keypoints(fr, hb, hn, f0)
+            gb, keep = gate_result(n)
             # mesh_generator.py:101-117 per video: the frames with exactly one person; the video is rejected
             # (process_video returns False, no npz) when they are fewer than 80 % of its frames
             c0 = f0 // T
@@ -232,20 +284,13 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
                 desc[:, 2] += f0   # keypoint rows of the batch's videos sit at their frame offsets
                 vids[len(acc):len(acc) + va.size] = desc
                 acc.extend((va + c0).tolist())
-            if concurrent:
-                cur = torch.cuda.current_stream(dev)
-                s_hmr.wait_stream(cur)
-                s_pose.wait_stream(cur)
-                with torch.cuda.stream(s_hmr):
-                    hmr(fr, hb, kept, off)
-                with torch.cuda.stream(s_pose):
-                    keypoints(fr, hb, hn, f0)
-                cur.wait_stream(s_hmr)
-                cur.wait_stream(s_pose)
-            else:
-                hmr(fr, hb, kept, off)
-                keypoints(fr, hb, hn, f0)
+            with torch.cuda.stream(s_hmr if concurrent else cur):
+                hmr(fr, gb, kept, off)
             off += int(kept.size)
+            heartbeat(f"extraction pass {f0 // FC + 1} / {-(-F // FC)}")
+        if concurrent:
+            cur.wait_stream(s_hmr)
+            cur.wait_stream(s_pose)
         nA = len(acc)
         gate["accepted"] += nA
         if nA == 0:
@@ -266,7 +311,7 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
                                   centroids)
         host_ac[:nA].copy_(ac, non_blocking=True)
         host_tc[:nA].copy_(tc, non_blocking=True)
-        if det is None:   # else the next step's first detection syncs the stream before the table is rewritten
+        if gdet is None:  # else the next step's first gate result syncs behind this step before the table is rewritten
             torch.cuda.current_stream(dev).synchronize()
 
     for _ in range(args.warmup):
@@ -281,6 +326,7 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
         dw.profile_begin(prof_steps * n_chunks)
         if det is not None:
             det.profile_begin(prof_steps * n_chunks)
+            gdet.profile_begin(prof_steps * n_chunks)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -304,6 +350,7 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
         dw.profile_begin(prof_steps * n_chunks)
         if det is not None:
             det.profile_begin(prof_steps * n_chunks)
+            gdet.profile_begin(prof_steps * n_chunks)
     # TokenHMR frames of one step (the same every step: the clips and the detector are deterministic)
     hmr_frames_step = (gate["hmr_frames"] - hmr_frames0) / args.steps
     if concurrent:
@@ -316,6 +363,7 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
     st, ncalls, gemm_flops_per_frame = ex.profile_read()
     dst, dcalls, dw_flops = dw.profile_read()
     yst, ycalls, y_flops = det.profile_read() if det is not None else ({}, 0, 0.0)
+    gst, gcalls, g_flops = gdet.profile_read() if gdet is not None else ({}, 0, (0.0, 0.0))
     assert np.isfinite(host_ac.numpy()).all() and np.isfinite(host_tc.numpy()).all()
     if rank != 0:
         return None
@@ -338,10 +386,11 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
         "dtype": "bf16 (extractor: bf16 operands, f32 accumulate / residual stream) + f32x3 (scorer)",
         "data": "synthetic 256x256 RGB frames (vge.synth.make_frame_pool, drawn by the detector's findings at setup); "
                 "random-init weights of the TokenHMR "
-                "(ViT-H/16 + decoder), YOLOX-L, RTMPose-l whole-body and scorer architectures",
-        "config": {"workload": "BASELINE config 3: TokenHMR + DWPose (YOLOX-L + RTMPose-l) extract -> featurise -> "
-                               "encoder -> AC/TC, 32-frame 256x256 clips, full frames resident in HBM (one YOLOX-L "
-                               "detection per frame for DWPose and TokenHMR's single-person gate; ViTDetDataset crops)"
+                "(ViT-H/16 + decoder), Faster R-CNN X101-32x8d-FPN, YOLOX-L, RTMPose-l whole-body and scorer "
+                "architectures",
+        "config": {"workload": "BASELINE config 3: TokenHMR (Faster R-CNN X101-FPN gate + ViT-H) + DWPose (YOLOX-L + "
+                               "RTMPose-l) extract -> featurise -> encoder -> AC/TC, 32-frame 256x256 clips, full frames "
+                               "resident in HBM (every frame through both detectors; ViTDetDataset crops)"
                                + (" [--no-detector: whole-frame boxes]" if det is None else ""),
                    "clips_per_gpu": C, "frames_per_step_per_gpu": F, "frames_per_extraction_pass": FC,
                    "parallelism": f"video-sharded x{world}"},
@@ -356,14 +405,27 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
                      "frames_per_call": hmr_frames_per_call},
         "stage_ms": {**{f"hmr_{k}": v / n for k, v in st.items()},
                      **{f"dwpose_{k}": v / max(dcalls, 1) for k, v in dst.items()},
-                     **{f"yolox_{k}": v / max(ycalls, 1) for k, v in yst.items()}},
+                     **{f"yolox_{k}": v / max(ycalls, 1) for k, v in yst.items()},
+                     **{f"frcnn_{k}": v / max(gcalls, 1) for k, v in gst.items()}},
+        "gate_detector": {"model": "detectron2 Faster R-CNN X101-32x8d-FPN (COCO), 800 px, bf16 operands",
+                          "gflop_per_frame": (sum(gdet.flops(Hf, Wf)) / 1e9) if gdet is not None else None,
+                          "backbone_gemm_tflops": (g_flops[0] / (gst["backbone_gemm"] / gcalls * 1e-3) / 1e12)
+                          if gcalls and gst["backbone_gemm"] else None,
+                          "head_gemm_tflops": (g_flops[1] / (gst["head_gemm"] / gcalls * 1e-3) / 1e12)
+                          if gcalls and gst["head_gemm"] else None,
+                          "frac_of_bf16_peak": (g_flops[0] + g_flops[1]) / ((gst["backbone_gemm"] + gst["head_gemm"])
+                                                                           / gcalls * 1e-3) / 1e12
+                          / BF16_MFMA_PEAK_TFLOPS if gcalls and gst["backbone_gemm"] else None,
+                          "traffic_per_call": e2e_traffic("frcnn_conv", FC) if gcalls else None,
+                          "chunk_frames": min(FC, FRCNN_CHUNK) if gdet is not None else None},
         "yolox_gemm_tflops": (y_flops / (yst["gemm"] / ycalls * 1e-3) / 1e12) if ycalls else None,
         "yolox_traffic_per_call": e2e_traffic("yolox_conv", FC) if ycalls else None,
         "yolox_chunk_frames": min(FC, YOLOX_CHUNK) if det is not None else None,
         "dwpose_gemm_tflops": dw_flops / (dst["gemm"] / max(dcalls, 1) * 1e-3) / 1e12,
         "frames_per_s": world * F * args.steps / dt,
-        "front_end": {"detector": ("YOLOX-L (stand-in for detectron2 Faster R-CNN X101-FPN; "
-                                   "vge.synth.make_gate_detector_state_dict)") if det is not None else None,
+        "front_end": {"detector": ("detectron2 Faster R-CNN X101-32x8d-FPN (vge.frcnn; "
+                                   "vge.synth.make_gate_frcnn_state_dict)") if gdet is not None else None,
+                      "dwpose_detector": "YOLOX-L (vge.synth.make_gate_detector_state_dict)" if det is not None else None,
                       "gate": "exactly one person box with score > 0.5 per frame, >= 80 % such frames per video, else "
                               "the video is rejected (mesh_generator.py:101-117)",
                       "single_person_fraction": (gate_timed["single_person"] / gate_timed["frames"])

@@ -1,21 +1,21 @@
-"""BASELINE config 3 end to end on the GPU: frames -> YOLOX-L person detection -> the single-person gate
-(mesh_generator.py:101-117) -> ViTDetDataset crops -> TokenHMR (ViT-H width) and DWPose (RTMPose-l, every frame) ->
-npz / keypoints.npy files (extract_mesh.py:35-43, process_video.py:59-94) -> the scorer (featurise -> encoder ->
-AC/TC, eval.py:350-466), each stage checked against its oracle on the chain's own data:
+"""BASELINE config 3 end to end on the GPU: frames -> detectron2 Faster R-CNN X101-32x8d-FPN person detection -> the
+single-person gate (mesh_generator.py:101-117) -> ViTDetDataset crops -> TokenHMR (ViT-H width); YOLOX-L persons ->
+DWPose (RTMPose-l, every frame) -> npz / keypoints.npy files (extract_mesh.py:35-43, process_video.py:59-94) -> the
+scorer (featurise -> encoder -> AC/TC, eval.py:350-466), each stage checked against its oracle on the chain's own data:
 
-  detector      per-anchor scores of the chain's frames vs oracle/yolox.py (same bf16 storage points), and the two
-                persons the gate reads equal the oracle's greedy NMS on the GPU's anchors
+  gate detector the Faster R-CNN's gate count and person box on two of the chain's frames vs oracle/frcnn.py's whole
+                predictor (the stage-by-stage parity is tests/test_frcnn.py)
   gate          which videos are kept and which frames, the reference's 80 % rule on the detector's output
-  crops         byte-identical to oracle/hmr.py vitdet_crop
+  crops         byte-identical to oracle/hmr.py vitdet_crop around the gate's person boxes
   TokenHMR      pose / global_orient / betas / token rows vs oracle/hmr.py at the extractor tests' tolerances
-  DWPose        SimCC logits vs oracle/dwpose.py; keypoints.npy rows = the oracle's composition of the decoded points
+  DWPose        YOLOX-L anchor scores vs oracle/yolox.py, the two persons = greedy NMS on the GPU's anchors, SimCC
+                logits vs oracle/dwpose.py; keypoints.npy rows = the oracle's composition of the decoded points
   scoring       the files the chain wrote, scored by vge.eval.run_eval and by oracle/evalflow.py's restatement of
                 eval.py: AC / TC within 1e-4 (the north star), video set and keys equal
 
 Parity of the networks vs the upstream TokenHMR / detectron2 / DWPose weights is UNPINNED (third-party code and
-weights absent offline, random weights here); the YOLOX-L detector stands in for
-detectron2's Faster R-CNN in the gate.  TokenHMR runs 2 of ViT-H's 32 blocks (full width, full decoder) so the CPU
-oracle finishes in seconds; RTMPose-l and YOLOX-L run at full size.
+weights absent offline, random weights here).  TokenHMR runs 2 of ViT-H's 32 blocks (full
+width, full decoder) so the CPU oracle finishes in seconds; the Faster R-CNN, RTMPose-l and YOLOX-L run at full size.
 """
 import numpy as np
 import pytest
@@ -34,21 +34,23 @@ def chain(golden_dataset, tmp_path_factory):
         pytest.skip("no GPU")
     from vge import synth
     from vge.dwpose import RTMPOSE_L, YOLOX_L, DwposeExtractor, YoloxDetector
-    from vge.extract import save_video_npz, single_person_frames, single_person_mask
+    from vge.extract import gate_mask, save_video_npz, single_person_frames
+    from vge.frcnn import FRCNN_X101, FrcnnDetector
     from vge.hmr import HmrConfig, HmrExtractor, crop_persons
     root = tmp_path_factory.mktemp("e2e")
     hcfg = HmrConfig(depth=2)
     hsd = synth.make_hmr_state_dict(hcfg)
+    fsd = synth.make_gate_frcnn_state_dict(FRCNN_X101)
     ysd = synth.make_gate_detector_state_dict(YOLOX_L)
     psd = synth.make_rtmpose_state_dict(RTMPOSE_L)
+    gdet = FrcnnDetector(fsd, FRCNN_X101, device=DEV, chunk=32)
     det = YoloxDetector(ysd, YOLOX_L, device=DEV, chunk=64)
     hmr = HmrExtractor(hsd, hcfg, device=DEV, max_frames=C * T)
     pose = DwposeExtractor(psd, RTMPOSE_L, device=DEV, max_instances=2 * C * T)
 
-    # the clips' frames from a pool of synthetic scenes, by what the detector finds in each (as the e2e bench does)
+    # the clips' frames from a pool of synthetic scenes, by what the gate detector finds in each (as the e2e bench does)
     pool = torch.from_numpy(synth.make_frame_pool(4242, 512)).to(DEV)
-    _, _, psc = det.detect(pool, with_scores=True)
-    one = single_person_mask(psc.cpu().numpy())
+    one = gate_mask(gdet.detect(pool)["n_person"].cpu().numpy())
     good, bad = np.flatnonzero(one), np.flatnonzero(~one)
     assert good.size >= C * T and bad.size >= sum(BAD), (good.size, bad.size)
     rs = np.random.default_rng(5)
@@ -57,15 +59,18 @@ def chain(golden_dataset, tmp_path_factory):
     frames = pool[torch.from_numpy(idx).to(DEV)].contiguous()
     del pool
 
-    # the chain: detection -> gate -> crops -> TokenHMR; DWPose on every frame (process_video.py has no gate)
-    cand = torch.empty((C * T, det.anchors, 5), device=DEV)
-    boxes, npers, scores = det.detect(frames, cand=cand, with_scores=True)
-    boxes, npers, scores = boxes.cpu().numpy(), npers.cpu().numpy(), scores.cpu().numpy()
-    keep = single_person_mask(scores)
+    # the chain: gate detection -> gate -> crops -> TokenHMR; YOLOX persons -> DWPose on every frame (process_video.py
+    # has no gate)
+    g = {k: v.cpu().numpy() for k, v in gdet.detect(frames).items()}
+    gboxes = g["person"][:, 0, :4]
+    keep = gate_mask(g["n_person"])
     kept = {c: single_person_frames(np.where(keep[c * T:(c + 1) * T], 1, 0)) for c in range(C)}
     acc = [c for c in range(C) if kept[c] is not None]
     fidx = np.concatenate([c * T + kept[c] for c in acc])
-    crops = crop_persons(frames, boxes[fidx, 0], fidx)
+    crops = crop_persons(frames, gboxes[fidx], fidx)
+    cand = torch.empty((C * T, det.anchors, 5), device=DEV)
+    boxes, npers, scores = det.detect(frames, cand=cand, with_scores=True)
+    boxes, npers, scores = boxes.cpu().numpy(), npers.cpu().numpy(), scores.cpu().numpy()
     mesh = {k: v.cpu().numpy() for k, v in hmr.extract(crops).items()}
     K, WXY = RTMPOSE_L.keypoints, RTMPOSE_L.split * (RTMPOSE_L.in_w + RTMPOSE_L.in_h)
     n_inst = pose.instances(npers)
@@ -91,13 +96,41 @@ def chain(golden_dataset, tmp_path_factory):
         d = gkp / stems[c]
         d.mkdir(parents=True)
         np.save(d / "keypoints.npy", rows[c * T:(c + 1) * T].astype(np.float32))
+    gdet.close()
     return dict(frames=frames.cpu().numpy(), cand=cand.cpu().numpy(), boxes=boxes, npers=npers, scores=scores,
-                keep=keep, kept=kept, acc=acc, fidx=fidx, crops=crops.cpu().numpy(), mesh=mesh, rows=rows,
-                simcc=simcc.cpu(), lv=lv.cpu(), hcfg=hcfg, hsd=hsd, ysd=ysd, psd=psd, gen=str(gen), gkp=str(gkp),
-                stems=stems, paths=golden_dataset[0], ckpt=golden_dataset[1])
+                gate=g, gboxes=gboxes, keep=keep, kept=kept, acc=acc, fidx=fidx, crops=crops.cpu().numpy(), mesh=mesh,
+                rows=rows, simcc=simcc.cpu(), lv=lv.cpu(), hcfg=hcfg, hsd=hsd, fsd=fsd, ysd=ysd, psd=psd, gen=str(gen),
+                gkp=str(gkp), stems=stems, paths=golden_dataset[0], ckpt=golden_dataset[1])
 
 
-def test_detector_and_gate(chain):
+def test_gate_detector_and_gate(chain):
+    """The Faster R-CNN's gate count and person box on two of the chain's frames (one kept, one not) vs the oracle's
+    whole predictor (unless an oracle person score lies within 0.05 of 0.5), then the 80 % rule."""
+    from oracle.frcnn import OracleFrcnn, gate_persons
+    from vge.frcnn import FRCNN_X101
+    g = chain["gate"]
+    f_keep, f_drop = int(np.flatnonzero(chain["keep"])[0]), int(np.flatnonzero(~chain["keep"])[0])
+    torch.set_num_threads(16)
+    res = OracleFrcnn(chain["fsd"], FRCNN_X101, bf16=True).detect(chain["frames"][[f_keep, f_drop]])
+    for r, f in zip(res, (f_keep, f_drop)):
+        ps = r["scores"][r["classes"] == 0]
+        print(f"frame {f}: persons > 0.5 gpu {int(g['n_person'][f])} oracle {gate_persons(r)}, "
+              f"oracle person scores {ps[:3].tolist()}")
+        if bool(((ps - 0.5).abs() < 0.05).any()):
+            continue
+        assert int(g["n_person"][f]) == gate_persons(r)
+        if gate_persons(r) == 1:
+            b = r["boxes"][r["classes"] == 0][0].numpy()
+            np.testing.assert_allclose(chain["gboxes"][f], b, atol=2.0)
+    # the 80 % rule (mesh_generator.py:113-117): clips 0-4 lose 1-2 frames and are kept, clip 5 is rejected
+    assert chain["acc"] == [0, 1, 2, 3, 4]
+    for c in chain["acc"]:
+        assert chain["kept"][c].size == T - BAD[c]
+
+
+def test_dwpose_detector(chain):
+    """DWPose's own YOLOX-L persons (process_video.py's Wholebody): anchor scores vs the oracle, and the two persons
+    the pose model reads = the greedy NMS on the GPU's anchors."""
     from oracle.yolox import OracleYolox, decode, two_persons
     from vge.dwpose import YOLOX_L
     fr = chain["frames"][:3]
@@ -105,20 +138,16 @@ def test_detector_and_gate(chain):
     serr = float(np.abs(chain["cand"][:3, :, 4] - osc).max())
     print(f"detector: anchor scores max|gpu - oracle| {serr:.2e}")
     assert serr < 2e-2
-    for f in range(chain["frames"].shape[0]):   # the persons the gate reads = greedy NMS on the GPU's anchors
+    for f in range(chain["frames"].shape[0]):
         kb, n = two_persons(chain["cand"][f, :, :4], chain["cand"][f, :, 4])
         assert int(chain["npers"][f]) == n
         np.testing.assert_array_equal(chain["boxes"][f, :n], kb)
-    # the 80 % rule (mesh_generator.py:113-117): clips 0-4 lose 1-2 frames and are kept, clip 5 is rejected
-    assert chain["acc"] == [0, 1, 2, 3, 4]
-    for c in chain["acc"]:
-        assert chain["kept"][c].size == T - BAD[c]
 
 
 def test_crops_are_the_oracle_crops(chain):
     from oracle.hmr import vitdet_crop
     for j, f in enumerate(chain["fidx"]):
-        want = vitdet_crop(chain["frames"][f], chain["boxes"][f, 0])
+        want = vitdet_crop(chain["frames"][f], chain["gboxes"][f])
         np.testing.assert_array_equal(chain["crops"][j], want, err_msg=f"crop of frame {f}")
 
 

@@ -1,14 +1,14 @@
 """The TokenHMR front end (mesh_generator.py:101-145): single-person gate and ViTDetDataset's crop.
 
 The crop geometry and warp are third-party (4D-Humans ViTDetDataset / generate_image_patch_cv2, cv2.warpAffine,
-skimage.filters.gaussian) restated in oracle/hmr.py; the detector is detectron2's Faster R-CNN in the reference and
-the YOLOX-L of vge.dwpose here (stand-in): parity UNPINNED.  Checked:
-  CPU   the gate rule (exactly one box > 0.5 among the first two NMS-kept persons, >= 80 % of the frames) and the
-        crop geometry (center, 2.5x scale, 192:256 aspect expansion, blur trigger) on hand-computed boxes
+skimage.filters.gaussian) restated in oracle/hmr.py; the detector is detectron2's Faster R-CNN X101-32x8d-FPN
+(vge.frcnn, checked stage by stage in test_frcnn.py): parity vs the upstream weights UNPINNED.  Checked:
+  CPU   the gate rule (exactly one person instance > 0.5, >= 80 % of the frames) and the crop geometry (center, 2.5x
+        scale, 192:256 aspect expansion, blur trigger) on hand-computed boxes
   GPU   vge_hmr_crop vs oracle.vitdet_crop: every byte equal on the unblurred path (float bilinear without
         contraction on both sides), within 1 where the anti-alias Gaussian applies; boxes partly outside the frame
-        (border 0); the full front end (YOLOX detect -> gate -> crops) against the oracle's gate and crops on the
-        detector's own boxes and scores
+        (border 0); the full front end (Faster R-CNN detect -> gate -> crops): the detector's person outputs agree
+        with its instance list, and the gate / crops equal the oracle's on the detector's own boxes
 """
 import numpy as np
 import pytest
@@ -19,13 +19,11 @@ gpu = pytest.mark.gpu
 
 
 def test_single_person_gate_rule():
-    from oracle.hmr import single_person_mask as oracle_mask
-    from vge.extract import SINGLE_PERSON_MIN_FRACTION, single_person_mask
-    s = np.array([[0.9, 0.0], [0.9, 0.6], [0.4, 0.0], [0.51, 0.5], [0.0, 0.0], [0.5, 0.2]], np.float32)
-    want = np.array([True, False, False, True, False, False])
-    assert np.array_equal(single_person_mask(s), want)
-    assert np.array_equal(oracle_mask(s), want)
+    from vge.extract import SINGLE_PERSON_MIN_FRACTION, gate_mask, single_person_frames
+    assert np.array_equal(gate_mask([1, 0, 2, 1, 5]), [True, False, False, True, False])
     assert SINGLE_PERSON_MIN_FRACTION == 0.8
+    assert single_person_frames([1] * 8 + [0, 2]).tolist() == list(range(8))    # 8 / 10: kept
+    assert single_person_frames([1] * 7 + [0, 2, 3]) is None                    # 7 / 10: rejected
 
 
 def test_vitdet_geometry_by_hand():
@@ -67,37 +65,41 @@ def test_crop_matches_oracle(size, boxes):
 
 @gpu
 def test_front_end_detect_gate_crop():
-    """YOLOX (small random-weight config) on full frames -> scores -> gate -> crops of the kept frames, against the
-    oracle gate and crop on the detector's own boxes (the detector network itself is checked in test_yolox.py)."""
+    """Faster R-CNN (a depth-50, 128-pixel random-weight config) on full frames -> person outputs -> gate -> crops of
+    the kept frames, against the instance list, the oracle crop, and the 80 % rule on the detector's own boxes."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
-    from oracle.hmr import single_person_mask as oracle_mask
     from oracle.hmr import vitdet_crop
     from vge import synth
-    from vge.dwpose import YoloxConfig, YoloxDetector
     from vge.extract import tokenhmr_front
-    cfg = YoloxConfig(in_size=128, width=16, depth=1, head_ch=64)
-    det = YoloxDetector(synth.make_yolox_state_dict(cfg, gain=2.0), cfg, device=DEV, chunk=8)
+    from vge.frcnn import FrcnnConfig, FrcnnDetector
+    cfg = FrcnnConfig(depth=50, min_size=128, max_size=213, rpn_pre_topk=300, rpn_post_topk=200)
+    sd = synth.make_frcnn_state_dict(cfg)
+    b = sd["roi_heads.box_predictor.cls_score.bias"]
+    b[0] = 6.0                                          # plenty of person instances
+    det = FrcnnDetector(sd, cfg, device=DEV, chunk=8)
     frames = synth.make_frames(5, 10, 256, 256)
     fr = torch.from_numpy(frames).to(DEV)
-    boxes, npers, scores = det.detect(fr, with_scores=True)
-    b, s = boxes.cpu().numpy(), scores.cpu().numpy()
-    n = npers.cpu().numpy()
-    assert np.array_equal(n, (s[:, 0] > 0).astype(np.int32) + (s[:, 1] > 0))  # scores sit beside the kept persons
+    out = {k: v.cpu().numpy() for k, v in det.detect(fr).items()}
+    for f in range(10):   # person outputs = the instance list's class-0 rows
+        d = out["dets"][f, :out["n_dets"][f]]
+        pers = d[d[:, 5] == 0]
+        assert out["n_person"][f] == int((pers[:, 4] > 0.5).sum())
+        for j in range(min(2, len(pers))):
+            np.testing.assert_array_equal(out["person"][f, j], pers[j, :5])
+    assert out["n_person"].max() > 0
     # force a deterministic mix of gate outcomes on the detector's own boxes
-    s2 = s.copy()
-    s2[:, 0] = np.where(np.arange(10) == 9, 0.2, 0.9)   # frame 9: nobody above 0.5
-    s2[:, 1] = np.where(np.arange(10) == 3, 0.7, 0.1)   # frame 3: two people above 0.5
-    b2 = b.copy()
-    b2[:, 0] = [[20 + i, 30, 120 + 5 * i, 230] for i in range(10)]
-    keep_ref = np.flatnonzero(oracle_mask(s2))
-    out = tokenhmr_front(det, fr, detections=(b2, n, s2))
-    assert out is not None
-    idx, crops = out
-    assert np.array_equal(idx, keep_ref) and len(idx) == 8
+    n2 = np.where(np.arange(10) == 9, 0, 1)
+    n2[3] = 2                                           # frame 3: two people; frame 9: nobody
+    b2 = np.array([[20 + i, 30, 120 + 5 * i, 230] for i in range(10)], np.float32)
+    res = tokenhmr_front(det, fr, detections=(b2, n2))
+    assert res is not None
+    idx, crops = res
+    assert idx.tolist() == [0, 1, 2, 4, 5, 6, 7, 8]
     c = crops.cpu().numpy()
     for j, f in enumerate(idx):
-        assert np.array_equal(c[j], vitdet_crop(frames[f], b2[f, 0]))
-    s3 = s2.copy()
-    s3[:1, 0] = 0.1                                    # one more frame fails: 7 / 10 < 80 % -> rejected
-    assert tokenhmr_front(det, fr, detections=(b2, n, s3)) is None
+        assert np.array_equal(c[j], vitdet_crop(frames[f], b2[f]))
+    n3 = n2.copy()
+    n3[0] = 0                                           # one more frame fails: 7 / 10 < 80 % -> rejected
+    assert tokenhmr_front(det, fr, detections=(b2, n3)) is None
+    det.close()

@@ -415,7 +415,8 @@ int vge_frcnn_destroy(vge_frcnn* m) {
 
 int vge_frcnn_profile_begin(vge_frcnn* m, int max_calls) {
   if (!m || max_calls < 0) return fail(VGE_ERR_ARG, "vge_frcnn_profile_begin: bad argument");
-  return m->prof.begin(max_calls, 512);
+  // event pairs per call: ~190 launches per chunk of frames, and a call may span several chunks
+  return m->prof.begin(max_calls, 8192);
 }
 
 int vge_frcnn_profile_read(vge_frcnn* m, double* stage_ms, int* n_calls, double* flops_per_call) {

@@ -3,8 +3,9 @@
 Mirrors the reference's extraction scripts, minus video decoding (cv2 is not part of this framework: callers pass
 decoded uint8 RGB frames):
 
-  mesh_generator.py:101-145   the TokenHMR front end: person detection, the single-person gate (exactly one person box
-                              with score > 0.5 per frame, >= 80 % of the frames), ViTDetDataset's crop (vge_hmr_crop)
+  mesh_generator.py:101-145   the TokenHMR front end: person detection (detectron2 Faster R-CNN X101-32x8d-FPN,
+                              vge.frcnn), the single-person gate (exactly one person instance with score > 0.5 per
+                              frame, >= 80 % of the frames), ViTDetDataset's crop (vge_hmr_crop)
 
   extract_mesh.py:12-43       mesh_info_to_arrays / save_video_npz -- one np.savez_compressed per video with
                               pose / betas / global_orient / vit / frame_idx / meta (JSON string); the file the scorer's
@@ -26,7 +27,7 @@ from typing import Dict, Optional, Sequence, Union
 import numpy as np
 
 SINGLE_PERSON_MIN_FRACTION = 0.8   # mesh_generator.py:116 (len(valid_frames) < 0.8 * len(frames) -> False)
-PERSON_SCORE_THRESH = 0.5          # mesh_generator.py:107 (pred_classes == 0) & (scores > 0.5)
+PERSON_SCORE_THRESH = 0.5          # mesh_generator.py:107 (pred_classes == 0) & (scores > 0.5): vge_frcnn's gate_thresh
 
 
 def mesh_info_to_arrays(mesh_info: dict):
@@ -83,32 +84,31 @@ def gate_videos(keep: np.ndarray, frames_per_video: int, frame_off: int = 0):
     return np.asarray(acc, np.int64), kept_idx, np.asarray(desc, np.int32).reshape(-1, 4)
 
 
-def single_person_mask(scores) -> np.ndarray:
-    """mesh_generator.py:103-111 per frame: exactly one person box with score > 0.5.  `scores` [F, 2] are the scores
-    of the first two boxes the detector's greedy NMS keeps (vge_yolox_detect_scored), so a frame has one such box
-    iff the first is above the threshold and the second is not."""
-    s = np.asarray(scores, np.float32).reshape(-1, 2)
-    return (s[:, 0] > PERSON_SCORE_THRESH) & ~(s[:, 1] > PERSON_SCORE_THRESH)
+def gate_mask(n_person) -> np.ndarray:
+    """mesh_generator.py:103-111 per frame: exactly one (pred_classes == 0) & (scores > 0.5) instance of the gate
+    detector (vge.frcnn.FrcnnDetector's n_person)."""
+    return np.asarray(n_person).reshape(-1) == 1
 
 
 def tokenhmr_front(detector, frames, detections=None):
-    """TokenHMRMeshGenerator.process_video's front end (mesh_generator.py:101-145) on the device: person detection
-    (the YOLOX-L of vge.dwpose standing in for detectron2's Faster R-CNN X101-FPN, absent offline), the per-frame
-    single-person gate, the 80 % rule, and ViTDetDataset's crop of every kept frame.
-    frames: uint8 [F, H, W, 3] RGB on the device; detections: optional (boxes [F,2,4], n_persons [F], scores [F,2])
-    host arrays already computed for these frames.  Returns (kept frame indices, uint8 crops [n, 256, 256, 3] on the
-    device), or None when the reference rejects the video (process_video returns False)."""
+    """TokenHMRMeshGenerator.process_video's front end (mesh_generator.py:101-145) on the device: detectron2's Faster
+    R-CNN X101-32x8d-FPN on every frame (vge.frcnn.FrcnnDetector, the reference's det2_predictor), the per-frame
+    single-person gate, the 80 % rule, and ViTDetDataset's crop of every kept frame around its one person box.
+    frames: uint8 [F, H, W, 3] RGB on the device; detections: optional (person boxes [F, 4] -- the first class-0
+    instance of each frame --, n_person [F]) host arrays already computed for these frames.  Returns (kept frame
+    indices, uint8 crops [n, 256, 256, 3] on the device), or None when the reference rejects the video
+    (process_video returns False)."""
     from .hmr import crop_persons
     if detections is None:
-        b, _, sc = detector.detect(frames, with_scores=True)
-        boxes, scores = b.cpu().numpy(), sc.cpu().numpy()
+        out = detector.detect(frames)
+        boxes, npers = out["person"][:, 0, :4].cpu().numpy(), out["n_person"].cpu().numpy()
     else:
-        boxes, scores = np.asarray(detections[0]), np.asarray(detections[2])
-    keep = np.flatnonzero(single_person_mask(scores))
+        boxes, npers = np.asarray(detections[0], np.float32).reshape(-1, 4), np.asarray(detections[1])
+    keep = np.flatnonzero(gate_mask(npers))
     F = int(frames.shape[0])
     if keep.size == 0 or keep.size < SINGLE_PERSON_MIN_FRACTION * F:
         return None
-    return keep, crop_persons(frames, boxes.reshape(F, 2, 4)[keep, 0], keep)
+    return keep, crop_persons(frames, boxes[keep], keep)
 
 
 def process_video_frames(hmr, detector, frames, detections=None):
@@ -161,10 +161,13 @@ def extract_video(hmr, wholebody, frames, crops, action: str, video: str, mesh_r
                   detector=None) -> Dict[str, Optional[str]]:
     """One video of extract_mesh.py:main + process_video.py: npz (or None when the single-person gate rejects the
     video, the reference's not-single list) and keypoints.npy paths.  crops None: the TokenHMR front end runs on the
-    full frames with `detector` (process_video_frames); otherwise crops are ready-made person crops."""
+    full frames with `detector` (a vge.frcnn.FrcnnDetector: process_video_frames); otherwise crops are ready-made person
+    crops.  DWPose (`wholebody`) runs its own YOLOX-L persons on every frame, as process_video.py does."""
     stem = Path(video).stem
     if crops is None:
-        mesh_info = process_video_frames(hmr, detector if detector is not None else wholebody.det, frames)
+        if detector is None:
+            raise ValueError("extract_video: the TokenHMR front end needs the gate detector (vge.frcnn.FrcnnDetector)")
+        mesh_info = process_video_frames(hmr, detector, frames)
     else:
         mesh_info = process_video(hmr, crops, person_counts)
     npz = None

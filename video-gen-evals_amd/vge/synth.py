@@ -556,7 +556,7 @@ def make_frcnn_state_dict(cfg, seed: int = SEED_WEIGHTS + 40, cls_gain: float = 
 # logits' ranking, hence which boxes the class-aware NMS keeps, is unchanged) puts the 0.5 threshold between the first
 # and second kept person instance of as many pool frames as possible.  GATE_FRCNN_BG is measured on make_frame_pool's
 # frames by tools/frcnn_gate_calib.py on the GPU; VGE_GATE_FRCNN_BG overrides it for a calibration run.
-GATE_FRCNN_BG = float(os.environ.get("VGE_GATE_FRCNN_BG", "0.0"))
+GATE_FRCNN_BG = float(os.environ.get("VGE_GATE_FRCNN_BG", "-0.5007"))
 
 
 def make_gate_frcnn_state_dict(cfg, bg: float = None) -> Dict[str, np.ndarray]:
