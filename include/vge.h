@@ -41,11 +41,12 @@ typedef enum {
   VGE_ERR_WEIGHT_SHAPE = 4,   /* a state_dict tensor has the wrong shape */
   VGE_ERR_NOMEM = 5,
   VGE_ERR_WORKSPACE = 6,      /* vge_encoder_reserve() was not called for this many windows */
-  VGE_ERR_UNSUPPORTED = 7,    /* a model shape the kernels are not built for (vge_encoder_create): d_model != 256,
-                                 time_heads != 8, clip_len != 32, or a modality set / input dims other than the
-                                 reference's five or its keypoint-less four (clip / dino modalities, other vit or
-                                 pose widths).  load_model (eval.py:136-165) reads these from the checkpoint;
-                                 time_layers is free (any >= 1). */
+  VGE_ERR_UNSUPPORTED = 7,    /* a model shape the kernels are not built for (vge_encoder_create): clip_len != 32,
+                                 a modality set / input dims other than the reference's five or its keypoint-less
+                                 four (clip / dino modalities, other vit or pose widths), or d_model / time_heads
+                                 other than 256 / 8 outside the exact-f32 generic path (VGE_F32 only: d_model a
+                                 multiple of 32 in [32, 256], head dim <= 64).  load_model (eval.py:136-165) reads
+                                 these from the checkpoint; time_layers is free (any >= 1). */
   VGE_ERR_DEVICE = 8          /* a kernel detected a broken invariant and raised the encoder's status word (the
                                  staggered conv kernel's half-workgroup exchange wait ran out of its bound): the
                                  outputs of that launch are wrong.  Reported by vge_encoder_status, by
@@ -84,7 +85,9 @@ int vge_layout_feat_dim(vge_layout layout); /* 2596 / 2356, 0 for an unknown lay
  * The kernels are built for the reference configuration: 5 modalities in the order
  * vit, global, pose, beta, kp2d with dims {1024,9,207,10,120} / {1024,3,69,10,120}, or the first 4 of them
  * (keypoint-less layout: 8 conv encoders, a 4-way fusion, feats rows of 2356), d_model 256, post-norm
- * layers, 8 heads, FFN 1024, clip_len 32. */
+ * layers, 8 heads, FFN 1024, clip_len 32.  Other checkpoint shapes (d_model 32..256 in steps of 32, any head count
+ * with a head dim <= 64, FFN 4 d_model) run on the generic exact-f32 kernels (vge_encoder_gen.hip) when created
+ * with VGE_F32; seq / frame embeddings are then d_model wide. */
 typedef struct {
   int n_modalities;
   int dims_raw[8];

@@ -194,14 +194,15 @@ def ac_scores(seq, cls_names, vid_names, cents, label_dict):
 
 
 def run_eval(real_dir, real_kp_dir, gen_dir, gen_kp_dir, state_dict, dims_raw, dims_diff, workers=0,
-             timings: Optional[dict] = None):
-    """Full eval.py flow; returns (combined_scores, extras)."""
+             timings: Optional[dict] = None, hp: Optional[dict] = None):
+    """Full eval.py flow; returns (combined_scores, extras).  hp: the checkpoint's d_model / time_layers /
+    time_heads (load_model, eval.py:136-152; default 256 / 4 / 8)."""
     t0 = time.perf_counter()
     real = scan_real(real_dir)
     train = split(real)
     stats = compute_stats(train, real_kp_dir)
     t1 = time.perf_counter()
-    enc = OracleEncoder(state_dict, dims_raw, dims_diff)
+    enc = OracleEncoder(state_dict, dims_raw, dims_diff, **(hp or {}))
     label_dict = {c: i for i, c in enumerate(sorted(real.keys()))}
     cents, counts = centroids(enc, train, real_kp_dir, stats, label_dict)
     t2 = time.perf_counter()

@@ -77,3 +77,26 @@ def golden_meta_nokp():
 def golden_state_dict_nokp():
     from tests.golden.dataset_spec import golden_state_dict
     return golden_state_dict("nokp")
+
+
+# ---- a checkpoint of another shape (d_model 64, 2 layers, 4 heads: dataset_spec.SMALL_HP)
+
+@pytest.fixture(scope="session")
+def golden_dataset_small(tmp_path_factory):
+    from tests.golden.dataset_spec import build_golden_dataset
+    root = tmp_path_factory.mktemp("golden_ds_small")
+    paths, ckpt, digest = build_golden_dataset(str(root), layout="small")
+    flow = np.load(GOLDEN / "golden_flow_small.npz")
+    assert bytes(flow["dataset_digest"]).hex() == digest, "synthetic generator drifted from the golden fixtures"
+    return paths, ckpt
+
+
+@pytest.fixture(scope="session")
+def golden_flow_small():
+    return dict(np.load(GOLDEN / "golden_flow_small.npz"))
+
+
+@pytest.fixture(scope="session")
+def golden_meta_small():
+    with open(GOLDEN / "golden_scores_small.json") as f:
+        return json.load(f)

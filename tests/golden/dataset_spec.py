@@ -21,10 +21,16 @@ GOLDEN_SPEC = {
 
 
 NOKP_MODS = ("vit", "global", "pose", "beta")  # the keypoint-less model (keypoint_dir None, utils.py:496-514)
+# a checkpoint of another shape (load_model reads d_model / time_layers / time_heads from it, eval.py:136-152)
+SMALL_HP = {"d_model": 64, "time_layers": 2, "time_heads": 4}
 
 
 def golden_state_dict(layout: str = "kp"):
-    """The golden checkpoint's weights: 5 modalities, or the keypoint-less 4 (same generator, no kp2d)."""
+    """The golden checkpoint's weights: 5 modalities, or the keypoint-less 4 (same generator, no kp2d), or "small":
+    5 modalities at SMALL_HP's shape."""
+    if layout == "small":
+        return synth.make_state_dict(synth.DIMS_RAW, synth.DIMS_DIFF, d_model=SMALL_HP["d_model"],
+                                     time_layers=SMALL_HP["time_layers"])
     if layout == "kp":
         return synth.make_state_dict(synth.DIMS_RAW, synth.DIMS_DIFF)
     return synth.make_state_dict({m: synth.DIMS_RAW[m] for m in NOKP_MODS},
@@ -33,7 +39,8 @@ def golden_state_dict(layout: str = "kp"):
 
 def build_golden_dataset(root: str, layout: str = "kp"):
     """Write dataset + checkpoint under `root`; returns (paths, checkpoint_path, sha256 hexdigest).  layout "nokp":
-    the same dataset with the 4-modality checkpoint (model_nokp.pt) of the keypoint-less flow."""
+    the same dataset with the 4-modality checkpoint (model_nokp.pt) of the keypoint-less flow; "small": the
+    5-modality flow with a d_model 64, 2-layer, 4-head checkpoint (model_small.pt)."""
     paths = synth.write_dataset(root, n_real_per_class=GOLDEN_SPEC["n_real_per_class"],
                                 n_gen=GOLDEN_SPEC["n_gen"], T_real=GOLDEN_SPEC["T_real"],
                                 T_gen=GOLDEN_SPEC["T_gen"], kp_short_every=GOLDEN_SPEC["kp_short_every"])
@@ -45,8 +52,8 @@ def build_golden_dataset(root: str, layout: str = "kp"):
     kd.mkdir(parents=True, exist_ok=True)
     np.save(kd / "keypoints.npy", clip.keypoints)
     sd = golden_state_dict(layout)
-    ckpt = os.path.join(root, "model.pt" if layout == "kp" else "model_nokp.pt")
-    synth.save_checkpoint(ckpt, sd)
+    ckpt = os.path.join(root, {"kp": "model.pt", "nokp": "model_nokp.pt", "small": "model_small.pt"}[layout])
+    synth.save_checkpoint(ckpt, sd, **(SMALL_HP if layout == "small" else {}))
     h = hashlib.sha256()
     for sub in ("real", "real_kp", "generated_meshes", "generated_kps"):
         for p in sorted(Path(paths[sub]).rglob("*")):

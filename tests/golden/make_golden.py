@@ -15,6 +15,9 @@ synthetic dataset and weights of vge.synth, and stores inputs/outputs as small f
                       the same flow without keypoints (keypoint_dir None for the real and generated sets: the
                       4-modality layout, raw 1250 | diff 1106, and a 4-modality checkpoint)
                       -- `python -B tests/golden/make_golden.py nokp` writes only these
+  golden_flow_small.npz / golden_scores_small.json
+                      the keypoint flow with a checkpoint of another shape (d_model 64, 2 layers, 4 heads;
+                      dataset_spec.SMALL_HP) -- `python -B tests/golden/make_golden.py small` writes only these
 
 Nothing from the reference is copied; only arrays and numbers it produced.  This script never runs
 on the GPU box (the reference is not there); tests regenerate the same synthetic inputs from seeds.
@@ -246,9 +249,61 @@ def main_nokp():
     print("keypoint-less golden written to", HERE)
 
 
+def main_small():
+    """The eval.py flow (keypoints) with a checkpoint whose d_model / time_layers / time_heads are 64 / 2 / 4:
+    load_model builds HumanActionScorer from the checkpoint's own hyper-parameters (eval.py:136-152)."""
+    from tests.golden.dataset_spec import SMALL_HP
+    sys.path.insert(0, REF)
+    import utils as U  # noqa
+    import eval as E  # noqa
+    torch.manual_seed(0)
+    with tempfile.TemporaryDirectory() as tmp:
+        paths, ckpt, digest = build_golden_dataset(tmp, layout="small")
+        real_ds = U.NpzVideoDataset(paths["real"], filter_classes=E.ACTION_CLASSES)
+        train_ds, _ = U.train_test_split(real_ds, train_ratio=0.8, seed=1337)
+        stats = U.compute_stats_from_npz(train_ds.items, keypoint_dir=paths["real_kp"])
+        dims_raw, dims_diff = E.infer_dims_from_stats(stats)
+        model = E.load_model(ckpt, dims_raw, dims_diff)
+        assert model.cls.shape[-1] == SMALL_HP["d_model"] and len(model.temporal.layers) == SMALL_HP["time_layers"]
+        assert model.temporal.layers[0].self_attn.num_heads == SMALL_HP["time_heads"]
+        centroids, label_dict = E.build_real_centroids(model, paths["real"], paths["real_kp"], stats, 32, 8)
+        loader = U.make_test_loader(train_ds, clip_len=32, stride=8, stats=stats, seed=1337, batch_size=64,
+                                    keypoint_dir=paths["real_kp"], num_workers=0)
+        _, counts = U.build_train_centroids_subset(model, loader, label_dict, device="cpu")
+        dataset = E.create_dataset_from_generated_meshes(paths["generated_meshes"])
+        samples = U.sample_all_windows_npz(dataset, clip_len=32, stride=8)
+        wds = U.WindowDataset(samples=samples, clip_len=32, stats=stats, keypoint_dir=paths["generated_kps"])
+        dl = torch.utils.data.DataLoader(wds, batch_size=32, shuffle=False, num_workers=0,
+                                         collate_fn=U.safe_collate)
+        features = E.extract_window_features(model, dl)
+        ac = E.compute_action_consistency_scores(features, centroids, label_dict)
+        tc = E.compute_temporal_coherence_scores(features)
+        combined = {}
+        for v in sorted(set(ac) | set(tc)):
+            e = {}
+            if v in ac:
+                e["ac"] = ac[v]
+            if v in tc:
+                e["tc"] = tc[v]
+            combined[v] = e
+        flow = {"centroids": centroids.numpy(), "counts": counts.numpy(),
+                "seq_embeds": features["seq_embeds"].numpy(),
+                "frame_embeds_first4": features["frame_embeds"][:4].numpy(),
+                "dataset_digest": np.frombuffer(bytes.fromhex(digest), np.uint8)}
+        np.savez_compressed(HERE / "golden_flow_small.npz", **flow)
+        meta = {"label_dict": label_dict, "window_vids": features["vid_names"], "window_cls": features["cls_names"],
+                "video_scores": combined, "hp": SMALL_HP}
+        with open(HERE / "golden_scores_small.json", "w") as f:
+            json.dump(meta, f, indent=1, sort_keys=True)
+    print("small-checkpoint golden written to", HERE)
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["nokp"]:
         main_nokp()
+    elif sys.argv[1:] == ["small"]:
+        main_small()
     else:
         main()
         main_nokp()
+        main_small()

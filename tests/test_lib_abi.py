@@ -152,6 +152,25 @@ def test_unsupported_model_shape_has_its_own_status(field, value):
     assert so.vge_encoder_create(C.byref(dims), (L.TensorView * 1)(), 0, 1, C.byref(h)) == 1  # VGE_ERR_ARG
 
 
+@pytest.mark.parametrize("d_model,heads,expect", [(128, 4, "missing"), (64, 4, "missing"), (96, 1, "unsupported"),
+                                                   (320, 8, "unsupported"), (80, 8, "unsupported"), (256, 2, "unsupported")])
+def test_generic_f32_shapes(d_model, heads, expect):
+    """VGE_F32 takes other checkpoint shapes on the generic kernels (d_model a multiple of 32 in [32, 256], head dim
+    <= 64): such a create gets past the shape check to the weights (an empty list: VGE_ERR_MISSING_WEIGHT); others
+    stay VGE_ERR_UNSUPPORTED.  No device work happens before the weights are complete."""
+    import ctypes as C
+    from vge import lib as L
+    from vge import ops
+    so = L.load()
+    dims = L.Dims()
+    dims.n_modalities, dims.d_model, dims.time_layers, dims.time_heads, dims.clip_len = 5, d_model, 2, heads, 32
+    for i in range(5):
+        dims.dims_raw[i], dims.dims_diff[i] = ops.DIMS_RAW[i], ops.DIMS_DIFF[i]
+    h = C.c_void_p()
+    st = so.vge_encoder_create(C.byref(dims), (L.TensorView * 1)(), 0, 0, C.byref(h))
+    assert st == (L.VGE_ERR_UNSUPPORTED if expect == "unsupported" else 3), st
+
+
 def test_load_model_refuses_clip_modality():
     """The keypoint-less four are built (tests/test_nokp_layout.py); a CLIP-embedding modality is not."""
     from vge import eval as VE

@@ -10,6 +10,7 @@
 #include <string>
 #include <unordered_map>
 #include <vector>
+#include <memory>
 #include <thread>
 #include <atomic>
 
@@ -86,6 +87,23 @@ hipError_t launch_fuse(const float*, int, const FuseParamsHost&, float*, hipStre
 hipError_t launch_gemm(int, const GemmArgsHost&, hipStream_t);
 hipError_t launch_attn(const float*, int, float*, hipStream_t);
 hipError_t launch_embed_tc(const float*, int, float*, float*, float*, hipStream_t);
+// the generic-shape exact-f32 path (vge_encoder_gen.hip)
+struct GenFuseHost {
+  const float* kv_w; const float* kv_b; const float* u;
+  float inv_tau[8], bias[8];
+  int n_mod, d;
+  int has_motion[8];
+};
+hipError_t launch_gen_conv(const float* x, int ldx, int xcol, int cin, const float* W, int cout, int taps, int dil, int epi,
+                           const float* res, float* out, int n_windows, hipStream_t s);
+hipError_t launch_gen_groupnorm(float* x, int n_windows, int d, const float* g, const float* b, hipStream_t s);
+hipError_t launch_gen_fuse(const float* enc_out, int n_rows, const GenFuseHost& f, float* pooled_pre, hipStream_t s);
+hipError_t launch_gen_gemm(const float* A, int lda, const float* W, int M, int N, int K, const float* bias, int epi,
+                           const float* res, const float* pe, const float* cls, float* out, int ldo, hipStream_t s);
+hipError_t launch_gen_attn(const float* qkv, int n_windows, int d, int heads, float* out, hipStream_t s);
+hipError_t launch_gen_add_ln(const float* a, const float* b, int rows, int d, const float* g, const float* be, float* out,
+                             hipStream_t s);
+hipError_t launch_gen_embed_tc(const float* x, int n_windows, int d, float* seq, float* frame, float* tc, hipStream_t s);
 hipError_t launch_centroid_accum(const float*, const int*, int, int, int, float*, float*, hipStream_t);
 hipError_t launch_centroid_final(const float*, const float*, int, int, float*, hipStream_t);
 hipError_t launch_tc_windows(const float*, int, int, int, float*, hipStream_t);
@@ -214,7 +232,34 @@ void pack_linear_x3(Get W, int N, int K_real, std::vector<_Float16>& out, std::v
 
 }  // namespace
 
+// A checkpoint whose d_model / time_heads differ from the tiled kernels' 256 / 8 (load_model reads both from the
+// checkpoint, eval.py:139-158): the exact-f32 VALU kernels of vge_encoder_gen.hip, reference weights as they are.
+struct GenModel {
+  int d = 0, heads = 0, layers = 0, ffn = 0, M = 0;
+  float* wbuf = nullptr;
+  struct Enc {
+    const float *stem, *conv[8], *proj, *gw[4], *gb[4];
+    int in_col, d_in;
+  };
+  std::vector<Enc> encs;
+  vge::GenFuseHost fuse{};
+  const float *Wov = nullptr, *cls = nullptr, *pe = nullptr;
+  struct Lyr {
+    const float *in_w, *in_b, *out_w, *out_b, *n1w, *n1b, *l1w, *l1b, *l2w, *l2b, *n2w, *n2b;
+  };
+  std::vector<Lyr> L;
+  int cap = 0;
+  float* ws = nullptr;
+  float *enc_out = nullptr, *a = nullptr, *b = nullptr, *c = nullptr, *pp = nullptr, *x = nullptr, *qkv = nullptr,
+        *att = nullptr, *x1 = nullptr, *h = nullptr, *tmp = nullptr;
+  ~GenModel() {
+    if (wbuf) (void)hipFree(wbuf);
+    if (ws) (void)hipFree(ws);
+  }
+};
+
 struct vge_encoder {
+  GenModel* gen = nullptr;  // set: every stage on the generic-shape exact-f32 kernels
   int mode = VGE_F32;
   int n_layers = 4;
   int n_mod = 5, n_enc = 10;     // modalities (5, or 4 keypoint-less) and conv encoders (state + motion)
@@ -385,12 +430,19 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
   if (dims->time_layers < 1) return fail(VGE_ERR_ARG, "vge_encoder_create: time_layers must be >= 1");
   // 5 modalities (keypoint_dir given) or the keypoint-less 4 (utils.py:496-514; infer_dims_from_stats, eval.py:104-133)
   const int M = dims->n_modalities;
-  if ((M != 5 && M != 4) || dims->d_model != 256 || dims->time_heads != 8 || dims->clip_len != 32)
+  // d_model / heads other than 256 / 8: the generic exact-f32 kernels (d_model a multiple of 32 up to 256, head dim
+  // <= 64), requested as VGE_F32; the tiled 3xfp16 / fp16 kernels are built around 256 columns x 8 heads of 32
+  const int Dm = dims->d_model, Hn = dims->time_heads;
+  const bool generic = Dm != 256 || Hn != 8;
+  const bool gen_ok = compute == VGE_F32 && Dm >= 32 && Dm <= 256 && Dm % 32 == 0 && Hn >= 1 && Dm % Hn == 0 &&
+                      Dm / Hn <= 64;
+  if ((M != 5 && M != 4) || dims->clip_len != 32 || (generic && !gen_ok))
     return fail(VGE_ERR_UNSUPPORTED,
-                "vge_encoder_create: kernels are built for 5 (or 4, keypoint-less) modalities, d_model 256, 8 heads, "
-                "clip 32 (got " +
-                    std::to_string(dims->n_modalities) + " modalities, d_model " + std::to_string(dims->d_model) +
-                    ", " + std::to_string(dims->time_heads) + " heads, clip " + std::to_string(dims->clip_len) + ")");
+                "vge_encoder_create: kernels are built for 5 (or 4, keypoint-less) modalities, clip 32, d_model 256 with "
+                "8 heads (any compute) or, on the exact-f32 path (VGE_F32), d_model a multiple of 32 up to 256 with a "
+                "head dim <= 64 (got " +
+                    std::to_string(dims->n_modalities) + " modalities, d_model " + std::to_string(Dm) + ", " +
+                    std::to_string(Hn) + " heads, clip " + std::to_string(dims->clip_len) + ")");
   for (int m = 0; m < M; ++m)
     if (dims->dims_raw[m] != kDimsRaw[m] || dims->dims_diff[m] != kDimsDiff[m])
       return fail(VGE_ERR_UNSUPPORTED, std::string("vge_encoder_create: unsupported dims for modality ") + kMods[m]);
@@ -413,6 +465,169 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
     return ok ? t->data : nullptr;
   };
   auto bail = [&]() { return fail(err.rfind("missing", 0) == 0 ? VGE_ERR_MISSING_WEIGHT : VGE_ERR_WEIGHT_SHAPE, err); };
+
+  if (generic) {  // ---- the generic-shape exact-f32 model: reference weights uploaded as they are (+ the fusion fold)
+    const int d = Dm, L = dims->time_layers, ffn = 4 * d;   // model.py:145: dim_feedforward = 4 * d_model
+    std::vector<float> hw;
+    std::vector<std::pair<const float**, size_t>> fix;      // device pointers resolved after the upload
+    auto put = [&](const float* src, size_t n, const float** dst) {
+      fix.push_back({dst, hw.size()});
+      hw.insert(hw.end(), src, src + n);
+      hw.resize((hw.size() + 63) / 64 * 64, 0.f);
+    };
+    auto* gm = new GenModel();
+    std::unique_ptr<GenModel> guard(gm);
+    gm->d = d; gm->heads = Hn; gm->layers = L; gm->ffn = ffn; gm->M = M;
+    gm->encs.resize(2 * M);
+    int col_raw = 0, col_diff = M == 5 ? VGE_RAW_DIM : VGE_RAW_DIM_NOKP;
+    for (int kind = 0; kind < 2; ++kind)
+      for (int m = 0; m < M; ++m) {
+        GenModel::Enc& E = gm->encs[kind * M + m];
+        const std::string pre = std::string(kind == 0 ? "state_enc." : "motion_enc.") + kMods[m];
+        const int d_in = kind == 0 ? kDimsRaw[m] : kDimsDiff[m];
+        E.d_in = d_in;
+        E.in_col = kind == 0 ? col_raw : col_diff;
+        if (kind == 0) col_raw += d_in; else col_diff += d_in;
+        const float* st = get(pre + ".stem.weight", {d, d_in, 1});
+        if (st) put(st, (size_t)d * d_in, &E.stem);
+        for (int b = 0; b < 4; ++b) {
+          for (int cv = 0; cv < 2; ++cv) {
+            const float* w = get(pre + ".blocks." + std::to_string(b) + ".conv" + std::to_string(cv + 1) + ".weight",
+                                 {d, d, 5});
+            if (w) put(w, (size_t)d * d * 5, &E.conv[b * 2 + cv]);
+          }
+          const float* g = get(pre + ".blocks." + std::to_string(b) + ".norm.weight", {d});
+          const float* be = get(pre + ".blocks." + std::to_string(b) + ".norm.bias", {d});
+          if (g && be) {
+            put(g, d, &E.gw[b]);
+            put(be, d, &E.gb[b]);
+          }
+        }
+        const float* pj = get(pre + ".proj.weight", {d, d});
+        if (pj) put(pj, (size_t)d * d, &E.proj);
+      }
+    const float* latent = get("fusion.latent", {1, 1, d});
+    const float* qw = get("fusion.q_ln.weight", {d});
+    const float* qb = get("fusion.q_ln.bias", {d});
+    const float* kvw = get("fusion.kv_ln.weight", {d});
+    const float* kvb = get("fusion.kv_ln.bias", {d});
+    const float* Wq = get("fusion.Wq.weight", {d, d});
+    const float* Wk = get("fusion.Wk.weight", {d, d});
+    const float* Wv = get("fusion.Wv.weight", {d, d});
+    const float* Wo = get("fusion.Wo.weight", {d, d});
+    const float* ltemp = get("fusion.logit_temp", {M});
+    const float* lbias = get("fusion.logit_bias", {M});
+    const float* clsw = get("cls", {1, 1, d});
+    const float* pe = nullptr;
+    {
+      auto it = wm.find("pos_enc.pe");
+      if (it == wm.end()) {
+        if (err.empty()) err = "missing weight: pos_enc.pe";
+      } else if (it->second->ndim == 3 && it->second->shape[0] == 1 && it->second->shape[1] >= 33 &&
+                 it->second->shape[2] == d && it->second->data) {
+        pe = it->second->data;
+      } else if (err.empty()) {
+        err = "bad shape for weight: pos_enc.pe";
+      }
+    }
+    std::vector<const float*> lw;
+    for (int l = 0; l < L; ++l) {
+      const std::string p = "temporal.layers." + std::to_string(l);
+      lw.push_back(get(p + ".self_attn.in_proj_weight", {3 * d, d}));
+      lw.push_back(get(p + ".self_attn.in_proj_bias", {3 * d}));
+      lw.push_back(get(p + ".self_attn.out_proj.weight", {d, d}));
+      lw.push_back(get(p + ".self_attn.out_proj.bias", {d}));
+      lw.push_back(get(p + ".norm1.weight", {d}));
+      lw.push_back(get(p + ".norm1.bias", {d}));
+      lw.push_back(get(p + ".linear1.weight", {ffn, d}));
+      lw.push_back(get(p + ".linear1.bias", {ffn}));
+      lw.push_back(get(p + ".linear2.weight", {d, ffn}));
+      lw.push_back(get(p + ".linear2.bias", {d}));
+      lw.push_back(get(p + ".norm2.weight", {d}));
+      lw.push_back(get(p + ".norm2.bias", {d}));
+    }
+    if (!err.empty()) return bail();
+    // fusion fold (double): q = q_ln(latent), u = Wk^T Wq q; Wov = Wo Wv (model.py:79-98)
+    std::vector<double> q(d), Q(d);
+    {
+      double mu = 0, var = 0;
+      for (int i = 0; i < d; ++i) mu += latent[i];
+      mu /= d;
+      for (int i = 0; i < d; ++i) var += (latent[i] - mu) * (latent[i] - mu);
+      var /= d;
+      const double rstd = 1.0 / std::sqrt(var + 1e-5);
+      for (int i = 0; i < d; ++i) q[i] = (latent[i] - mu) * rstd * qw[i] + qb[i];
+      for (int j = 0; j < d; ++j) {
+        double a = 0;
+        for (int i = 0; i < d; ++i) a += q[i] * Wq[(size_t)j * d + i];
+        Q[j] = a;
+      }
+    }
+    std::vector<float> u(d), wov((size_t)d * d);
+    for (int i = 0; i < d; ++i) {
+      double a = 0;
+      for (int j = 0; j < d; ++j) a += Q[j] * Wk[(size_t)j * d + i];
+      u[i] = (float)a;
+    }
+    for (int i = 0; i < d; ++i)
+      for (int j = 0; j < d; ++j) {
+        double a = 0;
+        for (int k = 0; k < d; ++k) a += (double)Wo[(size_t)i * d + k] * Wv[(size_t)k * d + j];
+        wov[(size_t)i * d + j] = (float)a;
+      }
+    put(u.data(), d, &gm->fuse.u);
+    put(kvw, d, &gm->fuse.kv_w);
+    put(kvb, d, &gm->fuse.kv_b);
+    put(wov.data(), (size_t)d * d, &gm->Wov);
+    put(clsw, d, &gm->cls);
+    put(pe, (size_t)33 * d, &gm->pe);
+    gm->fuse.n_mod = M;
+    gm->fuse.d = d;
+    for (int m = 0; m < M; ++m) {
+      const float x = ltemp[m];
+      const float sp = x > 20.0f ? x : log1pf(expf(x));  // F.softplus (beta 1, threshold 20)
+      gm->fuse.inv_tau[m] = 1.0f / (sp + 1e-3f);
+      gm->fuse.bias[m] = lbias[m];
+      gm->fuse.has_motion[m] = 1;
+    }
+    gm->L.resize(L);
+    for (int l = 0; l < L; ++l) {
+      GenModel::Lyr& Y = gm->L[l];
+      const float* const* w = lw.data() + 12 * l;
+      put(w[0], (size_t)3 * d * d, &Y.in_w);
+      put(w[1], (size_t)3 * d, &Y.in_b);
+      put(w[2], (size_t)d * d, &Y.out_w);
+      put(w[3], d, &Y.out_b);
+      put(w[4], d, &Y.n1w);
+      put(w[5], d, &Y.n1b);
+      put(w[6], (size_t)ffn * d, &Y.l1w);
+      put(w[7], ffn, &Y.l1b);
+      put(w[8], (size_t)d * ffn, &Y.l2w);
+      put(w[9], d, &Y.l2b);
+      put(w[10], d, &Y.n2w);
+      put(w[11], d, &Y.n2b);
+    }
+    hipError_t he = hipMalloc(&gm->wbuf, hw.size() * sizeof(float));
+    if (he == hipSuccess) he = hipMemcpy(gm->wbuf, hw.data(), hw.size() * sizeof(float), hipMemcpyHostToDevice);
+    if (he != hipSuccess) return fail(VGE_ERR_HIP, std::string("vge_encoder_create: ") + hipGetErrorString(he));
+    for (auto& f : fix) *f.first = gm->wbuf + f.second;
+    vge_encoder* enc = new vge_encoder();
+    enc->gen = guard.release();
+    enc->mode = VGE_F32;
+    enc->n_mod = M;
+    enc->n_enc = 2 * M;
+    enc->feat_dim = M == 5 ? VGE_FEAT_DIM : VGE_FEAT_DIM_NOKP;
+    enc->n_layers = L;
+    he = hipEventCreateWithFlags(&enc->conv_done, hipEventDisableTiming);
+    if (he == hipSuccess) he = hipEventCreateWithFlags(&enc->fuse_done, hipEventDisableTiming);
+    if (he == hipSuccess) he = hipEventCreateWithFlags(&enc->tail_done, hipEventDisableTiming);
+    if (he != hipSuccess) {
+      vge_encoder_destroy(enc);
+      return fail(VGE_ERR_HIP, std::string("vge_encoder_create: ") + hipGetErrorString(he));
+    }
+    *out = enc;
+    return VGE_OK;
+  }
 
   if (compute == VGE_F16 && dims->time_layers > 8)
     return fail(VGE_ERR_UNSUPPORTED, "vge_encoder_create: VGE_F16 runs the fused transformer, at most 8 layers");
@@ -830,6 +1045,32 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
 int vge_encoder_reserve(vge_encoder* enc, int B) {
   if (!enc || B < 1) return fail(VGE_ERR_ARG, "vge_encoder_reserve: bad argument");
   if (B <= enc->cap) return VGE_OK;
+  if (enc->gen) {  // the generic-shape model's planes, [rows][d_model] each
+    GenModel& g = *enc->gen;
+    if (g.ws) (void)hipFree(g.ws);
+    g.ws = nullptr;
+    enc->cap = 0;
+    const size_t d = g.d, frames = (size_t)B * 32, tok = (size_t)B * 33;
+    const size_t n_enc = 2 * (size_t)g.M * frames * d, n_f = frames * d, n_t = tok * d;
+    const size_t total = n_enc + 4 * n_f + 4 * n_t + tok * 3 * d + tok * g.ffn;
+    hipError_t he = hipMalloc(&g.ws, total * sizeof(float));
+    if (he == hipSuccess) he = hipMemset(g.ws, 0, total * sizeof(float));
+    if (he != hipSuccess) return fail(VGE_ERR_NOMEM, std::string("vge_encoder_reserve: ") + hipGetErrorString(he));
+    float* p = g.ws;
+    g.enc_out = p; p += n_enc;
+    g.a = p; p += n_f;
+    g.b = p; p += n_f;
+    g.c = p; p += n_f;
+    g.pp = p; p += n_f;
+    g.x = p; p += n_t;
+    g.att = p; p += n_t;
+    g.x1 = p; p += n_t;
+    g.tmp = p; p += n_t;
+    g.qkv = p; p += tok * 3 * d;
+    g.h = p;
+    enc->cap = g.cap = B;
+    return VGE_OK;
+  }
   if (enc->ws) {
     (void)hipFree(enc->ws);
     enc->ws = nullptr;
@@ -978,6 +1219,7 @@ int vge_encoder_destroy(vge_encoder* enc) {
   if (enc->tail_done) (void)hipEventDestroy(enc->tail_done);
   if (enc->hbuf) (void)hipFree(enc->hbuf);
   if (enc->status_h) (void)hipHostFree(enc->status_h);
+  delete enc->gen;
   delete enc;
   return VGE_OK;
 }
@@ -999,6 +1241,58 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
   auto mark = [&](int k) -> hipError_t {
     return (ev && ((enc->prof_mask >> k) & 1)) ? hipEventRecord(ev[k], s) : hipSuccess;
   };
+  auto tail_end = [&]() -> hipError_t {
+    if (!enc->tail_set) return hipSuccess;
+    enc->tail_pending = true;
+    return hipEventRecord(enc->tail_done, s);
+  };
+  if (enc->gen) {  // ---- generic-shape exact-f32 path (vge_encoder_gen.hip): one launch per stage
+    const GenModel& g = *enc->gen;
+    const int d = g.d;
+    HIPCHK(mark(0));
+    for (int e = 0; e < 2 * g.M; ++e) {  // MovementConvEncoder (model.py:43-58): stem, 4 dilated blocks, proj
+      const GenModel::Enc& E = g.encs[e];
+      float *cur = g.a, *tmp = g.b, *nxt = g.c;
+      HIPCHK(vge::launch_gen_conv(feats, enc->feat_dim, E.in_col, E.d_in, E.stem, d, 1, 1, 0, nullptr, cur, B, s));
+      for (int b = 0; b < 4; ++b) {  // TemporalConvBlock (model.py:21-40), dilation 1, 2, 4, 8
+        HIPCHK(vge::launch_gen_conv(cur, d, 0, d, E.conv[2 * b], d, 5, 1 << b, 1, nullptr, tmp, B, s));
+        HIPCHK(vge::launch_gen_conv(tmp, d, 0, d, E.conv[2 * b + 1], d, 5, 1 << b, 2, cur, nxt, B, s));
+        HIPCHK(vge::launch_gen_groupnorm(nxt, B, d, E.gw[b], E.gb[b], s));
+        std::swap(cur, nxt);
+      }
+      HIPCHK(vge::launch_gen_gemm(cur, d, E.proj, frames, d, d, nullptr, 0, nullptr, nullptr, nullptr,
+                                  g.enc_out + (size_t)e * frames * d, d, s));
+    }
+    HIPCHK(hipEventRecord(enc->conv_done, s));
+    enc->last_conv = enc->conv_done;
+    HIPCHK(mark(1));
+    if (enc->tail_pending) HIPCHK(hipStreamWaitEvent(s, enc->tail_done, 0));
+    HIPCHK(vge::launch_gen_fuse(g.enc_out, frames, g.fuse, g.pp, s));
+    HIPCHK(mark(2));
+    if (enc->tail_set) {
+      HIPCHK(hipEventRecord(enc->fuse_done, s));
+      HIPCHK(hipStreamWaitEvent(enc->tail, enc->fuse_done, 0));
+      s = enc->tail;
+    }
+    // frame tokens = pooled (Wo Wv)^T, CLS + sinusoidal positions (model.py:184-188)
+    HIPCHK(vge::launch_gen_gemm(g.pp, d, g.Wov, frames, d, d, nullptr, 3, nullptr, g.pe, g.cls, g.x, d, s));
+    HIPCHK(mark(3));
+    for (int l = 0; l < g.layers; ++l) {  // nn.TransformerEncoderLayer, post-norm, ReLU FFN of 4 d_model
+      const GenModel::Lyr& Y = g.L[l];
+      HIPCHK(vge::launch_gen_gemm(g.x, d, Y.in_w, M, 3 * d, d, Y.in_b, 0, nullptr, nullptr, nullptr, g.qkv, 3 * d, s));
+      HIPCHK(vge::launch_gen_attn(g.qkv, B, d, g.heads, g.att, s));
+      HIPCHK(vge::launch_gen_gemm(g.att, d, Y.out_w, M, d, d, Y.out_b, 0, nullptr, nullptr, nullptr, g.tmp, d, s));
+      HIPCHK(vge::launch_gen_add_ln(g.x, g.tmp, M, d, Y.n1w, Y.n1b, g.x1, s));
+      HIPCHK(vge::launch_gen_gemm(g.x1, d, Y.l1w, M, g.ffn, d, Y.l1b, 1, nullptr, nullptr, nullptr, g.h, g.ffn, s));
+      HIPCHK(vge::launch_gen_gemm(g.h, g.ffn, Y.l2w, M, d, g.ffn, Y.l2b, 0, nullptr, nullptr, nullptr, g.tmp, d, s));
+      HIPCHK(vge::launch_gen_add_ln(g.x1, g.tmp, M, d, Y.n2w, Y.n2b, g.x, s));
+    }
+    HIPCHK(mark(4));
+    HIPCHK(vge::launch_gen_embed_tc(g.x, B, d, seq_embed, frame_embed, tc_window, s));
+    HIPCHK(mark(5));
+    HIPCHK(tail_end());
+    return VGE_OK;
+  }
   const bool x3 = enc->mode == VGE_F32X3 || enc->mode == VGE_F16, split = enc->mode != VGE_F16;
   // one GEMM launcher for both modes (same epilogues; x3 = 3xfp16 split MFMA, f32 = exact f32 MFMA)
   auto gemm = [&](int epi, const float* A, int lda, const void* W, const float* cs, float* o, int ldo, int Mr, int K,
@@ -1056,11 +1350,6 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
     HIPCHK(hipStreamWaitEvent(enc->tail, enc->fuse_done, 0));
     s = enc->tail;
   }
-  auto tail_end = [&]() -> hipError_t {
-    if (!enc->tail_set) return hipSuccess;
-    enc->tail_pending = true;
-    return hipEventRecord(enc->tail_done, s);
-  };
   if (x3 && enc->tx_fused) {  // tokens + all layers + outputs in one launch, one window per workgroup
     HIPCHK(mark(3));
     const vge::TxArgsX3Host ta{enc->pooled, B, enc->n_layers, (const _Float16*)enc->Wov, enc->Wov_cs, enc->cls, enc->pe,

@@ -276,7 +276,7 @@ def _run_eval_phases(real_meshes_dir, model_path, keypoint_dir, real_kp_dir, cli
         with open(out_json, "w") as f:
             json.dump(merged, f, indent=2)
     if save_features:
-        save_window_features(fparts, save_features)
+        save_window_features(fparts, save_features, getattr(model, "d_model", 256))
     if human_scores_path and os.path.exists(human_scores_path):
         for key in ("ac", "tc"):
             sc = {v: e[key] for v, e in merged.items() if key in e}
@@ -339,7 +339,7 @@ def _real_set_phases(VE, ops, real_meshes_dir, model_path, real_kp_dir, clip_len
             warnings.warn(f"stats cache {stats_cache!r} not written: {e}")
     return model, stats, centroids, t1, t2
 
-def save_window_features(parts: List[Optional[dict]], path: str) -> None:
+def save_window_features(parts: List[Optional[dict]], path: str, d_model: int = 256) -> None:
     """window_features.pt (eval.py:197-204 layout) from the per-rank feature dicts, concatenated in rank order."""
     parts = [p for p in parts if p is not None]
     if parts:
@@ -348,7 +348,7 @@ def save_window_features(parts: List[Optional[dict]], path: str) -> None:
                "cls_names": [c for p in parts for c in p["cls_names"]],
                "vid_names": [v for p in parts for v in p["vid_names"]]}
     else:
-        out = {"seq_embeds": torch.empty(0, 256), "frame_embeds": torch.empty(0, 33, 256), "cls_names": [],
+        out = {"seq_embeds": torch.empty(0, d_model), "frame_embeds": torch.empty(0, 33, d_model), "cls_names": [],
                "vid_names": []}
     torch.save(out, path)
     print(f"Saved features to {path}")

@@ -115,11 +115,20 @@ def load_model(model_path, dims_map_raw=None, dims_map_diff=None, device="cuda",
                                         f"are built for the five-modality layout and its keypoint-less four; "
                                         f"VGE_ERR_UNSUPPORTED)")
     if isinstance(model_path, dict):
-        sd, hp = model_path, {"d_model": 256, "time_layers": 4, "time_heads": 8}
+        # a bare state dict: d_model and the layer count follow from its tensors (cls [1,1,d], temporal.layers.N.*);
+        # the head count is not recoverable from weights (pass (state_dict, hyper-parameters) for one other than 8)
+        sd = model_path
+        layers = {int(k.split(".")[2]) for k in sd if k.startswith("temporal.layers.")}
+        hp = {"d_model": int(np.asarray(sd["cls"]).shape[-1]) if "cls" in sd else 256,
+              "time_layers": max(layers) + 1 if layers else 4, "time_heads": 8}
     elif isinstance(model_path, tuple):  # (state_dict, hyper-parameters) as _load_state_dict returns them
         sd, hp = model_path
     else:
         sd, hp = _load_state_dict(model_path)
+    if (int(hp["d_model"]), int(hp["time_heads"])) != (ops.D_MODEL, 8) and compute != "f32":
+        # the tiled 3xfp16 / fp16 kernels are built for d_model 256 x 8 heads; other checkpoint shapes run on the
+        # generic exact-f32 kernels (vge_encoder_gen.hip)
+        compute = "f32"
     return ops.Encoder(sd, time_layers=int(hp["time_layers"]), time_heads=int(hp["time_heads"]),
                        d_model=int(hp["d_model"]), device=device, compute=compute, n_modalities=n_mod)
 
@@ -139,15 +148,16 @@ def _window_tensor(samples, name_to_idx, device):
 
 def encode_windows(model: ops.Encoder, store: ops.DeviceFrameStore, windows: torch.Tensor, stats: ModalityStatsGPU,
                    batch: int = 1024, frame_embed: bool = False):
-    """featurise + encode windows in batches; returns (seq [N,256], frame [N,33,256] | None, tc [N])."""
+    """featurise + encode windows in batches; returns (seq [N,d], frame [N,33,d] | None, tc [N]), d = d_model."""
     n = int(windows.shape[0])
     dev = windows.device
     if model.layout != stats.layout:
         raise ValueError(f"model takes the {model.layout!r} feature layout but the stats are {stats.layout!r} "
                          f"(the reference would fail on the feature width)")
-    seq = torch.empty((n, ops.D_MODEL), device=dev)
+    d = getattr(model, "d_model", ops.D_MODEL)
+    seq = torch.empty((n, d), device=dev)
     tcw = torch.empty((n,), device=dev)
-    fe = torch.empty((n, 33, ops.D_MODEL), device=dev) if frame_embed else None
+    fe = torch.empty((n, 33, d), device=dev) if frame_embed else None
     model.reserve(min(batch, max(n, 1)))
     feats = torch.empty((min(batch, max(n, 1)), 32, model.feat_dim), device=dev)
     for b0 in range(0, n, batch):
@@ -175,7 +185,7 @@ def build_real_centroids(model: ops.Encoder, real_meshes_dir: str, real_kp_dir: 
         train_items = train_ds.items
         label_dict = {cls: i for i, cls in enumerate(sorted({it.cls for it in real_ds.items}))}
     C_ = len(label_dict)
-    sums = torch.zeros((C_, ops.D_MODEL), device=device)
+    sums = torch.zeros((C_, getattr(model, "d_model", ops.D_MODEL)), device=device)
     counts = torch.zeros((C_,), device=device)
     if len(train_items):
         samples = enumerate_test_windows(NpzVideoDataset("", items=list(train_items)), clip_len, stride)

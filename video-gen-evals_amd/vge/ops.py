@@ -127,7 +127,9 @@ class Encoder:
 
     compute="f32x3" (default): split-precision 3xfp16 MFMA, f32-class results (~1e-7 from exact f32);
     compute="f32": exact f32 MFMA.  n_modalities 5 (vit, global, pose, beta, kp2d; feats rows of 2596) or 4 (the
-    keypoint-less model, feats rows of 2356)."""
+    keypoint-less model, feats rows of 2356).  A checkpoint with d_model / time_heads other than 256 / 8 runs on the
+    generic exact-f32 kernels (compute "f32" only; d_model 32..256 in steps of 32, head dim <= 64): its embeddings
+    are d_model wide."""
 
     def __init__(self, state_dict: Dict[str, np.ndarray], time_layers: int = 4, time_heads: int = 8,
                  d_model: int = 256, device=None, compute: str = "f32x3", n_modalities: int = 5):
@@ -159,6 +161,7 @@ class Encoder:
         self._lib = lib
         self.capacity = 0
         self.n_modalities = n_modalities
+        self.d_model = int(d_model)
         self.feat_dim = int(lib.vge_encoder_feat_dim(h))
         self.layout = "kp" if self.feat_dim == FEAT_DIM else "nokp"
 
@@ -170,18 +173,19 @@ class Encoder:
 
     def encode(self, feats: torch.Tensor, frame_embed: bool = False, tc: bool = True,
                seq_out: Optional[torch.Tensor] = None, tc_out: Optional[torch.Tensor] = None):
-        """feats [B,32,feat_dim] -> (seq_embed [B,256], frame_embeds [B,33,256] | None, tc_window [B] | None).
-        seq_out / tc_out: optional contiguous float32 destinations ([B,256] / [B]) written in place."""
+        """feats [B,32,feat_dim] -> (seq_embed [B,d], frame_embeds [B,33,d] | None, tc_window [B] | None), d = d_model.
+        seq_out / tc_out: optional contiguous float32 destinations ([B,d] / [B]) written in place."""
         B, T, D = feats.shape
         if D != self.feat_dim:
             raise L.VgeError(f"feats last dim {D} != {self.feat_dim}")
-        for t, shape in ((seq_out, (B, D_MODEL)), (tc_out, (B,))):
+        D_ = self.d_model
+        for t, shape in ((seq_out, (B, D_)), (tc_out, (B,))):
             if t is not None and (tuple(t.shape) != shape or t.dtype != torch.float32 or not t.is_contiguous()
                                   or t.device != feats.device):
                 raise L.VgeError(f"encode: output must be a contiguous float32 {shape} tensor on {feats.device}")
         self.reserve(B)
-        seq = seq_out if seq_out is not None else torch.empty((B, D_MODEL), device=feats.device, dtype=torch.float32)
-        fe = torch.empty((B, T + 1, D_MODEL), device=feats.device, dtype=torch.float32) if frame_embed else None
+        seq = seq_out if seq_out is not None else torch.empty((B, D_), device=feats.device, dtype=torch.float32)
+        fe = torch.empty((B, T + 1, D_), device=feats.device, dtype=torch.float32) if frame_embed else None
         tcw = (tc_out if tc_out is not None else torch.empty((B,), device=feats.device, dtype=torch.float32)) if tc else None
         L.check(self._lib.vge_encode(self._h, _ptr(feats), B, T, _ptr(seq), _ptr(fe), _ptr(tcw), _stream(feats.device)),
                 "vge_encode")

@@ -111,6 +111,7 @@ def load(path: Optional[str], fp: Dict) -> Optional[Dict]:
     except (OSError, ValueError, KeyError, EOFError, zipfile.BadZipFile):  # unreadable / truncated / corrupt: a miss
         return None
     if out["stats_sums"].shape != (2, 2596) or out["stats_counts"].shape != (2,) or \
-            out["cent_sums"].shape != (len(out["classes"]), 256) or out["cent_counts"].shape != (len(out["classes"]),):
+            out["cent_sums"].ndim != 2 or out["cent_sums"].shape[0] != len(out["classes"]) or \
+            out["cent_counts"].shape != (len(out["classes"]),):
         return None
     return out
