@@ -110,8 +110,14 @@ struct X3sAux {
   int ex[2][2][X3S_WMAX];           // [GEMM-input parity][group][window] exponents of the stored activations
   int cnt[2];                       // exchange arrivals per group (monotonic over the launch)
 };
-constexpr int X3S_LDS_BYTES = X3S_AUX_OFF + (int)sizeof(X3sAux);
+// Per wave: the next block-conv1 epilogue's fold operands of its 32 columns, landed by LDS-DMA during the stream
+// before it (registers held across that stream spilled): [32 columns][16 floats] of EncDescX3::fold, then
+// GroupNorm gamma [32] | beta [32]
+constexpr int X3S_PRE_WAVE = 32 * 64 + 256;
+constexpr int X3S_PRE_OFF = (X3S_AUX_OFF + (int)sizeof(X3sAux) + 15) / 16 * 16;
+constexpr int X3S_LDS_BYTES = X3S_PRE_OFF + 8 * X3S_PRE_WAVE;
 static_assert(X3S_AUX_OFF % 16 == 0, "aux alignment");
+static_assert(X3S_LDS_BYTES <= 160 * 1024, "LDS");
 
 // One part of a conv / proj GEMM without barriers: ntap taps x 8 chunks (input-channel blocks cb0..cb0+7 of each
 // tap).  B fragments 3 chunks ahead in a register ring; A fragments single-buffered per row tile (tile t's fragments
@@ -436,9 +442,8 @@ __device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, i
   // The epilogue's global operands (column scale; GroupNorm affine and folded corrections; the proj's corrections)
   // are loaded at the start of the phase before it (P2 of the same GEMM), so their latency -- long while the other
   // half streams weights -- hides behind that stream.
-  float pre_wcs = 0.f, pre_gw = 0.f, pre_gb = 0.f, pre_sx = 0.f, pre_sy = 0.f;
-  floatx4 pre_g, pre_b;   // per-tap sums of W1 gamma / W1 beta, taps 0..3
-  float pre_g4, pre_b4;   // ... tap 4
+  float pre_wcs = 0.f, pre_sx = 0.f, pre_sy = 0.f;
+  char* pre_lds = lds_raw + X3S_PRE_OFF + wave * X3S_PRE_WAVE;  // this wave's fold operands (X3S_PRE_WAVE)
   auto prefetch = [&](auto kind_tag, int gi) {
     constexpr int KIND = decltype(kind_tag)::value;
     const int blk = gi >> 1;
@@ -447,15 +452,14 @@ __device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, i
       pre_sx = gload(ed.fold + 3 * 256 * 16 + col * 2);
       pre_sy = gload(ed.fold + 3 * 256 * 16 + col * 2 + 1);
     } else if constexpr (KIND == 0) {
-      if (blk > 0) {
-        pre_gw = gload(ed.gn_w + (blk - 1) * 256 + col);
-        pre_gb = gload(ed.gn_b + (blk - 1) * 256 + col);
-        typedef const __attribute__((address_space(1))) floatx4* gf4;
-        const float* fb = ed.fold + ((size_t)(blk - 1) * 256 + col) * 16;
-        pre_g = *(gf4)fb;
-        pre_g4 = gload(fb + 4);
-        pre_b = *(gf4)(fb + 8);
-        pre_b4 = gload(fb + 12);
+      if (blk > 0) {  // LDS-DMA: the wave's 32 columns x 16 floats (2 KB, contiguous), then gamma | beta
+        const float* fb = ed.fold + ((size_t)(blk - 1) * 256 + wave * 32) * 16;
+        glds16(fb + lane * 4, pre_lds);
+        glds16(fb + 256 + lane * 4, pre_lds + 1024);
+        const float* gsrc = (h ? ed.gn_b : ed.gn_w) + (blk - 1) * 256 + col;
+        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)gsrc,
+                                         (__attribute__((address_space(3))) void*)(pre_lds + 2048), 4, 0, 0);
+        asm volatile("" ::: "memory");
       }
     }
   };
@@ -495,6 +499,14 @@ __device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, i
       if constexpr (KIND == 0) {
         if (blk > 0) {
           const int dil = 1 << blk;
+          vmcnt0();  // this wave's LDS-DMA of the fold operands (issued before the stream) has landed
+          const char* pl = pre_lds + i * 64;
+          const floatx4 pre_g = *reinterpret_cast<const floatx4*>(pl);
+          const float pre_g4 = *reinterpret_cast<const float*>(pl + 16);
+          const floatx4 pre_b = *reinterpret_cast<const floatx4*>(pl + 32);
+          const float pre_b4 = *reinterpret_cast<const float*>(pl + 48);
+          const float pre_gw = *reinterpret_cast<const float*>(pre_lds + 2048 + i * 4);
+          const float pre_gb = *reinterpret_cast<const float*>(pre_lds + 2048 + 128 + i * 4);
 #pragma unroll
           for (int f = 0; f < 16; ++f) {
             const int row = x3s_rfr0<W>(f / GH, f % GH) + 4 * h;  // row + (tap - 2) dil in [0, 32)
