@@ -1,0 +1,60 @@
+"""ISA guard (CPU): the hot kernels of libvge.so carry no FLAT memory instructions and no scratch.
+
+A FLAT instruction reaching an LDS operand through a generic pointer is the one instruction class in these kernels that
+can raise a memory violation from an LDS-intended address (ds_read / ds_write past the allocation read zeros / drop;
+the weight rings use buffer loads inside their images), and it is what the dropped 16x16x32 conv build used for its A
+fragments (the build that faulted once).  Scratch in a streaming kernel means registers held
+across its MFMA streams spilled.  tools/isa_guard.py extracts the gfx950 code objects from the library's offload
+bundles and reads each kernel's disassembly and metadata; no GPU and no compiler run.
+"""
+import os
+import shutil
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "tools"))
+
+LIB = os.path.join(REPO, "video-gen-evals_amd", "vge", "libvge.so")
+
+# kernel name fragments: the config-2 headline kernels, the gate detector's own kernels, the generic-shape path
+HOT = [
+    "conv_encoder_x3s_kernel",
+    "transformer_x3_kernelILb1ELb1ELi1ELi1E",   # f32x3, one window per workgroup
+    "transformer_x3_kernelILb1ELb0ELi1ELi1E",
+    "featurize_tiles_kernel",
+    "fuse_kernel",
+    "score_videos_kernel",
+    "rpn_select_kernel",
+    "rpn_nms_kernel",
+    "roi_align_kernel",
+    "det_post_kernel",
+    "gen_conv_kernel",
+    "gen_attn_kernel",
+]
+
+
+@pytest.fixture(scope="module")
+def table():
+    if not os.path.exists(LIB):
+        pytest.skip("libvge.so not built")
+    if not shutil.which("objcopy") or not os.path.exists("/opt/rocm/lib/llvm/bin/llvm-objdump"):
+        pytest.skip("objcopy / ROCm llvm-objdump not available")
+    import isa_guard
+    return isa_guard.kernels(LIB)
+
+
+@pytest.mark.parametrize("frag", HOT)
+def test_hot_kernel_isa(table, frag):
+    hits = {k: v for k, v in table.items() if frag in k}
+    assert hits, f"no kernel matching {frag} in libvge.so"
+    for name, r in hits.items():
+        assert r["flat"] == 0, f"{name}: {r['flat']} FLAT memory instructions"
+        assert r["scratch"] == 0 and r["scratch_ops"] == 0, f"{name}: {r['scratch']} B/lane scratch"
+
+
+def test_guard_sees_the_library(table):
+    """The extraction finds the code objects (every HIP translation unit's kernels)."""
+    assert len(table) > 60
+    assert any("conv_bf16_kernel" in k for k in table) and any("gemm_bf16_kernel" in k for k in table)

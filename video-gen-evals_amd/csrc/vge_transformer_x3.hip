@@ -397,9 +397,15 @@ __global__ void __launch_bounds__(256, OCC) transformer_x3_kernel(TxArgsX3 ta) {
     }
   }
 
+  // chunk order inside a segment rotated per workgroup (VGE_TX_ROT: the CUs of an XCD, which share its L2, then read
+  // different chunks of the same segment at a time instead of all hitting one chunk's lines together)
+#ifndef VGE_TX_ROT
+#define VGE_TX_ROT 0
+#endif
+  const int rot = VGE_TX_ROT ? __builtin_amdgcn_readfirstlane(((blockIdx.x >> 3) * VGE_TX_ROT) & 15) : 0;
   BFrag<2> b[TX_PF];
 #pragma unroll
-  for (int j = 0; j < TX_PF - 1; ++j) load_b<2, SPW>(seg_base(0), j, loff, b[j]);
+  for (int j = 0; j < TX_PF - 1; ++j) load_b<2, SPW>(seg_base(0), (j + rot) & 15, loff, b[j]);
 
   int s = 0;  // the current segment
   // lane-derived values re-derived per segment: stops the compiler from hoisting the ~100 (64-bit, loop-invariant)
@@ -429,6 +435,7 @@ __global__ void __launch_bounds__(256, OCC) transformer_x3_kernel(TxArgsX3 ta) {
   float xs[W], cl[W][2];
   auto stream = [&](const char* abase) __attribute__((always_inline)) {
     auto afn = [&](int c, AFragT<W>& f) __attribute__((always_inline)) {
+      if (VGE_TX_ROT) c = (c + rot) & 15;
 #pragma unroll
       for (int v = 0; v < W; ++v) {
         const char* ab = abase + v * AP_BYTES;
@@ -457,8 +464,8 @@ __global__ void __launch_bounds__(256, OCC) transformer_x3_kernel(TxArgsX3 ta) {
 #pragma unroll
     for (int c = 0; c < 16; ++c) {
 #if !(VGE_ABL & 2)
-      if (c + TX_PF - 1 < 16) load_b<2, SPW>(seg_cur, c + TX_PF - 1, loff, b[(c + TX_PF - 1) % TX_PF]);
-      else load_b<2, SPW>(seg_nxt, c + TX_PF - 1 - 16, loff, b[(c + TX_PF - 1) % TX_PF]);
+      if (c + TX_PF - 1 < 16) load_b<2, SPW>(seg_cur, (c + TX_PF - 1 + rot) & 15, loff, b[(c + TX_PF - 1) % TX_PF]);
+      else load_b<2, SPW>(seg_nxt, (c + TX_PF - 1 - 16 + rot) & 15, loff, b[(c + TX_PF - 1) % TX_PF]);
 #endif
       if (c + 1 < 16 && (!(VGE_ABL & 4) || c == 0)) afn(c + 1, a[(c + 1) & 1]);
       const AFragT<W>& f = a[c & 1];
