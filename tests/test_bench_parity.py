@@ -175,9 +175,11 @@ def test_f16_unit_kernel_is_position_independent_at_4096_windows(tx_w):
     """Config 5's encode chunk (4,096 windows: 27 rounds of 5- and 6-window units) checked without the oracle, by a
     property that pins the schedule: every window's outputs depend only on that window (per-window exponents, the
     same chunk order), so encoding a 256-window slice alone (two rounds, quint / hex / quad units) must reproduce its
-    rows of the 4,096-window encode bit for bit, wherever the big schedule placed them.  The transformer's windows per
-    workgroup are fixed for both encodes (at 2 a window shares its workgroup, and the CLS tile, with a neighbour whose
-    rows do not enter its own; the automatic choice differs between 4,096 and 256 windows)."""
+    rows of the 4,096-window encode, wherever the big schedule placed them: bit for bit in the conv stage, and within
+    f32 summation order after the transformer (its weight chunks are read in an order rotated by the workgroup's
+    position, DESIGN.md section 3.3, so a window's K-sum order depends on where it lands).  The transformer's windows
+    per workgroup are fixed for both encodes (at 2 a window shares its workgroup, and the CLS tile, with a neighbour
+    whose rows do not enter its own; the automatic choice differs between 4,096 and 256 windows)."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from vge import lib as L
@@ -194,7 +196,9 @@ def test_f16_unit_kernel_is_position_independent_at_4096_windows(tx_w):
         assert torch.isfinite(seq).all() and torch.isfinite(tcw).all()
         for lo in (0, 1000, 3841):
             s2, _, t2 = enc.encode(feats[lo:lo + 255].contiguous(), frame_embed=False, tc=True)
-            assert torch.equal(s2, seq[lo:lo + 255]) and torch.equal(t2, tcw[lo:lo + 255]), lo
+            d_s = (s2 - seq[lo:lo + 255]).abs().max().item()
+            d_t = (t2 - tcw[lo:lo + 255]).abs().max().item()
+            assert d_s < 2e-6 and d_t < 2e-6, (lo, d_s, d_t)
     finally:
         so.vge_debug_set_tx_windows(0)
 

@@ -51,7 +51,7 @@ struct GemmArgsX3Host {
 };
 hipError_t launch_conv_encoders_x3(const float*, int, const void*, int, unsigned, float*, bool, bool, hipStream_t);
 hipError_t encoder_x3s_kernel_setup();
-hipError_t launch_conv_encoders_x3s(const float*, int, const void*, int, unsigned, float*, int*, hipStream_t);
+hipError_t launch_conv_encoders_x3s(const float*, int, const void*, int, unsigned, float*, int*, bool, hipStream_t);
 
 bool conv_f16w_plan(int n_windows, int n_enc, int wmax, int& G, int& R, int& U);
 hipError_t launch_conv_f16w_table(int n_windows, int n_enc, int G, int R, int U, int* d_table, hipStream_t s);
@@ -665,8 +665,12 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
   // VGE_F32X3 runs the staggered conv kernel (vge_encoder_x3s.hip) unless VGE_X3S=0: each block's GroupNorm is folded
   // into the next GEMM -- conv1 of blocks 1..3 and proj packed as W diag(gamma) -- plus the per-row corrections
   // (sums of W gamma and W beta over the taps that fall inside the window; double, then f32)
+  // VGE_F16 with VGE_F16_X3S=1 (and the stem unsplit): the same staggered kernel in single fp16 (hi planes only)
   const char* x3s_env = getenv("VGE_X3S");
-  const bool x3s = compute == VGE_F32X3 && !(x3s_env && x3s_env[0] == '0');
+  const char* f16s_env = getenv("VGE_F16_X3S");
+  const char* mix_env = getenv("VGE_F16_MIX");
+  const bool f16_x3s = compute == VGE_F16 && f16s_env && f16s_env[0] == '1' && !((mix_env ? atoi(mix_env) : 2) & 1);
+  const bool x3s = (compute == VGE_F32X3 && !(x3s_env && x3s_env[0] == '0')) || f16_x3s;
   std::vector<std::vector<float>> folded;  // folded weight copies, alive until packed
   struct Off { Mat stem, conv, proj; size_t gnw, gnb, fold; int in_col, d_in, P; };
   const int n_enc = 2 * M;
@@ -1305,7 +1309,7 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
     return vge::launch_gemm(epi, g, s);
   };
   HIPCHK(mark(0));
-  if (x3 && !split && !(enc->f16_mix & 1) && enc->f16w > 0) {
+  if (x3 && !split && !(enc->f16_mix & 1) && enc->f16w > 0 && !enc->x3s) {
     // the unit table of this batch size: cached, else built on the device (stream-ordered, no host copy) into the
     // least recently used slot
     int k = -1;
@@ -1327,7 +1331,7 @@ int vge_encode(vge_encoder* enc, const float* feats, int B, int T, float* seq_em
                                           enc->tables[k].G, enc->tables[k].R, s));
   } else if (x3 && enc->x3s) {
     HIPCHK(vge::launch_conv_encoders_x3s(feats, B, enc->d_encs, enc->n_enc, enc->stem_heavy, enc->enc_out,
-                                         enc->status_d, s));
+                                         enc->status_d, split, s));
   } else if (x3) {
     HIPCHK(vge::launch_conv_encoders_x3(feats, B, enc->d_encs, enc->n_enc, enc->stem_heavy, enc->enc_out, split, enc->f16_mix & 1, s));
   } else {

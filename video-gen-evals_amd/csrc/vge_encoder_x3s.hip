@@ -67,6 +67,15 @@ constexpr int X3S_WMAX = 4;     // windows per unit (quads; pairs fill the remai
 #ifndef X3S_PF_PAIR
 #define X3S_PF_PAIR 8  // ... in a pair's
 #endif
+#ifndef X3S_PF16_QUAD
+#define X3S_PF16_QUAD 8  // ... single-fp16 mode (VGE_F16): half the bytes per chunk, a third of the MFMAs
+#endif
+#ifndef X3S_PF16_PAIR
+#define X3S_PF16_PAIR 8
+#endif
+#ifndef X3S_ROT
+#define X3S_ROT 0  // 1: chunk order inside a tap rotated per workgroup (see stream_part; measured 1-2 % slower)
+#endif
 #ifndef X3S_SKIP
 #define X3S_SKIP 1  // 1: a row tile skips the taps that put all its frames outside the window (dilated convs)
 #endif
@@ -125,13 +134,13 @@ static_assert(X3S_LDS_BYTES <= 160 * 1024, "LDS");
 // other tiles' MFMAs).  Addresses are formed once per tap -- LDS row bases (the zero row for taps outside the window)
 // plus immediate chunk offsets, uniform weight pointers plus the lane's offset -- so the stream issues almost no VALU
 // work besides its MFMAs (its partner wave's epilogue shares the SIMD's issue slots).
-template <int W, bool SKIP>
+template <int W, bool SKIP, bool SP>
 __device__ __forceinline__ void stream_part(Acc<W, 1>& acc, const char* wb, int ntap, unsigned loff, const char* xa,
-                                            int i, int dil, int ctr) {
+                                            int i, int dil, int ctr, int rot) {
   constexpr int R = W, G = x3s_g<W>();
   // chunks in flight: a pair's chunk is only 6 MFMAs (192 cycles) -- 3 chunks ahead would not cover the weight
   // stream's L2 latency while one wave per SIMD streams -- and it has the registers for 7
-  constexpr int PF = R >= 4 ? X3S_PF_QUAD : X3S_PF_PAIR;
+  constexpr int PF = SP ? (R >= 4 ? X3S_PF_QUAD : X3S_PF_PAIR) : (R >= 4 ? X3S_PF16_QUAD : X3S_PF16_PAIR);
   // the ring's slots restart at every tap (chunk j of a tap sits in slot j % PF, and the last steps of a tap load the
   // next tap's first chunks into the slots they will be read from): a depth that does not divide a tap's 8 chunks
   // reads the wrong chunk (measured: depths 3 / 6 / 12 gave wrong scores)
@@ -147,10 +156,12 @@ __device__ __forceinline__ void stream_part(Acc<W, 1>& acc, const char* wb, int 
   const __amdgpu_buffer_rsrc_t rs =
       __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(wb), (short)0, 0x7FFFFFF0, 0x00020000);
   const unsigned loff_l = loff + PLANE_B;
+  // rot: this workgroup's chunk order inside a tap (logical chunk j is input-channel block (j + rot) & 7): the CUs of
+  // an XCD stream the same encoder's weights together, and rotated they do not all read one chunk's lines at once
   auto ldb = [&](int k, int j, BFrag<1>& b) {  // chunk j (0..7) of tap k
-    const int so = (k * 16 + j) * CHUNK_B;
+    const int so = (k * 16 + ((j + rot) & 7)) * CHUNK_B;
     b.h[0] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(rs, loff, so, 0));
-    b.l[0] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(rs, loff_l, so, 0));
+    if constexpr (SP) b.l[0] = __builtin_bit_cast(half8, __builtin_amdgcn_raw_buffer_load_b128(rs, loff_l, so, 0));
   };
   BFrag<1> b[PF];
 #pragma unroll
@@ -163,8 +174,8 @@ __device__ __forceinline__ void stream_part(Acc<W, 1>& acc, const char* wb, int 
     pt[t] = rowp(0, t);
     okc[t] = x3s_tap_ok<W, SKIP>(t, -ctr * dil);
     if (okc[t]) {
-      ah[t] = *reinterpret_cast<const half8*>(pt[t]);
-      al[t] = *reinterpret_cast<const half8*>(pt[t] + XLO);
+      ah[t] = *reinterpret_cast<const half8*>(pt[t] + rot * 32);
+      if constexpr (SP) al[t] = *reinterpret_cast<const half8*>(pt[t] + rot * 32 + XLO);
     }
   }
   for (int k = 0; k < ntap; ++k) {
@@ -188,15 +199,17 @@ __device__ __forceinline__ void stream_part(Acc<W, 1>& acc, const char* wb, int 
 #if !(VGE_ABL & 1)
         if (okc[t]) {
           acc.c[t][0] = mfma32(ah[t], b[j % PF].h[0], acc.c[t][0]);
-          acc.c[t][0] = mfma32(ah[t], b[j % PF].l[0], acc.c[t][0]);
-          acc.c[t][0] = mfma32(al[t], b[j % PF].h[0], acc.c[t][0]);
+          if constexpr (SP) {
+            acc.c[t][0] = mfma32(ah[t], b[j % PF].l[0], acc.c[t][0]);
+            acc.c[t][0] = mfma32(al[t], b[j % PF].h[0], acc.c[t][0]);
+          }
         }
 #endif
 #if !(VGE_ABL & 4)
         if (j < 7 ? okc[t] : okn[t]) {
-          const char* q = j < 7 ? pt[t] + (j + 1) * 32 : pn[t];
+          const char* q = j < 7 ? pt[t] + ((j + 1 + rot) & 7) * 32 : pn[t] + rot * 32;
           ah[t] = *reinterpret_cast<const half8*>(q);
-          al[t] = *reinterpret_cast<const half8*>(q + XLO);
+          if constexpr (SP) al[t] = *reinterpret_cast<const half8*>(q + XLO);
         }
 #endif
         __builtin_amdgcn_sched_barrier(0);  // tile by tile: the next fragments reuse this tile's registers
@@ -216,7 +229,7 @@ __device__ __forceinline__ float gload(const float* p) {
   return *(const __attribute__((address_space(1))) float*)p;
 }
 
-template <int W>
+template <int W, bool SP>
 __device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, int n_windows, int win0,
                                               const EncDescX3& ed, int e, float* __restrict__ enc_out, char* lds_raw,
                                               int& n_ex, int* __restrict__ status, int spin_limit,
@@ -262,7 +275,7 @@ __device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, i
     for (int t = 0; t < R; ++t) {  // MFMA row i of tile t: window i / G, frame G t + i % G
       const char* q = xa + (i / G) * WSB + (G * t + i % G) * XRB + c * 32;
       f.h[t] = *reinterpret_cast<const half8*>(q);
-      f.l[t] = *reinterpret_cast<const half8*>(q + XLO);
+      if constexpr (SP) f.l[t] = *reinterpret_cast<const half8*>(q + XLO);
     }
   };
   XTS(0);
@@ -307,7 +320,8 @@ __device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, i
 #pragma unroll
         for (int jc = 0; jc < 4; ++jc) {
           const int c = lane + 64 * jc;
-          split_store(xr + c, xr + XLO / 2 + c, ldexpf(a[q][jr][jc], -ex));
+          if constexpr (SP) split_store(xr + c, xr + XLO / 2 + c, ldexpf(a[q][jr][jc], -ex));
+          else xr[c] = (_Float16)ldexpf(a[q][jr][jc], -ex);
         }
       }
       __syncthreads();  // X and ecur complete
@@ -319,7 +333,7 @@ __device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, i
 #pragma unroll
           for (int r = 0; r < 16; ++r) acc.c[t][0][r] *= ldexpf(1.0f, eprev[crow(t, r)] - ecur[crow(t, r)]);
       }
-      run_stream<CONV_PF, true>(acc, reinterpret_cast<const char*>(ed.stem) + (size_t)p * 16 * CHUNK_B,
+      run_stream<SP ? CONV_PF : CONV_PF16, SP>(acc, reinterpret_cast<const char*>(ed.stem) + (size_t)p * 16 * CHUNK_B,
                                 ((kw + 127) >> 7) * STREAM_GROUP, loff, afn_stem);
       if (p == 0) XTS(123);
       __syncthreads();  // every wave is done reading X
@@ -391,7 +405,7 @@ __device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, i
         const _Float16 hi = (_Float16)y;
         const int off = cofs(t, r);
         *reinterpret_cast<_Float16*>(bh + off) = hi;
-        *reinterpret_cast<_Float16*>(bh + XLO + off) = (_Float16)(y - (float)hi);
+        if constexpr (SP) *reinterpret_cast<_Float16*>(bh + XLO + off) = (_Float16)(y - (float)hi);
       }
     }
     XTS(tslot + 3);
@@ -605,7 +619,8 @@ __device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, i
     const char* wb = reinterpret_cast<const char*>(proj ? ed.proj : ed.conv + (size_t)gi * 80 * (CHUNK_B / 2)) +
                      (size_t)part * 8 * CHUNK_B;
     if (X3S_PRIO) __builtin_amdgcn_s_setprio(1);
-    stream_part<W, SKIP>(acc, wb, proj ? 1 : 5, loff, xa + part * 8 * 32, i, proj ? 0 : 1 << (gi >> 1), proj ? 0 : 2);
+    stream_part<W, SKIP, SP>(acc, wb, proj ? 1 : 5, loff, xa + part * 8 * 32, i, proj ? 0 : 1 << (gi >> 1),
+                             proj ? 0 : 2, X3S_ROT ? __builtin_amdgcn_readfirstlane((int)(blockIdx.x >> 3) & 7) : 0);
     __builtin_amdgcn_s_setprio(0);
   };
 
@@ -659,6 +674,7 @@ __device__ __forceinline__ void conv_x3s_body(const float* __restrict__ feats, i
   if (grp == 0) phase_end();
 }
 
+template <bool SP>
 __global__ void __launch_bounds__(512, 1) conv_encoder_x3s_kernel(const float* __restrict__ feats,
                                                                    const EncDescX3* __restrict__ encs, vge::ConvSched cs,
                                                                    float* __restrict__ enc_out, int* __restrict__ status,
@@ -704,12 +720,12 @@ __global__ void __launch_bounds__(512, 1) conv_encoder_x3s_kernel(const float* _
     if (u < cs.Q) {
       int e, w0;
       conv_unit(cs, u, e, w0);
-      conv_x3s_body<4>(feats, n, w0, encs[e], e, enc_out, lds_raw, n_ex, status, spin_limit,
+      conv_x3s_body<4, SP>(feats, n, w0, encs[e], e, enc_out, lds_raw, n_ex, status, spin_limit,
                        round == X3S_TRACE_ROUND);
     } else {
       int e, w0;
       conv_unit(cs, u, e, w0);
-      conv_x3s_body<2>(feats, n, w0, encs[e], e, enc_out, lds_raw, n_ex, status, spin_limit,
+      conv_x3s_body<2, SP>(feats, n, w0, encs[e], e, enc_out, lds_raw, n_ex, status, spin_limit,
                        round == X3S_TRACE_ROUND);
     }
   }
@@ -724,8 +740,12 @@ __global__ void __launch_bounds__(512, 1) conv_encoder_x3s_kernel(const float* _
 namespace vge {
 
 hipError_t encoder_x3s_kernel_setup() {
-  return hipFuncSetAttribute((const void*)conv_encoder_x3s_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             X3S_LDS_BYTES);
+  hipError_t e = hipFuncSetAttribute((const void*)conv_encoder_x3s_kernel<true>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, X3S_LDS_BYTES);
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)conv_encoder_x3s_kernel<false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            X3S_LDS_BYTES);
+  return e;
 }
 
 // spin bound of the half-workgroup exchange (test hook vge_debug_set_x3s_spin_limit: 0 makes every wave that arrives
@@ -733,12 +753,16 @@ hipError_t encoder_x3s_kernel_setup() {
 static int g_x3s_spin_limit = 1 << 22;
 
 hipError_t launch_conv_encoders_x3s(const float* feats, int n_windows, const void* encs, int n_enc, unsigned heavy,
-                                    float* enc_out, int* status, hipStream_t s) {
+                                    float* enc_out, int* status, bool split, hipStream_t s) {
   if (n_windows < 1 || n_enc < 1) return hipSuccess;
   if (!status) return hipErrorInvalidValue;
   const ConvSched cs = conv_quad_sched(n_windows, n_enc, heavy);
-  hipLaunchKernelGGL(conv_encoder_x3s_kernel, dim3(cs.G), dim3(512), X3S_LDS_BYTES, s, feats,
-                     reinterpret_cast<const EncDescX3*>(encs), cs, enc_out, status, g_x3s_spin_limit);
+  if (split)
+    hipLaunchKernelGGL(conv_encoder_x3s_kernel<true>, dim3(cs.G), dim3(512), X3S_LDS_BYTES, s, feats,
+                       reinterpret_cast<const EncDescX3*>(encs), cs, enc_out, status, g_x3s_spin_limit);
+  else  // VGE_F16 (staggered single-fp16: hi planes only, one MFMA per product)
+    hipLaunchKernelGGL(conv_encoder_x3s_kernel<false>, dim3(cs.G), dim3(512), X3S_LDS_BYTES, s, feats,
+                       reinterpret_cast<const EncDescX3*>(encs), cs, enc_out, status, g_x3s_spin_limit);
   return hipGetLastError();
 }
 

@@ -400,7 +400,7 @@ __global__ void __launch_bounds__(256, OCC) transformer_x3_kernel(TxArgsX3 ta) {
   // chunk order inside a segment rotated per workgroup (VGE_TX_ROT: the CUs of an XCD, which share its L2, then read
   // different chunks of the same segment at a time instead of all hitting one chunk's lines together)
 #ifndef VGE_TX_ROT
-#define VGE_TX_ROT 0
+#define VGE_TX_ROT 1
 #endif
   const int rot = VGE_TX_ROT ? __builtin_amdgcn_readfirstlane(((blockIdx.x >> 3) * VGE_TX_ROT) & 15) : 0;
   BFrag<2> b[TX_PF];
