@@ -200,3 +200,37 @@ def test_predictor_end_to_end_vs_oracle(run, oracle_fwd):
         ps = r["scores"][r["classes"] == 0]
         if not bool(((ps - 0.5).abs() < 0.05).any()):
             assert int(out["n_person"][f]) == gate_persons(r)
+
+
+@pytest.mark.parametrize("gw,stride,C,H,W", [(8, 1, 256, 20, 37), (16, 2, 512, 21, 18), (32, 1, 1024, 13, 11),
+                                             (64, 1, 2048, 9, 10), (32, 2, 1024, 14, 13), (64, 2, 2048, 7, 6)])
+def test_grouped_conv_kernel_vs_torch(gw, stride, C, H, W):
+    """The bottlenecks' grouped 3x3 conv (vge_gconv.hip: + folded bias, ReLU) alone vs torch conv2d(groups = C / gw)
+    in f32 on the same bf16 operands: every group width of X101-32x8d (8 .. 64 channels per group), both strides,
+    ragged tiles.  The kernel rounds its f32 sums to bf16 once."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import ctypes as C_
+    import torch.nn.functional as F
+    from vge import lib as L
+    so = L.load()
+    g = torch.Generator().manual_seed(gw * 7 + stride)
+    x = torch.randn((2, H, W, C), generator=g).to(torch.bfloat16)
+    w = (torch.randn((C, gw, 3, 3), generator=g) / (3.0 * gw ** 0.5)).float()
+    b = (0.1 * torch.randn(C, generator=g)).float()
+    Ho, Wo = (H - 1) // stride + 1, (W - 1) // stride + 1
+    xd = x.to(DEV)
+    out = torch.full((2, Ho, Wo, C), float("nan"), dtype=torch.bfloat16, device=DEV)
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream().cuda_stream
+    rc = so.vge_debug_gconv3(C_.c_void_p(xd.data_ptr()), 2, H, W, C, gw, stride, C_.c_void_p(w.data_ptr()),
+                             C_.c_void_p(b.data_ptr()), C_.c_void_p(out.data_ptr()), C_.c_void_p(st))
+    assert rc == 0, L.load().vge_last_error()
+    ref = F.conv2d(x.float().permute(0, 3, 1, 2), w.to(torch.bfloat16).float(), b, stride=stride, padding=1,
+                   groups=C // gw).relu().permute(0, 2, 3, 1)
+    got = out.float().cpu()
+    assert torch.isfinite(got).all()
+    err = (got - ref).abs()
+    bound = 2.0 ** -7 * ref.abs() + 1e-4          # one bf16 rounding of the output (+ f32 summation order)
+    print(f"gw {gw} stride {stride}: max |d| {err.max():.2e}, max |ref| {ref.abs().max():.2e}")
+    assert bool((err <= bound).all()), float((err - bound).max())

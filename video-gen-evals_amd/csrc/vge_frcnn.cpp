@@ -123,6 +123,21 @@ struct vge_frcnn {
 
 namespace {
 
+// grouped 3x3 weight [width][cg][3][3] (BN folded) -> 64-channel slices [Npad][9 * 64]: k = tap * 64 + (input channel -
+// slice base), zero outside the output channel's group; bias [Npad]
+void pack_gconv(const float* W, const float* b, int width, int cg, std::vector<uint16_t>& h, std::vector<float>& bb) {
+  const int Npad = rup(width, 256), Kp = 9 * GSLICE;
+  h.assign((size_t)Npad * Kp, 0);
+  for (int n = 0; n < width; ++n) {
+    const int g = n / cg, base = (n / GSLICE) * GSLICE;
+    for (int ci = 0; ci < cg; ++ci)
+      for (int t = 0; t < 9; ++t)
+        h[(size_t)n * Kp + (size_t)t * GSLICE + (g * cg + ci - base)] = to_bf16(W[((size_t)n * cg + ci) * 9 + t]);
+  }
+  bb.assign(Npad, 0.f);
+  memcpy(bb.data(), b, width * 4);
+}
+
 struct FLoader {
   vge_frcnn* m;
   WeightMap& wm;
@@ -163,15 +178,9 @@ struct FLoader {
     L.KH = L.KW = 3;
     L.Kp = 9 * GSLICE;
     L.Npad = rup(width, 256);
-    std::vector<uint16_t> h((size_t)L.Npad * L.Kp, 0);
-    for (int n = 0; n < width; ++n) {
-      const int g = n / cg, base = (n / GSLICE) * GSLICE;
-      for (int ci = 0; ci < cg; ++ci)
-        for (int t = 0; t < 9; ++t)
-          h[(size_t)n * L.Kp + (size_t)t * GSLICE + (g * cg + ci - base)] = to_bf16(W[((size_t)n * cg + ci) * 9 + t]);
-    }
-    std::vector<float> bb(L.Npad, 0.f);
-    memcpy(bb.data(), b.data(), width * 4);
+    std::vector<uint16_t> h;
+    std::vector<float> bb;
+    pack_gconv(W.data(), b.data(), width, cg, h, bb);
     uint16_t* dw = nullptr;
     ok = upload(m->dev, h, &dw) && upload(m->dev, bb, &L.b);
     L.w = dw;
@@ -260,6 +269,13 @@ bool cfg_ok(const vge_frcnn_config& c, std::string& why) {
 
 int gconv(vge_frcnn* m, const ConvW& L, int cg, const void* x, int n, int H, int W, int stride, void* out,
           hipStream_t s) {
+  const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
+  static const bool direct = !(getenv("VGE_FRCNN_GCONV") && getenv("VGE_FRCNN_GCONV")[0] == '0');
+  if (direct) {  // the direct grouped kernel (vge_gconv.hip); VGE_FRCNN_GCONV=0: block-diagonal implicit GEMM
+    HIPCHK(vge::launch_gconv3(x, L.Cout, L.w, L.Kp, L.b, out, L.Cout, n, H, W, L.Cout, cg, stride, s));
+    m->flops[0] += 2.0 * n * Ho * Wo * (double)L.Cout * 9 * cg;
+    return VGE_OK;
+  }
   vge::ConvLaunch c{};
   c.x = x;
   c.ldx = L.Cout;
@@ -283,7 +299,6 @@ int gconv(vge_frcnn* m, const ConvW& L, int cg, const void* x, int n, int H, int
   c.gslice = 1;
   c.variant = 1;
   HIPCHK(vge::launch_conv_bf16(c, s));
-  const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
   m->flops[0] += 2.0 * n * Ho * Wo * (double)L.Cout * 9 * cg;  // the grouped conv's own FLOPs
   return VGE_OK;
 }
@@ -617,6 +632,37 @@ int vge_frcnn_detect(vge_frcnn* m, const uint8_t* frames, int F, int H, int W, f
 #undef STAGE
 #undef RC
   m->prof.end_call(m->flops[0] + m->flops[1]);
+  return VGE_OK;
+}
+
+// Test hook: the grouped 3x3 conv alone (tests/test_frcnn.py vs torch conv2d(groups)); x / out device NHWC bf16,
+// w [C][gw][3][3] and b [C] host f32 (packed as the detector packs them); the block-diagonal implicit GEMM with
+// VGE_FRCNN_GCONV=0
+int vge_debug_gconv3(const void* x, int n, int H, int W, int C, int gw, int stride, const float* w, const float* b,
+                     void* out, vge_stream_t stream) {
+  if (!x || !w || !b || !out || n < 1 || C % GSLICE || gw < 1 || GSLICE % gw)
+    return fail(VGE_ERR_ARG, "vge_debug_gconv3: bad argument");
+  std::vector<uint16_t> h;
+  std::vector<float> bb;
+  pack_gconv(w, b, C, gw, h, bb);
+  vge_frcnn tmp;
+  ConvW L;
+  L.Cin = L.Cinp = GSLICE;
+  L.Cout = C;
+  L.KH = L.KW = 3;
+  L.Kp = 9 * GSLICE;
+  L.Npad = rup(C, 256);
+  uint16_t* dw = nullptr;
+  std::vector<uint16_t> z(128, 0);
+  uint16_t* zp = nullptr;
+  if (!upload(tmp.dev, h, &dw) || !upload(tmp.dev, bb, &L.b) || !upload(tmp.dev, z, &zp))
+    return fail(VGE_ERR_NOMEM, "vge_debug_gconv3: upload");
+  L.w = dw;
+  tmp.zero = zp;
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  const int r = gconv(&tmp, L, gw, x, n, H, W, stride, out, s);
+  if (r != VGE_OK) return r;
+  HIPCHK(hipStreamSynchronize(s));
   return VGE_OK;
 }
 

@@ -54,5 +54,8 @@ hipError_t launch_rpn_merge(const float* kept, const int* kcount, int n, int pos
 hipError_t launch_roi_align(const RoiLevels& lv, const float* props, const int* n_prop, int n, int P, void* out,
                             hipStream_t s);
 hipError_t launch_det_post(const DetPostArgs& a, int n, hipStream_t s);
+// vge_gconv.hip: the bottlenecks' grouped 3x3 conv (+ folded FrozenBN bias, ReLU), HBM-bound direct kernel
+hipError_t launch_gconv3(const void* x, long ldx, const void* w, int Kp, const float* bias, void* out, long ldo,
+                         int n_img, int H, int W, int C, int gw, int stride, hipStream_t s);
 
 }  // namespace vge
