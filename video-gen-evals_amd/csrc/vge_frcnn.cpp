@@ -271,7 +271,10 @@ int gconv(vge_frcnn* m, const ConvW& L, int cg, const void* x, int n, int H, int
           hipStream_t s) {
   const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
   static const bool direct = !(getenv("VGE_FRCNN_GCONV") && getenv("VGE_FRCNN_GCONV")[0] == '0');
-  if (direct) {  // the direct grouped kernel (vge_gconv.hip); VGE_FRCNN_GCONV=0: block-diagonal implicit GEMM
+  // the direct grouped kernel (vge_gconv.hip) for group widths below 64 channels; at 64 (res5) a 64-channel slice
+  // is one whole group, the implicit GEMM wastes nothing and is faster (92 vs 157 us per 32 frames, r05h trace);
+  // VGE_FRCNN_GCONV=0: the implicit GEMM everywhere
+  if (direct && cg < GSLICE) {
     HIPCHK(vge::launch_gconv3(x, L.Cout, L.w, L.Kp, L.b, out, L.Cout, n, H, W, L.Cout, cg, stride, s));
     m->flops[0] += 2.0 * n * Ho * Wo * (double)L.Cout * 9 * cg;
     return VGE_OK;

@@ -37,8 +37,11 @@ struct GconvArgs {
 #endif
 constexpr int GC_NI = VGE_GC_NI;  // images per workgroup: its weights (up to 72 registers) are loaded once for all of them
 
+#ifndef VGE_GC_TH
+#define VGE_GC_TH 4
+#endif
 template <int S>
-constexpr int gc_th() { return 4; }
+constexpr int gc_th() { return S == 1 ? VGE_GC_TH : 4; }
 template <int S>
 constexpr int gc_tw() { return S == 1 ? 32 : 16; }
 template <int S>
@@ -142,7 +145,7 @@ hipError_t launch_gconv3(const void* x, long ldx, const void* w, int Kp, const f
     return hipErrorInvalidValue;
   GconvArgs a{reinterpret_cast<const __bf16*>(x), ldx, reinterpret_cast<const __bf16*>(w), Kp, bias,
               reinterpret_cast<__bf16*>(out), ldo, H, W, (H + 2 - 3) / stride + 1, (W + 2 - 3) / stride + 1, 0, n_img};
-  const int th = 4, tw = stride == 1 ? 32 : 16;
+  const int th = stride == 1 ? VGE_GC_TH : 4, tw = stride == 1 ? 32 : 16;
   a.tiles_x = (a.Wo + tw - 1) / tw;
   const dim3 grid(a.tiles_x * ((a.Ho + th - 1) / th), C / 64, (n_img + GC_NI - 1) / GC_NI);
   const int ks = gw <= 16 ? 1 : gw / 16;
