@@ -318,3 +318,34 @@ def test_extractor_profile_and_flops(D):
     # the GEMM FLOPs the library counts = the model's dense work minus the GAU token mixing (not a GEMM launch)
     want = 8 * (D.rtmpose_flops(cfg) - 2.0 * cfg.keypoints ** 2 * (cfg.gau_s + cfg.gau_e))
     assert abs(fl - want) < 1e-9 * want
+
+
+@gpu
+@pytest.mark.parametrize("n,H,W,Cin,Cout,act,res", [
+    (4, 25, 25, 1024, 1024, "relu", None),   # the detector's res4 conv1 shape class (ragged last row tile)
+    (2, 50, 50, 256, 256, "none", None),
+    (3, 13, 17, 512, 512, "relu", "pre"),    # bottleneck conv3: ReLU(conv + shortcut)
+    (2, 20, 20, 64, 256, "none", "post"),    # FPN lateral + top-down sum
+])
+def test_conv_1x1_gemm_variant_matches_default(D, n, H, W, Cin, Cout, act, res):
+    """Variant 9 (a 1x1 stride-1 conv on the ViT's bf16 GEMM kernel, a tuner candidate) against the default conv
+    kernel: the same per-element MFMA order over K (32-deep stages of two 16-k steps) and the same epilogue arithmetic
+    (bias, then the bf16 residual, then the activation) -> bit-identical, including a partial last row tile."""
+    import ctypes as C
+    from vge import lib as Lb
+    lib = Lb.load()
+    lib.vge_debug_set_conv_variant.argtypes = [C.c_int]
+    x = _bf((n, H, W, Cin), seed=31).to(DEV)
+    w = _bf((Cout, Cin, 1, 1), (2.0 / Cin) ** 0.5, seed=32).to(DEV)
+    b = (torch.randn(Cout, generator=torch.Generator().manual_seed(33)) * 0.1).to(DEV)
+    r = _bf((n, H, W, Cout), seed=34).to(DEV) if res else None
+    outs = []
+    try:
+        for force in (0, 9):
+            lib.vge_debug_set_conv_variant(force)
+            outs.append(D.conv_bf16(x, w, b, stride=1, pad=0, act=act, res=r, res_pre=res == "pre"))
+            torch.cuda.synchronize()
+    finally:
+        lib.vge_debug_set_conv_variant(0)
+    assert torch.isfinite(outs[0].float()).all()
+    assert torch.equal(outs[0], outs[1]), (outs[0].float() - outs[1].float()).abs().max().item()

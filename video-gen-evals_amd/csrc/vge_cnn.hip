@@ -20,6 +20,7 @@
 //   letterbox_focus_kernel  onnxdet.preprocess (resize by r, pad 114) + YOLOX Focus space-to-depth -> 16 ch.
 #include "vge_common.h"
 #include "vge_cnn.h"
+#include "vge_gemm.h"
 
 #include <cstdlib>
 #include <algorithm>
@@ -1275,6 +1276,20 @@ static hipError_t conv_go(const ConvArgs& a, int grid, hipStream_t s, int pmode)
   }
 }
 
+// variant 9: a 1x1 stride-1 conv as the bf16 GEMM of vge_vit.hip (out = act(x W^T + b (+ bf16 residual before the
+// activation))), for the shapes that kernel takes; -1 = not applicable
+int conv_gemm_epi(const ConvLaunch& c) {
+  if (c.KH != 1 || c.KW != 1 || c.stride != 1 || c.pad != 0 || c.gslice || c.out_f32 || c.Cout % 256 ||
+      c.Cin % 64 || c.Kp != c.Cin || c.ldx % 8 || c.ldo % 4)
+    return -1;
+  if (c.res_mode == RES_NONE) return c.act == ACT_NONE ? GEMM_BF16 : c.act == ACT_RELU ? GEMM_RELU_BF16 : -1;
+  if (c.ldr % 4) return -1;
+  // (residual after a ReLU is not the same as before it; with no activation both orders agree)
+  if (c.res_mode == RES_BF16_PRE) return c.act == ACT_NONE ? GEMM_RESB_BF16 : c.act == ACT_RELU ? GEMM_RESB_RELU_BF16 : -1;
+  if (c.res_mode == RES_BF16 && c.act == ACT_NONE) return GEMM_RESB_BF16;
+  return -1;
+}
+
 hipError_t launch_conv_bf16(const ConvLaunch& c, hipStream_t s) {
   ConvArgs a;
   a.x = static_cast<const bf16*>(c.x);
@@ -1302,7 +1317,28 @@ hipError_t launch_conv_bf16(const ConvLaunch& c, hipStream_t s) {
   a.M = c.n_img * a.Ho * a.Wo;
   a.gslice = c.gslice;
   int tn = c.tn, pmode = -1;
-  const int variant = c.variant == 0 && g_conv_force > 0 && !c.gslice ? g_conv_force : c.variant;
+  int variant = c.variant == 0 && g_conv_force > 0 && !c.gslice ? g_conv_force : c.variant;
+  if (variant == 9) {  // the GEMM kernel (tuner candidate, or forced by vge_debug_set_conv_variant(9))
+    const int epi = conv_gemm_epi(c);
+    if (epi >= 0) {
+      GemmBf16 g{};
+      g.A = c.x;
+      g.lda = c.ldx;
+      g.W = c.w;
+      g.ldw = c.Kp;
+      g.out = c.out;
+      g.ldo = c.ldo;
+      g.bias = c.bias;
+      g.ldr = c.ldr;
+      g.resb = c.res;
+      g.M = a.M;
+      g.N = c.Cout;
+      g.K = c.Cin;
+      return launch_gemm_bf16(epi, g, s);
+    }
+    if (c.variant == 9) return hipErrorInvalidValue;
+    variant = 0;  // forced globally: layers the GEMM cannot take keep the default kernel
+  }
   // grouped slices run on the 128- / 256-row kernel only, with the slice width as the column tile
   if (c.gslice && (variant == 2 || variant == 3 || variant == 6 || (c.tn != 64 && c.tn != 128) || c.Cin != c.tn ||
                    c.Cout % c.tn))

@@ -204,6 +204,11 @@ inline hipError_t conv_tuned_launch(ConvTuner& t, ConvLaunch& c, const std::arra
     // 512 x 128 persistent tile: residual-free layers only, like variant 3 (conv2_go keeps residual epilogues off the
     // persistent kernels: its hand-counted vmcnt budget is reasoned for RES_NONE)
     if (c.res_mode == 0 && c.Cout > 64 && c.Cout <= 128 && c.Cout % 4 == 0) cand.push_back(6000 + 128);
+    // 1x1 stride-1 convs with a ReLU / no activation: the bf16 GEMM kernel of the ViT (vge_vit.hip), whose 256 x 256
+    // tiles and LDS-staged epilogue run these shapes ~20 % faster than the implicit GEMM (tools/gemm_vs_conv.py);
+    // VGE_CONV_GEMM=0 keeps it out
+    static const bool gemm_ok = !(getenv("VGE_CONV_GEMM") && getenv("VGE_CONV_GEMM")[0] == '0');
+    if (gemm_ok && conv_gemm_epi(c) >= 0) cand.push_back(9000 + 256);
     int pick = -1;
     float best_ms = 0.f;
     for (int v : cand) {

@@ -521,8 +521,9 @@ int vge_op_conv_bf16(const void* x, long ldx, const void* w, const float* bias, 
                      int pad, int Cout, int act, int out_f32, int res_mode, vge_stream_t stream) {
   static void* zero = nullptr;
   if (!x || !w || !bias || !out || n_img <= 0 || H <= 0 || W <= 0 || !pow2(Cin) || Cin < 8 || KH <= 0 || KW <= 0 ||
-      KW > 16 || stride <= 0 || pad < 0 || Cout <= 0 || act < 0 || act > 2 || out_f32 < 0 || out_f32 > 1 ||
-      res_mode < 0 || res_mode > 2 || (res_mode == 1 && (act != 1 || out_f32)) || (res_mode == 2 && (act || out_f32)) ||
+      KW > 16 || stride <= 0 || pad < 0 || Cout <= 0 || act < 0 || act > 3 || out_f32 < 0 || out_f32 > 1 ||
+      res_mode < 0 || res_mode > 3 || (res_mode == 1 && ((act != 1 && act != 0) || out_f32)) || (res_mode == 2 && (act || out_f32)) ||
+      (res_mode == 3 && ((act != 0 && act != 3) || out_f32)) || (act == 3 && out_f32) ||
       (act == 2 && !out_f32) || ldx < Cin || ldx % 8 || ldo < Cout || (!out_f32 && (Cout % 8 || ldo % 8)) ||
       (res_mode && (!res || ldr < Cout)) || (res_mode == 2 && !rscale))
     return fail(VGE_ERR_ARG, "vge_op_conv_bf16: unsupported shape / arguments");

@@ -9,21 +9,12 @@
 #include <vector>
 
 #include "../../include/vge_hmr.h"
+#include "vge_gemm.h"
 
 namespace vge {
 void set_last_error(const std::string& msg);  // vge_api.cpp (vge_last_error)
-struct GemmBf16 {
-  const void* A; long lda;
-  const void* W; long ldw;
-  void* out; long ldo;
-  const float* bias;
-  const float* res; long ldr;
-  const float* pos; int tokens;
-  int M, N, K;
-};
 hipError_t vit_kernels_setup();
 hipError_t launch_hmr_crop(const uint8_t*, int, int, const float*, const int*, int, uint8_t*, hipStream_t);
-hipError_t launch_gemm_bf16(int, const GemmBf16&, hipStream_t);
 hipError_t launch_ln_bf16(const float*, long, void*, long, const float*, const float*, int, int, float, hipStream_t);
 hipError_t launch_cast_bf16(const float*, long, void*, long, int, int, hipStream_t);
 hipError_t launch_bcast_rows(const float*, float*, int, int, hipStream_t);

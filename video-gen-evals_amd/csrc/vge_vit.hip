@@ -20,6 +20,7 @@
 //   xattn1_kernel          the decoder's one-query cross-attention over the 192 context tokens.
 //   softmax_rows_kernel, readout_kernel (6D -> rotation matrix, mean-pose residuals), small helpers.
 #include "vge_common.h"
+#include "vge_gemm.h"
 #include <cstdlib>
 
 #ifndef VGE_GABL
@@ -43,7 +44,10 @@ constexpr int GB_M = 256, GB_N = 256, GB_K = 32, GB_ST = 5, GB_GM = 8;
 constexpr int GB_TILE = GB_M * GB_K * 2;      // 16 KB per operand per stage
 constexpr int GB_LDS = GB_ST * 2 * GB_TILE;   // 160 KB
 
-enum GemmEpi { GE_BF16 = 0, GE_GELU_BF16 = 1, GE_RES_F32 = 2, GE_PE_F32 = 3, GE_F32 = 4 };
+enum GemmEpi {  // = vge::GemmEpiPublic (vge_gemm.h)
+  GE_BF16 = 0, GE_GELU_BF16 = 1, GE_RES_F32 = 2, GE_PE_F32 = 3, GE_F32 = 4,
+  GE_RELU_BF16 = 5, GE_RESB_BF16 = 6, GE_RESB_RELU_BF16 = 7  // the 1x1 conv epilogues (bias, bf16 residual, ReLU)
+};
 
 struct GemmBf16Args {
   const bf16* A;     // [M][lda]   rows of the activation
@@ -54,21 +58,23 @@ struct GemmBf16Args {
   const float* pos;  // GE_PE_F32: pos_embed [tokens + 1][N]
   long lda, ldw, ldo, ldr;
   int M, N, K, tokens;
+  const bf16* resb;  // GE_RESB_*: bf16 residual [M][ldr]
 };
 
 // Stage a 256-row x 32-k operand tile (64-B rows) with NW waves: wave-instruction q (0..15) fills LDS bytes
 // [1024 q, 1024 q + 1024) = rows 16q .. 16q+15, lane L -> row 16q + L/4, physical 16-B chunk L%4.  Physical chunk
 // p of row r holds logical chunk p ^ ((r >> 2) & 3): the source address is pre-swizzled, the LDS image stays
 // lane-linear (global_load_lds), and the 16 rows a ds_read_b128 lane group reads land on 16 distinct 16-B slots.
-template <int NW>
+// rmax: the last valid row (rows past it re-read it: a partial last row tile of A)
+template <int NW, bool CLAMP>
 __device__ __forceinline__ void gb_stage(const bf16* __restrict__ X, long ld, int r0, int k0, char* tile, int wave,
-                                         int lane) {
+                                         int lane, int rmax) {
 #pragma unroll
   for (int j = 0; j < 16 / NW; ++j) {
     const int q = wave * (16 / NW) + j;
     const int row = 16 * q + (lane >> 2);
     const int ch = (lane & 3) ^ ((row >> 2) & 3);
-    glds16(X + (size_t)(r0 + row) * ld + k0 + ch * 8, tile + q * 1024);
+    glds16(X + (size_t)(CLAMP ? min(r0 + row, rmax) : r0 + row) * ld + k0 + ch * 8, tile + q * 1024);
   }
 }
 
@@ -82,7 +88,9 @@ __device__ __forceinline__ int gb_xcd_remap(int b, int nblk) {  // bijective: ea
 // SH = 1 (NW = 8 only): the same wave tile on v_mfma_f32_16x16x32_bf16 (8 x 4 tiles of 16 x 16, one MFMA per 32-k
 // stage and tile) -- same LDS fragment bytes and MFMA cycles per stage; the chip holds a higher clock on this shape
 // (MI355X_MICROARCH.md, DVFS give-back item 7).
-template <int EPI, int NW, int SH = 0>
+// PM: M is not a multiple of 256 (the last row tile's A loads clamp to row M - 1 and its stores stop at M); the ViT's
+// GEMMs (M = frames x 192) take the PM = false code unchanged
+template <int EPI, int NW, int SH = 0, bool PM = false>
 __global__ void __launch_bounds__(64 * NW, 1) gemm_bf16_kernel(GemmBf16Args g) {
   static_assert(SH == 0 || NW == 8, "16x16x32 variant: 8 waves");
   constexpr int TN = NW == 8 ? 2 : 4;  // 32-column tiles per wave
@@ -94,7 +102,7 @@ __global__ void __launch_bounds__(64 * NW, 1) gemm_bf16_kernel(GemmBf16Args g) {
   // tile order: each XCD takes a contiguous range of ids (gb_xcd_remap); inside it, groups of GB_GM row panels
   // walk the column panels with the row panel fastest, so the ~32 blocks an XCD runs at once cover ~8 A panels x
   // ~4 W panels and read the same K slices at about the same time (L2 hits instead of fabric re-fetches)
-  const int ntn = g.N / GB_N, mtn = g.M / GB_M;
+  const int ntn = g.N / GB_N, mtn = (g.M + GB_M - 1) / GB_M;
   const int bid = gb_xcd_remap(blockIdx.x, gridDim.x);
   const int grp = bid / (GB_GM * ntn), rem = bid % (GB_GM * ntn);
   const int gm = min(GB_GM, mtn - grp * GB_GM);
@@ -123,8 +131,8 @@ __global__ void __launch_bounds__(64 * NW, 1) gemm_bf16_kernel(GemmBf16Args g) {
 
   auto issue = [&](int st) {
     char* slot = lds + (st % GB_ST) * 2 * GB_TILE;
-    gb_stage<NW>(g.A, g.lda, m0, st * GB_K, slot, wave, lane);
-    gb_stage<NW>(g.W, g.ldw, n0, st * GB_K, slot + GB_TILE, wave, lane);
+    gb_stage<NW, PM>(g.A, g.lda, m0, st * GB_K, slot, wave, lane, g.M - 1);
+    gb_stage<NW, false>(g.W, g.ldw, n0, st * GB_K, slot + GB_TILE, wave, lane, g.N - 1);
   };
   struct Frag {
     bf16x8 a[2][4], b[2][TN];  // SH = 0: [16-k step][32-row / 32-column tile]; SH = 1: a = 8 16-row tiles, b = 4
@@ -230,12 +238,17 @@ __global__ void __launch_bounds__(64 * NW, 1) gemm_bf16_kernel(GemmBf16Args g) {
   // before that half's LDS round trip, and the next half's while this one is written, so the epilogue pays about one
   // memory latency instead of one per 4-iteration batch
   constexpr int NIT = 64 / RPI;                          // row-major iterations per half
-  constexpr bool LD = EPI == GE_RES_F32 || EPI == GE_PE_F32;
+  constexpr bool RB = EPI == GE_RESB_BF16 || EPI == GE_RESB_RELU_BF16;
+  constexpr bool LD = EPI == GE_RES_F32 || EPI == GE_PE_F32 || RB;
   constexpr int NPF = LD ? (NIT > 16 ? 16 : NIT) : 1;    // loads kept in flight (NW = 4: 16 of 32 per half)
   auto grow_of = [&](int half, int it) { return m0 + wm * 128 + half * 64 + it * RPI + lr; };
   auto rowload = [&](int half, int it) -> floatx4 {
-    const int grow = grow_of(half, it);
+    const int grow = PM ? min(grow_of(half, it), g.M - 1) : grow_of(half, it);  // (PM: rows past M are not stored)
     if constexpr (EPI == GE_RES_F32) return *reinterpret_cast<const floatx4*>(g.res + (grow * (int)g.ldr + gcol));
+    if constexpr (RB) {
+      const bf16x4 r = *reinterpret_cast<const bf16x4*>(g.resb + ((long)grow * g.ldr + gcol));
+      return floatx4{(float)r[0], (float)r[1], (float)r[2], (float)r[3]};
+    }
     if constexpr (EPI == GE_PE_F32)  // tokens per frame = 192 (checked by the host)
       return *reinterpret_cast<const floatx4*>(g.pos + ((1 + grow - (grow / 192) * 192) * g.N + gcol));
     return floatx4{0.f, 0.f, 0.f, 0.f};
@@ -270,7 +283,17 @@ __global__ void __launch_bounds__(64 * NW, 1) gemm_bf16_kernel(GemmBf16Args g) {
       const int grow = grow_of(half, it);
       floatx4 v = *reinterpret_cast<const floatx4*>(my + rl * WC + c4) + bb;
       const int o = grow * (int)g.ldo + gcol;
-      if constexpr (EPI == GE_BF16 || EPI == GE_GELU_BF16) {
+      if constexpr (RB || EPI == GE_RELU_BF16) {  // the 1x1 conv epilogues: bias (+ bf16 residual) (+ ReLU) -> bf16
+        if constexpr (RB) {
+          v += (it < NPF) ? rr[it % NPF] : rowload(half, it);
+          if (it < NPF && half == 0) rr[it % NPF] = rowload(1, it);
+        }
+        if constexpr (EPI == GE_RELU_BF16 || EPI == GE_RESB_RELU_BF16)
+          v = floatx4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
+        bf16x4 ob;
+        ob[0] = (bf16)v.x; ob[1] = (bf16)v.y; ob[2] = (bf16)v.z; ob[3] = (bf16)v.w;
+        if (!PM || grow < g.M) *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(g.out) + o) = ob;
+      } else if constexpr (EPI == GE_BF16 || EPI == GE_GELU_BF16) {
         if constexpr (EPI == GE_GELU_BF16) {  // exact-erf GELU: the one-exp2 form (|error| < 4.8e-7) flips enough
           floatx2 y[2] = {{v.x, v.y}, {v.z, v.w}};  // bf16 roundings to move TokenHMR's global_orient past the e2e
           gelu2_many(y);                              // chain's 1.5e-2 bound vs the bf16-point oracle (1.68e-2, r04 box)
@@ -278,10 +301,10 @@ __global__ void __launch_bounds__(64 * NW, 1) gemm_bf16_kernel(GemmBf16Args g) {
         }
         bf16x4 ob;
         ob[0] = (bf16)v.x; ob[1] = (bf16)v.y; ob[2] = (bf16)v.z; ob[3] = (bf16)v.w;
-        *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(g.out) + o) = ob;
+        if (!PM || grow < g.M) *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(g.out) + o) = ob;
       } else {
         v += (it < NPF) ? rr[it % NPF] : rowload(half, it);
-        *reinterpret_cast<floatx4*>(reinterpret_cast<float*>(g.out) + o) = v;
+        if (!PM || grow < g.M) *reinterpret_cast<floatx4*>(reinterpret_cast<float*>(g.out) + o) = v;
         if (it < NPF && half == 0) rr[it % NPF] = rowload(1, it);  // the next half's, in the freed register
       }
     }
@@ -615,21 +638,32 @@ __global__ void copy_rows_kernel(const float* __restrict__ x, long ldx, float* _
 // ================================================================================== host launchers
 namespace vge {
 
-struct GemmBf16 {
-  const void* A; long lda;
-  const void* W; long ldw;
-  void* out; long ldo;
-  const float* bias;
-  const float* res; long ldr;
-  const float* pos; int tokens;
-  int M, N, K;
-};
+static_assert((int)GE_RESB_RELU_BF16 == (int)GEMM_RESB_RELU_BF16 && (int)GE_RELU_BF16 == (int)GEMM_RELU_BF16,
+              "epilogue ids (vge_gemm.h)");
 
 template <int NW, int SH = 0>
 hipError_t gemm_setup_nw() {
-  const void* ks[5] = {(const void*)gemm_bf16_kernel<GE_BF16, NW, SH>, (const void*)gemm_bf16_kernel<GE_GELU_BF16, NW, SH>,
+  const void* ks[8] = {(const void*)gemm_bf16_kernel<GE_BF16, NW, SH>, (const void*)gemm_bf16_kernel<GE_GELU_BF16, NW, SH>,
                        (const void*)gemm_bf16_kernel<GE_RES_F32, NW, SH>, (const void*)gemm_bf16_kernel<GE_PE_F32, NW, SH>,
-                       (const void*)gemm_bf16_kernel<GE_F32, NW, SH>};
+                       (const void*)gemm_bf16_kernel<GE_F32, NW, SH>, (const void*)gemm_bf16_kernel<GE_RELU_BF16, NW, SH>,
+                       (const void*)gemm_bf16_kernel<GE_RESB_BF16, NW, SH>,
+                       (const void*)gemm_bf16_kernel<GE_RESB_RELU_BF16, NW, SH>};
+  for (auto k : ks) {
+    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, GB_LDS);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+hipError_t gemm_setup_pm() {  // the partial-M kernels (8 waves, 32x32x16): 1x1 convs over n x H x W rows
+  const void* ks[8] = {(const void*)gemm_bf16_kernel<GE_BF16, 8, 0, true>,
+                       (const void*)gemm_bf16_kernel<GE_GELU_BF16, 8, 0, true>,
+                       (const void*)gemm_bf16_kernel<GE_RES_F32, 8, 0, true>,
+                       (const void*)gemm_bf16_kernel<GE_PE_F32, 8, 0, true>,
+                       (const void*)gemm_bf16_kernel<GE_F32, 8, 0, true>,
+                       (const void*)gemm_bf16_kernel<GE_RELU_BF16, 8, 0, true>,
+                       (const void*)gemm_bf16_kernel<GE_RESB_BF16, 8, 0, true>,
+                       (const void*)gemm_bf16_kernel<GE_RESB_RELU_BF16, 8, 0, true>};
   for (auto k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, GB_LDS);
     if (e != hipSuccess) return e;
@@ -639,6 +673,7 @@ hipError_t gemm_setup_nw() {
 
 hipError_t vit_kernels_setup() {
   hipError_t e = gemm_setup_nw<8>();
+  if (e == hipSuccess) e = gemm_setup_pm();
   if (e == hipSuccess) e = gemm_setup_nw<4>();
   if (e == hipSuccess) e = gemm_setup_nw<8, 1>();
   if (e != hipSuccess) return e;
@@ -651,19 +686,24 @@ hipError_t vit_kernels_setup() {
 
 static int g_gemm_waves = 0;  // 8, 4 or 16 (= 8 waves on 16x16x32) (VGE_GEMM_WAVES), chosen once
 
-template <int NW, int SH = 0>
+template <int NW, int SH = 0, bool PM = false>
 void launch_gemm_nw(int epi, dim3 grid, const GemmBf16Args& g, hipStream_t s) {
   const dim3 blk(64 * NW);
   switch (epi) {
-    case GE_BF16: hipLaunchKernelGGL((gemm_bf16_kernel<GE_BF16, NW, SH>), grid, blk, GB_LDS, s, g); break;
-    case GE_GELU_BF16: hipLaunchKernelGGL((gemm_bf16_kernel<GE_GELU_BF16, NW, SH>), grid, blk, GB_LDS, s, g); break;
-    case GE_RES_F32: hipLaunchKernelGGL((gemm_bf16_kernel<GE_RES_F32, NW, SH>), grid, blk, GB_LDS, s, g); break;
-    case GE_PE_F32: hipLaunchKernelGGL((gemm_bf16_kernel<GE_PE_F32, NW, SH>), grid, blk, GB_LDS, s, g); break;
-    default: hipLaunchKernelGGL((gemm_bf16_kernel<GE_F32, NW, SH>), grid, blk, GB_LDS, s, g); break;
+    case GE_BF16: hipLaunchKernelGGL((gemm_bf16_kernel<GE_BF16, NW, SH, PM>), grid, blk, GB_LDS, s, g); break;
+    case GE_GELU_BF16: hipLaunchKernelGGL((gemm_bf16_kernel<GE_GELU_BF16, NW, SH, PM>), grid, blk, GB_LDS, s, g); break;
+    case GE_RES_F32: hipLaunchKernelGGL((gemm_bf16_kernel<GE_RES_F32, NW, SH, PM>), grid, blk, GB_LDS, s, g); break;
+    case GE_PE_F32: hipLaunchKernelGGL((gemm_bf16_kernel<GE_PE_F32, NW, SH, PM>), grid, blk, GB_LDS, s, g); break;
+    case GE_RELU_BF16: hipLaunchKernelGGL((gemm_bf16_kernel<GE_RELU_BF16, NW, SH, PM>), grid, blk, GB_LDS, s, g); break;
+    case GE_RESB_BF16: hipLaunchKernelGGL((gemm_bf16_kernel<GE_RESB_BF16, NW, SH, PM>), grid, blk, GB_LDS, s, g); break;
+    case GE_RESB_RELU_BF16:
+      hipLaunchKernelGGL((gemm_bf16_kernel<GE_RESB_RELU_BF16, NW, SH, PM>), grid, blk, GB_LDS, s, g);
+      break;
+    default: hipLaunchKernelGGL((gemm_bf16_kernel<GE_F32, NW, SH, PM>), grid, blk, GB_LDS, s, g); break;
   }
 }
 
-// shapes are validated by the caller (vge_hmr.cpp): M % 256 == N % 256 == K % 64 == 0, 16-B aligned rows
+// shapes are validated by the callers (vge_hmr.cpp, vge_cnn.hip): N % 256 == K % 64 == 0, 16-B aligned rows; any M
 hipError_t launch_gemm_bf16(int epi, const GemmBf16& a, hipStream_t s) {
   GemmBf16Args g;
   g.A = reinterpret_cast<const bf16*>(a.A);
@@ -674,14 +714,19 @@ hipError_t launch_gemm_bf16(int epi, const GemmBf16& a, hipStream_t s) {
   g.pos = a.pos;
   g.lda = a.lda; g.ldw = a.ldw; g.ldo = a.ldo; g.ldr = a.ldr;
   g.M = a.M; g.N = a.N; g.K = a.K; g.tokens = a.tokens;
-  if ((long)a.M * a.ldo >= (1L << 31) || (a.res && (long)a.M * a.ldr >= (1L << 31)) || (epi == GE_PE_F32 && a.tokens != AT_T))
+  g.resb = reinterpret_cast<const bf16*>(a.resb);
+  const bool rb = epi == GE_RESB_BF16 || epi == GE_RESB_RELU_BF16;
+  if (a.M < 1 || a.N % GB_N || a.K % 64 || (long)a.M * a.ldo >= (1L << 31) ||
+      ((a.res || rb) && (long)a.M * a.ldr >= (1L << 31)) || (rb && !a.resb) || (epi == GE_PE_F32 && a.tokens != AT_T))
     return hipErrorInvalidValue;
   if (g_gemm_waves == 0) {
     const char* e = getenv("VGE_GEMM_WAVES");
     g_gemm_waves = (e && (atoi(e) == 4 || atoi(e) == 16)) ? atoi(e) : 8;
   }
-  const dim3 grid((a.M / GB_M) * (a.N / GB_N));
-  if (g_gemm_waves == 4)
+  const dim3 grid(((a.M + GB_M - 1) / GB_M) * (a.N / GB_N));
+  if (a.M % GB_M)
+    launch_gemm_nw<8, 0, true>(epi, grid, g, s);
+  else if (g_gemm_waves == 4)
     launch_gemm_nw<4>(epi, grid, g, s);
   else if (g_gemm_waves == 16)
     launch_gemm_nw<8, 1>(epi, grid, g, s);

@@ -371,8 +371,9 @@ def pack_conv_weight(w: torch.Tensor) -> torch.Tensor:
 
 def conv_bf16(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, stride: int = 1, pad: int = 0, act: str = "silu",
               out_f32: bool = False, res: Optional[torch.Tensor] = None, rscale: Optional[torch.Tensor] = None,
-              out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """x: bf16 NHWC [n, H, W, Cin] (contiguous); w: f32/bf16 [Cout, Cin, KH, KW] -> NHWC [n, Ho, Wo, Cout]."""
+              out: Optional[torch.Tensor] = None, res_pre: bool = False) -> torch.Tensor:
+    """x: bf16 NHWC [n, H, W, Cin] (contiguous); w: f32/bf16 [Cout, Cin, KH, KW] -> NHWC [n, Ho, Wo, Cout].
+    act: none / silu / sigmoid / relu; res: bf16 added after the activation (res_pre: before it) or f32 x rscale."""
     lib = _sig(L.load())
     n, H, W, Cin = x.shape
     Cout, _, KH, KW = w.shape
@@ -382,12 +383,12 @@ def conv_bf16(x: torch.Tensor, w: torch.Tensor, bias: torch.Tensor, stride: int 
     bp[:Cout] = bias
     if out is None:
         out = torch.empty((n, Ho, Wo, Cout), dtype=torch.float32 if out_f32 else torch.bfloat16, device=x.device)
-    mode = 0 if res is None else (1 if res.dtype == torch.bfloat16 else 2)
+    mode = 0 if res is None else ((3 if res_pre else 1) if res.dtype == torch.bfloat16 else 2)
     rs = None
     if mode == 2:
         rs = torch.zeros(wp.shape[0], dtype=torch.float32, device=x.device)
         rs[:Cout] = rscale
-    actc = {"none": 0, "silu": 1, "sigmoid": 2}[act]
+    actc = {"none": 0, "silu": 1, "sigmoid": 2, "relu": 3}[act]
     L.check(lib.vge_op_conv_bf16(_ptr(x), Cin, _ptr(wp), _ptr(bp), _ptr(out), Cout, _ptr(res) if res is not None else None,
                                  Cout if res is not None else 0, _ptr(rs) if rs is not None else None, n, H, W, Cin, KH, KW,
                                  stride, pad, Cout, actc, int(out_f32), mode, _stream(x.device)), "vge_op_conv_bf16")
