@@ -35,7 +35,7 @@ E2E_KERNEL_SOURCES = {"gemm_bf16_kernel": ["vge_vit.hip"],
                       "yolox_conv": ["vge_cnn.hip", "vge_cnn_host.h", "vge_yolox.cpp"],
                       "frcnn_conv": ["vge_cnn.hip", "vge_cnn_host.h", "vge_frcnn.cpp"]}
 YOLOX_CHUNK = 256   # frames per detector pass (tools/yolox_prof.py --chunk: 637 vs 618 TFLOP/s at 64)
-FRCNN_CHUNK = 32    # frames per Faster R-CNN workspace chunk (~0.3 GB per 800 x 800 frame)
+FRCNN_CHUNK = 64    # frames per Faster R-CNN workspace chunk (~0.3 GB per 800 x 800 frame; 64: -6 % vs 32, profiles/ab_r05m_*)
 
 
 def e2e_traffic(kernel: str, frames: float):

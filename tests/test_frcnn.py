@@ -234,3 +234,17 @@ def test_grouped_conv_kernel_vs_torch(gw, stride, C, H, W):
     bound = 2.0 ** -7 * ref.abs() + 1e-4          # one bf16 rounding of the output (+ f32 summation order)
     print(f"gw {gw} stride {stride}: max |d| {err.max():.2e}, max |ref| {ref.abs().max():.2e}")
     assert bool((err <= bound).all()), float((err - bound).max())
+
+
+def test_chunk_is_capped_by_32bit_row_offsets(run):
+    """The conv kernels address a layer's rows through 32-bit byte offsets: vge_frcnn_reserve refuses a chunk whose
+    largest activation reaches 2 GiB (at 800 px: 104 frames) and FrcnnDetector caps its chunk there."""
+    from vge.frcnn import FrcnnDetector
+    det = FrcnnDetector(run["sd"], run["cfg"], device=DEV, chunk=1000)
+    try:
+        cap = det.max_chunk(256, 256)
+        assert det.chunk == cap == 104, (det.chunk, cap)
+        assert det.lib.vge_frcnn_reserve(det.h, cap + 1, 256, 256) == 1      # VGE_ERR_ARG
+        assert det.lib.vge_frcnn_reserve(det.h, cap, 256, 256) == 0
+    finally:
+        det.close()

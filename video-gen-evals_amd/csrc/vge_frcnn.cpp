@@ -358,6 +358,15 @@ int vge_frcnn_reserve(vge_frcnn* m, int chunk, int H, int W) {
   if (chunk <= m->chunk && H == m->rH && W == m->rW) return VGE_OK;
   int sh[15];
   vge_frcnn_shapes(m, H, W, sh);
+  {  // the conv kernels address a layer's input / output rows through 32-bit byte offsets: the largest activation of
+     // a chunk (the stem output, res2's, P2's) must stay under 2 GiB
+    const size_t s2 = (size_t)(sh[2] / 2) * (sh[3] / 2), s4 = (size_t)sh[4] * sh[5];
+    const size_t per = std::max({(size_t)sh[2] * sh[3] * 8, s2 * m->c.stem_ch,
+                                 s4 * std::max({m->c.res2_ch, m->c.groups * m->c.width_per_group, m->c.fpn_ch})}) * 2;
+    if ((size_t)chunk * per >= (1ull << 31))
+      return fail(VGE_ERR_ARG, "vge_frcnn_reserve: chunk too large for " + std::to_string(H) + " x " + std::to_string(W) +
+                                   " frames (at most " + std::to_string(((1ull << 31) - 1) / per) + ")");
+  }
   (void)hipDeviceSynchronize();  // the previous workspace (if any) is released only after its kernels completed
   m->ws.reset();
   m->ws = std::make_unique<DevAllocs>();

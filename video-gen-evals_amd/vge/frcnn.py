@@ -131,10 +131,12 @@ def _flops(cfg: FrcnnConfig, hp: int, wp: int) -> Tuple[float, float]:
 
 class FrcnnDetector:
     """detectron2 DefaultPredictor(faster_rcnn_X_101_32x8d_FPN_3x) resident in HBM: FrozenBN-folded bf16 NHWC
-    weights + a chunk workspace."""
+    weights + a chunk workspace.  chunk: frames per workspace pass (larger chunks fill the GPU better: 256 frames of
+    256 x 256 take 260 / 252 / 244 ms at chunks of 32 / 32 / 64 on one box); capped by the conv kernels' 32-bit row
+    offsets (`max_chunk`: 104 frames at detectron2's 800-pixel size)."""
 
     def __init__(self, state_dict: Dict[str, np.ndarray], cfg: FrcnnConfig = FRCNN_X101, device="cuda",
-                 chunk: int = 16, frame_hw: Tuple[int, int] = (256, 256)):
+                 chunk: int = 64, frame_hw: Tuple[int, int] = (256, 256)):
         from .dwpose import _views
         self.lib = _sig(L.load())
         self.cfg = cfg
@@ -146,9 +148,20 @@ class FrcnnDetector:
             L.check(self.lib.vge_frcnn_create(C.byref(cc), arr, n, C.byref(h)), "vge_frcnn_create")
             del keep
             self.h = h
-            self.chunk = int(chunk)
+            self.chunk_req = int(chunk)
+            self.chunk = min(self.chunk_req, self.max_chunk(*frame_hw))
             L.check(self.lib.vge_frcnn_reserve(self.h, self.chunk, int(frame_hw[0]), int(frame_hw[1])),
                     "vge_frcnn_reserve")
+            self.frame_hw = (int(frame_hw[0]), int(frame_hw[1]))
+
+    def max_chunk(self, H: int, W: int) -> int:
+        """The largest chunk vge_frcnn_reserve accepts for H x W frames (every activation of a chunk under 2 GiB)."""
+        sh = self.shapes(H, W)
+        (hp, wp), (h4, w4) = sh["padded"], sh["levels"][0]
+        c = self.cfg
+        per = max(hp * wp * 8, (hp // 2) * (wp // 2) * c.stem_ch,
+                  h4 * w4 * max(c.res2_ch, c.groups * c.width_per_group, c.fpn_ch)) * 2
+        return max(1, ((1 << 31) - 1) // per)
 
     def shapes(self, H: int, W: int) -> Dict[str, object]:
         out = (C.c_int * 15)()
@@ -195,6 +208,11 @@ class FrcnnDetector:
         if frames.dtype != torch.uint8 or frames.dim() != 4 or frames.shape[3] != 3 or not frames.is_contiguous():
             raise L.VgeError("frames must be contiguous uint8 [F,H,W,3]")
         F_, H_, W_ = (int(v) for v in frames.shape[:3])
+        if (H_, W_) != self.frame_hw:  # a new frame size: the workspace is rebuilt at a chunk that fits it
+            self.chunk = min(self.chunk_req, self.max_chunk(H_, W_))
+            with torch.cuda.device(self.device):
+                L.check(self.lib.vge_frcnn_reserve(self.h, self.chunk, H_, W_), "vge_frcnn_reserve")
+            self.frame_hw = (H_, W_)
         dev = frames.device
         out = {"dets": torch.zeros((F_, self.cfg.det_per_img, 6), dtype=torch.float32, device=dev),
                "n_dets": torch.empty((F_,), dtype=torch.int32, device=dev),
