@@ -302,8 +302,6 @@ __device__ __forceinline__ void featurize_vit(const float* __restrict__ vit, int
 // bytes taking as long as the vit part).
 constexpr int SLOTS = 33;
 constexpr int ROT_W = 9 + 207 + 10;  // a slot's global_orient | body_pose | betas
-constexpr int ROT_LOADS = (SLOTS * ROT_W + 255) / 256;
-constexpr int KP_LOADS = (SLOTS * 120 + 255) / 256;
 __device__ __forceinline__ int slot_frame(int mode, int start, int L, int slot) {
   const RowSrc r = row_src(mode, start, L, slot == 0 ? 0 : slot - 1);
   return slot == 0 ? r.prv : r.src;
@@ -315,7 +313,8 @@ __global__ void __launch_bounds__(256) featurize_tiles_kernel(
     const TileDesc* __restrict__ tiles, const int* __restrict__ windows, const float* __restrict__ mean,
     const float* __restrict__ stdv, float* __restrict__ feats, int ld, int dsh) {
   // ld: feats row width (2596, or 2356 keypoint-less); dsh: how far the diff columns sit before the 2596 layout's
-  __shared__ float stage[SLOTS * ROT_W];  // rotation workgroups: [slot][226]; keypoint workgroups: raw [slot][120]
+  // LDS for the keypoint workgroups only (16.4 KB: a featurise workgroup then fits beside a transformer workgroup's
+  // 139 KB on a CU, so the side-stream featurise does not hold back the transformer's workgroups)
   __shared__ float pn[SLOTS][120];        // normalised keypoints of every slot
   __shared__ float kR[32][4];             // per row: H = X_{t-1}^T X_t, then the Procrustes rotation R (row-major)
   TileDesc td;
@@ -343,41 +342,36 @@ __global__ void __launch_bounds__(256) featurize_tiles_kernel(
 #if defined(VGE_ABL) && (VGE_ABL & 1024)
   return;  // timing ablation: vit part only
 #endif
-  if (blockIdx.y == 1) {  // rotations + betas
-    const int nslot = mcount + 1;
-    {
-      float v[ROT_LOADS];
+  if (blockIdx.y == 1) {  // rotations + betas, straight from global memory: every load of a thread issued at once
+    // ---- (b) rotations: raw flattened rotmats + SO(3) log-map deltas (utils.py:165-174); 32 rows x 24 joints = 3
+    // items per thread, each R_t and R_{t-1} (the previous row's frame, or the window's previous frame for row 0)
+    constexpr int RI = 32 * 24 / 256;
+    float Rl[RI][9], Rpl[RI][9];
 #pragma unroll
-      for (int k = 0; k < ROT_LOADS; ++k) {
-        const int it = tid + 256 * k;
-        const int sl = it / ROT_W, c = it - sl * ROT_W;
-        v[k] = 0.f;
-        if (sl < nslot) {
-          const size_t f = (size_t)(foff + slot_frame(mode, td.mesh_start, L, sl));
-          v[k] = c < 9 ? gori[f * 9 + c] : (c < 216 ? pose[f * 207 + (c - 9)] : betas[f * 10 + (c - 216)]);
-        }
+    for (int k = 0; k < RI; ++k) {
+      const int it = tid + 256 * k, t = it / 24, j = it % 24;
+      const bool ok = t < mcount;
+      const size_t f = (size_t)(foff + slot_frame(mode, td.mesh_start, L, ok ? t + 1 : 0));
+      const size_t fp = (size_t)(foff + slot_frame(mode, td.mesh_start, L, ok ? t : 0));
+      const float* src = j == 0 ? gori + f * 9 : pose + f * 207 + (j - 1) * 9;
+      const float* srcp = j == 0 ? gori + fp * 9 : pose + fp * 207 + (j - 1) * 9;
+#pragma unroll
+      for (int i = 0; i < 9; ++i) {
+        Rl[k][i] = ok ? src[i] : 0.f;
+        Rpl[k][i] = ok ? srcp[i] : 0.f;
       }
-#pragma unroll
-      for (int k = 0; k < ROT_LOADS; ++k)
-        if (tid + 256 * k < SLOTS * ROT_W) stage[tid + 256 * k] = v[k];
     }
-    __syncthreads();
-    // ---- (b) rotations: raw flattened rotmats + SO(3) log-map deltas (utils.py:165-174)
-    for (int it = tid; it < 32 * 24; it += 256) {
-      const int t = it / 24, j = it % 24;
-      if (t >= mcount) continue;
-      const float* R = stage + (t + 1) * ROT_W + j * 9;   // (global_orient is slot column 0, joint j - 1 at 9 j)
-      const float* Rp = stage + t * ROT_W + j * 9;
-      float Rl[9], Rpl[9];
 #pragma unroll
-      for (int i = 0; i < 9; ++i) { Rl[i] = R[i]; Rpl[i] = Rp[i]; }
+    for (int k = 0; k < RI; ++k) {
+      const int it = tid + 256 * k, t = it / 24, j = it % 24;
+      if (t >= mcount) continue;
       float w[3];
-      rot_delta(Rpl, Rl, w);
+      rot_delta(Rpl[k], Rl[k], w);
       float* orow = out + (size_t)t * ld;
       int craw = (j == 0) ? C_GORI_RAW : C_POSE_RAW + (j - 1) * 9;
       int cdif = ((j == 0) ? C_GORI_DIFF : C_POSE_DIFF + (j - 1) * 3) - dsh;
 #pragma unroll
-      for (int i = 0; i < 9; ++i) orow[craw + i] = znorm(Rl[i], mean, stdv, craw + i);
+      for (int i = 0; i < 9; ++i) orow[craw + i] = znorm(Rl[k][i], mean, stdv, craw + i);
 #pragma unroll
       for (int i = 0; i < 3; ++i) orow[cdif + i] = znorm(w[i], mean, stdv, cdif + i);
     }
@@ -386,8 +380,8 @@ __global__ void __launch_bounds__(256) featurize_tiles_kernel(
     for (int it = tid; it < 32 * 10; it += 256) {
       const int t = it / 10, i = it % 10;
       if (t >= mcount) continue;
-      const float b = stage[(t + 1) * ROT_W + 216 + i];
-      const float bp = stage[t * ROT_W + 216 + i];
+      const float b = betas[(size_t)(foff + slot_frame(mode, td.mesh_start, L, t + 1)) * 10 + i];
+      const float bp = betas[(size_t)(foff + slot_frame(mode, td.mesh_start, L, t)) * 10 + i];
       float* orow = out + (size_t)t * ld;
       orow[C_BETA_RAW + i] = znorm(b, mean, stdv, C_BETA_RAW + i);
       orow[C_BETA_DIFF - dsh + i] = znorm(b - bp, mean, stdv, C_BETA_DIFF - dsh + i);
@@ -396,21 +390,8 @@ __global__ void __launch_bounds__(256) featurize_tiles_kernel(
   }
   // (the keypoint-less layout launches no keypoint workgroups)
   if (kcount == 0) return;
-  {
-    const int nslot = kcount + 1;
-    float v[KP_LOADS];
-#pragma unroll
-    for (int k = 0; k < KP_LOADS; ++k) {
-      const int it = tid + 256 * k;
-      const int sl = it / 120, c = it - sl * 120;
-      v[k] = sl < nslot ? kp[(size_t)(koff + slot_frame(mode, td.kp_start, Lk, sl)) * 120 + c] : 0.f;
-    }
-#pragma unroll
-    for (int k = 0; k < KP_LOADS; ++k)
-      if (tid + 256 * k < SLOTS * 120) stage[tid + 256 * k] = v[k];
-  }
-  __syncthreads();
-  // ---- (d1) keypoints: centre + Frobenius-normalise every slot (utils.py:191-196).  A wave's slots (wave, wave + 4,
+  // ---- (d1) keypoints: centre + Frobenius-normalise every slot (utils.py:191-196), loaded straight into registers
+  // (a wave's slots wave, wave + 4, ...; lane l holds point l), and the raw columns of the slot's row written from them.  A wave's slots (wave, wave + 4,
   // ...) are unrolled so their wave sums -- each a chain of six dependent lane shuffles -- run interleaved instead of
   // one after another (the keypoint workgroup was the kernel's long pole)
   {
@@ -420,8 +401,18 @@ __global__ void __launch_bounds__(256) featurize_tiles_kernel(
     for (int k = 0; k < KS; ++k) {
       const int slot = wave + 4 * k;
       const bool ok = slot <= kcount && lane < 60;
-      x[k] = ok ? stage[slot * 120 + 2 * lane] : 0.f;
-      y[k] = ok ? stage[slot * 120 + 2 * lane + 1] : 0.f;
+      const float* src = kp + (size_t)(koff + slot_frame(mode, td.kp_start, Lk, ok ? slot : 0)) * 120 + 2 * lane;
+      x[k] = ok ? src[0] : 0.f;
+      y[k] = ok ? src[1] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {  // slot s >= 1 is row s - 1's own frame: its raw keypoint columns
+      const int slot = wave + 4 * k;
+      if (slot >= 1 && slot <= kcount && lane < 60) {
+        float* orow = out + (size_t)(slot - 1) * ld;
+        orow[C_KP_RAW + 2 * lane] = znorm(x[k], mean, stdv, C_KP_RAW + 2 * lane);
+        orow[C_KP_RAW + 2 * lane + 1] = znorm(y[k], mean, stdv, C_KP_RAW + 2 * lane + 1);
+      }
     }
     // (wave_sum: the butterfly order the parity tests pinned; the Procrustes SVD is sensitive near rank 1)
 #pragma unroll
@@ -471,9 +462,6 @@ __global__ void __launch_bounds__(256) featurize_tiles_kernel(
     for (int k = 0; k < 8; ++k) {
       const int t = wave + 4 * k;
       if (t < kcount) {
-        float* orow = out + (size_t)t * ld;
-        for (int c = lane; c < 120; c += 64)
-          orow[C_KP_RAW + c] = znorm(stage[(t + 1) * 120 + c], mean, stdv, C_KP_RAW + c);
         if (lane == 0 && !row_src(mode, td.kp_start, Lk, t).first) {
           kR[t][0] = h[k][0]; kR[t][1] = h[k][1]; kR[t][2] = h[k][2]; kR[t][3] = h[k][3];
         }
