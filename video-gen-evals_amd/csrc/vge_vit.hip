@@ -9,9 +9,11 @@
 // Kernels (all bf16 operands, f32 accumulation, residual stream kept in f32):
 //   gemm_bf16_kernel<EPI>  C = A W^T (+ epilogue) for every Linear / the patch-embed conv (as im2col GEMM):
 //                          256 x 256 tiles, 8 waves (2 M x 4 N, 128 x 64 per wave) on
-//                          v_mfma_f32_32x32x16_bf16, both operands staged HBM -> LDS by global_load_lds
-//                          (16 B per lane) through a 5-stage x 32-k ring (160 KB, counted vmcnt), LDS image XOR-swizzled on the source
-//                          address so the fragment ds_read_b128 are conflict-free; XCD-grouped tile order.
+//                          v_mfma_f32_32x32x16_bf16 (16x16x32 for the bf16-output epilogues), both operands
+//                          staged HBM -> LDS by global_load_lds (16 B per lane) through a 5-stage x 32-k ring
+//                          (160 KB, counted vmcnt), LDS image XOR-swizzled on the source address so the fragment
+//                          ds_read_b128 are conflict-free; XCD-grouped tile order.
+//   gemm2_bf16_kernel<EPI> the same product on 128 x 256 tiles, two workgroups per CU (an A/B option, slower).
 //   ln_bf16_kernel         LayerNorm f32 -> bf16 (one wave per row).
 //   patchify_kernel        uint8 RGB crop -> normalised, zero-padded im2col rows of the 16x16 patches.
 //   vit_attn_kernel        softmax(Q K^T / sqrt(hd)) V per (frame, head) on MFMA: S^T = K Q^T so a query's
@@ -226,6 +228,20 @@ __global__ void __launch_bounds__(64 * NW, 1) gemm_bf16_kernel(GemmBf16Args g) {
   // accesses (256-B f32 rows, 128-B bf16 rows) instead of 2-4-byte column scatters.
   constexpr int WC = 32 * TN;            // wave tile columns
   constexpr int RPI = 64 / (WC / 4);     // rows per read instruction (16 B per lane)
+#if (VGE_GABL & 8) && defined(__HIP_DEVICE_COMPILE__)  // no epilogue (the accumulators kept live)
+  if constexpr (SH == 0) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int u = 0; u < TN; ++u) asm volatile("" ::"v"(acc[t][u]));
+  } else {
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) asm volatile("" ::"v"(acq[t][u]));
+  }
+  return;
+#endif
   vmcnt_b<0>();
   lds_barrier_b();
   float* my = reinterpret_cast<float*>(lds) + wave * (64 * WC);
@@ -309,6 +325,247 @@ __global__ void __launch_bounds__(64 * NW, 1) gemm_bf16_kernel(GemmBf16Args g) {
       }
     }
   }
+}
+
+// ------------------------------------------------------------- GEMM, two workgroups per CU (gemm2)
+// The 256 x 256 kernel above holds a CU alone (160 KB of LDS), so its epilogue -- the bias / GELU / residual pass, which
+// moves the output tile's bytes at the chip's HBM rate because every CU reaches it at the same time -- leaves the
+// matrix pipe idle: without it the ViT-H GEMMs run 13-36 % faster (`VGE_GABL` 8, profiles/ab_r05p_gemm_ablation.json).
+// gemm2 halves the tile (128 x 256, 4 waves of 64 x 128, same fragment bytes per MFMA) and the LDS (a 3-slot x 32-k
+// ring, 72 KB), so two workgroups share a CU and one's epilogue runs beside the other's MFMAs.  The epilogue needs no
+// LDS: the MFMA operands are swapped (weights as A, activations as B), so a lane's accumulators are 4 consecutive
+// output columns of one row (v_mfma_f32_32x32x16_bf16 D layout: lane l -> row l & 31, registers 4g..4g+3 -> columns
+// 8g + 4 (l >> 5) .. + 3) and bias / residual / position loads and the output stores are 16-B (f32) or 8-B (bf16)
+// vector accesses straight from the registers.  The products and their k order are the 256 x 256 kernel's.
+constexpr int G2_M = 128, G2_N = 256, G2_K = 32, G2_ST = 3, G2_GM = 16;
+constexpr int G2_TA = G2_M * G2_K * 2;       // 8 KB of A per stage
+constexpr int G2_SLOT = G2_TA + G2_N * G2_K * 2;  // + 16 KB of W = 24 KB
+constexpr int G2_LDS = G2_ST * G2_SLOT;     // 72 KB
+
+// ROWS x 32-k operand tile with 4 waves: the layout and swizzle of gb_stage
+template <int ROWS, bool CLAMP>
+__device__ __forceinline__ void g2_stage(const bf16* __restrict__ X, long ld, int r0, int k0, char* tile, int wave,
+                                         int lane, int rmax) {
+  constexpr int PW = ROWS / 16 / 4;  // 1-KB wave instructions per wave
+#pragma unroll
+  for (int j = 0; j < PW; ++j) {
+    const int q = wave * PW + j;
+    const int row = 16 * q + (lane >> 2);
+    const int ch = (lane & 3) ^ ((row >> 2) & 3);
+    glds16(X + (size_t)(CLAMP ? min(r0 + row, rmax) : r0 + row) * ld + k0 + ch * 8, tile + q * 1024);
+  }
+}
+
+template <bool B>
+struct BoolC {
+  static constexpr bool value = B;
+};
+
+template <int EPI, bool PM>
+__global__ void __launch_bounds__(256, 2) gemm2_bf16_kernel(GemmBf16Args g) {
+  constexpr int LPS = G2_M / 64 + G2_N / 64;  // global_load_lds per thread per stage (2 A + 4 W)
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  const int ntn = g.N / G2_N, mtn = (g.M + G2_M - 1) / G2_M;
+  const int bid = gb_xcd_remap(blockIdx.x, gridDim.x);
+  const int grp = bid / (G2_GM * ntn), rem = bid % (G2_GM * ntn);
+  const int gm = min(G2_GM, mtn - grp * G2_GM);
+  const int mt = grp * G2_GM + rem % gm, nt = rem / gm;
+  const int m0 = mt * G2_M, n0 = nt * G2_N;
+  const int nk = g.K / G2_K;  // >= 2, even
+  const int h = lane >> 5;
+  const int swz = (lane >> 2) & 3;
+  const int rowoff = (lane & 31) * 64;
+
+  floatx16 acc[2][4];  // [32-row tile t][32-column tile u]
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
+
+  auto issue = [&](int st) {
+    char* slot = lds + (st % G2_ST) * G2_SLOT;
+    g2_stage<G2_M, PM>(g.A, g.lda, m0, st * G2_K, slot, wave, lane, g.M - 1);
+    g2_stage<G2_N, false>(g.W, g.ldw, n0, st * G2_K, slot + G2_TA, wave, lane, g.N - 1);
+  };
+  struct Frag {
+    bf16x8 a[2][2], b[2][4];  // [16-k step][tile]
+  };
+  auto read = [&](int st, Frag& f) {
+    const char* cur = lds + (st % G2_ST) * G2_SLOT;
+    const char* As = cur + wm * 64 * 64 + rowoff;
+    const char* Bs = cur + G2_TA + wn * 128 * 64 + rowoff;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int co = ((2 * s + h) ^ swz) * 16;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) f.a[s][t] = *reinterpret_cast<const bf16x8*>(As + t * 32 * 64 + co);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) f.b[s][u] = *reinterpret_cast<const bf16x8*>(Bs + u * 32 * 64 + co);
+    }
+  };
+  auto mma = [&](const Frag& f, int s) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.b[s][u], f.a[s][t], acc[t][u], 0, 0, 0);
+  };
+  // Step kt: stage kt's fragments are in registers (read during step kt - 1).  Wait for stage kt + 1 (issued at step
+  // kt - 2; stage kt + 2 stays in flight) and barrier: every wave's reads of stage kt's slot have retired (the
+  // barrier's lgkmcnt(0)), so stage kt + 3 goes into that slot.  Past the last stage the loads re-fetch stage nk - 1
+  // (identical bytes; at step nk - 1 into its own slot, whose fragments are already in registers) and the reads
+  // re-read it, so every wait is the same count.
+  auto step = [&](int kt, Frag& cur, Frag& nxt) {
+    vmcnt_b<LPS>();
+    lds_barrier_b();
+    issue(min(kt + 3, nk - 1));
+    read(min(kt + 1, nk - 1), nxt);
+    mma(cur, 0);
+    mma(cur, 1);
+#pragma unroll
+    for (int j = 0; j < LPS; ++j) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read (global_load_lds)
+    }
+#pragma unroll
+    for (int j = 0; j < 6; ++j) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // DS read
+    }
+  };
+  issue(0);
+  issue(1);
+  issue(min(2, nk - 1));
+  vmcnt_b<2 * LPS>();  // retire stage 0
+  lds_barrier_b();
+  Frag f0, f1;
+  read(0, f0);
+  for (int kt = 0; kt < nk; kt += 2) {
+    step(kt, f0, f1);
+    step(kt + 1, f1, f0);
+  }
+  vmcnt_b<0>();  // the tail's re-fetches land before the workgroup's LDS can be handed on
+
+  // ---- epilogue from the registers: lane -> row m0 + 64 wm + 32 t + (lane & 31), columns nb .. nb + 3 of group g;
+  // UB column tiles per batch (every load of a batch in flight together; the position-embedding epilogue, with two
+  // row vectors per output, takes one tile at a time to stay inside 256 registers)
+  constexpr bool RB = EPI == GE_RESB_BF16 || EPI == GE_RESB_RELU_BF16;
+  constexpr int UB = EPI == GE_PE_F32 ? 1 : 4;
+  const int cb = n0 + wn * 128 + 4 * h;
+  // (one branch on the bias pointer around the whole epilogue: a per-load test makes hipcc branch and drain vmcnt
+  // around every load)
+  auto epilogue = [&](auto hb) {
+  constexpr bool HB = decltype(hb)::value;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int row = m0 + wm * 64 + t * 32 + (lane & 31);
+    const int lrow = PM ? min(row, g.M - 1) : row;  // (PM: rows past M are loaded clamped, never stored)
+    const bool st_ok = !PM || row < g.M;
+#pragma unroll
+    for (int u0 = 0; u0 < 4; u0 += UB) {
+      floatx4 v[UB][4];  // [u - u0][g]
+#pragma unroll
+      for (int u = 0; u < UB; ++u)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          v[u][q] = floatx4{acc[t][u0 + u][4 * q], acc[t][u0 + u][4 * q + 1], acc[t][u0 + u][4 * q + 2],
+                            acc[t][u0 + u][4 * q + 3]};
+      // (acc + (bias + pos_embed[0])) + pos_embed[1 + token]: the 256 x 256 kernel's operation order
+#pragma unroll
+      for (int u = 0; u < UB; ++u)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int c = cb + (u0 + u) * 32 + 8 * q;
+          floatx4 bb = {0.f, 0.f, 0.f, 0.f};
+          if constexpr (HB) bb = *reinterpret_cast<const floatx4*>(g.bias + c);
+          if constexpr (EPI == GE_PE_F32) bb += *reinterpret_cast<const floatx4*>(g.pos + c);
+          v[u][q] += bb;
+        }
+      if constexpr (EPI == GE_PE_F32) {  // tokens per frame = 192 (checked by the host)
+        const float* pr = g.pos + (long)(1 + lrow - (lrow / 192) * 192) * g.N + cb;
+#pragma unroll
+        for (int u = 0; u < UB; ++u)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[u][q] += *reinterpret_cast<const floatx4*>(pr + (u0 + u) * 32 + 8 * q);
+      }
+      if constexpr (EPI == GE_RES_F32) {
+        const float* rr = g.res + (long)lrow * g.ldr + cb;
+        floatx4 rv[UB][4];
+#pragma unroll
+        for (int u = 0; u < UB; ++u)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) rv[u][q] = *reinterpret_cast<const floatx4*>(rr + (u0 + u) * 32 + 8 * q);
+#pragma unroll
+        for (int u = 0; u < UB; ++u)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[u][q] += rv[u][q];
+      }
+      if constexpr (RB) {
+        const bf16* rr = g.resb + (long)lrow * g.ldr + cb;
+        bf16x4 rv[UB][4];
+#pragma unroll
+        for (int u = 0; u < UB; ++u)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) rv[u][q] = *reinterpret_cast<const bf16x4*>(rr + (u0 + u) * 32 + 8 * q);
+#pragma unroll
+        for (int u = 0; u < UB; ++u)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            v[u][q] += floatx4{(float)rv[u][q][0], (float)rv[u][q][1], (float)rv[u][q][2], (float)rv[u][q][3]};
+      }
+      if constexpr (EPI == GE_RELU_BF16 || EPI == GE_RESB_RELU_BF16) {
+#pragma unroll
+        for (int u = 0; u < UB; ++u)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            v[u][q] = floatx4{fmaxf(v[u][q].x, 0.f), fmaxf(v[u][q].y, 0.f), fmaxf(v[u][q].z, 0.f),
+                              fmaxf(v[u][q].w, 0.f)};
+      }
+      if constexpr (EPI == GE_GELU_BF16) {
+#pragma unroll
+        for (int u = 0; u < UB; ++u) {
+          floatx2 y[8];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            y[2 * q] = floatx2{v[u][q].x, v[u][q].y};
+            y[2 * q + 1] = floatx2{v[u][q].z, v[u][q].w};
+          }
+          gelu2_many(y);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) v[u][q] = floatx4{y[2 * q].x, y[2 * q].y, y[2 * q + 1].x, y[2 * q + 1].y};
+        }
+      }
+      if (st_ok) {
+        if constexpr (EPI == GE_RES_F32 || EPI == GE_PE_F32 || EPI == GE_F32) {
+          float* o = reinterpret_cast<float*>(g.out) + (long)row * g.ldo + cb;
+#pragma unroll
+          for (int u = 0; u < UB; ++u)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) *reinterpret_cast<floatx4*>(o + (u0 + u) * 32 + 8 * q) = v[u][q];
+        } else {
+          bf16* o = reinterpret_cast<bf16*>(g.out) + (long)row * g.ldo + cb;
+#pragma unroll
+          for (int u = 0; u < UB; ++u)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              bf16x4 ob;
+              ob[0] = (bf16)v[u][q].x; ob[1] = (bf16)v[u][q].y; ob[2] = (bf16)v[u][q].z; ob[3] = (bf16)v[u][q].w;
+              *reinterpret_cast<bf16x4*>(o + (u0 + u) * 32 + 8 * q) = ob;
+            }
+        }
+      }
+    }
+  }
+  };
+  if (g.bias)
+    epilogue(BoolC<true>{});
+  else
+    epilogue(BoolC<false>{});
 }
 
 // ------------------------------------------------------------------------------------- LayerNorm
@@ -671,8 +928,41 @@ hipError_t gemm_setup_pm() {  // the partial-M kernels (8 waves, 32x32x16): 1x1 
   return hipSuccess;
 }
 
+template <bool PM>
+hipError_t gemm2_setup() {
+  const void* ks[8] = {(const void*)gemm2_bf16_kernel<GE_BF16, PM>, (const void*)gemm2_bf16_kernel<GE_GELU_BF16, PM>,
+                       (const void*)gemm2_bf16_kernel<GE_RES_F32, PM>, (const void*)gemm2_bf16_kernel<GE_PE_F32, PM>,
+                       (const void*)gemm2_bf16_kernel<GE_F32, PM>, (const void*)gemm2_bf16_kernel<GE_RELU_BF16, PM>,
+                       (const void*)gemm2_bf16_kernel<GE_RESB_BF16, PM>,
+                       (const void*)gemm2_bf16_kernel<GE_RESB_RELU_BF16, PM>};
+  for (auto k : ks) {
+    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, G2_LDS);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+template <bool PM>
+void launch_gemm2(int epi, const GemmBf16Args& g, hipStream_t s) {
+  const dim3 grid(((g.M + G2_M - 1) / G2_M) * (g.N / G2_N)), blk(256);
+  switch (epi) {
+    case GE_BF16: hipLaunchKernelGGL((gemm2_bf16_kernel<GE_BF16, PM>), grid, blk, G2_LDS, s, g); break;
+    case GE_GELU_BF16: hipLaunchKernelGGL((gemm2_bf16_kernel<GE_GELU_BF16, PM>), grid, blk, G2_LDS, s, g); break;
+    case GE_RES_F32: hipLaunchKernelGGL((gemm2_bf16_kernel<GE_RES_F32, PM>), grid, blk, G2_LDS, s, g); break;
+    case GE_PE_F32: hipLaunchKernelGGL((gemm2_bf16_kernel<GE_PE_F32, PM>), grid, blk, G2_LDS, s, g); break;
+    case GE_RELU_BF16: hipLaunchKernelGGL((gemm2_bf16_kernel<GE_RELU_BF16, PM>), grid, blk, G2_LDS, s, g); break;
+    case GE_RESB_BF16: hipLaunchKernelGGL((gemm2_bf16_kernel<GE_RESB_BF16, PM>), grid, blk, G2_LDS, s, g); break;
+    case GE_RESB_RELU_BF16:
+      hipLaunchKernelGGL((gemm2_bf16_kernel<GE_RESB_RELU_BF16, PM>), grid, blk, G2_LDS, s, g);
+      break;
+    default: hipLaunchKernelGGL((gemm2_bf16_kernel<GE_F32, PM>), grid, blk, G2_LDS, s, g); break;
+  }
+}
+
 hipError_t vit_kernels_setup() {
   hipError_t e = gemm_setup_nw<8>();
+  if (e == hipSuccess) e = gemm2_setup<false>();
+  if (e == hipSuccess) e = gemm2_setup<true>();
   if (e == hipSuccess) e = gemm_setup_pm();
   if (e == hipSuccess) e = gemm_setup_nw<4>();
   if (e == hipSuccess) e = gemm_setup_nw<8, 1>();
@@ -684,7 +974,11 @@ hipError_t vit_kernels_setup() {
                              AttnCfg<64>::LDS);
 }
 
-static int g_gemm_waves = 0;  // 8, 4 or 16 (= 8 waves on 16x16x32) (VGE_GEMM_WAVES), chosen once
+// VGE_GEMM_WAVES, read once: 1 (default) = by epilogue: the bf16-output epilogues (bias, GELU) on the 16x16x32 form of
+// the 8-wave kernel, the rest on 32x32x16 (the 16x16x32 form is bit-identical and the chip holds a higher clock on
+// it: qkv +4-8 %, fc1 +2-3 %; proj / fc2 with their f32 residual 0-3 % slower: profiles/ab_r05p_gemm_ablation.json,
+// ab_r05q_gemm2.json); 8 / 16 = always 32x32x16 / 16x16x32; 4 = 4 waves of 128 x 128; 2 = gemm2
+static int g_gemm_waves = 0;
 
 template <int NW, int SH = 0, bool PM = false>
 void launch_gemm_nw(int epi, dim3 grid, const GemmBf16Args& g, hipStream_t s) {
@@ -721,14 +1015,21 @@ hipError_t launch_gemm_bf16(int epi, const GemmBf16& a, hipStream_t s) {
     return hipErrorInvalidValue;
   if (g_gemm_waves == 0) {
     const char* e = getenv("VGE_GEMM_WAVES");
-    g_gemm_waves = (e && (atoi(e) == 4 || atoi(e) == 16)) ? atoi(e) : 8;
+    g_gemm_waves = (e && (atoi(e) == 2 || atoi(e) == 4 || atoi(e) == 8 || atoi(e) == 16)) ? atoi(e) : 1;
+  }
+  if (g_gemm_waves == 2) {  // two 128 x 256 workgroups per CU
+    if (a.M % G2_M)
+      launch_gemm2<true>(epi, g, s);
+    else
+      launch_gemm2<false>(epi, g, s);
+    return hipGetLastError();
   }
   const dim3 grid(((a.M + GB_M - 1) / GB_M) * (a.N / GB_N));
   if (a.M % GB_M)
     launch_gemm_nw<8, 0, true>(epi, grid, g, s);
   else if (g_gemm_waves == 4)
     launch_gemm_nw<4>(epi, grid, g, s);
-  else if (g_gemm_waves == 16)
+  else if (g_gemm_waves == 16 || (g_gemm_waves == 1 && (epi == GE_BF16 || epi == GE_GELU_BF16)))
     launch_gemm_nw<8, 1>(epi, grid, g, s);
   else
     launch_gemm_nw<8>(epi, grid, g, s);
@@ -736,7 +1037,7 @@ hipError_t launch_gemm_bf16(int epi, const GemmBf16& a, hipStream_t s) {
 }
 
 extern "C" int vge_debug_set_gemm_waves(int nw) {  // A/B timing (tools/gemm_bench.py)
-  g_gemm_waves = (nw == 4 || nw == 16) ? nw : 8;
+  g_gemm_waves = (nw == 1 || nw == 2 || nw == 4 || nw == 16) ? nw : 8;
   return 0;
 }
 
