@@ -974,8 +974,8 @@ hipError_t vit_kernels_setup() {
                              AttnCfg<64>::LDS);
 }
 
-// VGE_GEMM_WAVES, read once: 1 (default) = by epilogue: the bf16-output epilogues (bias, GELU) on the 16x16x32 form of
-// the 8-wave kernel, the rest on 32x32x16 (the 16x16x32 form is bit-identical and the chip holds a higher clock on
+// VGE_GEMM_WAVES, read once: 1 (default) = by epilogue: the bf16-output epilogues (bias, GELU, the 1x1 convs' ReLU /
+// residual) on the 16x16x32 form of the 8-wave kernel, the f32-output ones on 32x32x16 (the 16x16x32 form is bit-identical and the chip holds a higher clock on
 // it: qkv +4-8 %, fc1 +2-3 %; proj / fc2 with their f32 residual 0-3 % slower: profiles/ab_r05p_gemm_ablation.json,
 // ab_r05q_gemm2.json); 8 / 16 = always 32x32x16 / 16x16x32; 4 = 4 waves of 128 x 128; 2 = gemm2
 static int g_gemm_waves = 0;
@@ -1029,7 +1029,7 @@ hipError_t launch_gemm_bf16(int epi, const GemmBf16& a, hipStream_t s) {
     launch_gemm_nw<8, 0, true>(epi, grid, g, s);
   else if (g_gemm_waves == 4)
     launch_gemm_nw<4>(epi, grid, g, s);
-  else if (g_gemm_waves == 16 || (g_gemm_waves == 1 && (epi == GE_BF16 || epi == GE_GELU_BF16)))
+  else if (g_gemm_waves == 16 || (g_gemm_waves == 1 && epi != GE_RES_F32 && epi != GE_PE_F32 && epi != GE_F32))
     launch_gemm_nw<8, 1>(epi, grid, g, s);
   else
     launch_gemm_nw<8>(epi, grid, g, s);
