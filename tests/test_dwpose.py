@@ -329,8 +329,9 @@ def test_extractor_profile_and_flops(D):
 ])
 def test_conv_1x1_gemm_variant_matches_default(D, n, H, W, Cin, Cout, act, res):
     """Variant 9 (a 1x1 stride-1 conv on the ViT's bf16 GEMM kernel, a tuner candidate) against the default conv
-    kernel: the same per-element MFMA order over K (32-deep stages of two 16-k steps) and the same epilogue arithmetic
-    (bias, then the bf16 residual, then the activation) -> bit-identical, including a partial last row tile."""
+    kernel: the same per-element MFMA order over K (32-deep stages of two 16-k steps; the GEMM's default 16x16x32 form
+    for these bf16 epilogues measures bit-identical to it) and the same epilogue arithmetic (bias, then the bf16
+    residual, then the activation) -> bit-identical, including a partial last row tile."""
     import ctypes as C
     from vge import lib as Lb
     lib = Lb.load()

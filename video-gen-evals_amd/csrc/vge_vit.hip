@@ -912,15 +912,16 @@ hipError_t gemm_setup_nw() {
   return hipSuccess;
 }
 
-hipError_t gemm_setup_pm() {  // the partial-M kernels (8 waves, 32x32x16): 1x1 convs over n x H x W rows
-  const void* ks[8] = {(const void*)gemm_bf16_kernel<GE_BF16, 8, 0, true>,
-                       (const void*)gemm_bf16_kernel<GE_GELU_BF16, 8, 0, true>,
-                       (const void*)gemm_bf16_kernel<GE_RES_F32, 8, 0, true>,
-                       (const void*)gemm_bf16_kernel<GE_PE_F32, 8, 0, true>,
-                       (const void*)gemm_bf16_kernel<GE_F32, 8, 0, true>,
-                       (const void*)gemm_bf16_kernel<GE_RELU_BF16, 8, 0, true>,
-                       (const void*)gemm_bf16_kernel<GE_RESB_BF16, 8, 0, true>,
-                       (const void*)gemm_bf16_kernel<GE_RESB_RELU_BF16, 8, 0, true>};
+template <int SH>
+hipError_t gemm_setup_pm() {  // the partial-M kernels (8 waves): 1x1 convs over n x H x W rows
+  const void* ks[8] = {(const void*)gemm_bf16_kernel<GE_BF16, 8, SH, true>,
+                       (const void*)gemm_bf16_kernel<GE_GELU_BF16, 8, SH, true>,
+                       (const void*)gemm_bf16_kernel<GE_RES_F32, 8, SH, true>,
+                       (const void*)gemm_bf16_kernel<GE_PE_F32, 8, SH, true>,
+                       (const void*)gemm_bf16_kernel<GE_F32, 8, SH, true>,
+                       (const void*)gemm_bf16_kernel<GE_RELU_BF16, 8, SH, true>,
+                       (const void*)gemm_bf16_kernel<GE_RESB_BF16, 8, SH, true>,
+                       (const void*)gemm_bf16_kernel<GE_RESB_RELU_BF16, 8, SH, true>};
   for (auto k : ks) {
     hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, GB_LDS);
     if (e != hipSuccess) return e;
@@ -963,7 +964,8 @@ hipError_t vit_kernels_setup() {
   hipError_t e = gemm_setup_nw<8>();
   if (e == hipSuccess) e = gemm2_setup<false>();
   if (e == hipSuccess) e = gemm2_setup<true>();
-  if (e == hipSuccess) e = gemm_setup_pm();
+  if (e == hipSuccess) e = gemm_setup_pm<0>();
+  if (e == hipSuccess) e = gemm_setup_pm<1>();
   if (e == hipSuccess) e = gemm_setup_nw<4>();
   if (e == hipSuccess) e = gemm_setup_nw<8, 1>();
   if (e != hipSuccess) return e;
@@ -1025,11 +1027,15 @@ hipError_t launch_gemm_bf16(int epi, const GemmBf16& a, hipStream_t s) {
     return hipGetLastError();
   }
   const dim3 grid(((a.M + GB_M - 1) / GB_M) * (a.N / GB_N));
-  if (a.M % GB_M)
-    launch_gemm_nw<8, 0, true>(epi, grid, g, s);
-  else if (g_gemm_waves == 4)
+  const bool sh = g_gemm_waves == 16 || (g_gemm_waves == 1 && epi != GE_RES_F32 && epi != GE_PE_F32 && epi != GE_F32);
+  if (a.M % GB_M) {
+    if (sh)
+      launch_gemm_nw<8, 1, true>(epi, grid, g, s);
+    else
+      launch_gemm_nw<8, 0, true>(epi, grid, g, s);
+  } else if (g_gemm_waves == 4)
     launch_gemm_nw<4>(epi, grid, g, s);
-  else if (g_gemm_waves == 16 || (g_gemm_waves == 1 && epi != GE_RES_F32 && epi != GE_PE_F32 && epi != GE_F32))
+  else if (sh)
     launch_gemm_nw<8, 1>(epi, grid, g, s);
   else
     launch_gemm_nw<8>(epi, grid, g, s);
