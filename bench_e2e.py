@@ -32,8 +32,8 @@ import torch.distributed as dist
 BF16_MFMA_PEAK_TFLOPS = 2516.6
 # kernel sources whose PMC pass (tools/profile_e2e.sh -> tools/pmc_e2e.py -> profiles/pmc_e2e.json) gives `traffic`
 E2E_KERNEL_SOURCES = {"gemm_bf16_kernel": ["vge_vit.hip"],
-                      "yolox_conv": ["vge_cnn.hip", "vge_cnn_host.h", "vge_yolox.cpp"],
-                      "frcnn_conv": ["vge_cnn.hip", "vge_cnn_host.h", "vge_frcnn.cpp"]}
+                      "yolox_conv": ["vge_cnn.hip", "vge_cnn_host.h", "vge_yolox.cpp", "vge_vit.hip"],
+                      "frcnn_conv": ["vge_cnn.hip", "vge_cnn_host.h", "vge_frcnn.cpp", "vge_vit.hip", "vge_gconv.hip"]}
 YOLOX_CHUNK = 256   # frames per detector pass (tools/yolox_prof.py --chunk: 637 vs 618 TFLOP/s at 64)
 FRCNN_CHUNK = 64    # frames per Faster R-CNN workspace chunk (~0.3 GB per 800 x 800 frame; 64: -6 % vs 32, profiles/ab_r05m_*)
 
