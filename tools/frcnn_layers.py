@@ -1,6 +1,6 @@
 """Per-layer kernel times of the gate detector from a rocprofv3 kernel-trace database (tools/time_frcnn.py under
 `rocprofv3 --kernel-trace`): the last detect chunk's dispatches, labelled in vge_frcnn.cpp's launch order.
-Usage: python tools/frcnn_layers.py <run_results.db> [depth] -> per-layer table + per-kind totals."""
+Usage: python tools/frcnn_layers.py <run_results.db | run_kernel_trace.csv> [depth] -> per-layer table + per-kind totals."""
 import sqlite3
 import sys
 from collections import defaultdict
@@ -28,8 +28,14 @@ def labels(depth=101):
 def main():
     db = sys.argv[1]
     depth = int(sys.argv[2]) if len(sys.argv) > 2 else 101
-    c = sqlite3.connect(db)
-    rows = c.execute("select name, duration, grid_x, workgroup_x from kernels order by start").fetchall()
+    if db.endswith(".csv"):  # rocprofv3 --output-format csv: run_kernel_trace.csv
+        import csv
+        rs = sorted(csv.DictReader(open(db)), key=lambda r: int(r["Start_Timestamp"]))
+        rows = [(r["Kernel_Name"], int(r["End_Timestamp"]) - int(r["Start_Timestamp"]), int(r["Grid_Size_X"]),
+                 int(r["Workgroup_Size_X"])) for r in rs]
+    else:
+        c = sqlite3.connect(db)
+        rows = c.execute("select name, duration, grid_x, workgroup_x from kernels order by start").fetchall()
     rows = [r for r in rows if not r[0].startswith("__amd_rocclr") and "at::" not in r[0]]
     lab = labels(depth)
     last = rows[-len(lab):]

@@ -17,11 +17,14 @@
 // K steps: a 16-channel output tile's inputs are its group's channels, max(group width, 16) of them (group width 8:
 // the 16 x 16 weight block holds two groups' 8 x 8 blocks and zeros, as packed by vge_frcnn.cpp's gconv_bn).
 #include "vge_common.h"
+#include <cstdlib>
+#include <type_traits>
 
 namespace {
 
 typedef short short4v __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
 
 constexpr int GC_PITCH = 144;  // LDS bytes per input pixel (64 bf16 channels + 8 pad)
 
@@ -47,9 +50,15 @@ constexpr int gc_tw() { return S == 1 ? 32 : 16; }
 template <int S>
 constexpr int gc_lds() { return ((gc_th<S>() - 1) * S + 3) * ((gc_tw<S>() - 1) * S + 3) * GC_PITCH; }
 
-// KS: 16-channel K steps per tap (max(group width, 16) / 16); S: stride
-template <int KS, int S>
-__global__ void __launch_bounds__(256) gconv3_kernel(GconvArgs a) {
+// KS: 16-channel K steps per tap (max(group width, 16) / 16); S: stride; MF: 0 = v_mfma_f32_16x16x16_bf16 (one per
+// 16-channel step), 1 = v_mfma_f32_16x16x32_bf16 (gfx950's full-rate bf16 form: the legacy 16x16x16 issues at half the
+// rate, 16 cycles per 8 kFLOP, profiles/pmc_r05u_frcnn_sq.json): KS >= 2 -> two steps of a tap per MFMA, KS = 1 -> two
+// taps per MFMA (lanes 0-31 carry tap 2p, lanes 32-63 tap 2p + 1; tap 9 is zero weights)
+#ifndef VGE_GC_OCC
+#define VGE_GC_OCC 1  // minimum waves per SIMD the register allocation must allow (= workgroups per CU)
+#endif
+template <int KS, int S, int MF>
+__global__ void __launch_bounds__(256, VGE_GC_OCC) gconv3_kernel(GconvArgs a) {
   constexpr int TH = gc_th<S>(), TW = gc_tw<S>(), NPT = TH * TW / 16;
   constexpr int IH = (TH - 1) * S + 3, IW = (TW - 1) * S + 3, NPIX = IH * IW;
   __shared__ __attribute__((aligned(16))) char tile[gc_lds<S>()];
@@ -79,14 +88,28 @@ __global__ void __launch_bounds__(256) gconv3_kernel(GconvArgs a) {
   const int n0 = wave * 16;
   constexpr int G16 = KS * 16;
   const int cbase = (n0 / G16) * G16;
-  short4v wa[9][KS];
-  const __bf16* wr = a.w + (size_t)(slice * 64 + n0 + (lane & 15)) * a.Kp + cbase + 4 * (lane >> 4);
+  // MF = 0: [tap][K step] short4v fragments (4 channels per lane); MF = 1, KS >= 2: [tap][KS / 2] bf16x8 (8 channels per
+  // lane); MF = 1, KS = 1: [tap pair][0] bf16x8 (lane half h -> tap 2p + h)
+  constexpr int NT = MF && KS == 1 ? 5 : 9;
+  constexpr int NJ = MF ? (KS == 1 ? 1 : KS / 2) : KS;
+  typedef typename std::conditional<MF != 0, bf16x8_t, short4v>::type Frag;
+  Frag wa[NT][NJ];
+  const int hh = lane >> 5;  // MF = 1, KS = 1: which tap of the pair
+  const int cl = MF ? (KS == 1 ? 8 * ((lane >> 4) & 1) : 8 * (lane >> 4)) : 4 * (lane >> 4);
+  const __bf16* wr = a.w + (size_t)(slice * 64 + n0 + (lane & 15)) * a.Kp + cbase + cl;
 #pragma unroll
-  for (int t = 0; t < 9; ++t)
+  for (int t = 0; t < NT; ++t)
 #pragma unroll
-    for (int j = 0; j < KS; ++j) wa[t][j] = *reinterpret_cast<const short4v*>(wr + t * 64 + 16 * j);
+    for (int j = 0; j < NJ; ++j) {
+      if constexpr (MF && KS == 1) {
+        const int tap = 2 * t + hh;
+        wa[t][j] = tap < 9 ? *reinterpret_cast<const Frag*>(wr + tap * 64) : Frag{};
+      } else {
+        wa[t][j] = *reinterpret_cast<const Frag*>(wr + t * 64 + (MF ? 32 : 16) * j);
+      }
+    }
   const int px = lane & 15;
-  const char* lb = tile + (cbase + 4 * (lane >> 4)) * 2;
+  const char* lb = tile + (cbase + cl) * 2;
   const int ch = slice * 64 + n0 + 4 * (lane >> 4);
   const floatx4 bv = *reinterpret_cast<const floatx4*>(a.bias + ch);
   for (int k = 0; k < nimg; ++k) {
@@ -109,12 +132,24 @@ __global__ void __launch_bounds__(256) gconv3_kernel(GconvArgs a) {
       const int op = pt * 16 + px, orow = op / TW, ocol = op % TW;
       const char* pb = lb + ((orow * S) * IW + ocol * S) * GC_PITCH;
 #pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        const int off = ((t / 3) * IW + (t % 3)) * GC_PITCH;
+      for (int t = 0; t < NT; ++t) {
+        if constexpr (MF && KS == 1) {
+          const int ta = 2 * t, tb = 2 * t + 1 < 9 ? 2 * t + 1 : 8;  // (tap 9: zero weights on finite data)
+          const int offa = ((ta / 3) * IW + (ta % 3)) * GC_PITCH, offb = ((tb / 3) * IW + (tb % 3)) * GC_PITCH;
+          const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(pb + (hh ? offb : offa));
+          acc[pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[t][0], b, acc[pt], 0, 0, 0);
+        } else {
+          const int off = ((t / 3) * IW + (t % 3)) * GC_PITCH;
 #pragma unroll
-        for (int j = 0; j < KS; ++j) {
-          const short4v b = *reinterpret_cast<const short4v*>(pb + off + 32 * j);
-          acc[pt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wa[t][j], b, acc[pt], 0, 0, 0);
+          for (int j = 0; j < NJ; ++j) {
+            if constexpr (MF) {
+              const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(pb + off + 64 * j);
+              acc[pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[t][j], b, acc[pt], 0, 0, 0);
+            } else {
+              const short4v b = *reinterpret_cast<const short4v*>(pb + off + 32 * j);
+              acc[pt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wa[t][j], b, acc[pt], 0, 0, 0);
+            }
+          }
         }
       }
     }
@@ -149,7 +184,16 @@ hipError_t launch_gconv3(const void* x, long ldx, const void* w, int Kp, const f
   a.tiles_x = (a.Wo + tw - 1) / tw;
   const dim3 grid(a.tiles_x * ((a.Ho + th - 1) / th), C / 64, (n_img + GC_NI - 1) / GC_NI);
   const int ks = gw <= 16 ? 1 : gw / 16;
-#define GC_LAUNCH(KS, S) hipLaunchKernelGGL((gconv3_kernel<KS, S>), grid, dim3(256), 0, s, a)
+  static int mf = -1;  // VGE_GC_MF: 1 (default) = 16x16x32, 0 = 16x16x16
+  if (mf < 0) {
+    const char* e = getenv("VGE_GC_MF");
+    mf = (e && e[0] == '0') ? 0 : 1;
+  }
+#define GC_LAUNCH(KS, S)                                                             \
+  do {                                                                               \
+    if (mf) hipLaunchKernelGGL((gconv3_kernel<KS, S, 1>), grid, dim3(256), 0, s, a); \
+    else hipLaunchKernelGGL((gconv3_kernel<KS, S, 0>), grid, dim3(256), 0, s, a);    \
+  } while (0)
   if (stride == 1) {
     if (ks == 1) GC_LAUNCH(1, 1);
     else if (ks == 2) GC_LAUNCH(2, 1);
