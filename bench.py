@@ -66,6 +66,16 @@ PEAK_BY_COMPUTE = {"f32": (F32_MFMA_PEAK_TFLOPS, "conv_encoder_kernel (10 Moveme
                                                       "3xfp16 split MFMA, staggered halves, peak = dense F16 MFMA / 3)"),
                    "f16": (F16_MFMA_PEAK_TFLOPS, "conv_encoder_f16w_kernel (10 MovementConvEncoders on 1..6-window "
                                                  "units, single fp16 MFMA per product, peak = dense F16 MFMA)")}
+F16_X3S_KNAME = ("conv_encoder_x3s_kernel<false> (10 MovementConvEncoders, staggered halves, single fp16 MFMA per "
+                 "product, peak = dense F16 MFMA)")
+
+
+def f16_conv_is_x3s() -> bool:
+    """The f16 mode's conv kernel, as vge_api.cpp picks it: the staggered x3s kernel in single fp16 unless
+    VGE_F16_X3S=0 (conv_encoder_f16w_kernel) or the stem is split (VGE_F16_MIX bit 1)."""
+    return os.environ.get("VGE_F16_X3S", "1") != "0" and not (int(os.environ.get("VGE_F16_MIX", "2")) & 1)
+
+
 ARITH = {"f32": "f32 in, f32 accumulate (v_mfma_f32_16x16x4_f32)",
          "f32x3": "f32 operands as fp16 hi + fp16 residual lo (power-of-two scaled per row/window/column), 3 f16 "
                   "MFMAs per product (hi*hi + hi*lo + lo*hi), f32 accumulate",
@@ -513,6 +523,9 @@ def pmc_traffic(compute: str, windows: int):
         e = pj[compute]
         if e.get("source_sha") != _kernel_sources_sha():
             return None
+        if compute == "f16" and e.get("kernel") != ("conv_encoder_x3s_kernel" if f16_conv_is_x3s()
+                                                     else "conv_encoder_f16w_kernel"):
+            return None
         return e["hbm_bytes_per_window"] * windows
     except (OSError, KeyError, ValueError):
         return None
@@ -764,6 +777,8 @@ def run_score(args, world, rank, dev):
     conv_ms = stage_ms["conv_encoders"] / max(ncalls, 1)
     achieved = CONV_FLOP_PER_WINDOW * CH / (conv_ms * 1e-3) / 1e12
     _, kname = PEAK_BY_COMPUTE[args.compute]
+    if args.compute == "f16" and f16_conv_is_x3s():
+        kname = F16_X3S_KNAME
     pk = device_peaks()
     peak = {"f16": pk["f16"], "f32x3": pk["f16"] / 3, "f32": pk["f32"]}[args.compute]
     total_videos = sum(v for _, v in per_rank) * args.steps

@@ -150,6 +150,7 @@ def test_f16_unit_kernel_matches_quad_kernel(n, monkeypatch):
     from vge import ops
     o = _oracle(max(n, 256)) if n <= 256 else _oracle(n)
     feats = torch.from_numpy(o["feats"][:n]).to(DEV)
+    monkeypatch.setenv("VGE_F16_X3S", "0")  # the f16w / quad kernels (the default f16 conv is the staggered x3s one)
     monkeypatch.setenv("VGE_F16W", "0")
     quad = ops.Encoder(o["sd"], device=DEV, compute="f16")
     monkeypatch.delenv("VGE_F16W")
@@ -170,8 +171,40 @@ def test_f16_unit_kernel_matches_quad_kernel(n, monkeypatch):
         assert torch.equal(s2, s_u[:64])
 
 
+@pytest.mark.parametrize("n", [1, 37, 256, 293, 600])
+def test_f16_staggered_kernel_matches_unit_kernel(n, monkeypatch):
+    """The f16 mode's default conv (conv_encoder_x3s_kernel<false>: the f32x3 kernel's staggered schedule, GroupNorm
+    fold and exchanges on hi planes only, one fp16 MFMA per product) against conv_encoder_f16w_kernel
+    (VGE_F16_X3S=0): the same per-row / per-window / per-column power-of-two scaling and fp16 operand rounding, but
+    a different K order and the GroupNorm folded into the next GEMM, so they agree to 1e-4 and both are bounded
+    against the oracle."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vge import ops
+    o = _oracle(max(n, 256)) if n <= 256 else _oracle(n)
+    feats = torch.from_numpy(o["feats"][:n]).to(DEV)
+    monkeypatch.setenv("VGE_F16_X3S", "0")
+    unit = ops.Encoder(o["sd"], device=DEV, compute="f16")
+    monkeypatch.delenv("VGE_F16_X3S")
+    stag = ops.Encoder(o["sd"], device=DEV, compute="f16")
+    for e in (unit, stag):
+        e.reserve(n)
+    s_u, f_u, t_u = unit.encode(feats, frame_embed=True, tc=True)
+    s_s, f_s, t_s = stag.encode(feats, frame_embed=True, tc=True)
+    d_seq = (s_s - s_u).abs().max().item()
+    d_fe = (f_s - f_u).abs().max().item()
+    d_tc = (t_s - t_u).abs().max().item()
+    e_seq = (s_s.cpu() - o["seq"][:n]).abs().max().item()
+    e_fe = (f_s.cpu() - o["fe"][:n]).abs().max().item()
+    print(f"n={n}: staggered vs unit seq {d_seq:.2e} frame {d_fe:.2e} tc {d_tc:.2e}; staggered vs oracle seq "
+          f"{e_seq:.2e} frame {e_fe:.2e}")
+    assert d_seq < 1e-4 and d_fe < 1e-4 and d_tc < 1e-4, (d_seq, d_fe, d_tc)
+    assert e_seq < 2e-4 and e_fe < 2e-4, (e_seq, e_fe)
+
+
+@pytest.mark.parametrize("f16_x3s", ["1", "0"])
 @pytest.mark.parametrize("tx_w", [1, 2])
-def test_f16_unit_kernel_is_position_independent_at_4096_windows(tx_w):
+def test_f16_unit_kernel_is_position_independent_at_4096_windows(tx_w, f16_x3s, monkeypatch):
     """Config 5's encode chunk (4,096 windows: 27 rounds of 5- and 6-window units) checked without the oracle, by a
     property that pins the schedule: every window's outputs depend only on that window (per-window exponents, the
     same chunk order), so encoding a 256-window slice alone (two rounds, quint / hex / quad units) must reproduce its
@@ -188,6 +221,7 @@ def test_f16_unit_kernel_is_position_independent_at_4096_windows(tx_w):
     sd = synth.make_state_dict(synth.DIMS_RAW, synth.DIMS_DIFF)
     g = torch.Generator(device=DEV).manual_seed(11)
     feats = torch.randn((4096, 32, ops.FEAT_DIM), device=DEV, generator=g)
+    monkeypatch.setenv("VGE_F16_X3S", f16_x3s)  # the staggered conv (default) and the unit-table one
     enc = ops.Encoder(sd, device=DEV, compute="f16")
     enc.reserve(4096)
     so.vge_debug_set_tx_windows(tx_w)
@@ -204,7 +238,7 @@ def test_f16_unit_kernel_is_position_independent_at_4096_windows(tx_w):
 
 
 @pytest.mark.parametrize("n", [1, 37, 256, 293, 4096])
-def test_f16_unit_table_built_on_device_matches_host_spec(n):
+def test_f16_unit_table_built_on_device_matches_host_spec(n, monkeypatch):
     """vge_encode builds the unit table on the device (conv_f16w_table_kernel: no host round trip inside encode); it
     must equal the host specification (conv_f16w_schedule via vge_debug_conv_schedule) entry for entry."""
     if not torch.cuda.is_available():
@@ -215,6 +249,7 @@ def test_f16_unit_table_built_on_device_matches_host_spec(n):
     from vge import lib, ops, synth
     so = lib.load()
     sd = synth.make_state_dict(synth.DIMS_RAW, synth.DIMS_DIFF)
+    monkeypatch.setenv("VGE_F16_X3S", "0")  # the unit-table kernel
     enc = ops.Encoder(sd, device=DEV, compute="f16")
     enc.reserve(n)
     enc.encode(torch.zeros((n, 32, ops.FEAT_DIM), device=DEV), tc=False)

@@ -26,7 +26,8 @@ ap.add_argument("--windows", type=int, default=256)
 ap.add_argument("--last", type=int, default=6)
 a = ap.parse_args()
 out_dir = ROOT / "gpurun_out"
-KNAME = {"f32x3": "conv_encoder_x3s_kernel", "f16": "conv_encoder_f16w_kernel",
+KNAME = {"f32x3": "conv_encoder_x3s_kernel",
+         "f16": "conv_encoder_x3s_kernel" if __import__("bench").f16_conv_is_x3s() else "conv_encoder_f16w_kernel",
          "f32": "conv_encoder_kernel("}[a.compute]
 
 

@@ -665,11 +665,13 @@ int vge_encoder_create(const vge_dims* dims, const vge_tensor_view* weights, int
   // VGE_F32X3 runs the staggered conv kernel (vge_encoder_x3s.hip) unless VGE_X3S=0: each block's GroupNorm is folded
   // into the next GEMM -- conv1 of blocks 1..3 and proj packed as W diag(gamma) -- plus the per-row corrections
   // (sums of W gamma and W beta over the taps that fall inside the window; double, then f32)
-  // VGE_F16 with VGE_F16_X3S=1 (and the stem unsplit): the same staggered kernel in single fp16 (hi planes only)
+  // VGE_F16 (with the stem unsplit): the same staggered kernel in single fp16 (hi planes only) unless VGE_F16_X3S=0
+  // selects conv_encoder_f16w_kernel (1..6-window units): conv 0.512 -> 0.489 ms at 256 windows, 6.95-6.99 -> 6.58-6.65
+  // ms per 4,096-window chunk (profiles/ab_r05x_f16_conv.json, ab_r05w_cfg5.json)
   const char* x3s_env = getenv("VGE_X3S");
   const char* f16s_env = getenv("VGE_F16_X3S");
   const char* mix_env = getenv("VGE_F16_MIX");
-  const bool f16_x3s = compute == VGE_F16 && f16s_env && f16s_env[0] == '1' && !((mix_env ? atoi(mix_env) : 2) & 1);
+  const bool f16_x3s = compute == VGE_F16 && !(f16s_env && f16s_env[0] == '0') && !((mix_env ? atoi(mix_env) : 2) & 1);
   const bool x3s = (compute == VGE_F32X3 && !(x3s_env && x3s_env[0] == '0')) || f16_x3s;
   std::vector<std::vector<float>> folded;  // folded weight copies, alive until packed
   struct Off { Mat stem, conv, proj; size_t gnw, gnb, fold; int in_col, d_in, P; };

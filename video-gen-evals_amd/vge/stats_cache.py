@@ -70,7 +70,7 @@ def fingerprint(train_items: Sequence[VideoItem], real_kp_dir: Optional[str], mo
 
 # environment switches that select kernels or change the f32x3 / f16 numerics of the encoder (vge_api.cpp and the
 # kernel launchers read them); a cache written under one setting is a miss under another
-KERNEL_ENV = ("VGE_X3S", "VGE_F16_MIX", "VGE_F16W", "VGE_X3_UNFUSED", "VGE_HOST_PACK", "VGE_TX_W", "VGE_TX_OCC",
+KERNEL_ENV = ("VGE_X3S", "VGE_F16_X3S", "VGE_F16_MIX", "VGE_F16W", "VGE_X3_UNFUSED", "VGE_HOST_PACK", "VGE_TX_W", "VGE_TX_OCC",
               "VGE_QUAD_ALIGN")
 
 
