@@ -18,7 +18,8 @@ sys.path.insert(0, os.path.join(REPO, "tools"))
 
 LIB = os.path.join(REPO, "video-gen-evals_amd", "vge", "libvge.so")
 
-# kernel name fragments: the config-2 headline kernels, the gate detector's own kernels, the generic-shape path
+# kernel name fragments: the config-2 headline kernels, the gate detector's own kernels, the generic-shape path, the
+# extractor GEMM and grouped conv
 HOT = [
     "conv_encoder_x3s_kernel",
     "transformer_x3_kernelILb1ELb1ELi1ELi1E",   # f32x3, one window per workgroup
@@ -32,6 +33,9 @@ HOT = [
     "det_post_kernel",
     "gen_conv_kernel",
     "gen_attn_kernel",
+    "gemm_bf16_kernel",    # the extractors' GEMM (ViT-H, the detector's 1x1 convs): every epilogue / shape variant
+    "gemm2_bf16_kernel",
+    "gconv3_kernel",       # the detector's grouped 3x3 convs
 ]
 
 
