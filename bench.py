@@ -8,13 +8,14 @@
 Workload (config 2 of BASELINE.json, "1 MI355X bf16"): 256 synthetic 32-frame clips per GPU with
 pre-extracted per-frame features (SMPL rotations, betas, 1024-d token, 120-d keypoints) resident in
 HBM.  One step = featurise all windows (HIP) -> HumanActionScorer forward (MFMA) -> per-video AC + TC
-(HIP reductions) -> scores copied to pinned host memory; each chunk's featurise is issued on a side stream once the
-previous encode's conv stage has consumed the feats buffer (vge_encoder_wait_conv), so it overlaps that chunk's
-fusion + transformer, and the per-video scores + host copies run on that side stream too, launched after the next
-step's conv stage and featurise (no marker behind the transformer), with the encodes alternating between two output
-buffers (--pipeline side3, the default; side2: the scores right after the transformer; --pipeline serial /
---serial-featurize: the plain serial order; every step's work, the last step's scores included, stays inside the
-timed region).  ModalityStats and the real-class centroids
+(HIP reductions) -> scores copied to pinned host memory, in that order on one stream (--pipeline serial, the default
+since round 5: the featurise no longer shares the CUs with the transformer, which then runs ~10 % faster, 0.262 vs
+0.288-0.290 ms, for 185.0k-185.4k vs 183.3k-185.0k videos/s, same box, profiles/ab_r05ae_pipeline.json).
+--pipeline side3: each chunk's featurise is issued on a side stream once the previous encode's conv stage has consumed
+the feats buffer (vge_encoder_wait_conv), so it overlaps that chunk's fusion + transformer, and the per-video scores +
+host copies run on that side stream too, launched after the next step's conv stage and featurise, with the encodes
+alternating between two output buffers (side2: the scores right after the transformer); every step's work, the last
+step's scores included, stays inside the timed region in every mode.  ModalityStats and the real-class centroids
 (the real set is sharded over ranks, sufficient statistics all-gathered over RCCL) are built once in
 the setup phase (`setup_s`).  Weak scaling: every rank scores its own 256 clips; no collective in the
 step.  Compute mode: `f32x3` (3xfp16 split-precision MFMA: f32-class results, the reference computes in fp32;
@@ -343,13 +344,14 @@ def main():
                          "the encode stream featurises the next chunk and queues its conv stage, which then takes CUs "
                          "as the transformer's workgroups finish (its hipEvents include that wait, so the conv "
                          "roofline is not measured in this mode); serial = one stream, featurise right before each "
-                         "encode; side3 (default) = side2 with each step's scores launched on the side stream after "
+                         "encode (default); side3 = side2 with each step's scores launched on the side stream after "
                          "the NEXT step's conv (which follows this step's transformer on the encode stream), ahead of "
                          "its featurise, so no marker follows the transformer (measured +0.9-1.1 %% videos/s, same "
                          "box); the last step's scores are launched after the loop, inside the timed region.  "
-                         "Default: side3 (score), serial (cfg5: its occupancy-2 fp16 transformer fills every register "
-                         "of a CU, so an overlapped featurise only waits for its workgroups -- measured 80.1k-80.6k "
-                         "vs 79.5k-79.7k videos/s for side3, same box)")
+                         "Default: serial (score: the overlapped featurise slows the transformer by about its own "
+                         "time, 185.0k-185.4k vs 183.3k-185.0k videos/s for side3, same box, round 5; cfg5: its "
+                         "occupancy-2 fp16 transformer fills every register of a CU, so an overlapped featurise only "
+                         "waits for its workgroups)")
     ap.add_argument("--serial-featurize", action="store_true", help="= --pipeline serial")
     ap.add_argument("--event-every", type=int, default=5,
                     help="record the conv stage's (and featurise's) hipEvents on every k-th timed step, from the first: "
@@ -377,7 +379,7 @@ def main():
     if args.workload == "cfg5" and args.clips == 256:
         args.clips = 10_000
     if args.pipeline is None:
-        args.pipeline = "serial" if args.workload == "cfg5" else "side3"
+        args.pipeline = "serial"
 
     cpu = json.loads(os.environ["VGE_BENCH_CPU_BASELINE"]) if os.environ.get("VGE_BENCH_CPU_BASELINE") else None
     if cpu is None and args.workload == "score" and int(os.environ.get("WORLD_SIZE", "1")) == 1 and \
