@@ -1,4 +1,5 @@
 #!/bin/bash
+# (side4 was an experiment build of bench.py, reverted after this A/B; see profiles/ab_r05ai_pipeline_side4.json)
 # Config 2: the transformer's stage time with the featurise overlapped on the side stream (side3, default) vs serial.
 R="$GRAFT_REPO_ROOT"; cd "$R" && mkdir -p gpurun_out
 for r in 1 2 3 4 5; do
