@@ -102,3 +102,33 @@ def test_bench_gpus_2_launches_two_ranks():
     slowest = min(per)  # every rank scores 256 clips per step, so the slowest rank has the lowest rate
     assert out["value"] == pytest.approx(2 * slowest, rel=1e-9)
     assert out["precision"]["max_abs_ac"] < 1e-4 and out["precision"]["max_abs_tc"] < 1e-4
+
+
+def test_f16_conv_kernel_choice_follows_the_library(monkeypatch):
+    """bench.py names the f16 mode's conv kernel (roofline `kernel`, the PMC entry it accepts) by the rule vge_api.cpp
+    applies: the staggered x3s kernel in single fp16 unless VGE_F16_X3S=0 or the stems are split (VGE_F16_MIX bit 0)."""
+    bench = _bench()
+    monkeypatch.delenv("VGE_F16_X3S", raising=False)
+    monkeypatch.delenv("VGE_F16_MIX", raising=False)
+    assert bench.f16_conv_is_x3s()
+    monkeypatch.setenv("VGE_F16_MIX", "0")
+    assert bench.f16_conv_is_x3s()
+    monkeypatch.setenv("VGE_F16_MIX", "3")
+    assert not bench.f16_conv_is_x3s()
+    monkeypatch.setenv("VGE_F16_MIX", "2")
+    monkeypatch.setenv("VGE_F16_X3S", "0")
+    assert not bench.f16_conv_is_x3s()
+
+
+def test_pmc_traffic_refuses_a_pass_of_the_other_f16_kernel(monkeypatch):
+    """The committed f16 PMC pass counts for the bench line only while it was taken on the kernel the line runs."""
+    bench = _bench()
+    pj = json.loads((REPO / "profiles" / "pmc_conv_encoder.json").read_text())
+    monkeypatch.delenv("VGE_F16_X3S", raising=False)
+    monkeypatch.delenv("VGE_F16_MIX", raising=False)
+    got = bench.pmc_traffic("f16", 256)
+    if pj["f16"].get("source_sha") == bench._kernel_sources_sha():
+        assert (got is not None) == (pj["f16"]["kernel"] == "conv_encoder_x3s_kernel")
+    monkeypatch.setenv("VGE_F16_X3S", "0")
+    if pj["f16"]["kernel"] == "conv_encoder_x3s_kernel":
+        assert bench.pmc_traffic("f16", 256) is None
