@@ -34,6 +34,11 @@ was taken on this tree's kernel sources, else null.  `cpu_baseline` is the oracl
 eval.py in the reference's structure (DataLoader workers=4, bs 32, torch-fp32 on the CPU share) timed on
 this host on a bounded sample before the GPU is touched.  `--workload cfg5` runs config 5 (10k 64-frame
 clips, strong scaling); `tag` config 4's flow; `e2e` config 3.
+
+At N = 1 the default line also carries `e2e`: BASELINE config 3 (1k clips x 32 frames at 256x256: the Faster R-CNN
+gate + TokenHMR and YOLOX + DWPose extractors -> featurise -> encoder -> AC/TC; bench_e2e.py) as one timed step after
+one warm-up, run in a child process after the config-2 measurements, with its own stage_ms, the ViT-H GEMM and gate
+detector rooflines, PMC traffic and CPU baseline (`--no-e2e` skips it).
 """
 from __future__ import annotations
 
@@ -361,6 +366,11 @@ def main():
                     help="e2e: run TokenHMR and DWPose one after the other on one stream (default: two streams)")
     ap.add_argument("--no-detector", action="store_true",
                     help="e2e: skip DWPose's YOLOX person detector (every frame takes the whole-frame pose box)")
+    ap.add_argument("--no-e2e", action="store_true",
+                    help="score at N = 1: skip the nested `e2e` record (config 3, run as a child process after the "
+                         "config-2 line's measurements)")
+    ap.add_argument("--e2e-clips", type=int, default=1000, help="clips of the nested config-3 record (config 3: 1k)")
+    ap.add_argument("--e2e-timeout", type=float, default=420.0, help="seconds the nested config-3 child may take")
     ap.add_argument("--workload", default="score", choices=["score", "e2e", "tag", "cfg5"],
                     help="score: config 2 (default, the bench line); e2e: config 3, frames -> TokenHMR + DWPose -> "
                          "scores (bench_e2e.py; --clips defaults to 8 there); tag: config 4 on pre-extracted "
@@ -422,10 +432,39 @@ def main():
                                                           "roofline", "stage_ms")}
     if rank == 0:
         out["cpu_baseline"] = cpu
+        if args.workload == "score" and world == 1 and not args.no_e2e:
+            out["e2e"] = run_e2e_child(args)
         print(json.dumps(out))
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+
+
+def run_e2e_child(args) -> dict:
+    """BASELINE config 3 -- the north star's "videos/sec on synthetic 32-frame 256x256 clips": frames in HBM -> the
+    Faster R-CNN gate + TokenHMR and YOLOX + DWPose extractors -> featurise -> encoder -> AC/TC (bench_e2e.py;
+    reference path eval.py:350-466 fed by extract_mesh.py:150-241 / process_video.py:59-94), `--e2e-clips` clips, 1
+    timed step after 1 warm-up, with its own stage_ms, rooflines (ViT-H GEMMs, the gate detector), PMC traffic and CPU
+    baseline.  Run as a child process (never exec) after this line's measurements, so its ~40 GB of frames and
+    extractor workspaces do not share the config-2 timing; its heartbeat lines go to stderr.  A failure or timeout is
+    recorded in the returned dict; the config-2 line is printed either way."""
+    import subprocess
+    cmd = [sys.executable, str(Path(__file__).resolve()), "--workload", "e2e", "--clips", str(args.e2e_clips),
+           "--steps", "1", "--warmup", "1", "--cpu-seconds", "15"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    t0 = time.perf_counter()
+    try:
+        r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=None, text=True, timeout=args.e2e_timeout)
+    except subprocess.TimeoutExpired:
+        return {"error": f"timed out after {args.e2e_timeout:.0f} s", "cmd": " ".join(cmd[1:])}
+    wall = time.perf_counter() - t0
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    if r.returncode != 0 or not lines:
+        return {"error": f"exit status {r.returncode}", "cmd": " ".join(cmd[1:]), "stdout_tail": r.stdout[-2000:]}
+    e = json.loads(lines[-1])
+    e["child_wall_s"] = wall
+    e["cmd"] = " ".join(cmd[1:])
+    return e
 
 
 def tx_peak(compute: str, pk: dict) -> float:

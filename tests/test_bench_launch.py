@@ -132,3 +132,15 @@ def test_pmc_traffic_refuses_a_pass_of_the_other_f16_kernel(monkeypatch):
     monkeypatch.setenv("VGE_F16_X3S", "0")
     if pj["f16"]["kernel"] == "conv_encoder_x3s_kernel":
         assert bench.pmc_traffic("f16", 256) is None
+
+
+def test_nested_e2e_record_failure_is_recorded_not_raised():
+    """The config-3 record of the default line runs as a child process (bench.py --workload e2e, 1 step after 1
+    warm-up); when it cannot run (here: no GPU) the record says why and the config-2 line still prints."""
+    if __import__("torch").cuda.is_available():
+        pytest.skip("CPU-only check of the failure path")
+    b = _bench()
+    rec = b.run_e2e_child(SimpleNamespace(e2e_clips=2, e2e_timeout=300.0))
+    assert "error" in rec and rec["error"].startswith("exit status"), rec
+    assert "--workload e2e --clips 2 --steps 1 --warmup 1" in rec["cmd"]
+    json.dumps(rec)

@@ -56,7 +56,7 @@ def test_oracle_small_scores(oracle_run_small, golden_meta_small):
     assert max(abs(ref[v][k] - combined[v][k]) for v in ref for k in ref[v]) < 1e-5
 
 
-def test_load_model_reads_the_checkpoint_shape(golden_dataset_small, monkeypatch):
+def test_load_model_reads_the_checkpoint_shape(golden_dataset_small, monkeypatch, tmp_path):
     """load_model passes the checkpoint's hyper-parameters and picks the exact-f32 path for a non-(256, 8) shape
     (no GPU: the Encoder constructor is intercepted)."""
     from vge import eval as VE
@@ -72,8 +72,15 @@ def test_load_model_reads_the_checkpoint_shape(golden_dataset_small, monkeypatch
     VE.load_model(ckpt, compute="f32x3")
     assert (seen["d_model"], seen["time_layers"], seen["time_heads"], seen["compute"]) == (64, 2, 4, "f32")
     from tests.golden.dataset_spec import golden_state_dict
-    VE.load_model(golden_state_dict("small"), compute="f16")   # a bare state dict: shape from its tensors
-    assert (seen["d_model"], seen["time_layers"], seen["time_heads"], seen["compute"]) == (64, 2, 8, "f32")
+    # a bare state dict takes the reference's defaults (eval.py:139-143), in memory as on disk
+    VE.load_model(golden_state_dict("small"), compute="f16")
+    assert (seen["d_model"], seen["time_layers"], seen["time_heads"], seen["compute"]) == (256, 4, 8, "f16")
+    torch.save({k: torch.as_tensor(np.asarray(v)) for k, v in golden_state_dict("small").items()}, tmp_path / "bare.pt")
+    VE.load_model(str(tmp_path / "bare.pt"), compute="f16")
+    assert (seen["d_model"], seen["time_layers"], seen["time_heads"], seen["compute"]) == (256, 4, 8, "f16")
+    from tests.golden.dataset_spec import SMALL_HP
+    VE.load_model((golden_state_dict("small"), dict(SMALL_HP)), compute="f16")
+    assert (seen["d_model"], seen["time_layers"], seen["time_heads"], seen["compute"]) == (64, 2, 4, "f32")
     VE.load_model(golden_state_dict("kp"), compute="f16")
     assert (seen["d_model"], seen["time_layers"], seen["compute"]) == (256, 4, "f16")
 

@@ -238,15 +238,31 @@ def test_grouped_conv_kernel_vs_torch(gw, stride, C, H, W):
     assert bool((err <= bound).all()), float((err - bound).max())
 
 
-def test_chunk_is_capped_by_32bit_row_offsets(run):
-    """The conv kernels address a layer's rows through 32-bit byte offsets: vge_frcnn_reserve refuses a chunk whose
-    largest activation reaches 2 GiB (at 800 px: 104 frames) and FrcnnDetector caps its chunk there."""
+def test_chunk_cap_and_128_frame_chunk_matches_64(run):
+    """Activations are addressed through 64-bit offsets (the 1x1 convs' GEMM epilogue included), so a chunk is bounded
+    only by int32 row / thread counts: 838 frames at 800 px (vge_frcnn_reserve refuses one more before allocating).
+    A 128-frame chunk -- T1 of res3.0's conv1 then holds 2.6e9 elements, past the old 2 GiB cap of 104 frames -- gives
+    the same detections, bit for bit, as the same frames in 64-frame chunks (every kernel is per frame or per output
+    element with a fixed K order, and the tuner's conv variants are bit-identical)."""
+    from vge import synth
     from vge.frcnn import FrcnnDetector
-    det = FrcnnDetector(run["sd"], run["cfg"], device=DEV, chunk=1000)
-    try:
-        cap = det.max_chunk(256, 256)
-        assert det.chunk == cap == 104, (det.chunk, cap)
-        assert det.lib.vge_frcnn_reserve(det.h, cap + 1, 256, 256) == 1      # VGE_ERR_ARG
-        assert det.lib.vge_frcnn_reserve(det.h, cap, 256, 256) == 0
-    finally:
-        det.close()
+    frames = torch.from_numpy(synth.make_frame_pool(9300, 128)).to(DEV)
+    outs = {}
+    for chunk in (128, 64):
+        det = FrcnnDetector(run["sd"], run["cfg"], device=DEV, chunk=chunk)
+        try:
+            if chunk == 128:
+                cap = det.max_chunk(256, 256)
+                assert cap == 838, cap
+                assert det.lib.vge_frcnn_reserve(det.h, cap + 1, 256, 256) == 1      # VGE_ERR_ARG, nothing allocated
+            assert det.chunk == chunk
+            o = det.detect(frames)
+            torch.cuda.synchronize()
+            outs[chunk] = {k: v.cpu() for k, v in o.items()}
+        finally:
+            det.close()
+        torch.cuda.empty_cache()
+    for k in outs[64]:
+        assert torch.equal(outs[128][k], outs[64][k]), k
+    print(f"128-frame chunk == 2 x 64: {int(outs[64]['n_dets'].sum())} instances, "
+          f"{int((outs[64]['n_person'] == 1).sum())} single-person frames")

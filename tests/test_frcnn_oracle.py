@@ -141,3 +141,23 @@ def test_oracle_detector_runs_end_to_end_small():
         assert (b[:, 0] >= 0).all() and (b[:, 2] <= 80).all() and (b[:, 3] <= 96).all()
         assert (b[:, 2] > b[:, 0]).all() and (b[:, 3] > b[:, 1]).all()
         assert OF.gate_persons(r) == int(((r["classes"] == 0) & (r["scores"] > 0.5)).sum())
+
+
+def test_detector_refuses_a_score_threshold_its_candidate_slots_cannot_hold():
+    """det_post_kernel keeps 4 candidate classes per proposal, exact only for score_thresh >= 0.2 (five classes above
+    0.2 would sum past 1): vge_frcnn_create refuses a lower threshold (detectron2's own default, 0.05, included) with
+    VGE_ERR_ARG before touching weights or the GPU; the reference's 0.25 passes the check."""
+    import ctypes as C
+    import dataclasses
+    from vge import lib as L
+    from vge.frcnn import FRCNN_X101, _cfg_c, _sig
+    so = _sig(L.load())
+    for thr in (0.05, 0.19, 1.5):
+        h = C.c_void_p()
+        cc = _cfg_c(dataclasses.replace(FRCNN_X101, score_thresh=thr))
+        assert so.vge_frcnn_create(C.byref(cc), None, 0, C.byref(h)) == 1
+        assert b"score_thresh" in so.vge_last_error()
+    h = C.c_void_p()
+    cc = _cfg_c(FRCNN_X101)
+    rc = so.vge_frcnn_create(C.byref(cc), None, 0, C.byref(h))   # no weights: fails on the first missing tensor
+    assert rc != 0 and b"score_thresh" not in so.vge_last_error()

@@ -19,6 +19,7 @@
 //                        RGB frame, BGR mean/std normalisation -> NHWC bf16 with 8 channels (3 used).
 //   letterbox_focus_kernel  onnxdet.preprocess (resize by r, pad 114) + YOLOX Focus space-to-depth -> 16 ch.
 #include "vge_common.h"
+#include "vge_lds_attr.h"
 #include "vge_cnn.h"
 #include "vge_gemm.h"
 
@@ -1203,13 +1204,8 @@ static int persistent_grid(int ntiles) {  // one workgroup per CU, a multiple of
 template <int BN, int ACT, int OUT, int RES, int BM = C2_M>
 static hipError_t conv2p_go(const ConvArgs& a, hipStream_t s) {
   constexpr int BYTES = C2Cfg<BN, BM>::RING;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv2p_bf16_kernel<BN, ACT, OUT, RES, BM>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, BYTES);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  static LdsAttrOnce attr;
+  if (const hipError_t e = attr(reinterpret_cast<const void*>(&conv2p_bf16_kernel<BN, ACT, OUT, RES, BM>), BYTES); e != hipSuccess) return e;
   const int ntiles = ((a.M + BM - 1) / BM) * ((a.Cout + BN - 1) / BN);
   const int grid = g_conv_persist == 2 ? ntiles : persistent_grid(ntiles);  // 2: A/B of the schedule alone
   hipLaunchKernelGGL((conv2p_bf16_kernel<BN, ACT, OUT, RES, BM>), dim3(grid), dim3(512), BYTES, s, a);
@@ -1226,13 +1222,8 @@ static hipError_t conv2_go(const ConvArgs& a, hipStream_t s, int pmode) {
   if constexpr (RES == RES_NONE)  // residual epilogues stay on conv2_bf16_kernel (their loads need vmcnt drains)
     if (pmode < 0 ? g_conv_persist : pmode) return conv2p_go<BN, ACT, OUT, RES>(a, s);
   constexpr int BYTES = C2Cfg<BN>::LDS;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv2_bf16_kernel<BN, ACT, OUT, RES>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, BYTES);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  static LdsAttrOnce attr;
+  if (const hipError_t e = attr(reinterpret_cast<const void*>(&conv2_bf16_kernel<BN, ACT, OUT, RES>), BYTES); e != hipSuccess) return e;
   const int grid = ((a.M + C2_M - 1) / C2_M) * ((a.Cout + BN - 1) / BN);
   hipLaunchKernelGGL((conv2_bf16_kernel<BN, ACT, OUT, RES>), dim3(grid), dim3(512), BYTES, s, a);
   return hipGetLastError();
@@ -1247,13 +1238,8 @@ static hipError_t conv1_go(const ConvArgs& a, int grid, hipStream_t s) {
   constexpr int LDS = CV_ST * (BM * CV_K * 2 + TN * CV_K * 2);
   constexpr int EPI = 64 * (TN + 4) * 4;
   constexpr int BYTES = LDS > EPI ? LDS : EPI;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&conv_bf16_kernel<TN, ACT, OUT, RES, BM>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, BYTES);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  static LdsAttrOnce attr;
+  if (const hipError_t e = attr(reinterpret_cast<const void*>(&conv_bf16_kernel<TN, ACT, OUT, RES, BM>), BYTES); e != hipSuccess) return e;
   hipLaunchKernelGGL((conv_bf16_kernel<TN, ACT, OUT, RES, BM>), dim3(grid), dim3(256), BYTES, s, a);
   return hipGetLastError();
 }
@@ -1402,14 +1388,9 @@ hipError_t launch_spp_pool(void* buf, long ld, int n_img, int H, int W, int C, i
   const long n = (long)n_img * H * W * (C / 8);
   if (n == 0) return hipSuccess;
   if (k0 == 5 && k1 == 9 && k2 == 13 && H * W <= SPP_LDS_MAX_HW) {
-    static bool attr = false;
+    static LdsAttrOnce attr;
     const int bytes = 3 * SPP_LDS_MAX_HW * 8 * 16;
-    if (!attr) {
-      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&spp_lds_kernel),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-      if (e != hipSuccess) return e;
-      attr = true;
-    }
+    if (const hipError_t e = attr(reinterpret_cast<const void*>(&spp_lds_kernel), bytes); e != hipSuccess) return e;
     hipLaunchKernelGGL(spp_lds_kernel, dim3(n_img, (C + 63) / 64), dim3(256), bytes, s, static_cast<bf16*>(buf), ld, H,
                        W, C);
     return hipGetLastError();

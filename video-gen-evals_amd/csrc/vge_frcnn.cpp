@@ -264,6 +264,13 @@ bool cfg_ok(const vge_frcnn_config& c, std::string& why) {
   if (c.num_classes < 1 || c.num_classes + 1 > 128) return why = "num_classes must be in [1, 127]", false;
   if (c.det_per_img < 1 || c.det_per_img > vge::FR_MAXK) return why = "det_per_img must be in [1, 1024]", false;
   if (!pow2(c.fc_dim) || c.fc_dim < 64) return why = "fc_dim must be a power of two >= 64", false;
+  // det_post_kernel keeps at most 4 candidate classes per proposal (vge_frcnn_kernels.hip, FR_MAXCAND = 4,096 slots):
+  // exact when no proposal can have 5 classes above the threshold, i.e. 5 x score_thresh >= 1 (softmax sums to 1);
+  // the reference's gate runs at 0.25 (mesh_generator.py:71)
+  if (!(c.score_thresh >= 0.2f && c.score_thresh < 1.f))
+    return why = "score_thresh must be in [0.2, 1): at most 4 classes per proposal pass it (det_post_kernel)", false;
+  if (!(c.nms_thresh > 0.f && c.nms_thresh <= 1.f) || !(c.rpn_nms > 0.f && c.rpn_nms <= 1.f))
+    return why = "NMS thresholds must be in (0, 1]", false;
   return true;
 }
 
@@ -358,11 +365,13 @@ int vge_frcnn_reserve(vge_frcnn* m, int chunk, int H, int W) {
   if (chunk <= m->chunk && H == m->rH && W == m->rW) return VGE_OK;
   int sh[15];
   vge_frcnn_shapes(m, H, W, sh);
-  {  // the conv kernels address a layer's input / output rows through 32-bit byte offsets: the largest activation of
-     // a chunk (the stem output, res2's, P2's) must stay under 2 GiB
+  {  // index widths: every kernel addresses activations through 64-bit offsets; what stays 32-bit is a layer's row
+     // count (n x h x w, the GEMM M) and the thread count of the elementwise kernels (resize: one per padded pixel,
+     // pool / upsample: one per 8 channels of a pixel) -- both must stay under 2^31 for the chunk
     const size_t s2 = (size_t)(sh[2] / 2) * (sh[3] / 2), s4 = (size_t)sh[4] * sh[5];
-    const size_t per = std::max({(size_t)sh[2] * sh[3] * 8, s2 * m->c.stem_ch,
-                                 s4 * std::max({m->c.res2_ch, m->c.groups * m->c.width_per_group, m->c.fpn_ch})}) * 2;
+    const size_t w0 = (size_t)m->c.groups * m->c.width_per_group;
+    const size_t per = std::max({(size_t)sh[2] * sh[3], s2 * m->c.stem_ch / 8,
+                                 s4 * std::max({(size_t)m->c.res2_ch, 2 * w0, (size_t)m->c.fpn_ch}) / 8});
     if ((size_t)chunk * per >= (1ull << 31))
       return fail(VGE_ERR_ARG, "vge_frcnn_reserve: chunk too large for " + std::to_string(H) + " x " + std::to_string(W) +
                                    " frames (at most " + std::to_string(((1ull << 31) - 1) / per) + ")");

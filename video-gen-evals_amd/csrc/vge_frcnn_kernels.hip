@@ -22,6 +22,7 @@
 // Every float expression keeps its operations separately rounded (no contraction), as the oracle (oracle/frcnn.py)
 // evaluates them.
 #include "vge_common.h"
+#include "vge_lds_attr.h"
 #include "vge_frcnn_k.h"
 
 #pragma clang fp contract(off)
@@ -791,13 +792,8 @@ hipError_t launch_rpn_select(const RpnLevels& lv, int n, float img_h, float img_
 hipError_t launch_rpn_nms(const RpnLevels& lv, const float* sel, const float* sel_max, int n, float thr, float* kept,
                           int* kcount, hipStream_t s) {
   if (n == 0) return hipSuccess;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&rpn_nms_kernel),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, NMS_LDS);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  static LdsAttrOnce attr;
+  if (const hipError_t e = attr(reinterpret_cast<const void*>(&rpn_nms_kernel), NMS_LDS); e != hipSuccess) return e;
   hipLaunchKernelGGL(rpn_nms_kernel, dim3(n, 5), dim3(1024), NMS_LDS, s, lv, sel, sel_max, thr, kept, kcount);
   return hipGetLastError();
 }

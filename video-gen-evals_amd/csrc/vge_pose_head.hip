@@ -12,6 +12,7 @@
 //                        normalisation (/ W, / H; hand points with score < 0.3 -> -1, body points unmasked) +
 //                        flatten_first_person_no_padding
 #include "vge_common.h"
+#include "vge_lds_attr.h"
 #include "vge_cnn.h"
 
 #include <algorithm>
@@ -439,25 +440,15 @@ hipError_t launch_gau_attn(const float* uv, int n_inst, int K, int E, int S, con
   }
   const size_t mb = gau_mfma_lds_bytes(K, S);
   if (!use_valu && K <= GAU_M_TILES * 32 && S % 2 == 0 && E % 128 == 0 && mb <= 160 * 1024) {
-    static bool mattr = false;
-    if (!mattr) {
-      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gau_mfma_kernel),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-      if (e != hipSuccess) return e;
-      mattr = true;
-    }
+    static LdsAttrOnce mattr;
+    if (const hipError_t e = mattr(reinterpret_cast<const void*>(&gau_mfma_kernel), 160 * 1024); e != hipSuccess) return e;
     hipLaunchKernelGGL(gau_mfma_kernel, dim3(n_inst), dim3(256), mb, s, uv, K, E, S, gamma, beta,
                        (float)std::sqrt((double)S), static_cast<bf16*>(out));
     return hipGetLastError();
   }
   const size_t bytes = gau_lds_bytes(S);
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&gau_attn_kernel<GAU_KMAX>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  static LdsAttrOnce attr;
+  if (const hipError_t e = attr(reinterpret_cast<const void*>(&gau_attn_kernel<GAU_KMAX>), 160 * 1024); e != hipSuccess) return e;
   hipLaunchKernelGGL(gau_attn_kernel<GAU_KMAX>, dim3(n_inst), dim3(256), bytes, s, uv, K, E, S, gamma, beta,
                      (float)std::sqrt((double)S), static_cast<bf16*>(out));
   return hipGetLastError();

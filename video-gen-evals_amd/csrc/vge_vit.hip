@@ -23,6 +23,7 @@
 //   softmax_rows_kernel, readout_kernel (6D -> rotation matrix, mean-pose residuals), small helpers.
 #include "vge_common.h"
 #include "vge_gemm.h"
+#include <atomic>
 #include <cstdlib>
 
 #ifndef VGE_GABL
@@ -260,7 +261,7 @@ __global__ void __launch_bounds__(64 * NW, 1) gemm_bf16_kernel(GemmBf16Args g) {
   auto grow_of = [&](int half, int it) { return m0 + wm * 128 + half * 64 + it * RPI + lr; };
   auto rowload = [&](int half, int it) -> floatx4 {
     const int grow = PM ? min(grow_of(half, it), g.M - 1) : grow_of(half, it);  // (PM: rows past M are not stored)
-    if constexpr (EPI == GE_RES_F32) return *reinterpret_cast<const floatx4*>(g.res + (grow * (int)g.ldr + gcol));
+    if constexpr (EPI == GE_RES_F32) return *reinterpret_cast<const floatx4*>(g.res + ((long)grow * g.ldr + gcol));
     if constexpr (RB) {
       const bf16x4 r = *reinterpret_cast<const bf16x4*>(g.resb + ((long)grow * g.ldr + gcol));
       return floatx4{(float)r[0], (float)r[1], (float)r[2], (float)r[3]};
@@ -298,7 +299,7 @@ __global__ void __launch_bounds__(64 * NW, 1) gemm_bf16_kernel(GemmBf16Args g) {
       const int rl = it * RPI + lr;
       const int grow = grow_of(half, it);
       floatx4 v = *reinterpret_cast<const floatx4*>(my + rl * WC + c4) + bb;
-      const int o = grow * (int)g.ldo + gcol;
+      const long o = (long)grow * g.ldo + gcol;  // 64-bit: a 1x1 conv's output may pass 2^31 elements
       if constexpr (RB || EPI == GE_RELU_BF16) {  // the 1x1 conv epilogues: bias (+ bf16 residual) (+ ReLU) -> bf16
         if constexpr (RB) {
           v += (it < NPF) ? rr[it % NPF] : rowload(half, it);
@@ -960,7 +961,23 @@ void launch_gemm2(int epi, const GemmBf16Args& g, hipStream_t s) {
   }
 }
 
+hipError_t vit_kernels_setup_dev();
+
+// the dynamic-LDS attributes of every GEMM / attention kernel of this file, once per device (any launch path may be the
+// first on a device: the extractors' create calls, the conv tuner's GEMM candidate, the op-level test hooks)
 hipError_t vit_kernels_setup() {
+  static std::atomic<unsigned long long> done{0};
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  const unsigned long long bit = 1ull << (dev & 63);
+  if (done.load(std::memory_order_acquire) & bit) return hipSuccess;
+  e = vit_kernels_setup_dev();
+  if (e == hipSuccess) done.fetch_or(bit, std::memory_order_release);
+  return e;
+}
+
+hipError_t vit_kernels_setup_dev() {
   hipError_t e = gemm_setup_nw<8>();
   if (e == hipSuccess) e = gemm2_setup<false>();
   if (e == hipSuccess) e = gemm2_setup<true>();
@@ -1012,9 +1029,9 @@ hipError_t launch_gemm_bf16(int epi, const GemmBf16& a, hipStream_t s) {
   g.M = a.M; g.N = a.N; g.K = a.K; g.tokens = a.tokens;
   g.resb = reinterpret_cast<const bf16*>(a.resb);
   const bool rb = epi == GE_RESB_BF16 || epi == GE_RESB_RELU_BF16;
-  if (a.M < 1 || a.N % GB_N || a.K % 64 || (long)a.M * a.ldo >= (1L << 31) ||
-      ((a.res || rb) && (long)a.M * a.ldr >= (1L << 31)) || (rb && !a.resb) || (epi == GE_PE_F32 && a.tokens != AT_T))
+  if (a.M < 1 || a.N % GB_N || a.K % 64 || (rb && !a.resb) || (epi == GE_PE_F32 && a.tokens != AT_T))
     return hipErrorInvalidValue;
+  if (const hipError_t e = vit_kernels_setup(); e != hipSuccess) return e;
   if (g_gemm_waves == 0) {
     const char* e = getenv("VGE_GEMM_WAVES");
     g_gemm_waves = (e && (atoi(e) == 2 || atoi(e) == 4 || atoi(e) == 8 || atoi(e) == 16)) ? atoi(e) : 1;

@@ -115,12 +115,11 @@ def load_model(model_path, dims_map_raw=None, dims_map_diff=None, device="cuda",
                                         f"are built for the five-modality layout and its keypoint-less four; "
                                         f"VGE_ERR_UNSUPPORTED)")
     if isinstance(model_path, dict):
-        # a bare state dict: d_model and the layer count follow from its tensors (cls [1,1,d], temporal.layers.N.*);
-        # the head count is not recoverable from weights (pass (state_dict, hyper-parameters) for one other than 8)
+        # a bare state dict takes the reference's defaults (eval.py:139-143: checkpoint.get("d_model", 256), 4 layers,
+        # 8 heads), exactly as the same dict saved to a .pt file does (_load_state_dict); a checkpoint of another
+        # shape passes its hyper-parameters: (state_dict, {"d_model": .., "time_layers": .., "time_heads": ..})
         sd = model_path
-        layers = {int(k.split(".")[2]) for k in sd if k.startswith("temporal.layers.")}
-        hp = {"d_model": int(np.asarray(sd["cls"]).shape[-1]) if "cls" in sd else 256,
-              "time_layers": max(layers) + 1 if layers else 4, "time_heads": 8}
+        hp = {"d_model": 256, "time_layers": 4, "time_heads": 8}
     elif isinstance(model_path, tuple):  # (state_dict, hyper-parameters) as _load_state_dict returns them
         sd, hp = model_path
     else:

@@ -132,8 +132,9 @@ def _flops(cfg: FrcnnConfig, hp: int, wp: int) -> Tuple[float, float]:
 class FrcnnDetector:
     """detectron2 DefaultPredictor(faster_rcnn_X_101_32x8d_FPN_3x) resident in HBM: FrozenBN-folded bf16 NHWC
     weights + a chunk workspace.  chunk: frames per workspace pass (larger chunks fill the GPU better: 256 frames of
-    256 x 256 take 260 / 252 / 244 ms at chunks of 32 / 32 / 64 on one box); capped by the conv kernels' 32-bit row
-    offsets (`max_chunk`: 104 frames at detectron2's 800-pixel size)."""
+    256 x 256 take 260 / 252 / 244 ms at chunks of 32 / 32 / 64 on one box); capped where a layer's row count or an
+    elementwise kernel's thread count would pass 2^31 (`max_chunk`: 838 frames at detectron2's 800-pixel size; every
+    activation is addressed through 64-bit offsets)."""
 
     def __init__(self, state_dict: Dict[str, np.ndarray], cfg: FrcnnConfig = FRCNN_X101, device="cuda",
                  chunk: int = 64, frame_hw: Tuple[int, int] = (256, 256)):
@@ -155,12 +156,13 @@ class FrcnnDetector:
             self.frame_hw = (int(frame_hw[0]), int(frame_hw[1]))
 
     def max_chunk(self, H: int, W: int) -> int:
-        """The largest chunk vge_frcnn_reserve accepts for H x W frames (every activation of a chunk under 2 GiB)."""
+        """The largest chunk vge_frcnn_reserve accepts for H x W frames (rows per layer and threads per elementwise
+        launch under 2^31, as vge_frcnn_reserve checks)."""
         sh = self.shapes(H, W)
         (hp, wp), (h4, w4) = sh["padded"], sh["levels"][0]
         c = self.cfg
-        per = max(hp * wp * 8, (hp // 2) * (wp // 2) * c.stem_ch,
-                  h4 * w4 * max(c.res2_ch, c.groups * c.width_per_group, c.fpn_ch)) * 2
+        per = max(hp * wp, (hp // 2) * (wp // 2) * c.stem_ch // 8,
+                  h4 * w4 * max(c.res2_ch, 2 * c.groups * c.width_per_group, c.fpn_ch) // 8)
         return max(1, ((1 << 31) - 1) // per)
 
     def shapes(self, H: int, W: int) -> Dict[str, object]:

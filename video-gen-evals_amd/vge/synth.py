@@ -469,8 +469,9 @@ def make_yolox_state_dict(cfg, seed: int = SEED_WEIGHTS + 30, gain: float = 1.0)
 # saturated (score = objectness), one common shift of the objectness logits (the anchors' ranking, hence which boxes
 # NMS keeps, is unchanged) puts the 0.5 threshold between the first and the second kept box of as many pool frames
 # as possible, and box sizes are person-like (about GATE_BOX_STRIDES (w, h) strides).  GATE_OBJ_SHIFT is measured on
-# make_frame_pool's frames by tools/yolox_gate_calib.py on the GPU (the detector runs in bf16 there);
-# VGE_GATE_OBJ_SHIFT overrides it for a calibration run.
+# make_frame_pool's frames on the GPU (the detector runs in bf16 there; it was the round-4 gate, whose calibration
+# script went with it -- the current gate is the Faster R-CNN, tools/frcnn_gate_calib.py); VGE_GATE_OBJ_SHIFT overrides
+# it for a calibration run.
 GATE_OBJ_SHIFT = float(os.environ.get("VGE_GATE_OBJ_SHIFT", "3.911"))
 GATE_BOX_STRIDES = (6.0, 60.0)
 
