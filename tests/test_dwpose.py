@@ -229,6 +229,39 @@ def test_conv_wide_tile_residual_matches_default(D, n, H, W, Cin, Cout, k, res):
 
 
 @gpu
+@pytest.mark.parametrize("n,H,W,Cin,Cout,act", [
+    (64, 25, 25, 1024, 1024, "relu"),   # the detector's res4 conv1 at a 64-frame chunk (628 tiles, ragged last row tile)
+    (48, 50, 50, 256, 256, "none"),     # K = 256: the shortest K the persistent ring takes (8 stages per tile)
+    (16, 100, 100, 256, 512, "relu"),   # res3.0 conv1's shape class
+])
+def test_conv_1x1_persistent_gemm_variant_matches_default(D, n, H, W, Cin, Cout, act):
+    """Variant 10 (the 1x1 conv on the persistent GEMM, gemmp_bf16_kernel, a tuner candidate where it applies) against
+    the default conv kernel: bit-identical, including the partial last row tile (its stores fall outside the tile's
+    buffer range); on a shape with fewer tiles than CUs the forced variant is refused, not run."""
+    import ctypes as C
+    from vge import lib as Lb
+    lib = Lb.load()
+    lib.vge_debug_set_conv_variant.argtypes = [C.c_int]
+    x = _bf((n, H, W, Cin), seed=41).to(DEV)
+    w = _bf((Cout, Cin, 1, 1), (2.0 / Cin) ** 0.5, seed=42).to(DEV)
+    b = (torch.randn(Cout, generator=torch.Generator().manual_seed(43)) * 0.1).to(DEV)
+    outs = []
+    try:
+        for force in (0, 10):
+            lib.vge_debug_set_conv_variant(force)
+            outs.append(D.conv_bf16(x, w, b, stride=1, pad=0, act=act))
+            torch.cuda.synchronize()
+        lib.vge_debug_set_conv_variant(10)
+        with pytest.raises(Exception):
+            D.conv_bf16(x[:1], w, b, stride=1, pad=0, act=act)
+            torch.cuda.synchronize()
+    finally:
+        lib.vge_debug_set_conv_variant(0)
+    assert torch.isfinite(outs[0].float()).all()
+    assert torch.equal(outs[0], outs[1]), (outs[0].float() - outs[1].float()).abs().max().item()
+
+
+@gpu
 def test_conv_bf16_rejects_bad_shapes(D):
     import ctypes as C
     from vge import lib as Lb

@@ -163,3 +163,30 @@ def test_extractor_vs_oracle(H, wide):
     # a second call with fewer frames reuses the workspace and gives the same rows
     again = ex.extract(torch.from_numpy(frames[:2]).to(DEV))
     assert torch.equal(again["vit"].cpu(), out["vit"][:2])
+
+
+@gpu
+@pytest.mark.parametrize("epi", ["bf16", "gelu_bf16"])
+@pytest.mark.parametrize("M,N,K", [(20480, 1280, 1280), (49152, 5120, 1280), (12288, 1280, 5120)])
+def test_gemm_persistent_matches_one_tile_kernel(H, M, N, K, epi):
+    """gemmp_bf16_kernel (one workgroup per CU, one continuous LDS ring across its tiles, the epilogue from registers
+    under the next tile's first loads) against the one-tile kernel: the same 16x16x32 MFMAs in the same K order and the
+    same epilogue arithmetic (bias, then the activation, then one bf16 rounding) -> bit-identical, on the ViT-H shapes
+    (qkv-like, fc1, fc2-like K) with more tiles than CUs."""
+    import ctypes as C
+    from vge import lib as Lb
+    lib = Lb.load()
+    lib.vge_debug_set_gemm_persist.argtypes = [C.c_int]
+    A = _bf((M, K), 1.0, 11).to(DEV)
+    W = _bf((N, K), K ** -0.5, 12).to(DEV)
+    bias = (torch.randn(N, generator=torch.Generator().manual_seed(13)) * 0.1).to(DEV)
+    outs = []
+    try:
+        for p in (0, 1):
+            lib.vge_debug_set_gemm_persist(p)
+            outs.append(H.gemm_bf16(A, W, epi, bias=bias))
+            torch.cuda.synchronize()
+    finally:
+        lib.vge_debug_set_gemm_persist(0)
+    assert torch.isfinite(outs[0].float()).all()
+    assert torch.equal(outs[0], outs[1]), (outs[0].float() - outs[1].float()).abs().max().item()

@@ -19,12 +19,13 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--frames", type=int, default=256)
 ap.add_argument("--rounds", type=int, default=5)
 ap.add_argument("--only", default="", help="one shape name (qkv/proj/fc1/fc2)")
-ap.add_argument("--waves", default="w8,w4,lib", help="variants to run (w8: 8 waves on 32x32x16, w8s: on 16x16x32, w2: gemm2, auto: the default)")
+ap.add_argument("--waves", default="w8,w4,lib", help="variants to run (w8: 8 waves on 32x32x16, w8s: on 16x16x32, w2: gemm2, "
+                                                     "auto: the default, p: the persistent kernel gemmp where it applies)")
 a = ap.parse_args()
 M = a.frames * 192
 shapes = {"qkv": (M, 3840, 1280, "bf16"), "proj": (M, 1280, 1280, "res_f32"), "fc1": (M, 5120, 1280, "gelu_bf16"),
           "fc2": (M, 1280, 5120, "res_f32")}
-NW = {"w8": 8, "w4": 4, "w8s": 16, "w2": 2, "auto": 1}
+NW = {"w8": 8, "w4": 4, "w8s": 16, "w2": 2, "auto": 1, "p": 1}
 res = {}
 g = torch.Generator(device="cuda").manual_seed(0)
 for name, (m, n, k, epi) in shapes.items():
@@ -41,6 +42,7 @@ for name, (m, n, k, epi) in shapes.items():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             if which != "lib":
                 so.vge_debug_set_gemm_waves(NW[which])
+                so.vge_debug_set_gemm_persist(1 if which == "p" else 0)
             e0.record()
             if which != "lib":
                 H.gemm_bf16(A, W, epi, bias=bias, res=r, out=out)
@@ -53,6 +55,7 @@ for name, (m, n, k, epi) in shapes.items():
         outs = {}
         for which in [w for w in t if w != "lib"]:
             so.vge_debug_set_gemm_waves(NW[which])
+            so.vge_debug_set_gemm_persist(1 if which == "p" else 0)
             o = torch.empty_like(out)
             if r is not None:
                 o2 = r.clone()
@@ -74,4 +77,5 @@ for name, (m, n, k, epi) in shapes.items():
         res[name][which + "_ms_med"] = v[len(v) // 2]
         res[name][which + "_tflops"] = fl / v[len(v) // 2] / 1e9
     so.vge_debug_set_gemm_waves(1)
+    so.vge_debug_set_gemm_persist(0)
 print(json.dumps(res, indent=1))

@@ -1276,6 +1276,20 @@ int conv_gemm_epi(const ConvLaunch& c) {
   return -1;
 }
 
+bool conv_gemm_persist_ok(const ConvLaunch& c) {
+  const int epi = conv_gemm_epi(c);
+  if (epi < 0) return false;
+  GemmBf16 g{};
+  g.lda = c.ldx;
+  g.ldw = c.Kp;
+  g.ldo = c.ldo;
+  g.bias = c.bias;
+  g.M = c.n_img * ((c.H + 2 * c.pad - c.KH) / c.stride + 1) * ((c.W + 2 * c.pad - c.KW) / c.stride + 1);
+  g.N = c.Cout;
+  g.K = c.Cin;
+  return gemm_persist_ok(epi, g);
+}
+
 hipError_t launch_conv_bf16(const ConvLaunch& c, hipStream_t s) {
   ConvArgs a;
   a.x = static_cast<const bf16*>(c.x);
@@ -1304,7 +1318,7 @@ hipError_t launch_conv_bf16(const ConvLaunch& c, hipStream_t s) {
   a.gslice = c.gslice;
   int tn = c.tn, pmode = -1;
   int variant = c.variant == 0 && g_conv_force > 0 && !c.gslice ? g_conv_force : c.variant;
-  if (variant == 9) {  // the GEMM kernel (tuner candidate, or forced by vge_debug_set_conv_variant(9))
+  if (variant == 9 || variant == 10) {  // the GEMM kernel (tuner candidates, or forced by vge_debug_set_conv_variant)
     const int epi = conv_gemm_epi(c);
     if (epi >= 0) {
       GemmBf16 g{};
@@ -1320,9 +1334,13 @@ hipError_t launch_conv_bf16(const ConvLaunch& c, hipStream_t s) {
       g.M = a.M;
       g.N = c.Cout;
       g.K = c.Cin;
+      if (variant == 10) {  // its persistent form (one workgroup per CU, the epilogue under the next tile's loads)
+        if (gemm_persist_ok(epi, g)) return launch_gemm_bf16_persistent(epi, g, s);
+        if (c.variant == 10) return hipErrorInvalidValue;
+      }
       return launch_gemm_bf16(epi, g, s);
     }
-    if (c.variant == 9) return hipErrorInvalidValue;
+    if (c.variant == 9 || c.variant == 10) return hipErrorInvalidValue;
     variant = 0;  // forced globally: layers the GEMM cannot take keep the default kernel
   }
   // grouped slices run on the 128- / 256-row kernel only, with the slice width as the column tile

@@ -30,5 +30,10 @@ struct GemmBf16 {
 };
 
 hipError_t launch_gemm_bf16(int epi, const GemmBf16& a, hipStream_t s);
+// the persistent form (gemmp_bf16_kernel: one workgroup per CU, one continuous LDS ring across tiles, the epilogue
+// from registers under the next tile's first loads) for the residual-free bf16 epilogues; hipErrorInvalidValue where
+// it does not apply (gemm_persist_ok)
+hipError_t launch_gemm_bf16_persistent(int epi, const GemmBf16& a, hipStream_t s);
+bool gemm_persist_ok(int epi, const GemmBf16& a);
 
 }  // namespace vge

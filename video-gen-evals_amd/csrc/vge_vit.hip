@@ -36,6 +36,7 @@ namespace {
 typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned uintx2_t __attribute__((ext_vector_type(2)));
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 // ------------------------------------------------------------------------------------------- GEMM
@@ -326,6 +327,214 @@ __global__ void __launch_bounds__(64 * NW, 1) gemm_bf16_kernel(GemmBf16Args g) {
       }
     }
   }
+}
+
+// ------------------------------------------------------------- GEMM, persistent (gemmp)
+// The 16x16x32 8-wave tile of gemm_bf16_kernel (SH = 1), persistent: one workgroup per CU walks its tiles (virtual
+// block b + i G through gb_xcd_remap, G a multiple of 8, so an XCD's workgroups take consecutive tiles of that XCD's
+// range at a time, as the one-tile kernel's do) through ONE continuous 5-slot ring: the next tile's first four stages
+// are issued during this tile's last four steps, and the epilogue -- bias, GELU / ReLU, bf16, 8-B stores straight from
+// the accumulators after a quad transpose (lane i of a quad takes row i, four consecutive columns), no LDS -- runs
+// while they land.  The one-tile kernel pays its epilogue (an LDS round trip and the stores) and the next workgroup's
+// prologue (four stages of loads before its first MFMA) back to back on every tile: 13-36 % of the ViT GEMMs' time
+// (VGE_GABL 8, profiles/ab_r05p_gemm_ablation.json).
+// vmcnt accounting (loads and stores retire in issue order): a step waits for its next stage with the two later stages
+// in flight (2 LPS); the tile's bias is loaded by inline asm at the top of its second-to-last step (hipcc's waitcnt
+// pass answers a compiler-visible load issued among LDS-DMA loads with vmcnt(0)), so the last step also lets those
+// NCL loads be outstanding and the epilogue retires them at 2 LPS; the epilogue's NST stores follow the next tile's
+// stage 3, so that tile's steps 0..2 let them be outstanding too.  Stores go through a per-tile buffer descriptor
+// (rows past M fall outside it and are dropped): one store instruction per (row tile, column tile) on every path,
+// which the counts rely on.  Residual-free bf16 epilogues only (GE_BF16, GE_GELU_BF16, GE_RELU_BF16), a bias, K / 32
+// >= 6 (so the bias and store windows of a tile never meet).
+constexpr int GP_LPS = 4;   // global_load_lds per thread per stage (2 A + 2 W)
+constexpr int GP_NST = 32;  // epilogue stores per thread: 8 row tiles x 4 column tiles of 16 x 16
+constexpr int GP_NCL = 4;   // bias loads per thread: one floatx4 per column tile
+
+template <int CTRL>
+__device__ __forceinline__ float gp_dpp(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xF, 0xF, true));
+}
+// 4x4 transpose inside each quad of lanes: on entry lane i holds column i of rows 0..3, on exit row i, columns 0..3
+__device__ __forceinline__ floatx4 gp_quad_t4(floatx4 v, bool o1, bool o2) {
+  float v0 = v.x, v1 = v.y, v2 = v.z, v3 = v.w;
+  float x = o1 ? v0 : v1, y = gp_dpp<0xB1>(x);  // quad_perm [1,0,3,2]
+  v0 = o1 ? y : v0;
+  v1 = o1 ? v1 : y;
+  x = o1 ? v2 : v3;
+  y = gp_dpp<0xB1>(x);
+  v2 = o1 ? y : v2;
+  v3 = o1 ? v3 : y;
+  x = o2 ? v0 : v2;
+  y = gp_dpp<0x4E>(x);  // quad_perm [2,3,0,1]
+  v0 = o2 ? y : v0;
+  v2 = o2 ? v2 : y;
+  x = o2 ? v1 : v3;
+  y = gp_dpp<0x4E>(x);
+  v1 = o2 ? y : v1;
+  v3 = o2 ? v3 : y;
+  return floatx4{v0, v1, v2, v3};
+}
+
+template <int EPI, bool PM>
+__global__ void __launch_bounds__(512, 1) gemmp_bf16_kernel(GemmBf16Args g) {
+  static_assert(EPI == GE_BF16 || EPI == GE_GELU_BF16 || EPI == GE_RELU_BF16, "residual-free bf16 epilogues");
+  constexpr int LPS = GP_LPS;
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / 4, wn = wave % 4;
+  const int ntn = g.N / GB_N, mtn = (g.M + GB_M - 1) / GB_M, ntiles = mtn * ntn;
+  const int G = gridDim.x, b = blockIdx.x;
+  const int T = (ntiles - b + G - 1) / G;  // >= 1 (host: G <= ntiles)
+  const int nk = g.K / GB_K;               // even, >= 6 (host)
+  const int total = T * nk;
+  auto tile_mn = [&](int i, int& m0, int& n0) {
+    const int bid = gb_xcd_remap(b + i * G, ntiles);
+    const int grp = bid / (GB_GM * ntn), rem = bid - grp * (GB_GM * ntn);
+    const int gm = min(GB_GM, mtn - grp * GB_GM);
+    m0 = (grp * GB_GM + rem % gm) * GB_M;
+    n0 = (rem / gm) * GB_N;
+  };
+
+  // ---- issue side: the next stage to load (global stage index is_g = tile is_i, k stage is_k); past the last stage
+  // it re-loads that stage into its own slot (identical bytes), so every step issues LPS loads
+  int is_g = 0, is_i = 0, is_k = 0, is_m0, is_n0;
+  tile_mn(0, is_m0, is_n0);
+  auto issue_next = [&]() {
+    char* slot = lds + (is_g % GB_ST) * 2 * GB_TILE;
+    gb_stage<8, PM>(g.A, g.lda, is_m0, is_k * GB_K, slot, wave, lane, g.M - 1);
+    gb_stage<8, false>(g.W, g.ldw, is_n0, is_k * GB_K, slot + GB_TILE, wave, lane, g.N - 1);
+    if (is_g + 1 < total) {
+      ++is_g;
+      if (++is_k == nk) {
+        is_k = 0;
+        tile_mn(++is_i, is_m0, is_n0);
+      }
+    }
+  };
+
+  // ---- compute side (gemm_bf16_kernel's SH = 1 fragments and MFMAs)
+  floatx4 acq[8][4];
+  auto zero = [&]() {
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acq[t][u] = (floatx4){0.f, 0.f, 0.f, 0.f};
+  };
+  zero();
+  struct Frag {
+    bf16x8 a[2][4], b[2][2];
+  };
+  const int co = ((lane >> 4) ^ ((lane >> 2) & 3)) * 16, ro = (lane & 15) * 64;
+  auto read = [&](int st, Frag& f) {
+    const char* cur = lds + (st % GB_ST) * 2 * GB_TILE;
+    const char* As = cur + wm * 128 * 64 + ro + co;
+    const char* Bs = cur + GB_TILE + wn * 64 * 64 + ro + co;
+#pragma unroll
+    for (int t = 0; t < 8; ++t) f.a[t >> 2][t & 3] = *reinterpret_cast<const bf16x8*>(As + t * 16 * 64);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) f.b[u >> 1][u & 1] = *reinterpret_cast<const bf16x8*>(Bs + u * 16 * 64);
+  };
+  auto mma = [&](const Frag& f, int s) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        acq[4 * s + t][u] =
+            __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[s][t], f.b[u >> 1][u & 1], acq[4 * s + t][u], 0, 0, 0);
+  };
+
+  // ---- epilogue state: the tile's bias, one column per lane and column tile (the bias and the activation are applied
+  // in the MFMA layout, where a lane holds one column of four rows, before the transpose); asm loads, retired by count
+  float bb[4];
+  const int cq = 4 * ((lane & 15) >> 2);  // this lane's first column of a 16-column tile after the transpose
+  auto load_consts = [&](int i) {
+    int m0, n0;
+    tile_mn(i, m0, n0);
+    int lc = lane & 15;
+    asm volatile("" : "+v"(lc));  // opaque per call: keeps LICM from hoisting the pointer (live across the loop, spilled)
+    const float* bp = g.bias + n0 + wn * 64 + lc;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      asm volatile("global_load_dword %0, %1, off" : "=v"(bb[u]) : "v"(bp + 16 * u) : "memory");
+  };
+  // wait: 1 = the previous epilogue's stores may be outstanding, 2 = this tile's bias loads may, 0 = neither; only
+  // the wait instruction is branched on (one copy of the step body: copies per mode raise the register pressure)
+  auto step = [&](int wait, bool consts, int gs, Frag& cur, Frag& nxt, int ci) {
+    if (wait == 1)
+      vmcnt_b<2 * LPS + GP_NST>();  // stage gs + 1 landed (its two successors, + what the mode names, in flight)
+    else if (wait == 2)
+      vmcnt_b<2 * LPS + GP_NCL>();
+    else
+      vmcnt_b<2 * LPS>();
+    lds_barrier_b();   // ... for every wave; every wave is done reading stage gs - 1's slot
+    if (consts) load_consts(ci);
+    __builtin_amdgcn_sched_barrier(0);
+    issue_next();      // stage gs + 4 into stage gs - 1's slot
+    read(min(gs + 1, total - 1), nxt);
+    mma(cur, 0);
+    mma(cur, 1);
+#pragma unroll
+    for (int j = 0; j < LPS; ++j) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 2 * 8 / LPS, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);            // VMEM read (global_load_lds)
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 4, 0);  // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x100, 3, 0);  // DS read
+    }
+  };
+  const bool o1 = lane & 1, o2 = lane & 2;
+  auto epilogue = [&](int i) {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(bb[0]), "+v"(bb[1]), "+v"(bb[2]), "+v"(bb[3]) : "i"(2 * LPS) : "memory");
+    int m0, n0;
+    tile_mn(i, m0, n0);
+    const int rows = min(GB_M, g.M - m0);
+    const __amdgpu_buffer_rsrc_t ob = __builtin_amdgcn_make_buffer_rsrc(
+        reinterpret_cast<char*>(g.out) + (size_t)m0 * g.ldo * 2, (short)0, (int)((size_t)rows * g.ldo * 2), 0x00020000);
+    int r0 = wm * 128 + 4 * (lane >> 4) + (lane & 3);
+    asm volatile("" : "+v"(r0));  // opaque per tile: the 32 store offsets are not hoisted out of the tile loop (spills)
+    const int c0 = n0 + wn * 64 + cq;
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        floatx4 v = acq[t][u] + bb[u];
+        if constexpr (EPI == GE_RELU_BF16) v = floatx4{fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f)};
+        if constexpr (EPI == GE_GELU_BF16) {
+          floatx2 y[2] = {{v.x, v.y}, {v.z, v.w}};
+          gelu2_many(y);
+          v = floatx4{y[0].x, y[0].y, y[1].x, y[1].y};
+        }
+        v = gp_quad_t4(v, o1, o2);
+        bf16x4 o;
+        o[0] = (bf16)v.x; o[1] = (bf16)v.y; o[2] = (bf16)v.z; o[3] = (bf16)v.w;
+        const int off = ((r0 + 16 * t) * (int)g.ldo + c0 + 16 * u) * 2;  // < rows x ldo x 2 < 2^31 (host)
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uintx2_t, o), ob, off, 0, 0);
+      }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  for (int st = 0; st < GB_ST - 1; ++st) issue_next();  // stages 0..3
+  vmcnt_b<3 * LPS>();                                     // stage 0 landed
+  lds_barrier_b();
+  Frag f0, f1;
+  read(0, f0);
+  // step kk of tile i: steps 0..2 of the tiles after the first let the previous epilogue's stores be outstanding, step
+  // nk - 2 loads the tile's bias ahead of its ring loads, step nk - 1 lets those loads be outstanding; f0 holds the
+  // fragments of even steps (nk is even)
+  int gs = 0;
+  for (int i = 0; i < T; ++i) {
+    for (int kk = 0; kk < nk; kk += 2) {
+      step((i > 0 && kk < 3) ? 1 : 0, kk == nk - 2, gs++, f0, f1, i);
+      step((i > 0 && kk + 1 < 3) ? 1 : kk + 1 == nk - 1 ? 2 : 0, false, gs++, f1, f0, i);
+    }
+    epilogue(i);
+    zero();
+  }
+  vmcnt_b<0>();
 }
 
 // ------------------------------------------------------------- GEMM, two workgroups per CU (gemm2)
@@ -931,6 +1140,17 @@ hipError_t gemm_setup_pm() {  // the partial-M kernels (8 waves): 1x1 convs over
 }
 
 template <bool PM>
+hipError_t gemmp_setup() {
+  const void* ks[3] = {(const void*)gemmp_bf16_kernel<GE_BF16, PM>, (const void*)gemmp_bf16_kernel<GE_GELU_BF16, PM>,
+                       (const void*)gemmp_bf16_kernel<GE_RELU_BF16, PM>};
+  for (auto k : ks) {
+    hipError_t e = hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, GB_LDS);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+template <bool PM>
 hipError_t gemm2_setup() {
   const void* ks[8] = {(const void*)gemm2_bf16_kernel<GE_BF16, PM>, (const void*)gemm2_bf16_kernel<GE_GELU_BF16, PM>,
                        (const void*)gemm2_bf16_kernel<GE_RES_F32, PM>, (const void*)gemm2_bf16_kernel<GE_PE_F32, PM>,
@@ -985,6 +1205,8 @@ hipError_t vit_kernels_setup_dev() {
   if (e == hipSuccess) e = gemm_setup_pm<1>();
   if (e == hipSuccess) e = gemm_setup_nw<4>();
   if (e == hipSuccess) e = gemm_setup_nw<8, 1>();
+  if (e == hipSuccess) e = gemmp_setup<false>();
+  if (e == hipSuccess) e = gemmp_setup<true>();
   if (e != hipSuccess) return e;
   e = hipFuncSetAttribute((const void*)vit_attn_kernel<80>, hipFuncAttributeMaxDynamicSharedMemorySize,
                           AttnCfg<80>::LDS);
@@ -1017,7 +1239,72 @@ void launch_gemm_nw(int epi, dim3 grid, const GemmBf16Args& g, hipStream_t s) {
 }
 
 // shapes are validated by the callers (vge_hmr.cpp, vge_cnn.hip): N % 256 == K % 64 == 0, 16-B aligned rows; any M
+// VGE_GEMMP, read once: 1 = the residual-free bf16 epilogues run on the persistent kernel (gemmp_bf16_kernel) whenever
+// it applies (gemm_persist_ok); 0 (default) = only where a caller asks for it (the conv tuner's variant 10)
+static int g_gemm_persist = -1;
+
+static int device_cus() {
+  static std::atomic<int> cus{0};
+  int c = cus.load(std::memory_order_relaxed);
+  if (c > 0) return c;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      c <= 0)
+    c = 256;
+  cus.store(c, std::memory_order_relaxed);
+  return c;
+}
+
+// the persistent kernel's conditions: a residual-free bf16 epilogue with a bias, K / 32 >= 6, more tiles than CUs (one
+// workgroup per CU, a multiple of 8 of them), a tile's stores inside a 32-bit buffer range
+bool gemm_persist_ok(int epi, const GemmBf16& a) {
+  if ((epi != GE_BF16 && epi != GE_GELU_BF16 && epi != GE_RELU_BF16) || !a.bias || a.K / GB_K < 6 || a.N % GB_N ||
+      a.K % 64 || a.M < 1)
+    return false;
+  const long ntiles = (long)((a.M + GB_M - 1) / GB_M) * (a.N / GB_N);
+  return ntiles > device_cus() && (long)GB_M * a.ldo * 2 < (1L << 31);
+}
+
+template <int EPI, bool PM>
+static void launch_gemmp_t(const GemmBf16Args& g, int grid, hipStream_t s) {
+  hipLaunchKernelGGL((gemmp_bf16_kernel<EPI, PM>), dim3(grid), dim3(512), GB_LDS, s, g);
+}
+
+static hipError_t launch_gemmp(int epi, const GemmBf16Args& g, hipStream_t s) {
+  const int grid = device_cus() & ~7;  // one workgroup per CU, a multiple of 8 (the XCD-grouped tile walk)
+  const bool pm = g.M % GB_M != 0;
+  switch (epi) {
+    case GE_BF16: pm ? launch_gemmp_t<GE_BF16, true>(g, grid, s) : launch_gemmp_t<GE_BF16, false>(g, grid, s); break;
+    case GE_GELU_BF16:
+      pm ? launch_gemmp_t<GE_GELU_BF16, true>(g, grid, s) : launch_gemmp_t<GE_GELU_BF16, false>(g, grid, s);
+      break;
+    default: pm ? launch_gemmp_t<GE_RELU_BF16, true>(g, grid, s) : launch_gemmp_t<GE_RELU_BF16, false>(g, grid, s);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_gemm_bf16_persistent(int epi, const GemmBf16& a, hipStream_t s) {
+  if (!gemm_persist_ok(epi, a)) return hipErrorInvalidValue;
+  if (const hipError_t e = vit_kernels_setup(); e != hipSuccess) return e;
+  GemmBf16Args g;
+  g.A = reinterpret_cast<const bf16*>(a.A);
+  g.W = reinterpret_cast<const bf16*>(a.W);
+  g.out = a.out;
+  g.bias = a.bias;
+  g.res = a.res;
+  g.pos = a.pos;
+  g.lda = a.lda; g.ldw = a.ldw; g.ldo = a.ldo; g.ldr = a.ldr;
+  g.M = a.M; g.N = a.N; g.K = a.K; g.tokens = a.tokens;
+  g.resb = reinterpret_cast<const bf16*>(a.resb);
+  return launch_gemmp(epi, g, s);
+}
+
 hipError_t launch_gemm_bf16(int epi, const GemmBf16& a, hipStream_t s) {
+  if (g_gemm_persist < 0) {
+    const char* e = getenv("VGE_GEMMP");
+    g_gemm_persist = (e && e[0] == '1') ? 1 : 0;
+  }
+  if (g_gemm_persist == 1 && gemm_persist_ok(epi, a)) return launch_gemm_bf16_persistent(epi, a, s);
   GemmBf16Args g;
   g.A = reinterpret_cast<const bf16*>(a.A);
   g.W = reinterpret_cast<const bf16*>(a.W);
@@ -1057,6 +1344,11 @@ hipError_t launch_gemm_bf16(int epi, const GemmBf16& a, hipStream_t s) {
   else
     launch_gemm_nw<8>(epi, grid, g, s);
   return hipGetLastError();
+}
+
+extern "C" int vge_debug_set_gemm_persist(int on) {  // tests / A/B: the persistent kernel wherever it applies (1) or not
+  g_gemm_persist = on ? 1 : 0;
+  return 0;
 }
 
 extern "C" int vge_debug_set_gemm_waves(int nw) {  // A/B timing (tools/gemm_bench.py)
