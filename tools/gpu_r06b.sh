@@ -26,3 +26,5 @@ for c in 128 64 128; do
   timeout -k 10 180 python -u tools/time_frcnn.py 256 $c 2 > gpurun_out/r06b_frcnn_c$c.json 2>/dev/null || { echo "frcnn $c failed"; exit 1; }
   python -c "import json;d=json.load(open('gpurun_out/r06b_frcnn_c$c.json'));print('chunk',d['chunk'],d['ms_per_pass'],d['backbone_tflops'])"
 done
+timeout -k 10 560 python -u bench.py > gpurun_out/r06b_bench.json 2> gpurun_out/r06b_bench.err || { echo "bench failed"; tail -20 gpurun_out/r06b_bench.err; exit 1; }
+python -c "import json;d=json.load(open('gpurun_out/r06b_bench.json'));e=d.get('e2e',{});print(d['value'],d['ms_per_step'],e.get('value'),e.get('error'),e.get('child_wall_s'))"
