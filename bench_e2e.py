@@ -35,7 +35,9 @@ E2E_KERNEL_SOURCES = {"gemm_bf16_kernel": ["vge_vit.hip"],
                       "yolox_conv": ["vge_cnn.hip", "vge_cnn_host.h", "vge_yolox.cpp", "vge_vit.hip"],
                       "frcnn_conv": ["vge_cnn.hip", "vge_cnn_host.h", "vge_frcnn.cpp", "vge_vit.hip", "vge_gconv.hip"]}
 YOLOX_CHUNK = 256   # frames per detector pass (tools/yolox_prof.py --chunk: 637 vs 618 TFLOP/s at 64)
-FRCNN_CHUNK = 64    # frames per Faster R-CNN workspace chunk (~0.3 GB per 800 x 800 frame; 64: -6 % vs 32, profiles/ab_r05m_*)
+# frames per Faster R-CNN workspace chunk (~0.3 GB per 800 x 800 frame): 64 was -6 % vs 32 (profiles/ab_r05m_*); 128,
+# possible since the 1x1 convs' GEMM epilogue addresses through 64-bit offsets, -1.2 % vs 64 (profiles/ab_r06b_frcnn_chunk.json)
+FRCNN_CHUNK = 128
 
 
 def e2e_traffic(kernel: str, frames: float):

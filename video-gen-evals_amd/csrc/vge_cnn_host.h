@@ -209,9 +209,10 @@ inline hipError_t conv_tuned_launch(ConvTuner& t, ConvLaunch& c, const std::arra
     // VGE_CONV_GEMM=0 keeps it out
     static const bool gemm_ok = !(getenv("VGE_CONV_GEMM") && getenv("VGE_CONV_GEMM")[0] == '0');
     if (gemm_ok && conv_gemm_epi(c) >= 0) cand.push_back(9000 + 256);
-    // ... and its persistent form where it applies (residual-free bf16 epilogues, more 256 x 256 tiles than CUs);
-    // VGE_CONV_GEMMP=0 keeps it out
-    static const bool gemmp_ok = !(getenv("VGE_CONV_GEMMP") && getenv("VGE_CONV_GEMMP")[0] == '0');
+    // ... and its persistent form where it applies (residual-free bf16 epilogues, more 256 x 256 tiles than CUs) with
+    // VGE_CONV_GEMMP=1: measured no faster on the detector (236.2 vs 236.6 ms per 256 frames, the tuner keeps the
+    // one-tile kernel) and 7-20 % slower on the ViT-H shapes (profiles/ab_r06b_gemmp.json), so off by default
+    static const bool gemmp_ok = getenv("VGE_CONV_GEMMP") && getenv("VGE_CONV_GEMMP")[0] == '1';
     if (gemm_ok && gemmp_ok && conv_gemm_persist_ok(c)) cand.push_back(10000 + 256);
     int pick = -1;
     float best_ms = 0.f;
