@@ -185,11 +185,12 @@ def cpu_share() -> int:
 
 
 class _ClipWindows(torch.utils.data.Dataset):
-    """The reference's WindowDataset role (utils.py:383-516) for the CPU baseline: one 32-frame window per clip,
-    featurised by the oracle in the DataLoader worker (clips are in memory: no npz decode, like the GPU leg)."""
+    """The reference's WindowDataset role (utils.py:383-516) for the CPU baseline: the 32-frame windows of a clip
+    (starts 0, 8, ...: one for config 2's 32-frame clips, five for config 5's 64-frame ones), featurised by the oracle
+    in the DataLoader worker (clips are in memory: no npz decode, like the GPU leg)."""
 
-    def __init__(self, clips, mean, std):
-        self.clips, self.mean, self.std = clips, mean, std
+    def __init__(self, clips, mean, std, starts=(0,)):
+        self.clips, self.mean, self.std, self.starts = clips, mean, std, tuple(starts)
 
     def __len__(self):
         return len(self.clips)
@@ -197,15 +198,17 @@ class _ClipWindows(torch.utils.data.Dataset):
     def __getitem__(self, i):
         from oracle.featurize import featurize_window
         c = self.clips[i]
-        f = featurize_window(c["pose"], c["global_orient"], c["betas"], c["vit"], c["keypoints"], 0, None)
+        f = np.stack([featurize_window(c["pose"], c["global_orient"], c["betas"], c["vit"], c["keypoints"], s0, None)
+                      for s0 in self.starts])
         return torch.from_numpy((f - self.mean) / (self.std + np.float32(1e-6))), i
 
 
-def cpu_baseline(seconds: float, clips_per_batch: int = 32, workers: int = 4):
+def cpu_baseline(seconds: float, clips_per_batch: int = 32, workers: int = 4, T: int = CLIP_LEN):
     """Oracle CPU restatement of eval.py's generated-set pass in the reference's structure (eval.py:410-418,
     168-206): DataLoader(batch_size=32, num_workers=4) featurising in worker processes, the torch-fp32 encoder in
-    the main process on this process's CPU share, then AC/TC.  Bounded: batches of 32 clips until `seconds` of
-    wall time have elapsed.  Runs before the GPU is touched (the workers are forked)."""
+    the main process on this process's CPU share, then AC/TC (a clip's windows: its AC from their mean embedding, its
+    TC the mean of their terms).  T: frames per clip (32: config 2, one window; 64: config 5, five).  Bounded: batches
+    of 32 clips until `seconds` of wall time have elapsed.  Runs before the GPU is touched (the workers are forked)."""
     from oracle import evalflow
     from oracle.encoder import OracleEncoder
     from vge import synth
@@ -220,22 +223,23 @@ def cpu_baseline(seconds: float, clips_per_batch: int = 32, workers: int = 4):
     label = {c: i for i, c in enumerate(evalflow.ACTION_CLASSES)}
     # a pool of clips generated up front (data synthesis is not part of the reference's work), passed over
     # repeatedly until `seconds` have elapsed
-    n_clips = 1024
-    clips = make_clips(synth.SEED_GEN, 10_000, n_clips, CLIP_LEN)
+    n_clips = 1024 if T == CLIP_LEN else 512
+    starts = list(range(0, T - CLIP_LEN + 1, 8))
+    clips = make_clips(synth.SEED_GEN, 10_000, n_clips, T)
     names = [synth.generated_name(10_000 + i) + ".npz" for i in range(n_clips)]
     cls_all = [evalflow.ACTION_CLASSES[((10_000 + i) // 5) % 10] for i in range(n_clips)]
-    loader = torch.utils.data.DataLoader(_ClipWindows(clips, mean, std), batch_size=clips_per_batch, shuffle=False,
-                                         num_workers=workers, multiprocessing_context="fork")
+    loader = torch.utils.data.DataLoader(_ClipWindows(clips, mean, std, starts), batch_size=clips_per_batch,
+                                         shuffle=False, num_workers=workers, multiprocessing_context="fork")
     n_done = 0
     marks = []  # (seconds, clips) after every batch: the spread over the sample's quarters is reported
     t0 = time.perf_counter()
     while time.perf_counter() - t0 < seconds:
         for feats, idx in loader:
-            seq, fe, _ = enc.forward(feats)
-            idx = idx.tolist()
+            seq, fe, _ = enc.forward(feats.reshape(-1, *feats.shape[2:]))
+            idx = [i for i in idx.tolist() for _ in starts]   # one name per window (eval.py groups by video)
             evalflow.ac_scores(seq, [cls_all[i] for i in idx], [names[i] for i in idx], cents, label)
             evalflow.tc_scores(fe, [names[i] for i in idx])
-            n_done += len(idx)
+            n_done += len(idx) // len(starts)
             marks.append((time.perf_counter() - t0, n_done))
             if time.perf_counter() - t0 >= seconds:
                 break
@@ -249,7 +253,8 @@ def cpu_baseline(seconds: float, clips_per_batch: int = 32, workers: int = 4):
             quarters.append((seg[-1][1] - seg[0][1]) / max(seg[-1][0] - seg[0][0], 1e-9))
     return {"value": n_done / t_used, "unit": "videos/s", "cores": share, "kind": "port",
             "quarter_rates": [round(v, 1) for v in quarters],
-            "sample": f"{n_done} synthetic 32-frame clips (in-memory features, no npz decode) through the reference's "
+            "sample": f"{n_done} synthetic {T}-frame clips ({len(starts)} window(s) each; in-memory features, no npz "
+                      f"decode) through the reference's "
                       f"structure: DataLoader(batch_size={clips_per_batch}, num_workers={workers}) running the oracle "
                       f"featuriser (numpy) in worker processes, torch-fp32 oracle encoder on {share} threads (the "
                       f"process's CPU share) + AC/TC, {t_used:.1f} s wall"}
@@ -312,9 +317,9 @@ def launch_ranks(args, cmd) -> int:
     rank 0's JSON line goes straight to this process's stdout.  Returns the children's exit status."""
     import subprocess
     env = dict(os.environ)
-    if args.workload in ("score", "tag") and not args.no_cpu_baseline:
-        if args.workload == "score":
-            cpu = cpu_baseline(args.cpu_seconds)
+    if args.workload in ("score", "tag", "cfg5") and not args.no_cpu_baseline:
+        if args.workload in ("score", "cfg5"):
+            cpu = cpu_baseline(args.cpu_seconds, T=64 if args.workload == "cfg5" else CLIP_LEN)
         else:
             import bench_tag
             cpu = bench_tag.cpu_baseline()
@@ -392,9 +397,10 @@ def main():
         args.pipeline = "serial"
 
     cpu = json.loads(os.environ["VGE_BENCH_CPU_BASELINE"]) if os.environ.get("VGE_BENCH_CPU_BASELINE") else None
-    if cpu is None and args.workload == "score" and int(os.environ.get("WORLD_SIZE", "1")) == 1 and \
+    if cpu is None and args.workload in ("score", "cfg5") and int(os.environ.get("WORLD_SIZE", "1")) == 1 and \
             not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_seconds)  # before the GPU is initialised: its DataLoader workers are forked
+        # before the GPU is initialised: its DataLoader workers are forked
+        cpu = cpu_baseline(args.cpu_seconds, T=64 if args.workload == "cfg5" else CLIP_LEN)
     if cpu is None and args.workload == "tag" and int(os.environ.get("WORLD_SIZE", "1")) == 1 and \
             not args.no_cpu_baseline:
         import bench_tag
