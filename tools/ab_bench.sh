@@ -6,7 +6,7 @@ R=$1; shift
 for r in $(seq 1 "$R"); do
   for spec in "$@"; do
     tag=${spec%%:*}; opts=${spec#*:}
-    timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-throughput-mode --steps 50 $opts \
+    timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-throughput-mode --no-e2e --steps 50 $opts \
       > gpurun_out/ab_${tag}_$r.log 2>&1 || { tail -20 gpurun_out/ab_${tag}_$r.log; exit 1; }
     python3 - "$tag" "gpurun_out/ab_${tag}_$r.log" <<'PY'
 import json, sys

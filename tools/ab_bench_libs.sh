@@ -10,7 +10,7 @@ for r in $(seq 1 "$R"); do
       default) L=$PWD/video-gen-evals_amd/vge/libvge.so ;;
       *) L=$PWD/video-gen-evals_amd/csrc/build/$v/libvge.so ;;
     esac
-    VGE_LIB=$L timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-throughput-mode --steps 50 \
+    VGE_LIB=$L timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-throughput-mode --no-e2e --steps 50 \
       > gpurun_out/abl_${v}_$r.log 2>&1 || { tail -20 gpurun_out/abl_${v}_$r.log; exit 1; }
     python3 - "$v" "gpurun_out/abl_${v}_$r.log" <<'PY'
 import json, sys

@@ -10,7 +10,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-BENCH="$R/bench.py --steps 6 --warmup 2 --no-cpu-baseline --no-throughput-mode --compute $COMPUTE"
+BENCH="$R/bench.py --steps 6 --warmup 2 --no-cpu-baseline --no-throughput-mode --no-e2e --compute $COMPUTE"
 run() {  # name, extra rocprofv3 args...
   local name=$1; shift
   timeout -k 10 300 rocprofv3 "$@" --output-format csv -d "$OUT/prof_${TAG}_$name" -o run -- python3 $BENCH \
