@@ -322,7 +322,7 @@ def launch_ranks(args, cmd) -> int:
             cpu = cpu_baseline(args.cpu_seconds, T=64 if args.workload == "cfg5" else CLIP_LEN)
         else:
             import bench_tag
-            cpu = bench_tag.cpu_baseline()
+            cpu = bench_tag.cpu_baseline_extract(args.cpu_seconds) if args.extract else bench_tag.cpu_baseline()
         env["VGE_BENCH_CPU_BASELINE"] = json.dumps(cpu)
     env.setdefault("OMP_NUM_THREADS", str(max(1, cpu_share() // args.gpus)))
     return subprocess.run(cmd, env=env).returncode
@@ -371,6 +371,10 @@ def main():
                     help="e2e: run TokenHMR and DWPose one after the other on one stream (default: two streams)")
     ap.add_argument("--no-detector", action="store_true",
                     help="e2e: skip DWPose's YOLOX person detector (every frame takes the whole-frame pose box)")
+    ap.add_argument("--extract", action="store_true",
+                    help="tag: config 4 end to end -- each rank extracts its shard of the generated videos from frames "
+                         "(gate detector + TokenHMR, YOLOX-L + DWPose -> npz / keypoints.npy) before the sharded flow "
+                         "(bench_tag.run_extract)")
     ap.add_argument("--no-e2e", action="store_true",
                     help="score at N = 1: skip the nested `e2e` record (config 3, run as a child process after the "
                          "config-2 line's measurements)")
@@ -404,11 +408,11 @@ def main():
     if cpu is None and args.workload == "tag" and int(os.environ.get("WORLD_SIZE", "1")) == 1 and \
             not args.no_cpu_baseline:
         import bench_tag
-        cpu = bench_tag.cpu_baseline()
+        cpu = bench_tag.cpu_baseline_extract(args.cpu_seconds) if args.extract else bench_tag.cpu_baseline()
     world, rank, dev = setup_dist()
     if args.workload == "tag":
         import bench_tag
-        out = bench_tag.run(args, world, rank, dev, METRIC, cpu)
+        out = (bench_tag.run_extract if args.extract else bench_tag.run)(args, world, rank, dev, METRIC, cpu)
         if rank == 0:
             print(json.dumps(out))
         if world > 1:

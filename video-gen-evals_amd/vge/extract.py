@@ -176,3 +176,59 @@ def extract_video(hmr, wholebody, frames, crops, action: str, video: str, mesh_r
                              meta={"action": action, "video": video, "source_path": source_path})
     kp = save_keypoints(keypoint_rows(wholebody, frames), kp_root, action, stem)
     return {"npz": npz, "keypoints": kp}
+
+
+def extract_videos(hmr, wholebody, detector, videos, mesh_root, kp_root, max_frames: int = 1024) -> Dict[str, Optional[str]]:
+    """extract_mesh.py:150-241 + process_video.py:59-94 over a list of videos, batched for the GPU: videos are
+    (stem, uint8 [T, H, W, 3] device frames) of any lengths; consecutive videos are packed into passes of at most
+    `max_frames` frames (a longer video is a pass of its own), and each pass runs the gate detector (detectron2 Faster
+    R-CNN, `detector`) and DWPose (`wholebody`: YOLOX-L persons -> RTMPose-l) once over all its frames, then TokenHMR
+    once over the crops of every kept frame of the pass's accepted videos.  Per video, as the reference does one at a
+    time: the single-person gate and its 80 % rule (mesh_generator.py:101-117), <mesh_root>/<stem>.npz of the kept
+    frames (extract_mesh.py:35-43; a rejected video gets none: the not-single list) and
+    <kp_root>/<stem>/keypoints.npy of every frame (process_video.py writes them for every video).
+    Returns {stem: npz path or None}."""
+    import torch
+    from .hmr import crop_persons
+    out: Dict[str, Optional[str]] = {}
+    passes, cur, n = [], [], 0
+    for stem, fr in videos:
+        t = int(fr.shape[0])
+        if cur and n + t > max_frames:
+            passes.append(cur)
+            cur, n = [], 0
+        cur.append((stem, fr))
+        n += t
+    if cur:
+        passes.append(cur)
+    for group in passes:
+        fr = group[0][1] if len(group) == 1 else torch.cat([f for _, f in group], 0)
+        det = detector.detect(fr)
+        kp = wholebody(fr).cpu().numpy()
+        boxes = det["person"][:, 0, :4].cpu().numpy()
+        npers = det["n_person"].cpu().numpy()
+        kept, spans, f0 = [], [], 0
+        for stem, f in group:
+            t = int(f.shape[0])
+            valid = single_person_frames(np.where(gate_mask(npers[f0:f0 + t]), 1, 0))
+            spans.append((stem, f0, t, valid))
+            if valid is not None:
+                kept.append(valid + f0)
+            f0 += t
+        rows = None
+        if kept:
+            kf = np.concatenate(kept)
+            crops = crop_persons(fr, boxes[kf], kf)
+            rows = {k: v.cpu().numpy() for k, v in hmr.extract(crops).items()}
+        r = 0
+        for stem, f0, t, valid in spans:
+            save_keypoints(kp[f0:f0 + t], Path(kp_root), "", stem)
+            if valid is None:
+                out[stem] = None
+                continue
+            mesh_info = {int(fi): {"pose": rows["pose"][r + j].reshape(23, 3, 3), "betas": rows["betas"][r + j],
+                                   "global_orient": rows["global_orient"][r + j].reshape(1, 3, 3),
+                                   "vit": rows["vit"][r + j]} for j, fi in enumerate(valid)}
+            r += valid.size
+            out[stem] = save_video_npz(stem, mesh_info, out_root=mesh_root, meta={"video": stem})
+    return out
