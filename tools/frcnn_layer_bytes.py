@@ -12,7 +12,7 @@ in vge_frcnn.cpp's launch order (tools/frcnn_layers.py).  Per layer and per fram
   GF       algorithmic GFLOP (grouped convs at their grouped size)
   us       the trace pass's duration of the dispatch, per chunk; TB/s and TF/s from alg_MB and GF over it
 
-Usage: python tools/frcnn_layer_bytes.py TAG [frames_per_chunk] [H W] -> table on stdout + JSON (profiles/ by -o)."""
+Usage: python tools/frcnn_layer_bytes.py TAG [frames_per_chunk] [H W] [-o] -> table on stdout (+ profiles/frcnn_layer_bytes_TAG.json with -o)."""
 import csv
 import json
 import sys
@@ -74,7 +74,8 @@ def layer_shapes(H=800, W=800, depth=101):
     L["rpn_select"] = (sum(px(a, b) * 16 * 4 for a, b in sizes), 0, 0)
     L["rpn_nms"] = (5 * 1024 * 8 * 4 * 2, 0, 0)
     L["rpn_merge"] = (5 * 1024 * 8 * 4 + P * 5 * 4, 0, 0)
-    L["roi_align"] = (P * 49 * F * B + P * 49 * 4 * 4 * F * B, 0, 0)  # output + at most 4 corners x 4 samples read
+    # output + every P2..P5 feature it samples read once (the lower bound: the 4 corners x 4 samples of a bin overlap)
+    L["roi_align"] = (P * 49 * F * B + sum(px(a, b) for a, b in sizes[:4]) * F * B, 0, 0)
     L["fc1"] = (P * 49 * F * B + P * fc * B, fc * 49 * F * B, 2.0 * P * fc * 49 * F)
     L["fc2"] = (P * fc * 2 * B, fc * fc * B, 2.0 * P * fc * fc)
     L["predictor"] = (P * fc * B + P * 408 * 4, 401 * fc * B, 2.0 * P * 401 * fc)
@@ -102,10 +103,11 @@ def last_call(rows, lab):
 
 
 def main():
-    tag = sys.argv[1]
-    chunk = int(sys.argv[2]) if len(sys.argv) > 2 else 64
-    H = int(sys.argv[3]) if len(sys.argv) > 3 else 800
-    W = int(sys.argv[4]) if len(sys.argv) > 4 else 800
+    pos = [a for a in sys.argv[1:] if a != "-o"]
+    tag = pos[0]
+    chunk = int(pos[1]) if len(pos) > 1 else 64
+    H = int(pos[2]) if len(pos) > 2 else 800
+    W = int(pos[3]) if len(pos) > 3 else 800
     OUT = ROOT / "gpurun_out"
     lab = labels(101)
     tr = list(csv.DictReader(open(next((OUT / f"pe_{tag}_frcnn_trace").glob("**/*kernel_trace.csv")))))
@@ -126,7 +128,8 @@ def main():
         us = t[2]
         k = l.split(".")[-1] if l.startswith("res") else l.rstrip("0123456789").rstrip("_p")
         stage = l.split(".")[0] if l.startswith("res") else k
-        res.append({"layer": l, "kernel": t[1].split("(")[0][-48:], "us_per_chunk": us, "alg_bytes_per_frame": alg,
+        kname = t[1][t[1].find("::") + 2:] if "namespace)::" in t[1] else t[1]
+        res.append({"layer": l, "kernel": kname.split("(")[0][:60], "us_per_chunk": us, "alg_bytes_per_frame": alg,
                     "pmc_bytes_per_frame": pmc, "gflop_per_frame": fl / 1e9})
         for key in (f"kind:{k}", f"stage:{stage}", "total"):
             kind[key]["us"] += us
