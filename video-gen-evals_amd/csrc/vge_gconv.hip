@@ -54,9 +54,6 @@ constexpr int gc_lds() { return ((gc_th<S>() - 1) * S + 3) * ((gc_tw<S>() - 1) *
 // 16-channel step), 1 = v_mfma_f32_16x16x32_bf16 (gfx950's full-rate bf16 form: the legacy 16x16x16 issues at half the
 // rate, 16 cycles per 8 kFLOP, profiles/pmc_r05u_frcnn_sq.json): KS >= 2 -> two steps of a tap per MFMA, KS = 1 -> two
 // taps per MFMA (lanes 0-31 carry tap 2p, lanes 32-63 tap 2p + 1; tap 9 is zero weights)
-#ifndef VGE_GC_ORDER
-#define VGE_GC_ORDER 1  // MFMA loop order: 1 tap-major (independent accumulators back to back), 0 pixel-tile-major
-#endif
 #ifndef VGE_GC_OCC
 #define VGE_GC_OCC 1  // minimum waves per SIMD the register allocation must allow (= workgroups per CU)
 #endif
@@ -126,55 +123,10 @@ __global__ void __launch_bounds__(256, VGE_GC_OCC) gconv3_kernel(GconvArgs a) {
     __syncthreads();
     if (k + 1 < nimg) load_tile(img + 1);  // the next image's loads in flight during this one's MFMAs
 
-    // ---- MFMAs: pixel tile pt = output pixels pt * 16 .. + 15 of the tile (row-major, TW / 16 tiles per row).
-    // VGE_GC_ORDER 1 (default): tap-major -- for each tap (and K step) the NPT pixel tiles' B operands are read and
-    // their MFMAs issued into NPT independent accumulators, so a tap's LDS reads are all in flight together and no MFMA
-    // waits on the one before it; 0: pixel-tile-major (each tile's 9 taps as one dependent chain, a read ahead of each).
-    // Each accumulator sums its taps / K steps in the same order either way: bit-identical outputs.
+    // ---- MFMAs: pixel tile pt = output pixels pt * 16 .. + 15 of the tile (row-major, TW / 16 tiles per row)
     floatx4 acc[NPT];
 #pragma unroll
     for (int pt = 0; pt < NPT; ++pt) acc[pt] = floatx4{0.f, 0.f, 0.f, 0.f};
-#if VGE_GC_ORDER
-    const char* pbs[NPT];
-#pragma unroll
-    for (int pt = 0; pt < NPT; ++pt) {
-      const int op = pt * 16 + px, orow = op / TW, ocol = op % TW;
-      pbs[pt] = lb + ((orow * S) * IW + ocol * S) * GC_PITCH;
-    }
-#pragma unroll
-    for (int t = 0; t < NT; ++t) {
-      if constexpr (MF && KS == 1) {
-        const int ta = 2 * t, tb = 2 * t + 1 < 9 ? 2 * t + 1 : 8;  // (tap 9: zero weights on finite data)
-        const int offa = ((ta / 3) * IW + (ta % 3)) * GC_PITCH, offb = ((tb / 3) * IW + (tb % 3)) * GC_PITCH;
-        const int o = hh ? offb : offa;
-        bf16x8_t b[NPT];
-#pragma unroll
-        for (int pt = 0; pt < NPT; ++pt) b[pt] = *reinterpret_cast<const bf16x8_t*>(pbs[pt] + o);
-#pragma unroll
-        for (int pt = 0; pt < NPT; ++pt) acc[pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[t][0], b[pt], acc[pt], 0, 0, 0);
-      } else {
-        const int off = ((t / 3) * IW + (t % 3)) * GC_PITCH;
-#pragma unroll
-        for (int j = 0; j < NJ; ++j) {
-          if constexpr (MF) {
-            bf16x8_t b[NPT];
-#pragma unroll
-            for (int pt = 0; pt < NPT; ++pt) b[pt] = *reinterpret_cast<const bf16x8_t*>(pbs[pt] + off + 64 * j);
-#pragma unroll
-            for (int pt = 0; pt < NPT; ++pt)
-              acc[pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[t][j], b[pt], acc[pt], 0, 0, 0);
-          } else {
-            short4v b[NPT];
-#pragma unroll
-            for (int pt = 0; pt < NPT; ++pt) b[pt] = *reinterpret_cast<const short4v*>(pbs[pt] + off + 32 * j);
-#pragma unroll
-            for (int pt = 0; pt < NPT; ++pt)
-              acc[pt] = __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(wa[t][j], b[pt], acc[pt], 0, 0, 0);
-          }
-        }
-      }
-    }
-#else
 #pragma unroll
     for (int pt = 0; pt < NPT; ++pt) {
       const int op = pt * 16 + px, orow = op / TW, ocol = op % TW;
@@ -201,7 +153,6 @@ __global__ void __launch_bounds__(256, VGE_GC_OCC) gconv3_kernel(GconvArgs a) {
         }
       }
     }
-#endif
     // ---- epilogue: lane = pixel l & 15 of the tile, output channels n0 + 4 (l >> 4) .. + 3
 #pragma unroll
     for (int pt = 0; pt < NPT; ++pt) {
