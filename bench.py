@@ -318,11 +318,14 @@ def launch_ranks(args, cmd) -> int:
     import subprocess
     env = dict(os.environ)
     if args.workload in ("score", "tag", "cfg5") and not args.no_cpu_baseline:
-        if args.workload in ("score", "cfg5"):
-            cpu = cpu_baseline(args.cpu_seconds, T=64 if args.workload == "cfg5" else CLIP_LEN)
+        if args.workload == "score":
+            cpu = cpu_baseline(args.cpu_seconds)
+        elif args.workload == "cfg5":
+            cpu = cpu_baseline(args.cpu_seconds, T=64)
         else:
             import bench_tag
-            cpu = bench_tag.cpu_baseline_extract(args.cpu_seconds) if args.extract else bench_tag.cpu_baseline()
+            cpu = (bench_tag.cpu_baseline_extract(args.cpu_seconds) if getattr(args, "extract", False)
+                   else bench_tag.cpu_baseline())
         env["VGE_BENCH_CPU_BASELINE"] = json.dumps(cpu)
     env.setdefault("OMP_NUM_THREADS", str(max(1, cpu_share() // args.gpus)))
     return subprocess.run(cmd, env=env).returncode
@@ -363,6 +366,9 @@ def main():
                          "occupancy-2 fp16 transformer fills every register of a CU, so an overlapped featurise only "
                          "waits for its workgroups)")
     ap.add_argument("--serial-featurize", action="store_true", help="= --pipeline serial")
+    ap.add_argument("--host-scores", default="direct", choices=["direct", "copy"],
+                    help="score/cfg5: the per-video AC / TC reach pinned host memory written by the score kernel itself "
+                         "(direct, default: no copy kernels in the step) or through two device-to-host copies (copy)")
     ap.add_argument("--event-every", type=int, default=5,
                     help="record the conv stage's (and featurise's) hipEvents on every k-th timed step, from the first: "
                          "each event is a queue marker (measured: all steps 184.2k-185.4k videos/s, every 5th "
@@ -671,12 +677,19 @@ def run_score(args, world, rank, dev):
 
     deferred = [None]  # side3: (seq, tc) buffers of the step whose scores are not launched yet
 
+    def scores_to_host(sq, tw):
+        """per-video AC / TC into the pinned host buffers: written by the score kernel itself (--host-scores direct,
+        the default) or computed on the device and copied (copy: two blit kernels after it)"""
+        if args.host_scores == "direct":
+            return ops.score_videos(sq, tw, first, vcls, centroids, out=(host_ac, host_tc))
+        ac, tc = ops.score_videos(sq, tw, first, vcls, centroids)
+        host_ac.copy_(ac, non_blocking=True)
+        host_tc.copy_(tc, non_blocking=True)
+        return ac, tc
+
     def launch_scores(stream, sq, tw):
         with torch.cuda.stream(stream):
-            ac, tc = ops.score_videos(sq, tw, first, vcls, centroids)
-            host_ac.copy_(ac, non_blocking=True)
-            host_tc.copy_(tc, non_blocking=True)
-        return ac, tc
+            return scores_to_host(sq, tw)
 
     def launch_feat(c):
         # featurise chunk c on the side stream once the last encode's conv stage (the last reader of feats) is done:
@@ -747,14 +760,13 @@ def run_score(args, world, rank, dev):
             side.wait_event(tx_done)
         sst = tail if tail is not None else (side if mode == "side2" else cur)
         with torch.cuda.stream(sst):
-            ac, tc = ops.score_videos(sq, tw, first, vcls, centroids)
-            host_ac.copy_(ac, non_blocking=True)
-            host_tc.copy_(tc, non_blocking=True)
+            ac, tc = scores_to_host(sq, tw)
         return ac, tc
 
     # precision evidence for the timed mode: the untimed first step's scores vs the oracle on a sample of clips
     ac_a, tc_a = step(flush=True)
     torch.cuda.synchronize()  # the scores may come from the tail stream
+    ac_a, tc_a = ac_a.clone(), tc_a.clone()  # (--host-scores direct: the pinned buffers every step rewrites)
     precision = oracle_precision(gen_clips, stats.mean, stats.std, centroids, vcls, seq, ac_a, tc_a, starts,
                                  n=16 if cfg5 else V) if rank == 0 else None
     torch.cuda.synchronize()

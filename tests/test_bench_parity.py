@@ -473,3 +473,32 @@ def test_config5_chunk_schedule_vs_oracle(compute, mix, monkeypatch):
     assert torch.isfinite(ac).all() and torch.isfinite(tc).all()
     assert e_ac < 1e-4 and e_tc < 1e-4, (e_ac, e_tc)
     assert e_seq < (2e-5 if compute == "f32x3" else 2e-4), e_seq
+
+
+def test_scores_written_directly_into_pinned_host_memory():
+    """bench.py --host-scores direct (the default): the per-video score kernel writes AC / TC straight into the pinned
+    host buffers (page-locked host memory is mapped into the GPU's address space) instead of device tensors + two copy
+    kernels.  Over several videos per class, an unknown class (no AC: NaN) and repeated launches into the same buffers:
+    bit-identical to the device outputs once the stream is synchronised."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from vge import ops
+    g = torch.Generator().manual_seed(3)
+    V, per = 97, 3
+    seq = torch.nn.functional.normalize(torch.randn(V * per, 256, generator=g), dim=-1).to(DEV)
+    tcw = torch.rand(V * per, generator=g).to(DEV)
+    first = torch.arange(0, V * per + 1, per, dtype=torch.int32, device=DEV)
+    vcls = torch.tensor([(i % 11) - 1 for i in range(V)], dtype=torch.int32, device=DEV)   # -1: unknown class
+    cent = torch.nn.functional.normalize(torch.randn(10, 256, generator=g), dim=-1).to(DEV)
+    ac_d, tc_d = ops.score_videos(seq, tcw, first, vcls, cent)
+    hac = torch.full((V,), 7.0, dtype=torch.float32, pin_memory=True)
+    htc = torch.full((V,), 7.0, dtype=torch.float64, pin_memory=True)
+    for _ in range(3):
+        out = ops.score_videos(seq, tcw, first, vcls, cent, out=(hac, htc))
+        assert out[0].data_ptr() == hac.data_ptr() and out[1].data_ptr() == htc.data_ptr()
+    torch.cuda.synchronize()
+    assert np.array_equal(hac.numpy(), ac_d.cpu().numpy(), equal_nan=True)
+    assert np.array_equal(htc.numpy(), tc_d.cpu().numpy())
+    assert int(torch.isnan(hac).sum()) == sum(1 for i in range(V) if i % 11 == 0)
+    with pytest.raises(Exception):
+        ops.score_videos(seq, tcw, first, vcls, cent, out=(torch.empty(V), torch.empty(V, dtype=torch.float64)))

@@ -261,16 +261,31 @@ def tc_windows(frame_embeds: torch.Tensor) -> torch.Tensor:
 
 
 def score_videos(seq: torch.Tensor, tc_window: torch.Tensor, video_first_win: torch.Tensor, video_class: torch.Tensor,
-                 centroids: Optional[torch.Tensor]) -> Tuple[torch.Tensor, torch.Tensor]:
+                 centroids: Optional[torch.Tensor], out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None
+                 ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Per-video AC (float32) / TC (float64).  out: (ac [V] float32, tc [V] float64) to write instead of new device
+    tensors -- device tensors, or pinned (page-locked) host tensors, which the kernel then writes directly over the
+    bus (no copy kernels; the values are the host's once the stream is synchronised)."""
     lib = L.load()
     V = int(video_class.shape[0])
     d = int(seq.shape[1])
-    ac = torch.empty((V,), device=seq.device, dtype=torch.float32)
-    tc = torch.empty((V,), device=seq.device, dtype=torch.float64)
+    if out is not None:
+        ac, tc = out
+        if (ac.dtype, tc.dtype) != (torch.float32, torch.float64) or ac.numel() < V or tc.numel() < V or \
+                not ac.is_contiguous() or not tc.is_contiguous() or \
+                any(not t.is_cuda and not t.is_pinned() for t in (ac, tc)):
+            raise L.VgeError("score_videos: out must be contiguous (float32, float64) tensors of >= V elements, on the "
+                             "device or in pinned host memory")
+    else:
+        ac = torch.empty((V,), device=seq.device, dtype=torch.float32)
+        tc = torch.empty((V,), device=seq.device, dtype=torch.float64)
     if centroids is None:
         centroids = torch.zeros((1, d), device=seq.device, dtype=torch.float32)
+    # (a pinned host tensor's address is also its device address: HIP maps page-locked host memory into the GPU's
+    # virtual address space at the same address)
+    op = lambda t: _ptr(t) if t.is_cuda else t.data_ptr()  # noqa: E731
     L.check(lib.vge_score_videos(_ptr(seq), _ptr(tc_window), _ptr(video_first_win), _ptr(video_class), _ptr(centroids),
-                                 V, d, _ptr(ac), _ptr(tc), _stream(seq.device)), "vge_score_videos")
+                                 V, d, op(ac), op(tc), _stream(seq.device)), "vge_score_videos")
     return ac, tc
 
 
