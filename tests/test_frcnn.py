@@ -204,12 +204,16 @@ def test_predictor_end_to_end_vs_oracle(run, oracle_fwd):
 
 @pytest.mark.parametrize("gw,stride,C,H,W", [(8, 1, 256, 20, 37), (16, 2, 512, 21, 18), (32, 1, 1024, 13, 11),
                                              (64, 1, 2048, 9, 10), (32, 2, 1024, 14, 13), (64, 2, 2048, 7, 6),
-                                             (8, 2, 256, 15, 16), (16, 1, 512, 10, 33)])
+                                             (8, 2, 256, 15, 16), (16, 1, 512, 10, 33),
+                                             (32, 1, 1024, 50, 50), (16, 1, 512, 100, 100), (8, 1, 256, 200, 200),
+                                             (32, 2, 1024, 100, 100), (16, 2, 512, 200, 200), (32, 1, 1024, 51, 47)])
 def test_grouped_conv_kernel_vs_torch(gw, stride, C, H, W):
     """The bottlenecks' grouped 3x3 conv (vge_gconv.hip: + folded bias, ReLU) alone vs torch conv2d(groups = C / gw)
     in f32 on the same bf16 operands: every group width of X101-32x8d (8 .. 64 channels per group), both strides,
     ragged tiles (group widths 8 / 16 run two taps per 16x16x32 MFMA, the ninth against zero weights; 32 / 64 one or
-    two MFMAs per tap).  The kernel rounds its f32 sums to bf16 once."""
+    two MFMAs per tap).  The kernel rounds its f32 sums to bf16 once.  The output tile is picked per shape
+    (gc_pick_tile): the detector's 200 / 100 / 50-wide maps at both strides take tiles whose 16-pixel groups run across
+    rows (5 x 25, 6 x 10), the small shapes whole-image tiles, 51 x 47 a partial last group."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     import ctypes as C_

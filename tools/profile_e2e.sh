@@ -6,7 +6,7 @@
 #   frcnn_{trace,fetch,write}  kernel trace + stats and PMC of the gate detector (tools/time_frcnn.py, 128 frames in
 #                        one 128-frame chunk, the product's: a warm call + 1 timed call; the counters of the timed call)
 # Summarise with tools/pmc_e2e.py TAG (-> profiles/pmc_e2e.json) and tools/yolox_prof_check.py.
-#   Usage (repo root, GPU box): bash tools/profile_e2e.sh TAG
+#   Usage (repo root, GPU box): bash tools/profile_e2e.sh TAG   (ONLY=frcnn: the three frcnn passes only)
 set -u
 TAG=$1
 R=${GRAFT_REPO_ROOT:-$(pwd)}; OUT=$R/gpurun_out; mkdir -p "$OUT"
@@ -23,6 +23,7 @@ FRCNN="$R/tools/time_frcnn.py 128 128 1"
 run frcnn_trace "$FRCNN" --kernel-trace --stats &&
 run frcnn_fetch "$FRCNN" --pmc FETCH_SIZE --kernel-trace &&
 run frcnn_write "$FRCNN" --pmc WRITE_SIZE --kernel-trace &&
+{ [ "${ONLY:-}" = frcnn ] && exit 0; true; } &&
 run yolox_trace "$YOLOX" --kernel-trace --stats &&
 run yolox_fetch "$YOLOX" --pmc FETCH_SIZE --kernel-trace &&
 run yolox_write "$YOLOX" --pmc WRITE_SIZE --kernel-trace &&

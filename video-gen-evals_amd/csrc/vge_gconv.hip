@@ -9,6 +9,9 @@
 // during this one's MFMAs; the weights are read once for all of them):
 //   * the input tile with its halo ((TH-1) S + 3) x ((TW-1) S + 3) pixels x 64 channels is read once into LDS (rows of
 //     144 B: 64 channels + 8 pad, so 16 consecutive pixels' 8-B reads fall on distinct banks);
+//   * TH x TW is chosen per layer shape on the host (gc_pick_tile: up to 128 output pixels, the pixel tiles of 16 run
+//     across the tile's rows), so that the tiles cover the output with little overhang: 5 x 25 at the detector's 200 /
+//     100 / 50-wide stride-1 maps, where the fixed 4 x 32 tile ran 33 % idle pixel slots at 50 x 50 (res4);
 //   * wave w owns output channels 16w..16w+15 of the slice; its weights (9 taps x the 16-channel K steps of its group,
 //     v_mfma_f32_16x16x16_bf16 A fragments, 2 registers each) stay in registers for the whole tile;
 //   * per 16-pixel tile, tap and K step one MFMA: A = weights [16 out ch x 16 in ch], B = input [16 in ch x 16 pixels]
@@ -17,7 +20,9 @@
 // K steps: a 16-channel output tile's inputs are its group's channels, max(group width, 16) of them (group width 8:
 // the 16 x 16 weight block holds two groups' 8 x 8 blocks and zeros, as packed by vge_frcnn.cpp's gconv_bn).
 #include "vge_common.h"
+#include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 namespace {
@@ -25,6 +30,9 @@ namespace {
 typedef short short4v __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+typedef unsigned uintx4_t __attribute__((ext_vector_type(4)));
+typedef unsigned uintx2_t __attribute__((ext_vector_type(2)));
+constexpr int GC_OOB = 0x7FFFFFF0;  // buffer offset past every record count: loads return 0, stores are dropped
 
 constexpr int GC_PITCH = 144;  // LDS bytes per input pixel (64 bf16 channels + 8 pad)
 
@@ -34,21 +42,35 @@ struct GconvArgs {
   const float* bias;
   __bf16* out;      long ldo;
   int H, W, Ho, Wo, tiles_x, n_img;
+  int th, tw, iw, npix;         // output tile th x tw (th * tw <= 16 gc_npt), input tile iw wide, npix pixels
+  float inv_tw, inv_iw;         // 1 / tw, 1 / iw (gc_div)
+  int ntiles, nslices, xcd;     // workgroup = (tile, 64-channel slice, image group), tile fastest; xcd: gc_xcd order
 };
+
+// Workgroup b of nblk -> its (tile, slice, image group) id.  Workgroups are dealt to the 8 XCDs round robin, so in
+// launch order a tile's neighbours -- which read its halo rows -- run on other XCDs and fetch those rows into their own
+// L2s; with xcd set each XCD takes a contiguous range of ids instead (bijective), the tiles of a slice and image group
+// run side by side on one XCD and the halo rows hit its L2.
+__device__ __forceinline__ int gc_xcd(int b, int nblk, int on) {
+  if (!on) return b;
+  const int q8 = nblk >> 3, r8 = nblk & 7, x8 = b & 7;
+  return (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (b >> 3);
+}
 #ifndef VGE_GC_NI
 #define VGE_GC_NI 4
 #endif
 constexpr int GC_NI = VGE_GC_NI;  // images per workgroup: its weights (up to 72 registers) are loaded once for all of them
 
-#ifndef VGE_GC_TH
-#define VGE_GC_TH 4
-#endif
+// 16-pixel tiles per output tile at most: th * tw <= 128 at stride 1, 64 at stride 2 (its wider input tile per pixel)
 template <int S>
-constexpr int gc_th() { return S == 1 ? VGE_GC_TH : 4; }
+constexpr int gc_npt() { return S == 1 ? 8 : 4; }
+// input tile pixels at most (LDS: 216 x 144 B = 31 KB at stride 1, 297 x 144 B = 42.8 KB at stride 2 -- the 4 x 16 tile)
 template <int S>
-constexpr int gc_tw() { return S == 1 ? 32 : 16; }
-template <int S>
-constexpr int gc_lds() { return ((gc_th<S>() - 1) * S + 3) * ((gc_tw<S>() - 1) * S + 3) * GC_PITCH; }
+constexpr int gc_npix_max() { return S == 1 ? 216 : 297; }
+
+// n / d for 0 <= n < 2^12 and 1 <= d < 2^8 from inv = 1 / d: (n + 0.5) / d lies at least 1 / 512 from an integer, far
+// more than the float product's error, so the truncation is exact
+__device__ __forceinline__ int gc_div(int n, float inv) { return (int)(((float)n + 0.5f) * inv); }
 
 // KS: 16-channel K steps per tap (max(group width, 16) / 16); S: stride; MF: 0 = v_mfma_f32_16x16x16_bf16 (one per
 // 16-channel step), 1 = v_mfma_f32_16x16x32_bf16 (gfx950's full-rate bf16 form: the legacy 16x16x16 issues at half the
@@ -57,32 +79,50 @@ constexpr int gc_lds() { return ((gc_th<S>() - 1) * S + 3) * ((gc_tw<S>() - 1) *
 #ifndef VGE_GC_OCC
 #define VGE_GC_OCC 1  // minimum waves per SIMD the register allocation must allow (= workgroups per CU)
 #endif
+#ifndef VGE_GC_OCC_SMALL
+#define VGE_GC_OCC_SMALL 3  // the same for group widths <= 32 (res2-4): 3 fit without scratch (<= 163 VGPRs)
+#endif
 template <int KS, int S, int MF>
-__global__ void __launch_bounds__(256, VGE_GC_OCC) gconv3_kernel(GconvArgs a) {
-  constexpr int TH = gc_th<S>(), TW = gc_tw<S>(), NPT = TH * TW / 16;
-  constexpr int IH = (TH - 1) * S + 3, IW = (TW - 1) * S + 3, NPIX = IH * IW;
-  __shared__ __attribute__((aligned(16))) char tile[gc_lds<S>()];
+__global__ void __launch_bounds__(256, KS <= 2 ? VGE_GC_OCC_SMALL : VGE_GC_OCC) gconv3_kernel(GconvArgs a) {
+  constexpr int NPIXM = gc_npix_max<S>();
+  __shared__ __attribute__((aligned(16))) char tile[NPIXM * GC_PITCH];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int slice = blockIdx.y, img0 = blockIdx.z * GC_NI, nimg = min(GC_NI, a.n_img - img0);
-  const int ty = blockIdx.x / a.tiles_x, tx = blockIdx.x - ty * a.tiles_x;
-  const int oy0 = ty * TH, ox0 = tx * TW;
+  const int bid = gc_xcd(blockIdx.x, gridDim.x, a.xcd), tile_id = bid % a.ntiles, rest = bid / a.ntiles;
+  const int slice = rest % a.nslices, img0 = (rest / a.nslices) * GC_NI, nimg = min(GC_NI, a.n_img - img0);
+  const int ty = tile_id / a.tiles_x, tx = tile_id - ty * a.tiles_x;
+  const int TW = a.tw, IW = a.iw, NPIX = a.npix, NPX = a.th * TW, npt = (NPX + 15) >> 4;
+  const int oy0 = ty * a.th, ox0 = tx * TW;
   const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
 
-  // ---- the input tile of image img (zeros outside the image: the conv's padding) into registers
-  constexpr int NLD = (NPIX * 8 + 255) / 256;
-  uint4 v[NLD];
-  auto load_tile = [&](int img) {
-    const __bf16* xs = a.x + (size_t)img * a.H * a.W * a.ldx + slice * 64;
+  // ---- the input tile of image img into registers: buffer loads through a per-image resource, a pixel outside the
+  // image (the conv's zero padding) at an offset past the record count, so that every load issues unconditionally and
+  // the next image's loads stay in flight across this image's MFMAs (a branch around each load made the compiler wait
+  // for them right after issuing; stores count in the same vmcnt, so the epilogue stores are buffer stores too)
+  constexpr int NLD = (NPIXM * 8 + 255) / 256;
+  uintx4_t v[NLD];
+  int gofs[NLD];  // byte offsets inside an image (the same for every image of the workgroup)
+#pragma unroll
+  for (int q = 0; q < NLD; ++q) {
+    const int c = tid + 256 * q, p = c >> 3, j = c & 7;
+    const int dy = gc_div(p, a.inv_iw), iy = iy0 + dy, ix = ix0 + p - dy * IW;
+    gofs[q] = (p < NPIX && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
+                  ? ((iy * a.W + ix) * (int)a.ldx + j * 8) * 2 : GC_OOB;
+  }
+  const int in_bytes = (a.H * a.W * (int)a.ldx - slice * 64) * 2;
+  auto load_tile = [&](int img, bool real) {  // real = false: the same instructions on an empty record range
+    const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<__bf16*>(a.x + (size_t)img * a.H * a.W * a.ldx + slice * 64), (short)0, real ? in_bytes : 0,
+        0x00020000);
+#pragma unroll
+    for (int q = 0; q < NLD; ++q) v[q] = __builtin_amdgcn_raw_buffer_load_b128(xr, gofs[q], 0, 0);
+  };
+  auto store_tile = [&]() {
 #pragma unroll
     for (int q = 0; q < NLD; ++q) {
       const int c = tid + 256 * q, p = c >> 3, j = c & 7;
-      const int iy = iy0 + p / IW, ix = ix0 + p % IW;
-      v[q] = make_uint4(0, 0, 0, 0);
-      if (p < NPIX && (unsigned)iy < (unsigned)a.H && (unsigned)ix < (unsigned)a.W)
-        v[q] = *reinterpret_cast<const uint4*>(xs + ((long)iy * a.W + ix) * a.ldx + j * 8);
+      if (p < NPIX) *reinterpret_cast<uintx4_t*>(tile + p * GC_PITCH + j * 16) = v[q];
     }
   };
-  load_tile(img0);
   // ---- this wave's weights: 16 output channels x 9 taps x KS K steps (A fragments: lane = output channel l & 15,
   // input channels 4 (l >> 4) .. + 3 of the step)
   const int n0 = wave * 16;
@@ -101,9 +141,10 @@ __global__ void __launch_bounds__(256, VGE_GC_OCC) gconv3_kernel(GconvArgs a) {
   for (int t = 0; t < NT; ++t)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      if constexpr (MF && KS == 1) {
+      if constexpr (MF && KS == 1) {  // (tap 9 loads tap 8 and zeroes it: no branch around a load)
         const int tap = 2 * t + hh;
-        wa[t][j] = tap < 9 ? *reinterpret_cast<const Frag*>(wr + tap * 64) : Frag{};
+        const Frag f = *reinterpret_cast<const Frag*>(wr + min(tap, 8) * 64);
+        wa[t][j] = tap < 9 ? f : Frag{};
       } else {
         wa[t][j] = *reinterpret_cast<const Frag*>(wr + t * 64 + (MF ? 32 : 16) * j);
       }
@@ -112,24 +153,25 @@ __global__ void __launch_bounds__(256, VGE_GC_OCC) gconv3_kernel(GconvArgs a) {
   const char* lb = tile + (cbase + cl) * 2;
   const int ch = slice * 64 + n0 + 4 * (lane >> 4);
   const floatx4 bv = *reinterpret_cast<const floatx4*>(a.bias + ch);
+  // Per image: the next image's loads, this image's MFMAs and stores, then the next tile into LDS.  Every iteration
+  // issues the same loads and stores unconditionally (the last one's loads out of range), so the compiler's vmcnt wait
+  // for a tile register counts the 8 stores issued after it instead of waiting for them too.
+  load_tile(img0, true);  // after the weights and bias: waiting for the tile waits for them
+  store_tile();
+  __syncthreads();
   for (int k = 0; k < nimg; ++k) {
     const int img = img0 + k;
-    if (k > 0) __syncthreads();  // every wave is done reading the previous image's tile
-#pragma unroll
-    for (int q = 0; q < NLD; ++q) {
-      const int c = tid + 256 * q, p = c >> 3, j = c & 7;
-      if (p < NPIX) *reinterpret_cast<uint4*>(tile + p * GC_PITCH + j * 16) = v[q];
-    }
-    __syncthreads();
-    if (k + 1 < nimg) load_tile(img + 1);  // the next image's loads in flight during this one's MFMAs
+    load_tile(img0 + min(k + 1, nimg - 1), k + 1 < nimg);  // in flight during this image's MFMAs
 
-    // ---- MFMAs: pixel tile pt = output pixels pt * 16 .. + 15 of the tile (row-major, TW / 16 tiles per row)
-    floatx4 acc[NPT];
+    // ---- MFMAs: pixel tile pt = output pixels pt * 16 .. + 15 of the tile (row-major, running across rows; lanes past
+    // the tile's last pixel recompute that pixel and store nothing)
+    floatx4 acc[gc_npt<S>()];
 #pragma unroll
-    for (int pt = 0; pt < NPT; ++pt) acc[pt] = floatx4{0.f, 0.f, 0.f, 0.f};
+    for (int pt = 0; pt < gc_npt<S>(); ++pt) acc[pt] = floatx4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int pt = 0; pt < NPT; ++pt) {
-      const int op = pt * 16 + px, orow = op / TW, ocol = op % TW;
+    for (int pt = 0; pt < gc_npt<S>(); ++pt) {
+      if (pt >= npt) break;
+      const int op = min(pt * 16 + px, NPX - 1), orow = gc_div(op, a.inv_tw), ocol = op - orow * TW;
       const char* pb = lb + ((orow * S) * IW + ocol * S) * GC_PITCH;
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
@@ -154,17 +196,66 @@ __global__ void __launch_bounds__(256, VGE_GC_OCC) gconv3_kernel(GconvArgs a) {
       }
     }
     // ---- epilogue: lane = pixel l & 15 of the tile, output channels n0 + 4 (l >> 4) .. + 3
+    const __amdgpu_buffer_rsrc_t orr = __builtin_amdgcn_make_buffer_rsrc(
+        a.out + (size_t)img * a.Ho * a.Wo * a.ldo, (short)0, a.Ho * a.Wo * (int)a.ldo * 2, 0x00020000);
 #pragma unroll
-    for (int pt = 0; pt < NPT; ++pt) {
-      const int op = pt * 16 + px, oy = oy0 + op / TW, ox = ox0 + op % TW;
-      if (oy < a.Ho && ox < a.Wo) {
-        bf16x4_t o;
+    for (int pt = 0; pt < gc_npt<S>(); ++pt) {  // all of them (out of range past npt): a fixed store count
+      const int op = pt * 16 + px, r = gc_div(op, a.inv_tw), oy = oy0 + r, ox = ox0 + op - r * TW;
+      const int oo = (op < NPX && oy < a.Ho && ox < a.Wo) ? ((oy * a.Wo + ox) * (int)a.ldo + ch) * 2 : GC_OOB;
+      bf16x4_t o;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) o[i] = (__bf16)fmaxf(acc[pt][i] + bv[i], 0.f);
-        *reinterpret_cast<bf16x4_t*>(a.out + (((size_t)img * a.Ho + oy) * a.Wo + ox) * a.ldo + ch) = o;
-      }
+      for (int i = 0; i < 4; ++i) o[i] = (__bf16)fmaxf(acc[pt][i] + bv[i], 0.f);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uintx2_t, o), orr, oo, 0, 0);
+    }
+    if (k + 1 < nimg) {
+      __syncthreads();  // every wave is done reading this image's tile
+      store_tile();
+      __syncthreads();
     }
   }
+}
+
+// Output tile of a grouped conv: th x tw pixels (th * tw <= 16 gc_npt, the input tile within gc_npix_max), by a
+// cost per workgroup and image in LDS-byte units: 16-pixel slots x 9 taps x 64 B x 4 waves of B-fragment reads
+// (idle slots of a partial tile cost the same), the input tile's global loads and LDS stores, and a fixed part
+// (barriers, epilogue).  VGE_GC_TILE="THxTW" forces a tile (A/B), "legacy" the fixed 4 x 32 (stride 1) / 4 x 16.
+void gc_pick_tile(int Ho, int Wo, int S, int& th, int& tw) {
+  static int fth = -1, ftw = -1;
+  if (fth < 0) {
+    fth = ftw = 0;
+    const char* e = getenv("VGE_GC_TILE");
+    if (e && !strcmp(e, "legacy")) fth = ftw = -2;
+    else if (e && sscanf(e, "%dx%d", &fth, &ftw) != 2) fth = ftw = 0;
+  }
+  const int npm = S == 1 ? gc_npix_max<1>() : gc_npix_max<2>(), npx = 16 * (S == 1 ? gc_npt<1>() : gc_npt<2>());
+  auto fits = [&](int h, int w) {
+    return h >= 1 && w >= 1 && h * w <= npx && ((h - 1) * S + 3) * ((w - 1) * S + 3) <= npm;
+  };
+  if (fth == -2) {
+    th = 4;
+    tw = S == 1 ? 32 : 16;
+    return;
+  }
+  if (fth > 0 && fits(fth, ftw)) {
+    th = fth;
+    tw = ftw;
+    return;
+  }
+  double best = 1e300;
+  th = 4;
+  tw = S == 1 ? 32 : 16;
+  for (int w = 8; w <= 64; ++w)
+    for (int h = 1; h <= 16; ++h) {
+      if (!fits(h, w)) continue;
+      const double tiles = (double)((Ho + h - 1) / h) * ((Wo + w - 1) / w);
+      const int npix = ((h - 1) * S + 3) * ((w - 1) * S + 3);
+      const double cost = tiles * (((h * w + 15) / 16) * 16.0 * 9 * 64 * 4 / 128 + npix * 5.0 + 600);
+      if (cost < best) {
+        best = cost;
+        th = h;
+        tw = w;
+      }
+    }
 }
 
 }  // namespace
@@ -176,13 +267,31 @@ namespace vge {
 hipError_t launch_gconv3(const void* x, long ldx, const void* w, int Kp, const float* bias, void* out, long ldo,
                          int n_img, int H, int W, int C, int gw, int stride, hipStream_t s) {
   if (C % 64 || gw < 1 || 64 % gw || (stride != 1 && stride != 2) || Kp != 9 * 64 || n_img < 1 || H < 1 || W < 1 ||
-      ldx % 4 || ldo % 4)
-    return hipErrorInvalidValue;
+      ldx % 4 || ldo % 4 || (double)H * W * ldx * 2 >= 2147483632.0 ||
+      (double)((H + 2 - 3) / stride + 1) * ((W + 2 - 3) / stride + 1) * ldo * 2 >= 2147483632.0)
+    return hipErrorInvalidValue;  // per-image byte offsets and record counts are int, below GC_OOB
   GconvArgs a{reinterpret_cast<const __bf16*>(x), ldx, reinterpret_cast<const __bf16*>(w), Kp, bias,
               reinterpret_cast<__bf16*>(out), ldo, H, W, (H + 2 - 3) / stride + 1, (W + 2 - 3) / stride + 1, 0, n_img};
-  const int th = stride == 1 ? VGE_GC_TH : 4, tw = stride == 1 ? 32 : 16;
+  int th, tw;
+  gc_pick_tile(a.Ho, a.Wo, stride, th, tw);
+  a.th = th;
+  a.tw = tw;
+  a.iw = (tw - 1) * stride + 3;
+  a.npix = ((th - 1) * stride + 3) * a.iw;
+  a.inv_tw = 1.f / tw;
+  a.inv_iw = 1.f / a.iw;
   a.tiles_x = (a.Wo + tw - 1) / tw;
-  const dim3 grid(a.tiles_x * ((a.Ho + th - 1) / th), C / 64, (n_img + GC_NI - 1) / GC_NI);
+  a.ntiles = a.tiles_x * ((a.Ho + th - 1) / th);
+  a.nslices = C / 64;
+  static int xcd = -1;  // VGE_GC_XCD=0: launch order
+  if (xcd < 0) {
+    const char* e = getenv("VGE_GC_XCD");
+    xcd = (e && e[0] == '0') ? 0 : 1;
+  }
+  a.xcd = xcd;
+  const long nblk = (long)a.ntiles * a.nslices * ((n_img + GC_NI - 1) / GC_NI);
+  if (nblk >= 2147483647L) return hipErrorInvalidValue;
+  const dim3 grid((unsigned)nblk);
   const int ks = gw <= 16 ? 1 : gw / 16;
   static int mf = -1;  // VGE_GC_MF: 1 (default) = 16x16x32, 0 = 16x16x16
   if (mf < 0) {
