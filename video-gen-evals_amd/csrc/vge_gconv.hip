@@ -8,7 +8,10 @@
 // 64-channel slice (64 / group-width whole groups), for GC_NI images in turn (the next image's tile loads in flight
 // during this one's MFMAs; the weights are read once for all of them):
 //   * the input tile with its halo ((TH-1) S + 3) x ((TW-1) S + 3) pixels x 64 channels is read once into LDS (rows of
-//     144 B: 64 channels + 8 pad, so 16 consecutive pixels' 8-B reads fall on distinct banks);
+//     160 B per pixel and 192 B more per tile row at stride 1 (144 and 80 at stride 2): with those pads the 16-B B-fragment
+//     reads of a pixel tile -- 16 pixels that may run across a row end -- hit distinct banks in every ds_read_b128 lane
+//     group (2.4x conflicted at the round-5 144-B pitch on the 5 x 25 tiles; a bank model of every tile, tap and lane
+//     group picked the pads);
 //   * TH x TW is chosen per layer shape on the host (gc_pick_tile: up to 128 output pixels, the pixel tiles of 16 run
 //     across the tile's rows), so that the tiles cover the output with little overhang: 5 x 25 at the detector's 200 /
 //     100 / 50-wide stride-1 maps, where the fixed 4 x 32 tile ran 33 % idle pixel slots at 50 x 50 (res4);
@@ -34,7 +37,11 @@ typedef unsigned uintx4_t __attribute__((ext_vector_type(4)));
 typedef unsigned uintx2_t __attribute__((ext_vector_type(2)));
 constexpr int GC_OOB = 0x7FFFFFF0;  // buffer offset past every record count: loads return 0, stores are dropped
 
-constexpr int GC_PITCH = 144;  // LDS bytes per input pixel (64 bf16 channels + 8 pad)
+// LDS bytes per input pixel (64 bf16 channels + pad) and extra bytes per input row (the header's bank model)
+template <int S>
+constexpr int gc_pitch() { return S == 1 ? 160 : 144; }
+template <int S>
+constexpr int gc_rowpad() { return S == 1 ? 192 : 80; }
 
 struct GconvArgs {
   const __bf16* x;  long ldx;   // NHWC input, channel stride ldx (= width)
@@ -64,9 +71,11 @@ constexpr int GC_NI = VGE_GC_NI;  // images per workgroup: its weights (up to 72
 // 16-pixel tiles per output tile at most: th * tw <= 128 at stride 1, 64 at stride 2 (its wider input tile per pixel)
 template <int S>
 constexpr int gc_npt() { return S == 1 ? 8 : 4; }
-// input tile pixels at most (LDS: 216 x 144 B = 31 KB at stride 1, 297 x 144 B = 42.8 KB at stride 2 -- the 4 x 16 tile)
+// input tile pixels at most (297 at stride 2: the 4 x 16 tile), and its LDS bytes with up to (16 - 1) S + 3 rows
 template <int S>
 constexpr int gc_npix_max() { return S == 1 ? 216 : 297; }
+template <int S>
+constexpr int gc_lds_bytes() { return gc_npix_max<S>() * gc_pitch<S>() + (15 * S + 3) * gc_rowpad<S>(); }
 
 // n / d for 0 <= n < 2^12 and 1 <= d < 2^8 from inv = 1 / d: (n + 0.5) / d lies at least 1 / 512 from an integer, far
 // more than the float product's error, so the truncation is exact
@@ -85,7 +94,8 @@ __device__ __forceinline__ int gc_div(int n, float inv) { return (int)(((float)n
 template <int KS, int S, int MF>
 __global__ void __launch_bounds__(256, KS <= 2 ? VGE_GC_OCC_SMALL : VGE_GC_OCC) gconv3_kernel(GconvArgs a) {
   constexpr int NPIXM = gc_npix_max<S>();
-  __shared__ __attribute__((aligned(16))) char tile[NPIXM * GC_PITCH];
+  constexpr int PITCH = gc_pitch<S>(), ROWPAD = gc_rowpad<S>();
+  __shared__ __attribute__((aligned(16))) char tile[gc_lds_bytes<S>()];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int bid = gc_xcd(blockIdx.x, gridDim.x, a.xcd), tile_id = bid % a.ntiles, rest = bid / a.ntiles;
   const int slice = rest % a.nslices, img0 = (rest / a.nslices) * GC_NI, nimg = min(GC_NI, a.n_img - img0);
@@ -120,7 +130,7 @@ __global__ void __launch_bounds__(256, KS <= 2 ? VGE_GC_OCC_SMALL : VGE_GC_OCC) 
 #pragma unroll
     for (int q = 0; q < NLD; ++q) {
       const int c = tid + 256 * q, p = c >> 3, j = c & 7;
-      if (p < NPIX) *reinterpret_cast<uintx4_t*>(tile + p * GC_PITCH + j * 16) = v[q];
+      if (p < NPIX) *reinterpret_cast<uintx4_t*>(tile + p * PITCH + gc_div(p, a.inv_iw) * ROWPAD + j * 16) = v[q];
     }
   };
   // ---- this wave's weights: 16 output channels x 9 taps x KS K steps (A fragments: lane = output channel l & 15,
@@ -172,16 +182,17 @@ __global__ void __launch_bounds__(256, KS <= 2 ? VGE_GC_OCC_SMALL : VGE_GC_OCC) 
     for (int pt = 0; pt < gc_npt<S>(); ++pt) {
       if (pt >= npt) break;
       const int op = min(pt * 16 + px, NPX - 1), orow = gc_div(op, a.inv_tw), ocol = op - orow * TW;
-      const char* pb = lb + ((orow * S) * IW + ocol * S) * GC_PITCH;
+      const char* pb = lb + ((orow * S) * IW + ocol * S) * PITCH + orow * S * ROWPAD;
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         if constexpr (MF && KS == 1) {
           const int ta = 2 * t, tb = 2 * t + 1 < 9 ? 2 * t + 1 : 8;  // (tap 9: zero weights on finite data)
-          const int offa = ((ta / 3) * IW + (ta % 3)) * GC_PITCH, offb = ((tb / 3) * IW + (tb % 3)) * GC_PITCH;
+          const int offa = ((ta / 3) * IW + (ta % 3)) * PITCH + (ta / 3) * ROWPAD;
+          const int offb = ((tb / 3) * IW + (tb % 3)) * PITCH + (tb / 3) * ROWPAD;
           const bf16x8_t b = *reinterpret_cast<const bf16x8_t*>(pb + (hh ? offb : offa));
           acc[pt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa[t][0], b, acc[pt], 0, 0, 0);
         } else {
-          const int off = ((t / 3) * IW + (t % 3)) * GC_PITCH;
+          const int off = ((t / 3) * IW + (t % 3)) * PITCH + (t / 3) * ROWPAD;
 #pragma unroll
           for (int j = 0; j < NJ; ++j) {
             if constexpr (MF) {
