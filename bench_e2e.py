@@ -13,8 +13,9 @@ persons, RTMPose-l on persons 0 / 1, the whole frame when nobody is found -> key
 TokenHMR chain runs on one HIP stream, YOLOX + DWPose on another.  `--no-detector`: neither detector (whole-frame
 boxes, every frame kept).  Parity for the upstream models is unpinned.
 
-Roofline: the backbone GEMM kernel (gemm_bf16_kernel, MFMA bound): achieved = algorithmic FLOPs of every backbone
-GEMM launch / their summed durations (hipEvents recorded around each launch on the extract stream inside the timed
+Roofline: the backbone GEMMs (MFMA bound: hipBLASLt for the bias / f32-residual linears, gemm_bf16_kernel for the GELU
+and position-embedding ones; vge_blaslt.cpp): achieved = algorithmic FLOPs of every backbone GEMM launch / their
+summed durations (hipEvents recorded around each launch on the extract stream inside the timed
 steps); peak = dense bf16 MFMA 2516.6 TFLOP/s.  cpu_baseline = oracle/hmr.py (the fp32 torch restatement of the
 same ViT-H + head) + the scoring restatement on this host, bounded sample.
 """
@@ -31,9 +32,10 @@ import torch.distributed as dist
 
 BF16_MFMA_PEAK_TFLOPS = 2516.6
 # kernel sources whose PMC pass (tools/profile_e2e.sh -> tools/pmc_e2e.py -> profiles/pmc_e2e.json) gives `traffic`
-E2E_KERNEL_SOURCES = {"gemm_bf16_kernel": ["vge_vit.hip"],
-                      "yolox_conv": ["vge_cnn.hip", "vge_cnn_host.h", "vge_yolox.cpp", "vge_vit.hip"],
-                      "frcnn_conv": ["vge_cnn.hip", "vge_cnn_host.h", "vge_frcnn.cpp", "vge_vit.hip", "vge_gconv.hip"]}
+E2E_KERNEL_SOURCES = {"gemm_bf16_kernel": ["vge_vit.hip", "vge_blaslt.cpp", "vge_hmr.cpp"],
+                      "yolox_conv": ["vge_cnn.hip", "vge_cnn_host.h", "vge_yolox.cpp", "vge_vit.hip", "vge_blaslt.cpp"],
+                      "frcnn_conv": ["vge_cnn.hip", "vge_cnn_host.h", "vge_frcnn.cpp", "vge_vit.hip", "vge_gconv.hip",
+                                     "vge_blaslt.cpp"]}
 YOLOX_CHUNK = 256   # frames per detector pass (tools/yolox_prof.py --chunk: 637 vs 618 TFLOP/s at 64)
 # frames per Faster R-CNN workspace chunk (~0.3 GB per 800 x 800 frame): 64 was -6 % vs 32 (profiles/ab_r05m_*); 128,
 # possible since the 1x1 convs' GEMM epilogue addresses through 64-bit offsets, -1.2 % vs 64 (profiles/ab_r06b_frcnn_chunk.json)
@@ -396,12 +398,12 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
                                + (" [--no-detector: whole-frame boxes]" if det is None else ""),
                    "clips_per_gpu": C, "frames_per_step_per_gpu": F, "frames_per_extraction_pass": FC,
                    "parallelism": f"video-sharded x{world}"},
-        "roofline": {"bound": "mfma", "kernel": "gemm_bf16_kernel (ViT-H/16 backbone: patch-embed, qkv, proj, fc1, "
-                                                "fc2; dense bf16 MFMA peak)",
+        "roofline": {"bound": "mfma", "kernel": "ViT-H/16 backbone GEMMs: qkv, proj, fc2 on hipBLASLt, patch-embed and "
+                                                "fc1 (GELU) on gemm_bf16_kernel; dense bf16 MFMA peak",
                      "achieved": achieved, "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / BF16_MFMA_PEAK_TFLOPS,
                      "traffic": e2e_traffic("gemm_bf16_kernel", hmr_frames_per_call),
-                     "traffic_source": "profiles/pmc_e2e.json (tools/profile_e2e.sh: PMC of the same kernel on "
+                     "traffic_source": "profiles/pmc_e2e.json (tools/profile_e2e.sh: PMC of the same GEMM dispatches on "
                                        "tools/time_hmr.py, bytes per frame x frames per call)",
                      "flop_per_call": gemm_flops_per_frame * hmr_frames_per_call, "gemm_ms_per_call": gemm_ms,
                      "frames_per_call": hmr_frames_per_call},

@@ -193,6 +193,59 @@ def test_gemm_persistent_matches_one_tile_kernel(H, M, N, K, epi):
 
 
 @gpu
+@pytest.mark.parametrize("epi", ["bf16", "res_f32", "f32"])
+@pytest.mark.parametrize("M,N,K", [(49152, 3840, 1280), (12288, 1280, 5120), (1000, 256, 64), (333, 768, 1024)])
+def test_library_gemm_matches_kernel(H, M, N, K, epi):
+    """The library path (hipBLASLt through vge_op_gemm_lib: the ViT's bias / f32-residual / f32-out linears and the
+    detector's 1x1 convs run there) against gemm_bf16_kernel on the same operands: both accumulate in f32 in their own K
+    order, so f32 outputs agree to accumulation error and bf16 outputs to one rounding of it.  Also ragged M, N, K
+    that the kernel does not take (compared against the torch f32 product instead)."""
+    A = _bf((M, K), 1.0, 21).to(DEV)
+    W = _bf((N, K), K ** -0.5, 22).to(DEV)
+    bias = (torch.randn(N, generator=torch.Generator().manual_seed(23)) * 0.1).to(DEV)
+    res = (torch.randn((M, N), generator=torch.Generator().manual_seed(24)) * 0.5).to(DEV) if epi == "res_f32" else None
+    got = H.gemm_lib(A, W, epi, bias=bias, res=res)
+    ref32 = A.float() @ W.float().t() + bias
+    if res is not None:
+        ref32 = ref32 + res
+    kernel_takes = M % 256 == 0 and N % 256 == 0 and K % 64 == 0
+    ref = H.gemm_bf16(A, W, epi, bias=bias, res=res) if kernel_takes else ref32
+    torch.cuda.synchronize()
+    g, r = got.float(), ref.float()
+    assert torch.isfinite(g).all()
+    scale = float(ref32.abs().max())
+    if epi == "bf16":
+        bound = 2.0 ** -7 * r.abs() + 1e-5 * scale
+    else:
+        bound = torch.full_like(r, 2e-6 * scale * K ** 0.5)
+    err = (g - r).abs()
+    print(f"{epi} {M}x{N}x{K}: max |lib - {'kernel' if kernel_takes else 'torch f32'}| {float(err.max()):.2e}")
+    assert bool((err <= bound).all()), float((err - bound).max())
+
+
+@gpu
+def test_library_path_off_switch(H):
+    """vge_debug_set_gemm_lib(0) takes the library path out (VGE_ERR_UNSUPPORTED from vge_op_gemm_lib), and the GELU
+    epilogue is never on it (the library's GELU is the tanh form)."""
+    import ctypes as C
+    from vge import lib as Lb
+    lib = Lb.load()
+    lib.vge_debug_set_gemm_lib.argtypes = [C.c_int]
+    A = _bf((256, 256), 1.0, 31).to(DEV)
+    W = _bf((256, 256), 1.0 / 16, 32).to(DEV)
+    with pytest.raises(Lb.VgeError):
+        H.gemm_lib(A, W, "gelu_bf16")
+    try:
+        lib.vge_debug_set_gemm_lib(0)
+        with pytest.raises(Lb.VgeError):
+            H.gemm_lib(A, W, "bf16")
+    finally:
+        lib.vge_debug_set_gemm_lib(1)
+    H.gemm_lib(A, W, "bf16")
+    torch.cuda.synchronize()
+
+
+@gpu
 def test_full_depth_extractor_vs_oracle(H):
     """The whole TokenHMR extractor at full size -- HMR2's ViT-H/16 (32 blocks, E 1280, 16 heads, MLP 5120) and the
     6-layer decoder, the configuration config 3 runs (vge.hmr.TOKENHMR) -- on 3 frames vs oracle/hmr.py with the

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """HBM traffic per frame of config 3's two GEMM engines from tools/profile_e2e.sh TAG (FETCH_SIZE x 2 + WRITE_SIZE, the
 MI355X_MICROARCH.md HBM recipe, summed over dispatches):
-  gemm_bf16_kernel  the TokenHMR ViT-H/16 backbone GEMMs, every dispatch of tools/time_hmr.py's calls / its frames
+  gemm_bf16_kernel  the TokenHMR ViT-H/16 backbone GEMMs (gemm_bf16_kernel and the hipBLASLt Cijk_ kernels), every
+                    dispatch of tools/time_hmr.py's calls / its frames
   yolox_conv        the YOLOX-L detector's implicit-GEMM convs (and 1x1 convs the tuner put on gemm_bf16_kernel), the
                     dispatches of tools/yolox_prof.py's profiled calls (from the first of their letterbox_focus launches
                     on, in dispatch order) / their frames
@@ -49,14 +50,18 @@ def total(kind, keep):
 
 hinfo = last_json(f"pe_{tag}_hmr_fetch.log")
 h_frames = hinfo["frames"] * 3   # the warm call + 2 timed calls (tools/time_hmr.py --iters 2)
-h_bytes, h_n = total("hmr", lambda i, k: "gemm_bf16_kernel" in k)
+def lib_gemm(k):  # hipBLASLt (Tensile) GEMM kernels
+    return k.startswith("Cijk_") or "Cijk_" in k[:40]
+
+
+h_bytes, h_n = total("hmr", lambda i, k: "gemm_bf16_kernel" in k or lib_gemm(k))
 
 yinfo = last_json(f"pe_{tag}_yolox_fetch.log")
 fe = dispatches("yolox_fetch")
 lb = [i for i in sorted(fe) if "letterbox_focus" in fe[i][0]]
 first = lb[-yinfo["calls"] * yinfo["chunks_per_call"]]
 def conv_like(k):
-    return ("conv" in k and "bf16" in k) or "gemm_bf16_kernel" in k or "gconv3_kernel" in k
+    return ("conv" in k and "bf16" in k) or "gemm_bf16_kernel" in k or "gconv3_kernel" in k or lib_gemm(k)
 
 
 y_bytes, y_n = total("yolox", lambda i, k: i >= first and conv_like(k))
@@ -70,7 +75,7 @@ ffirst = rz[-finfo["passes"] * chunks]
 f_bytes, f_n = total("frcnn", lambda i, k: i >= ffirst and conv_like(k))
 f_frames = finfo["passes"] * finfo["frames"]
 
-res = {"gemm_bf16_kernel": {"what": "TokenHMR ViT-H/16 backbone GEMMs", "dispatches": h_n, "frames": h_frames,
+res = {"gemm_bf16_kernel": {"what": "TokenHMR ViT-H/16 backbone GEMMs (gemm_bf16_kernel + hipBLASLt)", "dispatches": h_n, "frames": h_frames,
                             "hbm_bytes_per_frame": h_bytes / h_frames,
                             "source_sha": bench.sources_sha(E2E_KERNEL_SOURCES["gemm_bf16_kernel"]),
                             "source": f"gpurun_out/pe_{tag}_hmr_*/ (tools/profile_e2e.sh {tag})"},
@@ -78,7 +83,7 @@ res = {"gemm_bf16_kernel": {"what": "TokenHMR ViT-H/16 backbone GEMMs", "dispatc
                       "frames": y_frames, "chunk": yinfo["chunk"], "hbm_bytes_per_frame": y_bytes / y_frames,
                       "source_sha": bench.sources_sha(E2E_KERNEL_SOURCES["yolox_conv"]),
                       "source": f"gpurun_out/pe_{tag}_yolox_*/ (tools/profile_e2e.sh {tag})"},
-       "frcnn_conv": {"what": "Faster R-CNN X101-32x8d-FPN convs (backbone, FPN, RPN, box head: implicit GEMM, 1x1 on gemm_bf16, grouped 3x3 on gconv3)",
+       "frcnn_conv": {"what": "Faster R-CNN X101-32x8d-FPN convs (backbone, FPN, RPN, box head: implicit GEMM, 1x1 on hipBLASLt, grouped 3x3 on gconv3)",
                       "dispatches": f_n, "frames": f_frames, "chunk": finfo["chunk"],
                       "hbm_bytes_per_frame": f_bytes / f_frames,
                       "source_sha": bench.sources_sha(E2E_KERNEL_SOURCES["frcnn_conv"]),

@@ -1318,6 +1318,27 @@ hipError_t launch_conv_bf16(const ConvLaunch& c, hipStream_t s) {
   a.gslice = c.gslice;
   int tn = c.tn, pmode = -1;
   int variant = c.variant == 0 && g_conv_force > 0 && !c.gslice ? g_conv_force : c.variant;
+  if (variant == 11) {  // the library GEMM (vge_blaslt.cpp; conv_tuned_launch's choice for the shapes it takes)
+    const int epi = conv_gemm_epi(c);
+    if (epi >= 0) {
+      GemmBf16 g{};
+      g.A = c.x;
+      g.lda = c.ldx;
+      g.W = c.w;
+      g.ldw = c.Kp;
+      g.out = c.out;
+      g.ldo = c.ldo;
+      g.bias = c.bias;
+      g.ldr = c.ldr;
+      g.resb = c.res;
+      g.M = a.M;
+      g.N = c.Cout;
+      g.K = c.Cin;
+      const hipError_t e = launch_gemm_lib(epi, g, s);
+      if (e != hipErrorNotSupported) return e;
+    }
+    variant = 9;  // not on the library path: the GEMM kernel where it applies, else the default below
+  }
   if (variant == 9 || variant == 10) {  // the GEMM kernel (tuner candidates, or forced by vge_debug_set_conv_variant)
     const int epi = conv_gemm_epi(c);
     if (epi >= 0) {
@@ -1341,7 +1362,7 @@ hipError_t launch_conv_bf16(const ConvLaunch& c, hipStream_t s) {
       return launch_gemm_bf16(epi, g, s);
     }
     if (c.variant == 9 || c.variant == 10) return hipErrorInvalidValue;
-    variant = 0;  // forced globally: layers the GEMM cannot take keep the default kernel
+    variant = 0;  // forced globally (or the library's fallback): layers the GEMM cannot take keep the default kernel
   }
   // grouped slices run on the 128- / 256-row kernel only, with the slice width as the column tile
   if (c.gslice && (variant == 2 || variant == 3 || variant == 6 || (c.tn != 64 && c.tn != 128) || c.Cin != c.tn ||

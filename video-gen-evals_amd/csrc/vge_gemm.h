@@ -35,5 +35,11 @@ hipError_t launch_gemm_bf16(int epi, const GemmBf16& a, hipStream_t s);
 // it does not apply (gemm_persist_ok)
 hipError_t launch_gemm_bf16_persistent(int epi, const GemmBf16& a, hipStream_t s);
 bool gemm_persist_ok(int epi, const GemmBf16& a);
+// the same product through hipBLASLt (vge_blaslt.cpp) for the epilogues a library epilogue expresses (bias, ReLU, a
+// bf16 residual before the ReLU, the f32 residual stream, f32 out); hipErrorNotSupported where it does not apply or
+// VGE_GEMM_LIB=0 (callers then run launch_gemm_bf16)
+hipError_t launch_gemm_lib(int epi, const GemmBf16& a, hipStream_t s);
+bool gemm_lib_ok(int epi);
+void gemm_lib_set(int on);
 
 }  // namespace vge

@@ -157,6 +157,11 @@ bool upload_lin(vge_hmr* m, const float* W, int N, int K, long ldk, const float*
 int gemm(int epi, const void* A, long lda, const Lin& L, void* out, long ldo, int M, hipStream_t s,
          const float* res = nullptr, long ldr = 0, const float* pos = nullptr, int tokens = 1) {
   vge::GemmBf16 g{A, lda, L.W, (long)L.K, out, ldo, L.b, res, ldr, pos, tokens, M, L.Npad, L.K};
+  if (vge::gemm_lib_ok(epi)) {  // bias / f32-residual epilogues: hipBLASLt (vge_blaslt.cpp); GELU, PE: the kernel
+    const hipError_t e = vge::launch_gemm_lib(epi, g, s);
+    if (e == hipSuccess) return VGE_OK;
+    if (e != hipErrorNotSupported) HIPCHK(e);
+  }
   HIPCHK(vge::launch_gemm_bf16(epi, g, s));
   return VGE_OK;
 }
@@ -515,6 +520,21 @@ int vge_op_gemm_bf16(int epi, const void* A, long lda, const void* W, long ldw, 
   HIPCHK(vge::launch_gemm_bf16(epi, g, S(stream)));
   return VGE_OK;
 }
+
+int vge_op_gemm_lib(int epi, const void* A, long lda, const void* W, long ldw, void* out, long ldo, const float* bias,
+                    const float* res, long ldr, int M, int N, int K, vge_stream_t stream) {
+  if (epi < 0 || epi > 4 || !A || !W || !out || M <= 0 || N <= 0 || K <= 0 || lda < K || ldw < K || ldo < N ||
+      (epi == GE_RES_F32 && (!res || ldr < N)))
+    return fail(VGE_ERR_ARG, "vge_op_gemm_lib: unsupported shape / arguments");
+  if (!vge::gemm_lib_ok(epi)) return fail(VGE_ERR_UNSUPPORTED, "vge_op_gemm_lib: epilogue not on the library path");
+  vge::GemmBf16 g{A, lda, W, ldw, out, ldo, bias, res, ldr, nullptr, 1, M, N, K};
+  const hipError_t e = vge::launch_gemm_lib(epi, g, S(stream));
+  if (e == hipErrorNotSupported) return fail(VGE_ERR_UNSUPPORTED, "vge_op_gemm_lib: no library algorithm");
+  HIPCHK(e);
+  return VGE_OK;
+}
+
+void vge_debug_set_gemm_lib(int on) { vge::gemm_lib_set(on); }
 
 int vge_op_vit_attention(const void* qkv, void* out, int F, int D, int heads, vge_stream_t stream) {
   if (!qkv || !out || F <= 0 || heads <= 0 || D % heads || (D / heads != 64 && D / heads != 80) || D % 8)

@@ -66,6 +66,7 @@ def _sig(lib):
         "vge_hmr_profile_read": [vp, C.POINTER(C.c_double), C.POINTER(C.c_int), C.POINTER(C.c_double)],
         "vge_op_gemm_bf16": [i32, vp, C.c_long, vp, C.c_long, vp, C.c_long, vp, vp, C.c_long, vp, i32, i32, i32, i32,
                              vp],
+        "vge_op_gemm_lib": [i32, vp, C.c_long, vp, C.c_long, vp, C.c_long, vp, vp, C.c_long, i32, i32, i32, vp],
         "vge_op_vit_attention": [vp, vp, i32, i32, i32, vp],
         "vge_hmr_crop": [vp, i32, i32, i32, vp, vp, i32, vp, vp],
         "vge_op_layernorm_bf16": [vp, vp, vp, vp, i32, i32, C.c_float, vp],
@@ -174,6 +175,21 @@ def gemm_bf16(A: torch.Tensor, W: torch.Tensor, epi: str = "bf16", bias=None, re
     L.check(lib.vge_op_gemm_bf16(EPI[epi], _ptr(A), A.stride(0), _ptr(W), W.stride(0), _ptr(out), out.stride(0),
                                  _ptr(bias), _ptr(res), res.stride(0) if res is not None else 0, _ptr(pos), tokens,
                                  M, N, K, _stream(A.device)), "vge_op_gemm_bf16")
+    return out
+
+
+def gemm_lib(A: torch.Tensor, W: torch.Tensor, epi: str = "bf16", bias=None, res=None,
+             out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """The same product through the library path (hipBLASLt; vge_blaslt.cpp) for the "bf16", "res_f32" and "f32"
+    epilogues; raises VGE_ERR_UNSUPPORTED for the others."""
+    lib = _sig(L.load())
+    M, K = A.shape
+    N = W.shape[0]
+    if out is None:
+        out = torch.empty((M, N), device=A.device, dtype=torch.bfloat16 if epi == "bf16" else torch.float32)
+    L.check(lib.vge_op_gemm_lib(EPI[epi], _ptr(A), A.stride(0), _ptr(W), W.stride(0), _ptr(out), out.stride(0),
+                                _ptr(bias), _ptr(res), res.stride(0) if res is not None else 0, M, N, K,
+                                _stream(A.device)), "vge_op_gemm_lib")
     return out
 
 
