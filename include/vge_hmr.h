@@ -83,11 +83,9 @@ int vge_op_gemm_bf16(int epi, const void* A, long lda, const void* W, long ldw, 
                      vge_stream_t stream);
 /* The same product through hipBLASLt (the extractor's library path for the bias, f32-residual and f32-out
  * epilogues 0, 2, 4; any M, N, K): VGE_ERR_UNSUPPORTED for the epilogues it does not take (GELU, PE) or with the
- * library path off (VGE_GEMM_LIB=0 / vge_debug_set_gemm_lib(0)). */
+ * library path off (VGE_GEMM_LIB=0). */
 int vge_op_gemm_lib(int epi, const void* A, long lda, const void* W, long ldw, void* out, long ldo, const float* bias,
                     const float* res, long ldr, int M, int N, int K, vge_stream_t stream);
-/* 1 (default) / 0: the extractors' bias / residual linears and 1x1 convs on hipBLASLt / on gemm_bf16_kernel */
-void vge_debug_set_gemm_lib(int on);
 /* qkv bf16 [F*192][3D] -> out bf16 [F*192][D]; head dim D / heads in {64, 80} */
 int vge_op_vit_attention(const void* qkv, void* out, int F, int D, int heads, vge_stream_t stream);
 /* LayerNorm f32 [rows][D] -> bf16, D in {256, 512, 768, 1024, 1280} */

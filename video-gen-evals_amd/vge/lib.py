@@ -24,7 +24,7 @@ EXPORTS = ["vge_featurize", "vge_featurize_layout", "vge_layout_feat_dim", "vge_
            "vge_ingest_decode",
            "vge_ingest_default_threads",
            "vge_hmr_create", "vge_hmr_reserve", "vge_hmr_destroy", "vge_hmr_extract", "vge_hmr_profile_begin",
-           "vge_hmr_profile_read", "vge_op_gemm_bf16", "vge_op_gemm_lib", "vge_debug_set_gemm_lib", "vge_op_vit_attention", "vge_op_layernorm_bf16",
+           "vge_hmr_profile_read", "vge_op_gemm_bf16", "vge_op_gemm_lib", "vge_op_vit_attention", "vge_op_layernorm_bf16",
            "vge_dwpose_create", "vge_dwpose_reserve", "vge_dwpose_destroy", "vge_dwpose_keypoints",
            "vge_dwpose_profile_begin", "vge_dwpose_profile_read", "vge_op_conv_bf16",
            "vge_yolox_create", "vge_yolox_reserve", "vge_yolox_destroy", "vge_yolox_detect", "vge_yolox_detect_scored",
