@@ -263,6 +263,37 @@ def test_conv_1x1_persistent_gemm_variant_matches_default(D, n, H, W, Cin, Cout,
 
 
 @gpu
+@pytest.mark.parametrize("n,H,W,Cin,Cout,k,stride,act,res", [
+    (2, 40, 40, 256, 256, 3, 1, "silu", None), (3, 21, 19, 128, 512, 3, 2, "silu", None),
+    (2, 50, 50, 256, 256, 3, 1, "relu", None), (2, 33, 17, 512, 256, 1, 1, "none", "post"),
+    (1, 25, 25, 256, 256, 3, 1, "relu", "pre"), (2, 20, 20, 64, 256, 3, 1, "silu", "post")])
+def test_conv_16x16x32_variant_matches_32x32x16(D, n, H, W, Cin, Cout, k, stride, act, res):
+    """Variant 12 (conv2_bf16_kernel on v_mfma_f32_16x16x32_bf16, a tuner candidate) against variant 2 (the same tile
+    and schedule on 32x32x16) and the default kernel: the same products in the same K order and the same epilogue ->
+    bit-identical, on 3x3 / 1x1 shapes with SiLU / ReLU, both residual orders, stride 2 and ragged row tiles."""
+    import ctypes as C
+    from vge import lib as Lb
+    lib = Lb.load()
+    lib.vge_debug_set_conv_variant.argtypes = [C.c_int]
+    x = _bf((n, H, W, Cin), seed=51).to(DEV)
+    w = _bf((Cout, Cin, k, k), (2.0 / (Cin * k * k)) ** 0.5, seed=52).to(DEV)
+    b = (torch.randn(Cout, generator=torch.Generator().manual_seed(53)) * 0.1).to(DEV)
+    Ho, Wo = (H + 2 * (k // 2) - k) // stride + 1, (W + 2 * (k // 2) - k) // stride + 1
+    r = _bf((n, Ho, Wo, Cout), seed=54).to(DEV) if res else None
+    outs = []
+    try:
+        for force in (0, 2, 12):
+            lib.vge_debug_set_conv_variant(force)
+            outs.append(D.conv_bf16(x, w, b, stride=stride, pad=k // 2, act=act, res=r, res_pre=res == "pre"))
+            torch.cuda.synchronize()
+    finally:
+        lib.vge_debug_set_conv_variant(0)
+    assert torch.isfinite(outs[0].float()).all()
+    assert torch.equal(outs[1], outs[2]), (outs[1].float() - outs[2].float()).abs().max().item()
+    assert torch.equal(outs[0], outs[2]), (outs[0].float() - outs[2].float()).abs().max().item()
+
+
+@gpu
 def test_conv_bf16_rejects_bad_shapes(D):
     import ctypes as C
     from vge import lib as Lb

@@ -302,7 +302,10 @@ struct C2Cfg {
   static constexpr int LDS = RING > EPI ? RING : EPI;
 };
 
-template <int BN, int ACT, int OUT, int RES>
+// SH = 1: the same wave tile on v_mfma_f32_16x16x32_bf16 (2 TM x 2 TN tiles of 16 x 16, one MFMA per 32-k stage and
+// tile; gemm_bf16_kernel's SH form): the same LDS fragment bytes, MFMA cycles and K order, bit-identical outputs, and
+// the chip holds a higher clock on this shape (MI355X_MICROARCH.md, DVFS give-back item 7)
+template <int BN, int ACT, int OUT, int RES, int SH = 0>
 __global__ void __launch_bounds__(512, 1) conv2_bf16_kernel(ConvArgs a) {
   using Cf = C2Cfg<BN>;
   constexpr int TM = Cf::TM, TN = Cf::TN, LPS = Cf::LPS, BQ = Cf::BQ;
@@ -340,32 +343,58 @@ __global__ void __launch_bounds__(512, 1) conv2_bf16_kernel(ConvArgs a) {
   };
   auto read = [&](int st, Frag& f) {
     const char* cur = lds + (st % C2_ST) * Cf::SLOT;
-    const char* As = cur + wm * Cf::WR * 64 + rowoff;
-    const char* Bs = cur + Cf::TA + wn * Cf::WC * 64 + rowoff;
+    if constexpr (SH == 0) {
+      const char* As = cur + wm * Cf::WR * 64 + rowoff;
+      const char* Bs = cur + Cf::TA + wn * Cf::WC * 64 + rowoff;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int co = ((2 * s + h) ^ swz) * 16;
+      for (int s = 0; s < 2; ++s) {
+        const int co = ((2 * s + h) ^ swz) * 16;
 #pragma unroll
-      for (int t = 0; t < TM; ++t) f.a[s][t] = *reinterpret_cast<const bf16x8*>(As + t * 32 * 64 + co);
+        for (int t = 0; t < TM; ++t) f.a[s][t] = *reinterpret_cast<const bf16x8*>(As + t * 32 * 64 + co);
 #pragma unroll
-      for (int u = 0; u < TN; ++u) f.b[s][u] = *reinterpret_cast<const bf16x8*>(Bs + u * 32 * 64 + co);
+        for (int u = 0; u < TN; ++u) f.b[s][u] = *reinterpret_cast<const bf16x8*>(Bs + u * 32 * 64 + co);
+      }
+    } else {
+      // 16x16x32 fragments: lane -> row (lane & 15) of a 16-row tile, k chunk lane >> 4 of the stage's 32;
+      // a[t / TM][t % TM] = 16-row tile t, b[u / TN][u % TN] = 16-column tile u
+      const int co = ((lane >> 4) ^ ((lane >> 2) & 3)) * 16, ro = (lane & 15) * 64;
+      const char* As = cur + wm * Cf::WR * 64 + ro + co;
+      const char* Bs = cur + Cf::TA + wn * Cf::WC * 64 + ro + co;
+#pragma unroll
+      for (int t = 0; t < 2 * TM; ++t) f.a[t / TM][t % TM] = *reinterpret_cast<const bf16x8*>(As + t * 16 * 64);
+#pragma unroll
+      for (int u = 0; u < 2 * TN; ++u) f.b[u / TN][u % TN] = *reinterpret_cast<const bf16x8*>(Bs + u * 16 * 64);
     }
   };
-  floatx16 acc[TM][TN];
+  floatx16 acc[SH ? 1 : TM][SH ? 1 : TN];
+  floatx4 acq[SH ? 2 * TM : 1][SH ? 2 * TN : 1];  // SH = 1: [16-row tile][16-column tile]
 #pragma unroll
-  for (int t = 0; t < TM; ++t)
+  for (int t = 0; t < (SH ? 1 : TM); ++t)
 #pragma unroll
-    for (int u = 0; u < TN; ++u)
+    for (int u = 0; u < (SH ? 1 : TN); ++u)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[t][u][r] = 0.f;
-  auto mma = [&](const Frag& f, int s) {
 #pragma unroll
-    for (int t = 0; t < TM; ++t)
+  for (int t = 0; t < (SH ? 2 * TM : 1); ++t)
 #pragma unroll
-      for (int u = 0; u < TN; ++u)
-        acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[s][t], f.b[s][u], acc[t][u], 0, 0, 0);
+    for (int u = 0; u < (SH ? 2 * TN : 1); ++u) acq[t][u] = floatx4{0.f, 0.f, 0.f, 0.f};
+  auto mma = [&](const Frag& f, int s) {  // SH = 1: s = 16-row tiles TM s .. TM s + TM - 1
+    if constexpr (SH == 0) {
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int u = 0; u < TN; ++u)
+          acc[t][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.a[s][t], f.b[s][u], acc[t][u], 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int t = 0; t < TM; ++t)
+#pragma unroll
+        for (int u = 0; u < 2 * TN; ++u)
+          acq[TM * s + t][u] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(f.a[s][t], f.b[u / TN][u % TN], acq[TM * s + t][u], 0, 0, 0);
+    }
   };
-  constexpr int NM = TM * TN;  // MFMAs per 16-k half-stage
+  constexpr int NM = TM * TN * (SH ? 2 : 1);  // MFMAs per half-stage call of mma
   auto step = [&](int kt, Frag& cur, Frag& nxt) {
     vmcnt_b<2 * LPS>();  // stage kt + 1 landed (kt + 2, kt + 3 in flight)
     lds_barrier_b();
@@ -415,13 +444,23 @@ __global__ void __launch_bounds__(512, 1) conv2_bf16_kernel(ConvArgs a) {
   if constexpr (RES == RES_F32S) rsc = *reinterpret_cast<const floatx4*>(a.rscale + gcol);
 #pragma unroll
   for (int half = 0; half < TM / 2; ++half) {
+    if constexpr (SH == 0) {
 #pragma unroll
-    for (int tt = 0; tt < 2; ++tt)
+      for (int tt = 0; tt < 2; ++tt)
 #pragma unroll
-      for (int u = 0; u < TN; ++u)
+        for (int u = 0; u < TN; ++u)
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          my[(tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * WC + u * 32 + (lane & 31)] = acc[2 * half + tt][u][r];
+          for (int r = 0; r < 16; ++r)
+            my[(tt * 32 + (r & 3) + 8 * (r >> 2) + 4 * h) * WC + u * 32 + (lane & 31)] = acc[2 * half + tt][u][r];
+    } else {
+#pragma unroll
+      for (int tt = 0; tt < 4; ++tt)
+#pragma unroll
+        for (int u = 0; u < 2 * TN; ++u)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            my[(tt * 16 + 4 * (lane >> 4) + r) * WC + u * 16 + (lane & 15)] = acq[4 * half + tt][u][r];
+    }
 #pragma unroll 4
     for (int it = 0; it < 64 / RPI; ++it) {
       const int rl = it * RPI + lr;
@@ -1219,6 +1258,19 @@ static hipError_t conv2_go(const ConvArgs& a, hipStream_t s, int pmode) {
     const char* e = getenv("VGE_CONV_PERSIST");
     g_conv_persist = (e && atoi(e) == 0) ? 0 : 1;
   }
+  if (pmode == 7) {  // the 16x16x32 form (variant 12)
+    if constexpr (C2Cfg<BN>::TM % 2 == 0) {
+      constexpr int BYTES = C2Cfg<BN>::LDS;
+      static LdsAttrOnce attr;
+      if (const hipError_t e = attr(reinterpret_cast<const void*>(&conv2_bf16_kernel<BN, ACT, OUT, RES, 1>), BYTES);
+          e != hipSuccess)
+        return e;
+      const int grid = ((a.M + C2_M - 1) / C2_M) * ((a.Cout + BN - 1) / BN);
+      hipLaunchKernelGGL((conv2_bf16_kernel<BN, ACT, OUT, RES, 1>), dim3(grid), dim3(512), BYTES, s, a);
+      return hipGetLastError();
+    }
+    return hipErrorInvalidValue;
+  }
   if constexpr (RES == RES_NONE)  // residual epilogues stay on conv2_bf16_kernel (their loads need vmcnt drains)
     if (pmode < 0 ? g_conv_persist : pmode) return conv2p_go<BN, ACT, OUT, RES>(a, s);
   constexpr int BYTES = C2Cfg<BN>::LDS;
@@ -1365,7 +1417,7 @@ hipError_t launch_conv_bf16(const ConvLaunch& c, hipStream_t s) {
     variant = 0;  // forced globally (or the library's fallback): layers the GEMM cannot take keep the default kernel
   }
   // grouped slices run on the 128- / 256-row kernel only, with the slice width as the column tile
-  if (c.gslice && (variant == 2 || variant == 3 || variant == 6 || (c.tn != 64 && c.tn != 128) || c.Cin != c.tn ||
+  if (c.gslice && (variant == 2 || variant == 3 || variant == 6 || variant == 12 || (c.tn != 64 && c.tn != 128) || c.Cin != c.tn ||
                    c.Cout % c.tn))
     return hipErrorInvalidValue;
   if (variant == 6) {  // 512 x 128 persistent tiles
@@ -1374,10 +1426,10 @@ hipError_t launch_conv_bf16(const ConvLaunch& c, hipStream_t s) {
   }
   if (variant == 1 || variant == 5) tn = tn > 128 ? 128 : tn;
   if (variant == 5 || (variant == 0 && g_conv_tall && tn < 256)) pmode = 5;  // 256-row tiles, 64 / 128 columns
-  if (variant == 2 || variant == 3) {
+  if (variant == 2 || variant == 3 || variant == 12) {
     if (c.Npad % 256) return hipErrorInvalidValue;
     tn = 256;
-    pmode = variant == 3 ? 1 : 0;
+    pmode = variant == 3 ? 1 : variant == 12 ? 7 : 0;
   }
   const int tn1 = tn > 128 ? 128 : tn;  // v1 grid (the tn 256 case runs conv2 with its own grid)
   const int grid = ((a.M + CV_M - 1) / CV_M) * ((c.Cout + tn1 - 1) / tn1);

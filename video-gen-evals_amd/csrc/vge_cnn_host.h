@@ -201,7 +201,10 @@ inline hipError_t conv_tuned_launch(ConvTuner& t, ConvLaunch& c, const std::arra
     it = t.best.emplace(key, 11000 + 256).first;
   if (it == t.best.end()) {
     if (!t.e0 && (hipEventCreate(&t.e0) != hipSuccess || hipEventCreate(&t.e1) != hipSuccess)) return hipErrorUnknown;
+    // (12: variant 2 on the 16x16x32 MFMA form, bit-identical; VGE_CONV_SH=0 keeps it out)
+    static const bool sh_ok = !(getenv("VGE_CONV_SH") && getenv("VGE_CONV_SH")[0] == '0');
     std::vector<int> cand = {1000 + 128, 5000 + 128, 2000 + 256};
+    if (sh_ok) cand.push_back(12000 + 256);
     if (c.Cout <= 192) {
       cand.push_back(1000 + 64);
       cand.push_back(5000 + 64);
