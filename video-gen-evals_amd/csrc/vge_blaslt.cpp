@@ -1,6 +1,7 @@
 // Library GEMMs (hipBLASLt) for the extractors' plain linear layers: out = act(A W^T + bias (+ C)) with A [M][K] and
 // W [N][K] bf16 row-major, the epilogues of vge_gemm.h that a library epilogue expresses exactly in kind -- bias, bias
-// + ReLU, a bf16 residual added before the ReLU, the ViT's f32 residual stream -- and f32 accumulation throughout.
+// + ReLU, bias + SiLU (Swish), a bf16 residual added before the ReLU, the ViT's f32 residual stream -- and f32
+// accumulation throughout.
 // The hand-written gemm_bf16_kernel (vge_vit.hip) stays for GELU (the library's is the tanh form, the reference's
 // nn.GELU is erf), the position-embedding epilogue, and every shape or epilogue below; it is also what the tuner's
 // bit-identity tests pin.  Measured on the MI355X (tools/lib_gemm_probe.py, profiles/lib_gemm_probe_r06t.json):
@@ -75,7 +76,8 @@ void gemm_lib_set(int on) { g_lt_on = on ? 1 : 0; }
 
 bool gemm_lib_ok(int epi) {
   return gemm_lib_enabled() && (epi == GEMM_BF16 || epi == GEMM_RELU_BF16 || epi == GEMM_RESB_BF16 ||
-                                epi == GEMM_RESB_RELU_BF16 || epi == GEMM_RES_F32 || epi == GEMM_F32);
+                                epi == GEMM_RESB_RELU_BF16 || epi == GEMM_RES_F32 || epi == GEMM_F32 ||
+                                epi == GEMM_SILU_BF16);
 }
 
 hipError_t launch_gemm_lib(int epi, const GemmBf16& a, hipStream_t s) {
@@ -103,8 +105,10 @@ hipError_t launch_gemm_lib(int epi, const GemmBf16& a, hipStream_t s) {
   const hipblasOperation_t ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
   LT_OK(hipblasLtMatmulDescSetAttribute(d.op, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta)));
   LT_OK(hipblasLtMatmulDescSetAttribute(d.op, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb)));
-  const hipblasLtEpilogue_t ep = a.bias ? (relu ? HIPBLASLT_EPILOGUE_RELU_BIAS : HIPBLASLT_EPILOGUE_BIAS)
-                                        : (relu ? HIPBLASLT_EPILOGUE_RELU : HIPBLASLT_EPILOGUE_DEFAULT);
+  const bool silu = epi == GEMM_SILU_BF16;  // Swish(x, 1) = x sigmoid(x) = SiLU
+  const hipblasLtEpilogue_t ep =
+      a.bias ? (relu ? HIPBLASLT_EPILOGUE_RELU_BIAS : silu ? HIPBLASLT_EPILOGUE_SWISH_BIAS_EXT : HIPBLASLT_EPILOGUE_BIAS)
+             : (relu ? HIPBLASLT_EPILOGUE_RELU : silu ? HIPBLASLT_EPILOGUE_SWISH_EXT : HIPBLASLT_EPILOGUE_DEFAULT);
   LT_OK(hipblasLtMatmulDescSetAttribute(d.op, HIPBLASLT_MATMUL_DESC_EPILOGUE, &ep, sizeof(ep)));
   if (a.bias) {
     const void* bp = a.bias;

@@ -32,6 +32,7 @@ struct PoseInst {  // kp120_kernel: box center and aspect-fixed scale
 hipError_t launch_conv_bf16(const ConvLaunch& c, hipStream_t s);
 // the GEMM epilogue (vge_gemm.h) that runs c as variant 9 (a 1x1 stride-1 conv on gemm_bf16_kernel), -1 = none
 int conv_gemm_epi(const ConvLaunch& c);
+int conv_lib_epi(const ConvLaunch& c);
 bool conv_gemm_persist_ok(const ConvLaunch& c);  // variant 10 applies (the persistent GEMM, vge_vit.hip gemmp)
 hipError_t launch_dwconv(const void* x, long ldx, const float* w, const float* b, void* y, long ldy, int n_img, int H,
                          int W, int C, int K, hipStream_t s);

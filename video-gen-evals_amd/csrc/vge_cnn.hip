@@ -1328,6 +1328,20 @@ int conv_gemm_epi(const ConvLaunch& c) {
   return -1;
 }
 
+// the library GEMM path (variant 11, vge_blaslt.cpp) for a 1x1 stride-1 conv: any Cin / Cout (16-B rows), the epilogues
+// a library epilogue expresses (bias; + ReLU or SiLU; a bf16 residual before the ReLU or with no activation); -1 = no
+int conv_lib_epi(const ConvLaunch& c) {
+  if (c.KH != 1 || c.KW != 1 || c.stride != 1 || c.pad != 0 || c.gslice || c.out_f32 || c.Cout % 8 || c.Cin % 8 ||
+      c.Kp < c.Cin || c.Kp % 8 || c.ldx % 8 || c.ldo % 8)
+    return -1;
+  if (c.res_mode == RES_NONE)
+    return c.act == ACT_NONE ? GEMM_BF16 : c.act == ACT_RELU ? GEMM_RELU_BF16 : c.act == ACT_SILU ? GEMM_SILU_BF16 : -1;
+  if (c.ldr % 8) return -1;
+  if (c.res_mode == RES_BF16_PRE) return c.act == ACT_NONE ? GEMM_RESB_BF16 : c.act == ACT_RELU ? GEMM_RESB_RELU_BF16 : -1;
+  if (c.res_mode == RES_BF16 && c.act == ACT_NONE) return GEMM_RESB_BF16;
+  return -1;
+}
+
 bool conv_gemm_persist_ok(const ConvLaunch& c) {
   const int epi = conv_gemm_epi(c);
   if (epi < 0) return false;
@@ -1371,7 +1385,7 @@ hipError_t launch_conv_bf16(const ConvLaunch& c, hipStream_t s) {
   int tn = c.tn, pmode = -1;
   int variant = c.variant == 0 && g_conv_force > 0 && !c.gslice ? g_conv_force : c.variant;
   if (variant == 11) {  // the library GEMM (vge_blaslt.cpp; conv_tuned_launch's choice for the shapes it takes)
-    const int epi = conv_gemm_epi(c);
+    const int epi = conv_lib_epi(c);
     if (epi >= 0) {
       GemmBf16 g{};
       g.A = c.x;

@@ -194,10 +194,11 @@ struct ConvCtx {
 // encoded choice: variant * 1000 + tn
 inline hipError_t conv_tuned_launch(ConvTuner& t, ConvLaunch& c, const std::array<long, 10>& key, hipStream_t s) {
   auto it = t.best.find(key);
-  // 1x1 stride-1 convs with the epilogues the library expresses go to hipBLASLt without a timing contest
+  // 1x1 stride-1 convs with the epilogues the library expresses (bias, ReLU / SiLU, a bf16 residual before the ReLU)
+  // go to hipBLASLt without a timing contest
   // (vge_blaslt.cpp: 1,165 vs 934-943 TFLOP/s on the detector's res4 shapes, profiles/lib_gemm_probe_r06t.json): a
   // choice that never depends on timing noise, so a layer's outputs do not change from run to run
-  if (it == t.best.end() && conv_gemm_epi(c) >= 0 && gemm_lib_ok(conv_gemm_epi(c)))
+  if (it == t.best.end() && conv_lib_epi(c) >= 0 && gemm_lib_ok(conv_lib_epi(c)))
     it = t.best.emplace(key, 11000 + 256).first;
   if (it == t.best.end()) {
     if (!t.e0 && (hipEventCreate(&t.e0) != hipSuccess || hipEventCreate(&t.e1) != hipSuccess)) return hipErrorUnknown;

@@ -15,7 +15,8 @@ enum GemmEpiPublic {
   GEMM_F32 = 4,            // + bias -> f32
   GEMM_RELU_BF16 = 5,      // ReLU(+ bias) -> bf16
   GEMM_RESB_BF16 = 6,      // + bias + resb (bf16) -> bf16
-  GEMM_RESB_RELU_BF16 = 7  // ReLU(+ bias + resb) -> bf16
+  GEMM_RESB_RELU_BF16 = 7, // ReLU(+ bias + resb) -> bf16
+  GEMM_SILU_BF16 = 8       // SiLU(+ bias) -> bf16 (library path only: the YOLOX / RTMPose 1x1 convs)
 };
 
 struct GemmBf16 {
