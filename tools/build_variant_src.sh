@@ -9,4 +9,4 @@ src=$2; base=${src%.hip}
 extra=""; [ "$base" = vge_encoder_x3s ] && extra="-fno-slp-vectorize"
 /opt/rocm/bin/hipcc -O3 -fPIC -std=c++17 --offload-arch=gfx950 $extra $3 -c $src -o build/$1/$base.o
 objs=$(ls build/*.o | grep -v "build/$base.o")
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build/$1/libvge.so $objs build/$1/$base.o -lz -lpthread
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o build/$1/libvge.so $objs build/$1/$base.o -L/opt/rocm/lib -lhipblaslt -Wl,-rpath,/opt/rocm/lib -lz -lpthread

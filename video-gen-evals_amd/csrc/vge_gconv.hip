@@ -64,7 +64,10 @@ __device__ __forceinline__ int gc_xcd(int b, int nblk, int on) {
   return (x8 < r8 ? x8 * (q8 + 1) : r8 * (q8 + 1) + (x8 - r8) * q8) + (b >> 3);
 }
 #ifndef VGE_GC_NI
-#define VGE_GC_NI 4
+#define VGE_GC_NI 8  // (r06ad, same box: 8 images per workgroup -0.6 % on the detector vs 4)
+#endif
+#ifndef VGE_GC_PD
+#define VGE_GC_PD 1  // images whose tile loads are in flight during an image's MFMAs: 2 measured no faster (r06ad)
 #endif
 constexpr int GC_NI = VGE_GC_NI;  // images per workgroup: its weights (up to 72 registers) are loaded once for all of them
 
@@ -109,7 +112,6 @@ __global__ void __launch_bounds__(256, KS <= 2 ? VGE_GC_OCC_SMALL : VGE_GC_OCC) 
   // the next image's loads stay in flight across this image's MFMAs (a branch around each load made the compiler wait
   // for them right after issuing; stores count in the same vmcnt, so the epilogue stores are buffer stores too)
   constexpr int NLD = (NPIXM * 8 + 255) / 256;
-  uintx4_t v[NLD];
   int gofs[NLD];  // byte offsets inside an image (the same for every image of the workgroup)
 #pragma unroll
   for (int q = 0; q < NLD; ++q) {
@@ -119,14 +121,14 @@ __global__ void __launch_bounds__(256, KS <= 2 ? VGE_GC_OCC_SMALL : VGE_GC_OCC) 
                   ? ((iy * a.W + ix) * (int)a.ldx + j * 8) * 2 : GC_OOB;
   }
   const int in_bytes = (a.H * a.W * (int)a.ldx - slice * 64) * 2;
-  auto load_tile = [&](int img, bool real) {  // real = false: the same instructions on an empty record range
+  auto load_tile = [&](uintx4_t (&v)[NLD], int img, bool real) {  // real = false: the same loads, empty record range
     const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<__bf16*>(a.x + (size_t)img * a.H * a.W * a.ldx + slice * 64), (short)0, real ? in_bytes : 0,
         0x00020000);
 #pragma unroll
     for (int q = 0; q < NLD; ++q) v[q] = __builtin_amdgcn_raw_buffer_load_b128(xr, gofs[q], 0, 0);
   };
-  auto store_tile = [&]() {
+  auto store_tile = [&](const uintx4_t (&v)[NLD]) {
 #pragma unroll
     for (int q = 0; q < NLD; ++q) {
       const int c = tid + 256 * q, p = c >> 3, j = c & 7;
@@ -163,18 +165,11 @@ __global__ void __launch_bounds__(256, KS <= 2 ? VGE_GC_OCC_SMALL : VGE_GC_OCC) 
   const char* lb = tile + (cbase + cl) * 2;
   const int ch = slice * 64 + n0 + 4 * (lane >> 4);
   const floatx4 bv = *reinterpret_cast<const floatx4*>(a.bias + ch);
-  // Per image: the next image's loads, this image's MFMAs and stores, then the next tile into LDS.  Every iteration
-  // issues the same loads and stores unconditionally (the last one's loads out of range), so the compiler's vmcnt wait
-  // for a tile register counts the 8 stores issued after it instead of waiting for them too.
-  load_tile(img0, true);  // after the weights and bias: waiting for the tile waits for them
-  store_tile();
-  __syncthreads();
-  for (int k = 0; k < nimg; ++k) {
-    const int img = img0 + k;
-    load_tile(img0 + min(k + 1, nimg - 1), k + 1 < nimg);  // in flight during this image's MFMAs
 
-    // ---- MFMAs: pixel tile pt = output pixels pt * 16 .. + 15 of the tile (row-major, running across rows; lanes past
-    // the tile's last pixel recompute that pixel and store nothing)
+  // ---- one image from the LDS tile: MFMAs over pixel tiles pt = output pixels pt * 16 .. + 15 of the tile (row-major,
+  // running across rows; lanes past the tile's last pixel recompute that pixel and store nothing), then bias + ReLU
+  // and the 8 stores (all of them, out of range past npt or for real = false: a fixed store count)
+  auto compute = [&](int img, bool real) {
     floatx4 acc[gc_npt<S>()];
 #pragma unroll
     for (int pt = 0; pt < gc_npt<S>(); ++pt) acc[pt] = floatx4{0.f, 0.f, 0.f, 0.f};
@@ -206,11 +201,11 @@ __global__ void __launch_bounds__(256, KS <= 2 ? VGE_GC_OCC_SMALL : VGE_GC_OCC) 
         }
       }
     }
-    // ---- epilogue: lane = pixel l & 15 of the tile, output channels n0 + 4 (l >> 4) .. + 3
+    // epilogue: lane = pixel l & 15 of the tile, output channels n0 + 4 (l >> 4) .. + 3
     const __amdgpu_buffer_rsrc_t orr = __builtin_amdgcn_make_buffer_rsrc(
-        a.out + (size_t)img * a.Ho * a.Wo * a.ldo, (short)0, a.Ho * a.Wo * (int)a.ldo * 2, 0x00020000);
+        a.out + (size_t)img * a.Ho * a.Wo * a.ldo, (short)0, real ? a.Ho * a.Wo * (int)a.ldo * 2 : 0, 0x00020000);
 #pragma unroll
-    for (int pt = 0; pt < gc_npt<S>(); ++pt) {  // all of them (out of range past npt): a fixed store count
+    for (int pt = 0; pt < gc_npt<S>(); ++pt) {
       const int op = pt * 16 + px, r = gc_div(op, a.inv_tw), oy = oy0 + r, ox = ox0 + op - r * TW;
       const int oo = (op < NPX && oy < a.Ho && ox < a.Wo) ? ((oy * a.Wo + ox) * (int)a.ldo + ch) * 2 : GC_OOB;
       bf16x4_t o;
@@ -218,12 +213,42 @@ __global__ void __launch_bounds__(256, KS <= 2 ? VGE_GC_OCC_SMALL : VGE_GC_OCC) 
       for (int i = 0; i < 4; ++i) o[i] = (__bf16)fmaxf(acc[pt][i] + bv[i], 0.f);
       __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(uintx2_t, o), orr, oo, 0, 0);
     }
-    if (k + 1 < nimg) {
-      __syncthreads();  // every wave is done reading this image's tile
-      store_tile();
-      __syncthreads();
-    }
+  };
+  auto swap_tile = [&](const uintx4_t (&v)[NLD]) {
+    __syncthreads();  // every wave is done reading the previous image's tile
+    store_tile(v);
+    __syncthreads();
+  };
+  // Every step issues the same loads and stores unconditionally (past the last image: an empty record range for the
+  // loads, stores dropped), so the compiler's vmcnt wait for a tile register counts exactly the operations issued
+  // after it instead of waiting for them too.  The weights and bias are loaded before the first tile: waiting for
+  // the tile waits for them.
+#if VGE_GC_PD == 2
+  // two images' loads in flight: image k + 2's behind image k's MFMAs, in two alternating register sets
+  uintx4_t va[NLD], vb[NLD];
+  load_tile(va, img0, true);
+  load_tile(vb, img0 + min(1, nimg - 1), 1 < nimg);
+  store_tile(va);
+  __syncthreads();
+  for (int k = 0; k < nimg; k += 2) {
+    load_tile(va, img0 + min(k + 2, nimg - 1), k + 2 < nimg);
+    compute(img0 + k, true);
+    swap_tile(vb);
+    load_tile(vb, img0 + min(k + 3, nimg - 1), k + 3 < nimg);
+    compute(img0 + min(k + 1, nimg - 1), k + 1 < nimg);
+    if (k + 2 < nimg) swap_tile(va);
   }
+#else
+  uintx4_t v[NLD];
+  load_tile(v, img0, true);
+  store_tile(v);
+  __syncthreads();
+  for (int k = 0; k < nimg; ++k) {
+    load_tile(v, img0 + min(k + 1, nimg - 1), k + 1 < nimg);  // in flight during this image's MFMAs
+    compute(img0 + k, true);
+    if (k + 1 < nimg) swap_tile(v);
+  }
+#endif
 }
 
 // Output tile of a grouped conv: th x tw pixels (th * tw <= 16 gc_npt, the input tile within gc_npix_max), by a
