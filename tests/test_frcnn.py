@@ -127,6 +127,38 @@ def test_box_features_vs_oracle_on_gpu_levels(run):
         assert same > 0.999 and float((d - ref.abs() * 2 ** -7).max()) <= 1e-6
 
 
+def test_roi_align_separable_matches_sample_order(run):
+    """The default ROIAlign (separable per-bin cell weights, roi_align_sep_kernel) against torchvision's sample order
+    (roi_align_kernel, vge_debug_set_roi_direct) on the same levels and proposals: the same sums reassociated, so
+    bins identical but for rare 1-ulp bf16 differences."""
+    import ctypes as C
+    from vge import synth
+    from vge.frcnn import FrcnnDetector
+    frames = torch.from_numpy(synth.make_frame_pool(9100, NF)).to(DEV)
+    lib = L_load()
+    lib.vge_debug_set_roi_direct.argtypes = [C.c_int]
+    got = {}
+    det = FrcnnDetector(run["sd"], run["cfg"], device=DEV, chunk=NF)
+    try:
+        for direct in (0, 1):
+            lib.vge_debug_set_roi_direct(direct)
+            taps = det.make_taps(NF, 256, 256)
+            det.detect(frames, taps=taps)
+            torch.cuda.synchronize()
+            got[direct] = (taps["box_features"].cpu(), taps["n_proposals"].cpu())
+    finally:
+        lib.vge_debug_set_roi_direct(0)
+        det.close()
+    assert torch.equal(got[0][1], got[1][1])
+    for f in range(NF):
+        n = int(got[0][1][f])
+        a, b = got[0][0][f, :n].float(), got[1][0][f, :n].float()
+        d = (a - b).abs()
+        same = float((d == 0).float().mean())
+        print(f"frame {f}: {n} ROIs, bins identical {same:.6f}")
+        assert n > 0 and same > 0.999 and float((d - b.abs() * 2 ** -7).max()) <= 1e-6
+
+
 def test_box_head_vs_oracle_on_gpu_features(run):
     o, t, K = run["oracle"], run["taps"], run["cfg"].num_classes
     for f in range(2):

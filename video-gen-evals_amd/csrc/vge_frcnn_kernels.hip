@@ -13,8 +13,9 @@
 //       (max + 1)), the IoU > thr matrix as 64-bit ballot words in LDS, the greedy scan by one wave
 //   rpn_merge_kernel          the levels' kept boxes in (score desc, level, rank) order = one stable sort of the
 //       concatenation, first post_nms_topk (rank by binary search in the other levels' sorted lists)
-//   roi_align_kernel          ROIPooler: level = floor(4 + log2(sqrt(area) / 224 + 1e-8)) in [2, 5], ROIAlignV2
-//       (aligned, adaptive sampling grid) with torchvision's sample / weight / sum order, 8 channels per lane
+//   roi_align_sep_kernel      ROIPooler: level = floor(4 + log2(sqrt(area) / 224 + 1e-8)) in [2, 5], ROIAlignV2
+//       (aligned, adaptive sampling grid) as separable per-bin cell weights, 8 channels per lane (default);
+//       roi_align_kernel the same in torchvision's sample / weight / sum order
 //   det_post_kernel           FastRCNNOutputLayers.inference + detector_postprocess per frame: softmax, per-class
 //       decode (10, 10, 5, 5) + clip, candidates with score > thresh in (proposal, class) order, per-class NMS
 //       (coordinate trick, bitmask + greedy scan), top det_per_img by (score desc, candidate order), scaling to the
@@ -32,6 +33,7 @@ namespace {
 typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned long long u64;
+typedef unsigned uintx4_t __attribute__((ext_vector_type(4)));
 
 constexpr float SCALE_CLAMP = 4.135166556742356f;  // log(1000 / 16), Box2BoxTransform
 
@@ -528,6 +530,173 @@ __global__ void __launch_bounds__(256) roi_align_kernel(vge::RoiLevels L, const 
   }
 }
 
+// ROIAlignV2, separable form (the default).  A bin's sum over its gh x gw samples of the four bilinear taps is a sum
+// over the cells of its support: sum_(cy, cx) Wy(cy) Wx(cx) f(cy, cx), with Wy(cy) = sum over the valid samples iy of
+// the y-weight they give cell cy (hy to yl, ly to yh) and Wx likewise -- the sample grid is a product, a sample is
+// valid iff its y and its x are, and the per-sample tap weights are products hy * hx.  The sample spacing is at most one
+// cell, so a bin's support is gh + 1 cells along y (gh + 2 at most, float rounding), gw + 1 along x: (gh + 1)(gw + 1)
+// cell terms instead of 4 gh gw sample taps (9 vs 16 at 2 x 2 samples, 16 vs 36 at 3 x 3), each one 16-B load and 8
+// FMAs, and the per-sample coordinate / weight arithmetic leaves the channel loop.  Per ROI the
+// 14 axis tables (7 bins x 2 axes) are built once in LDS; group g of 32 lanes (8 channels each) computes output row
+// ph = g, loading a bin's cells in batches of 2 rows x 4 columns (8 loads in flight before their FMAs; the cells past
+// the support read 0 through an empty buffer offset, with weight 0).  Bins wider than RA_MAXC - 3 samples (elongated boxes on a fine level) take the sample loop of
+// roi_align_kernel.  The sums are reassociated relative to torchvision's sample order: rare 1-ulp bf16 differences.
+constexpr int RA_MAXC = 16;
+constexpr int RA_OOB = 0x7FFFFFF0;
+// rows of cells per load batch (x 4 columns): 2 x 4 measured faster than 4 x 4, and skipping the FMAs of the cells
+// outside the support (a uniform branch per column) no faster than weight 0 x a zero load (profiles/ab_r06ae_roi_align.json)
+constexpr int RA_BR = 2;  // a buffer offset past any record range: the load returns 0
+
+__device__ __forceinline__ void roi_axis_table(float s, float bs, int n, int p, int L, float* tab, int& c0, int& nc) {
+#pragma unroll
+  for (int j = 0; j < RA_MAXC + 4; ++j) tab[j] = 0.f;
+  c0 = 0;
+  nc = 0;
+  bool first = true;
+  for (int i = 0; i < n; ++i) {
+    const float v = (s + (float)p * bs) + (((float)i + 0.5f) * bs) / (float)n;  // roi_align_kernel's y / x
+    if (v < -1.0f || v > (float)L) continue;
+    float vv = v <= 0.f ? 0.f : v;
+    int lo = (int)vv, hi;
+    if (lo >= L - 1) {
+      hi = lo = L - 1;
+      vv = (float)lo;
+    } else {
+      hi = lo + 1;
+    }
+    const float l = vv - (float)lo, h = 1.f - l;
+    if (first) {
+      c0 = lo;
+      first = false;
+    }
+    if (hi - c0 >= RA_MAXC) break;  // not reached: the caller bounds n + 3 <= RA_MAXC
+    tab[lo - c0] += h;
+    tab[hi - c0] += l;
+    nc = hi - c0 + 1;
+  }
+}
+
+__global__ void __launch_bounds__(224) roi_align_sep_kernel(vge::RoiLevels L, const float* __restrict__ props,
+                                                            const int* __restrict__ n_prop, int P,
+                                                            bf16* __restrict__ out) {
+  __shared__ float wtab[14][RA_MAXC + 4];  // + 4: a batch's columns past the table read 0
+  __shared__ int c0s[14], ncs[14];
+  const int f = blockIdx.x / P, r = blockIdx.x - f * P;
+  bf16* o = out + (size_t)blockIdx.x * 49 * 256;
+  const int g = threadIdx.x >> 5, c8 = (threadIdx.x & 31) * 8;  // g = output row ph
+  if (r >= n_prop[f]) {
+    bf16x8 z;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) z[c] = (bf16)0.f;
+    for (int pw = 0; pw < 7; ++pw) *reinterpret_cast<bf16x8*>(o + (g * 7 + pw) * 256 + c8) = z;
+    return;
+  }
+  const float* pb = props + ((size_t)f * P + r) * 5;
+  const float x1 = pb[0], y1 = pb[1], x2 = pb[2], y2 = pb[3];
+  const float area = (x2 - x1) * (y2 - y1);
+  float lvf = floorf(4.0f + log2f(sqrtf(area) / 224.0f + 1e-8f));
+  lvf = fminf(fmaxf(lvf, 2.f), 5.f);
+  const int l = (int)lvf - 2;
+  const bf16* feat = static_cast<const bf16*>(l == 0 ? L.p[0] : l == 1 ? L.p[1] : l == 2 ? L.p[2] : L.p[3]);
+  const int H = l == 0 ? L.h[0] : l == 1 ? L.h[1] : l == 2 ? L.h[2] : L.h[3];
+  const int W = l == 0 ? L.w[0] : l == 1 ? L.w[1] : l == 2 ? L.w[2] : L.w[3];
+  const float scale = l == 0 ? 0.25f : l == 1 ? 0.125f : l == 2 ? 0.0625f : 0.03125f;
+  const bf16* fbase = feat + (size_t)f * H * W * 256;  // uniform: the buffer resource's base
+  feat = fbase + c8;
+  const float sw = x1 * scale - 0.5f, sh = y1 * scale - 0.5f;
+  const float ew = x2 * scale - 0.5f, eh = y2 * scale - 0.5f;
+  const float rw = ew - sw, rh = eh - sh;
+  const float bw = rw / 7.f, bh = rh / 7.f;
+  const int gh = (int)ceilf(rh / 7.f), gw = (int)ceilf(rw / 7.f);
+  const float cnt = (float)max(gh * gw, 1);
+  if (gh + 3 > RA_MAXC || gw + 3 > RA_MAXC) {  // the sample loop (uniform per workgroup)
+    for (int pw = 0; pw < 7; ++pw) {
+      const int ph = g;
+      float acc[8];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) acc[c] = 0.f;
+      for (int iy = 0; iy < gh; ++iy) {
+        float y = (sh + (float)ph * bh) + (((float)iy + 0.5f) * bh) / (float)gh;
+        for (int ix = 0; ix < gw; ++ix) {
+          float x = (sw + (float)pw * bw) + (((float)ix + 0.5f) * bw) / (float)gw;
+          if (y < -1.0f || y > (float)H || x < -1.0f || x > (float)W) continue;
+          float yy = y <= 0.f ? 0.f : y, xx = x <= 0.f ? 0.f : x;
+          int yl = (int)yy, xl = (int)xx, yh, xh;
+          if (yl >= H - 1) {
+            yh = yl = H - 1;
+            yy = (float)yl;
+          } else {
+            yh = yl + 1;
+          }
+          if (xl >= W - 1) {
+            xh = xl = W - 1;
+            xx = (float)xl;
+          } else {
+            xh = xl + 1;
+          }
+          const float ly = yy - (float)yl, lx = xx - (float)xl, hy = 1.f - ly, hx = 1.f - lx;
+          const float w1 = hy * hx, w2 = hy * lx, w3 = ly * hx, w4 = ly * lx;
+          const bf16x8 v1 = *reinterpret_cast<const bf16x8*>(feat + ((size_t)yl * W + xl) * 256);
+          const bf16x8 v2 = *reinterpret_cast<const bf16x8*>(feat + ((size_t)yl * W + xh) * 256);
+          const bf16x8 v3 = *reinterpret_cast<const bf16x8*>(feat + ((size_t)yh * W + xl) * 256);
+          const bf16x8 v4 = *reinterpret_cast<const bf16x8*>(feat + ((size_t)yh * W + xh) * 256);
+#pragma unroll
+          for (int c = 0; c < 8; ++c) {
+            float t = w1 * (float)v1[c] + w2 * (float)v2[c];
+            t = t + w3 * (float)v3[c];
+            t = t + w4 * (float)v4[c];
+            acc[c] = acc[c] + t;
+          }
+        }
+      }
+      bf16x8 q;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) q[c] = (bf16)(acc[c] / cnt);
+      *reinterpret_cast<bf16x8*>(o + (ph * 7 + pw) * 256 + c8) = q;
+    }
+    return;
+  }
+  if (threadIdx.x < 14) {  // tables: 0..6 the rows ph, 7..13 the columns pw
+    const int t = threadIdx.x;
+    const bool ya = t < 7;
+    roi_axis_table(ya ? sh : sw, ya ? bh : bw, ya ? gh : gw, ya ? t : t - 7, ya ? H : W, wtab[t], c0s[t], ncs[t]);
+  }
+  __syncthreads();
+  // cells in batches of 2 rows x 4 columns, the 8 loads issued before their FMAs; cells past the bin's support read
+  // through an empty offset (buffer loads return 0 there) with weight 0 from the zero-filled tables
+  const __amdgpu_buffer_rsrc_t fr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<bf16*>(fbase), (short)0, H * W * 512, 0x00020000);
+  const int ph = g, y0 = c0s[ph], ny = ncs[ph];
+  for (int pw = 0; pw < 7; ++pw) {
+    const int x0 = c0s[7 + pw], nx = ncs[7 + pw];
+    float acc[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[c] = 0.f;
+    for (int j0 = 0; j0 < ny; j0 += RA_BR)
+      for (int k0 = 0; k0 < nx; k0 += 4) {
+        uintx4_t v[4 * RA_BR];
+        float w[4 * RA_BR];
+#pragma unroll
+        for (int q = 0; q < 4 * RA_BR; ++q) {
+          const int j = j0 + (q >> 2), k = k0 + (q & 3);
+          const bool in = j < ny && k < nx;
+          v[q] = __builtin_amdgcn_raw_buffer_load_b128(fr, in ? ((y0 + j) * W + x0 + k) * 512 + c8 * 2 : RA_OOB, 0, 0);
+          w[q] = wtab[ph][j] * wtab[7 + pw][k];
+        }
+#pragma unroll
+        for (int q = 0; q < 4 * RA_BR; ++q) {
+          const bf16x8 x = __builtin_bit_cast(bf16x8, v[q]);
+#pragma unroll
+          for (int c = 0; c < 8; ++c) acc[c] = __builtin_fmaf(w[q], (float)x[c], acc[c]);
+        }
+      }
+    bf16x8 q;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) q[c] = (bf16)(acc[c] / cnt);
+    *reinterpret_cast<bf16x8*>(o + (ph * 7 + pw) * 256 + c8) = q;
+  }
+}
+
 // ------------------------------------------------------------------------------------------------ box inference
 // softmax of one head row over K + 1 <= 128 logits held two per lane (lane l: class l and 64 + l); returns the
 // probabilities (0 outside the row)
@@ -805,10 +974,19 @@ hipError_t launch_rpn_merge(const float* kept, const int* kcount, int n, int pos
   return hipGetLastError();
 }
 
+static bool g_roi_direct = false;  // vge_debug_set_roi_direct(1): the sample-order kernel (tests)
+
 hipError_t launch_roi_align(const RoiLevels& lv, const float* props, const int* n_prop, int n, int P, void* out,
                             hipStream_t s) {
   if (n == 0 || P == 0) return hipSuccess;
-  hipLaunchKernelGGL(roi_align_kernel, dim3(n * P), dim3(256), 0, s, lv, props, n_prop, P, static_cast<bf16*>(out));
+  static const bool sep = [] {  // VGE_ROI_SEP=0: the sample-order kernel (A/B, tests)
+    const char* e = getenv("VGE_ROI_SEP");
+    return !(e && e[0] == '0');
+  }();
+  if (sep && !g_roi_direct)
+    hipLaunchKernelGGL(roi_align_sep_kernel, dim3(n * P), dim3(224), 0, s, lv, props, n_prop, P, static_cast<bf16*>(out));
+  else
+    hipLaunchKernelGGL(roi_align_kernel, dim3(n * P), dim3(256), 0, s, lv, props, n_prop, P, static_cast<bf16*>(out));
   return hipGetLastError();
 }
 
@@ -820,3 +998,8 @@ hipError_t launch_det_post(const DetPostArgs& a, int n, hipStream_t s) {
 }
 
 }  // namespace vge
+
+extern "C" int vge_debug_set_roi_direct(int on) {  // tests / A/B: 1 = roi_align_kernel (torchvision's sample order)
+  vge::g_roi_direct = on != 0;
+  return 0;
+}
