@@ -40,7 +40,7 @@ for f in glob.glob(f"{d}/**/*kernel_trace.csv", recursive=True):
         rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]))
 rows.sort()
 starts = [i for i, r in enumerate(rows) if "letterbox_focus" in r[2]]
-chunk = [r for r in rows[starts[-1]:] if "conv" in r[2] and "bf16" in r[2]]
+chunk = [r for r in rows[starts[-1]:] if ("conv" in r[2] and "bf16" in r[2]) or "Cijk_" in r[2]]  # library GEMMs too
 assert len(chunk) == len(L), (len(chunk), len(L))
 tot_ms = tot_fl = 0.0
 agg = {}

@@ -15,6 +15,11 @@
 #include <array>
 #include <cstdlib>
 
+#ifndef VGE_LIB_MIN_K_DEFAULT
+#define VGE_LIB_MIN_K_DEFAULT 128  // Cin 64 layers: the tuner's kernels, YOLOX -0.8 % (profiles/ab_r06ai_lib_min_k.json)
+#endif
+#include <cstdlib>
+
 #include "../../include/vge.h"
 #include "vge_cnn.h"
 
@@ -198,7 +203,11 @@ inline hipError_t conv_tuned_launch(ConvTuner& t, ConvLaunch& c, const std::arra
   // go to hipBLASLt without a timing contest
   // (vge_blaslt.cpp: 1,165 vs 934-943 TFLOP/s on the detector's res4 shapes, profiles/lib_gemm_probe_r06t.json): a
   // choice that never depends on timing noise, so a layer's outputs do not change from run to run
-  if (it == t.best.end() && conv_lib_epi(c) >= 0 && gemm_lib_ok(conv_lib_epi(c)))
+  static const int lib_min_k = [] {  // VGE_LIB_MIN_K: layers with fewer input channels stay on the tuner's kernels
+    const char* e = getenv("VGE_LIB_MIN_K");
+    return e ? atoi(e) : VGE_LIB_MIN_K_DEFAULT;
+  }();
+  if (it == t.best.end() && c.Cin >= lib_min_k && conv_lib_epi(c) >= 0 && gemm_lib_ok(conv_lib_epi(c)))
     it = t.best.emplace(key, 11000 + 256).first;
   if (it == t.best.end()) {
     if (!t.e0 && (hipEventCreate(&t.e0) != hipSuccess || hipEventCreate(&t.e1) != hipSuccess)) return hipErrorUnknown;

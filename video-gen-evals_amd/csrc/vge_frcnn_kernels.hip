@@ -10,7 +10,8 @@
 //       an 8-bit radix select on order-preserving keys (ties: lower anchor index), a bitonic sort of the k winners,
 //       anchor + Box2BoxTransform decode, clip, nonempty, and the level's largest kept coordinate
 //   rpn_nms_kernel            batched_nms(0.7) per (frame, level): torchvision's coordinate trick (boxes + level x
-//       (max + 1)), the IoU > thr matrix as 64-bit ballot words in LDS, the greedy scan by one wave
+//       (max + 1)), the IoU > thr upper triangle as 64-bit ballot words in LDS, the greedy scan by one wave (bit scan
+//       to the next live box), the kept boxes copied out after it
 //   rpn_merge_kernel          the levels' kept boxes in (score desc, level, rank) order = one stable sort of the
 //       concatenation, first post_nms_topk (rank by binary search in the other levels' sorted lists)
 //   roi_align_sep_kernel      ROIPooler: level = floor(4 + log2(sqrt(area) / 224 + 1e-8)) in [2, 5], ROIAlignV2
@@ -389,27 +390,65 @@ __global__ void __launch_bounds__(1024) rpn_nms_kernel(vge::RpnLevels L, const f
   }
   __syncthreads();
   const int nw = (k + 63) >> 6;
-  for (int p = wave; p < k * nw; p += 16) {
-    const int i = p / nw, w = p - i * nw, j = 64 * w + lane;
-    bool sup = false;
-    if (vld[i] && j > i && j < k && vld[j]) sup = iou_gt(bx[i], area[i], bx[j], area[j], thr);
-    const u64 bits = __ballot(sup);
-    if (lane == 0) mask[i * 16 + w] = bits;
+  // the upper triangle only: row i's words from i's own (the scan never reads a word below it: those boxes are
+  // decided); a pair without intersection is not > thr (thr >= 0) and skips the division
+  for (int i = wave; i < k; i += 16) {
+    if (!vld[i]) {
+      for (int w = i >> 6; w < nw; ++w)
+        if (lane == 0) mask[i * 16 + w] = 0ull;
+      continue;
+    }
+    const float4 bi = bx[i];
+    const float ai = area[i];
+    for (int w = i >> 6; w < nw; ++w) {
+      const int j = 64 * w + lane;
+      bool sup = false;
+      if (j > i && j < k && vld[j]) {
+        const float4 bj = bx[j];
+        const float left = fmaxf(bi.x, bj.x), right = fminf(bi.z, bj.z);
+        const float top = fmaxf(bi.y, bj.y), bottom = fminf(bi.w, bj.w);
+        const float inter = fmaxf(right - left, 0.f) * fmaxf(bottom - top, 0.f);
+        if (inter > 0.f || thr < 0.f) sup = inter / ((ai + area[j]) - inter) > thr;  // iou_gt
+      }
+      const u64 bits = __ballot(sup);
+      if (lane == 0) mask[i * 16 + w] = bits;
+    }
   }
   __syncthreads();
+  // the greedy scan by one wave: lane w holds the removed-bits word of boxes 64w .. 64w + 63 (invalid boxes start
+  // removed), the next live box is the lowest clear bit (a box only suppresses later ones, so this is torchvision's
+  // order), and only the kept boxes' indices are recorded (in LDS, over the areas); the copy-out runs after the scan
+  __shared__ int s_nk;
+  int* keep = reinterpret_cast<int*>(area);
   if (wave == 0) {
     u64 remv = 0;
+    for (int w = 0; w < nw; ++w) {
+      const int j = 64 * w + lane;
+      const u64 v = __ballot(j < k && vld[j]);
+      if (lane == w) remv = ~v;
+    }
     int nk = 0;
-    float* ko = kept + (size_t)(f * 5 + l) * vge::FR_MAXK * vge::FR_SEL;
-    for (int i = 0; i < k; ++i) {
-      const u64 word = readlane64(remv, i >> 6);
-      if (((word >> (i & 63)) & 1ull) == 0ull && vld[i]) {
+    for (int w = 0; w < nw; ++w) {
+      for (;;) {
+        const u64 live = ~readlane64(remv, w);
+        if (live == 0ull) break;
+        const int b = __builtin_ctzll(live), i = 64 * w + b;
         if (lane < nw) remv |= mask[i * 16 + lane];
-        if (lane < 5) ko[nk * vge::FR_SEL + lane] = sl[i * vge::FR_SEL + lane];
+        if (lane == w) remv |= 1ull << b;
+        if (lane == 0) keep[nk] = i;
         ++nk;
       }
     }
-    if (lane == 0) kcount[f * 5 + l] = nk;
+    if (lane == 0) {
+      s_nk = nk;
+      kcount[f * 5 + l] = nk;
+    }
+  }
+  __syncthreads();
+  float* ko = kept + (size_t)(f * 5 + l) * vge::FR_MAXK * vge::FR_SEL;
+  for (int t = tid; t < s_nk * 5; t += 1024) {
+    const int r = t / 5, q = t - 5 * r;
+    ko[r * vge::FR_SEL + q] = sl[keep[r] * vge::FR_SEL + q];
   }
 }
 
@@ -544,7 +583,7 @@ __global__ void __launch_bounds__(256) roi_align_kernel(vge::RoiLevels L, const 
 constexpr int RA_MAXC = 16;
 constexpr int RA_OOB = 0x7FFFFFF0;
 // rows of cells per load batch (x 4 columns): 2 x 4 measured faster than 4 x 4, and skipping the FMAs of the cells
-// outside the support (a uniform branch per column) no faster than weight 0 x a zero load (profiles/ab_r06ae_roi_align.json)
+// outside the support (a uniform branch per column) no faster than weight 0 x a zero load (profiles/ab_r06ae_frcnn_roi_nms.json)
 constexpr int RA_BR = 2;  // a buffer offset past any record range: the load returns 0
 
 __device__ __forceinline__ void roi_axis_table(float s, float bs, int n, int p, int L, float* tab, int& c0, int& nc) {
