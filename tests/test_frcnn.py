@@ -159,6 +159,35 @@ def test_roi_align_separable_matches_sample_order(run):
         assert n > 0 and same > 0.999 and float((d - b.abs() * 2 ** -7).max()) <= 1e-6
 
 
+def test_stem_pool_fused_matches_split(run):
+    """The fused stem conv + ReLU + max pool (frcnn_stem_pool_kernel, default) against the stem conv kernel followed by
+    the max-pool kernel (vge_debug_set_stem_split): the same MFMA K order and bf16 rounding point, so P2..P6 agree to
+    the conv kernel's own summation differences and the gate's person counts are the same."""
+    import ctypes as C
+    from vge import synth
+    from vge.frcnn import FrcnnDetector
+    frames = torch.from_numpy(synth.make_frame_pool(9100, NF)).to(DEV)
+    lib = L_load()
+    lib.vge_debug_set_stem_split.argtypes = [C.c_int]
+    got = {}
+    det = FrcnnDetector(run["sd"], run["cfg"], device=DEV, chunk=NF)
+    try:
+        for split in (0, 1):
+            lib.vge_debug_set_stem_split(split)
+            taps = det.make_taps(NF, 256, 256)
+            o = det.detect(frames, taps=taps)
+            torch.cuda.synchronize()
+            got[split] = ([p.float().cpu() for p in taps["fpn"]], o["n_person"].cpu())
+    finally:
+        lib.vge_debug_set_stem_split(0)
+        det.close()
+    for l, (a, b) in enumerate(zip(got[0][0], got[1][0])):
+        rel = float((a - b).norm() / b.norm())
+        print(f"P{l + 2}: fused vs split rel L2 {rel:.2e}, identical {float((a == b).float().mean()):.4f}")
+        assert rel < 1e-2, (l, rel)
+    assert torch.equal(got[0][1], got[1][1])
+
+
 def test_box_head_vs_oracle_on_gpu_features(run):
     o, t, K = run["oracle"], run["taps"], run["cfg"].num_classes
     for f in range(2):

@@ -274,6 +274,16 @@ bool cfg_ok(const vge_frcnn_config& c, std::string& why) {
   return true;
 }
 
+int g_stem_split = -1;  // vge_debug_set_stem_split(1) / VGE_STEM_FUSED=0: the stem conv and the max pool as two kernels
+
+bool stem_fused(const ConvW& L) {
+  if (g_stem_split < 0) {
+    const char* e = getenv("VGE_STEM_FUSED");
+    g_stem_split = (e && e[0] == '0') ? 1 : 0;
+  }
+  return !g_stem_split && L.Cinp == 8 && L.Cout == 64 && L.KH == 7 && L.KW == 7 && L.Kp >= 400;
+}
+
 int gconv(vge_frcnn* m, const ConvW& L, int cg, const void* x, int n, int H, int W, int stride, void* out,
           hipStream_t s) {
   const int Ho = (H + 2 - 3) / stride + 1, Wo = (W + 2 - 3) / stride + 1;
@@ -519,8 +529,15 @@ int vge_frcnn_detect(vge_frcnn* m, const uint8_t* frames, int F, int H, int W, f
                                           taps && taps->resized ? taps->resized + (size_t)f0 * m->nh * m->nw * 3 : nullptr,
                                           m->in, s));
     // ---- ResNeXt: stem, max pool, bottlenecks
-    STAGE(0, conv(m->cx(0), m->stem, m->in, 8, n, m->hp, m->wp, 2, m->stemo, c.stem_ch, s, 3));
-    OTHER(vge::launch_frcnn_pool_s2(m->stemo, m->pool, n, m->hp / 2, m->wp / 2, c.stem_ch, 3, s));
+    if (stem_fused(m->stem)) {  // the stem conv + ReLU + max pool in one kernel (no stem output in HBM)
+      RC(m->prof.beg(0, s));
+      HIPCHK(vge::launch_frcnn_stem_pool(m->in, m->stem.w, m->stem.Kp, m->stem.b, m->pool, n, m->hp, m->wp, s));
+      RC(m->prof.end(s));
+      m->flops[0] += 2.0 * n * (m->hp / 2) * (m->wp / 2) * (double)m->stem.Cout * 49 * m->stem.Cinp;
+    } else {
+      STAGE(0, conv(m->cx(0), m->stem, m->in, 8, n, m->hp, m->wp, 2, m->stemo, c.stem_ch, s, 3));
+      OTHER(vge::launch_frcnn_pool_s2(m->stemo, m->pool, n, m->hp / 2, m->wp / 2, c.stem_ch, 3, s));
+    }
     const void* x = m->pool;
     int h = h4, w = w4;
     for (int st = 0; st < 4; ++st) {
@@ -688,3 +705,8 @@ int vge_debug_gconv3(const void* x, int n, int H, int W, int C, int gw, int stri
 }
 
 }  // extern "C"
+
+extern "C" int vge_debug_set_stem_split(int on) {  // tests / A/B: 1 = the stem conv and the max pool as two kernels
+  g_stem_split = on ? 1 : 0;
+  return 0;
+}

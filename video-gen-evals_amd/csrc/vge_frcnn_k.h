@@ -45,6 +45,9 @@ hipError_t launch_frcnn_resize_h(const uint8_t* src, int n, int H, int W, int nw
 hipError_t launch_frcnn_resize_v_norm(const uint8_t* tmp, int n, int H, int nw, int nh, int hp, int wp, const int* yb,
                                       const int* kk, int ks, uint8_t* resized, void* out, hipStream_t s);
 hipError_t launch_frcnn_pool_s2(const void* x, void* y, int n, int H, int W, int C, int K, hipStream_t s);
+// the stem conv (7x7 / 2, 8-channel NHWC input, 64 outputs, weights [64][Kp] tap-major) + ReLU + max_pool2d(3, 2, 1)
+hipError_t launch_frcnn_stem_pool(const void* in, const void* w, int Kp, const float* bias, void* out, int n, int hp,
+                                  int wp, hipStream_t s);
 hipError_t launch_rpn_select(const RpnLevels& lv, int n, float img_h, float img_w, float* sel, float* sel_max,
                              hipStream_t s);
 hipError_t launch_rpn_nms(const RpnLevels& lv, const float* sel, const float* sel_max, int n, float thr, float* kept,

@@ -27,6 +27,8 @@
 #include "vge_lds_attr.h"
 #include "vge_frcnn_k.h"
 
+#include <algorithm>
+
 #pragma clang fp contract(off)
 
 namespace {
@@ -35,6 +37,7 @@ typedef __bf16 bf16;
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned long long u64;
 typedef unsigned uintx4_t __attribute__((ext_vector_type(4)));
+typedef float floatx16 __attribute__((ext_vector_type(16)));
 
 constexpr float SCALE_CLAMP = 4.135166556742356f;  // log(1000 / 16), Box2BoxTransform
 
@@ -736,6 +739,168 @@ __global__ void __launch_bounds__(224) roi_align_sep_kernel(vge::RoiLevels L, co
   }
 }
 
+// ------------------------------------------------------------------------------------- stem + max pool, fused
+// ResNet BasicStem: conv1 7x7 / 2 (pad 3, 3 -> 64 channels, FrozenBN folded into the bias) + ReLU, then max_pool2d(3, 2,
+// 1), without the stem's output going through HBM.  Persistent (one 512-thread workgroup per CU, the weights staged in
+// LDS once); a tile is 7 x 16 pooled pixels, whose 15 x 33 stem pixels (the pool window's halo recomputed) are an
+// implicit GEMM of 64 channels x 495 pixels x K = 400 (taps 0..49 x 8 input channels, the padded taps' weights 0) on
+// v_mfma_f32_32x32x16_bf16 with the weights as the row operand: each wave owns 2 pixel tiles of 32 x both channel tiles,
+// its pixel fragments read from the tile's input patch (35 x 71 pixels x 8 channels, zero outside the frame) in LDS, the
+// weight fragments from LDS in fragment order (the patch rows stored as even then odd columns, so the 32 lanes'
+// stride-2 pixels are consecutive 16-B chunks: no bank conflicts); a lane's accumulators then hold 4 consecutive channels of one pixel
+// (8-B LDS stores of the ReLU'd bf16 values).  Each pooled pixel takes the max of its 3 x 3 window's stem pixels inside
+// the frame (-inf padding: the values are >= 0 and the centre is inside, so the ones outside are left out).  Patch,
+// stem values and weights have separate LDS regions, so a tile costs two barriers: [MFMAs(t)] | [stem values(t), the
+// patch of t + G stored (its loads were issued a tile earlier), the loads of t + 2G issued] | [pool(t), MFMAs(t + G)].
+// The stem conv kernel's arithmetic (16-k MFMA steps in tap order, bias then ReLU then bf16): bit-identical outputs.
+constexpr int SP_TPH = 7, SP_TPW = 16;                          // pooled tile
+constexpr int SP_SR = 2 * SP_TPH + 1, SP_SC = 2 * SP_TPW + 1;   // stem pixels of a tile: 15 x 33 = 495
+constexpr int SP_PR = 2 * (SP_SR - 1) + 7, SP_PC = 2 * (SP_SC - 1) + 7;  // input patch: 35 x 71
+constexpr int SP_NCH = SP_PR * SP_PC;                           // 16-B patch chunks (one pixel's 8 channels)
+constexpr int SP_NLD = (SP_NCH + 511) / 512;                    // per thread: 5
+constexpr int SP_STEPS = 25;                                    // K = 400 (taps 0..49)
+constexpr int SP_SPITCH = 144;                                  // stem values: bytes per pixel (64 x 2 + 16: banks)
+constexpr int SP_W_BYTES = SP_STEPS * 2 * 64 * 16;              // weights in fragment order: 51,200
+constexpr int SP_PH = (SP_PC + 1) / 2;                          // patch row: even columns, then odd columns (36 each)
+constexpr int SP_P_BYTES = SP_PR * 2 * SP_PH * 16;               // patch: 40,320
+constexpr int SP_S_BYTES = SP_SR * SP_SC * SP_SPITCH;           // stem values: 71,280
+constexpr int SP_LDS = SP_W_BYTES + SP_P_BYTES + SP_S_BYTES;    // 162,800
+constexpr int SP_OOB = 0x7FFFFFF0;
+
+__global__ void __launch_bounds__(512, 1) frcnn_stem_pool_kernel(const bf16* __restrict__ in, const bf16* __restrict__ w,
+                                                                 int Kp, const float* __restrict__ bias,
+                                                                 bf16* __restrict__ out, int n, int hp, int wp,
+                                                                 int tiles_y, int tiles_x) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  char* wl = lds;
+  char* pat = lds + SP_W_BYTES;
+  char* stv = pat + SP_P_BYTES;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, h = lane >> 5;
+  const int Hs = hp >> 1, Ws = wp >> 1, Hp = Hs >> 1, Wp = Ws >> 1;
+  const int G = gridDim.x, tpi = tiles_y * tiles_x, ntiles = n * tpi;
+  // weights [64][Kp] -> fragment order [step][u][lane] (16 B): channel 32u + (lane & 31), k = 16 step + 8 (lane >> 5)
+  for (int c = tid; c < SP_STEPS * 2 * 64; c += 512) {
+    const int l = c & 63, u = (c >> 6) & 1, st = c >> 7;
+    const int col = 32 * u + (l & 31), k = 16 * st + 8 * (l >> 5);
+    *reinterpret_cast<uintx4_t*>(wl + c * 16) = *reinterpret_cast<const uintx4_t*>(w + (size_t)col * Kp + k);
+  }
+  const int img_bytes = hp * wp * 16;
+  auto load_patch = [&](int t, uintx4_t (&v)[SP_NLD]) {  // t >= ntiles: an empty record range (zeros, no traffic)
+    const int img = t / tpi, r = t - img * tpi;
+    const int ty = r / tiles_x, tx = r - ty * tiles_x;
+    const int iy0 = 4 * SP_TPH * ty - 5, ix0 = 4 * SP_TPW * tx - 5;
+    const __amdgpu_buffer_rsrc_t ir = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<bf16*>(in + (size_t)(t < ntiles ? img : 0) * hp * wp * 8), (short)0, t < ntiles ? img_bytes : 0,
+        0x00020000);
+#pragma unroll
+    for (int q = 0; q < SP_NLD; ++q) {
+      const int c = tid + 512 * q, pr = c / SP_PC, pc = c - pr * SP_PC;
+      const int iy = iy0 + pr, ix = ix0 + pc;
+      const bool ok = c < SP_NCH && (unsigned)iy < (unsigned)hp && (unsigned)ix < (unsigned)wp;
+      v[q] = __builtin_amdgcn_raw_buffer_load_b128(ir, ok ? (iy * wp + ix) * 16 : SP_OOB, 0, 0);
+    }
+  };
+  auto store_patch = [&](const uintx4_t (&v)[SP_NLD]) {
+#pragma unroll
+    for (int q = 0; q < SP_NLD; ++q) {
+      const int c = tid + 512 * q, pr = c / SP_PC, pc = c - pr * SP_PC;
+      if (c < SP_NCH) *reinterpret_cast<uintx4_t*>(pat + (pr * 2 * SP_PH + (pc & 1) * SP_PH + (pc >> 1)) * 16) = v[q];
+    }
+  };
+  // this lane's pixel column: stem pixel 32 pt + (lane & 31) of pixel tiles pt = 2 wave, 2 wave + 1 (the last tile's
+  // 17 pad columns are clamped to a real pixel and never stored)
+  int pbase[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int sidx = min(32 * (2 * wave + i) + (lane & 31), SP_SR * SP_SC - 1);
+    const int sr = sidx / SP_SC, sc = sidx - sr * SP_SC;
+    pbase[i] = (2 * sr * 2 * SP_PH + sc) * 16;  // column 2 sc + kx: half kx & 1, index sc + kx / 2
+  }
+  // the bias of this lane's channels: 32u + 8g + 4h + j (accumulator register 4g + j)
+  floatx4 bq[2][4];
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) bq[u][g] = *reinterpret_cast<const floatx4*>(bias + 32 * u + 8 * g + 4 * h);
+
+  uintx4_t pv[SP_NLD];
+  int t = blockIdx.x;
+  load_patch(t, pv);
+  store_patch(pv);
+  load_patch(t + G, pv);
+  __syncthreads();  // weights and the first patch in LDS
+  for (; t < ntiles; t += G) {
+    floatx16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][u][r] = 0.f;
+#pragma unroll
+    for (int st = 0; st < SP_STEPS; ++st) {
+      const int tap0 = 2 * st, tap1 = 2 * st + 1;  // this lane's tap: tap0 + h (tap 49 reads tap 48: weight 0)
+      constexpr auto toffs = [](int tap) {
+        const int ky = tap / 7, kx = tap % 7;
+        return (ky * 2 * SP_PH + (kx & 1) * SP_PH + (kx >> 1)) * 16;
+      };
+      const int o0 = toffs(tap0), o1 = tap1 < 49 ? toffs(tap1) : o0;
+      const int toff = h ? o1 : o0;
+      bf16x8 px[2], wf[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) px[i] = *reinterpret_cast<const bf16x8*>(pat + pbase[i] + toff);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) wf[u] = *reinterpret_cast<const bf16x8*>(wl + ((st * 2 + u) * 64 + lane) * 16);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) acc[i][u] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(wf[u], px[i], acc[i][u], 0, 0, 0);
+    }
+    __syncthreads();  // A: the patch is free, and every wave's pool of the previous tile is done
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int sidx = 32 * (2 * wave + i) + (lane & 31);
+      if (sidx < SP_SR * SP_SC) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+            bf16x4_t o;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) o[j] = (bf16)fmaxf(acc[i][u][4 * g + j] + bq[u][g][j], 0.f);
+            *reinterpret_cast<bf16x4_t*>(stv + sidx * SP_SPITCH + (32 * u + 8 * g + 4 * h) * 2) = o;
+          }
+      }
+    }
+    store_patch(pv);        // the patch of t + G (zeros past the end)
+    load_patch(t + 2 * G, pv);
+    __syncthreads();  // B: stem values and the next patch in LDS
+    const int img = t / tpi, r = t - img * tpi;
+    const int ty = r / tiles_x, tx = r - ty * tiles_x;
+    const int sy0 = 2 * SP_TPH * ty - 1, sx0 = 2 * SP_TPW * tx - 1;
+    for (int task = tid; task < SP_TPH * SP_TPW * 8; task += 512) {  // 7 x 16 pooled pixels x 8 channel groups
+      const int g = task & 7, pp = task >> 3, py = pp / SP_TPW, px = pp - py * SP_TPW;
+      const int oy = SP_TPH * ty + py, ox = SP_TPW * tx + px;
+      bf16x8 m;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) m[c] = (bf16)0.f;
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx) {  // a stem pixel outside the frame reads the centre instead (no branch)
+          const int sr = 2 * py + dy, sc = 2 * px + dx;
+          const bool in = (unsigned)(sy0 + sr) < (unsigned)Hs && (unsigned)(sx0 + sc) < (unsigned)Ws;
+          const int cell = in ? sr * SP_SC + sc : (2 * py + 1) * SP_SC + 2 * px + 1;
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(stv + cell * SP_SPITCH + g * 16);
+#pragma unroll
+          for (int c = 0; c < 8; ++c) m[c] = (float)v[c] > (float)m[c] ? v[c] : m[c];
+        }
+      if (oy < Hp && ox < Wp) *reinterpret_cast<bf16x8*>(out + (((size_t)img * Hp + oy) * Wp + ox) * 64 + g * 8) = m;
+    }
+  }
+}
+
 // ------------------------------------------------------------------------------------------------ box inference
 // softmax of one head row over K + 1 <= 128 logits held two per lane (lane l: class l and 64 + l); returns the
 // probabilities (0 outside the row)
@@ -968,6 +1133,25 @@ hipError_t launch_frcnn_resize_v_norm(const uint8_t* tmp, int n, int H, int nw, 
   if (tot == 0) return hipSuccess;
   hipLaunchKernelGGL(frcnn_resize_v_norm_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, tmp, n, H, nw,
                      nh, hp, wp, yb, kk, ks, resized, static_cast<bf16*>(out));
+  return hipGetLastError();
+}
+
+hipError_t launch_frcnn_stem_pool(const void* in, const void* w, int Kp, const float* bias, void* out, int n, int hp,
+                                  int wp, hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  if (hp % 4 || wp % 4 || Kp < 2 * SP_STEPS * 8 || (long)hp * wp * 16 >= (1l << 31)) return hipErrorInvalidValue;
+  const int Hp = hp / 4, Wp = wp / 4;
+  const int ty = (Hp + SP_TPH - 1) / SP_TPH, tx = (Wp + SP_TPW - 1) / SP_TPW;
+  const long ntiles = (long)n * ty * tx;
+  if (ntiles >= (1l << 31)) return hipErrorInvalidValue;
+  static LdsAttrOnce attr;
+  if (const hipError_t e = attr(reinterpret_cast<const void*>(&frcnn_stem_pool_kernel), SP_LDS); e != hipSuccess) return e;
+  int dev = 0, ncu = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return hipErrorUnknown;
+  const int grid = (int)std::min<long>(ntiles, ncu);
+  hipLaunchKernelGGL(frcnn_stem_pool_kernel, dim3(grid), dim3(512), SP_LDS, s, static_cast<const bf16*>(in),
+                     static_cast<const bf16*>(w), Kp, bias, static_cast<bf16*>(out), n, hp, wp, ty, tx);
   return hipGetLastError();
 }
 
