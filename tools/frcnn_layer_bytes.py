@@ -35,6 +35,7 @@ def layer_shapes(H=800, W=800, depth=101):
     h, w = H // 2, W // 2
     L["stem"] = (H * W * 8 * B + px(h, w) * 64 * B, 64 * 7 * 7 * 8 * B, 2.0 * px(h, w) * 64 * 3 * 49)
     L["maxpool"] = (px(h, w) * 64 * B + px(h // 2, w // 2) * 64 * B, 0, 0)
+    L["stem_pool"] = (H * W * 8 * B + px(h // 2, w // 2) * 64 * B, L["stem"][1], L["stem"][2])  # fused: no stem output
     h, w = h // 2, w // 2
     cin, width, cout = 64, 256, 256
     lv = {}
@@ -109,8 +110,8 @@ def main():
     H = int(pos[2]) if len(pos) > 2 else 800
     W = int(pos[3]) if len(pos) > 3 else 800
     OUT = ROOT / "gpurun_out"
-    lab = labels(101)
     tr = list(csv.DictReader(open(next((OUT / f"pe_{tag}_frcnn_trace").glob("**/*kernel_trace.csv")))))
+    lab = labels(101, any("frcnn_stem_pool" in r["Kernel_Name"] for r in tr))
     tr.sort(key=lambda r: int(r["Start_Timestamp"]))
     trows = last_call([(0, r["Kernel_Name"], (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
                        for r in tr], lab)

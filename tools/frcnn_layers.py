@@ -6,9 +6,10 @@ import sys
 from collections import defaultdict
 
 
-def labels(depth=101):
+def labels(depth=101, stem_fused=True):
+    """stem_fused: the stem conv + max pool as one dispatch (frcnn_stem_pool_kernel, the default since round 6)"""
     nb = {50: (3, 4, 6, 3), 101: (3, 4, 23, 3), 152: (3, 8, 36, 3)}[depth]
-    L = ["resize_h", "resize_v", "stem", "maxpool"]
+    L = ["resize_h", "resize_v"] + (["stem_pool"] if stem_fused else ["stem", "maxpool"])
     for s, n in enumerate(nb):
         for b in range(n):
             p = f"res{s + 2}.{b}"
@@ -37,7 +38,7 @@ def main():
         c = sqlite3.connect(db)
         rows = c.execute("select name, duration, grid_x, workgroup_x from kernels order by start").fetchall()
     rows = [r for r in rows if not r[0].startswith("__amd_rocclr") and "at::" not in r[0]]
-    lab = labels(depth)
+    lab = labels(depth, any("frcnn_stem_pool" in r[0] for r in rows))
     last = rows[-len(lab):]
     if not last[-1][0].startswith("_ZN12_GLOBAL__N_115det_post") and "det_post" not in last[-1][0]:
         print("warning: the trace does not end with det_post_kernel")

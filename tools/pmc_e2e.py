@@ -7,7 +7,7 @@ MI355X_MICROARCH.md HBM recipe, summed over dispatches):
                     dispatches of tools/yolox_prof.py's profiled calls (from the first of their letterbox_focus launches
                     on, in dispatch order) / their frames
   frcnn_conv        the Faster R-CNN gate detector's convs (backbone, FPN, RPN, box head: the implicit-GEMM kernels,
-                    the 1x1 convs on gemm_bf16_kernel, the grouped 3x3 on gconv3_kernel), the dispatches of
+                    the 1x1 convs on gemm_bf16_kernel, the grouped 3x3 on gconv3_kernel, the fused stem + pool), the dispatches of
                     tools/time_frcnn.py's timed call (from its first frcnn_resize_h launch on) / its frames
 -> profiles/pmc_e2e.json, keyed by the kernels' source hash (bench_e2e.py reports `traffic` only while it matches).
     python tools/pmc_e2e.py TAG"""
@@ -61,7 +61,8 @@ fe = dispatches("yolox_fetch")
 lb = [i for i in sorted(fe) if "letterbox_focus" in fe[i][0]]
 first = lb[-yinfo["calls"] * yinfo["chunks_per_call"]]
 def conv_like(k):
-    return ("conv" in k and "bf16" in k) or "gemm_bf16_kernel" in k or "gconv3_kernel" in k or lib_gemm(k)
+    return (("conv" in k and "bf16" in k) or "gemm_bf16_kernel" in k or "gconv3_kernel" in k or lib_gemm(k)
+            or "frcnn_stem_pool" in k)
 
 
 y_bytes, y_n = total("yolox", lambda i, k: i >= first and conv_like(k))
