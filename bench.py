@@ -469,6 +469,7 @@ def run_e2e_child(args) -> dict:
            "--steps", "1", "--warmup", "1", "--cpu-seconds", "15"]
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     t0 = time.perf_counter()
+    print("[bench] config-2 line measured; the nested config-3 run starts", file=sys.stderr, flush=True)
     try:
         r = subprocess.run(cmd, env=env, stdout=subprocess.PIPE, stderr=None, text=True, timeout=args.e2e_timeout)
     except subprocess.TimeoutExpired:

@@ -114,6 +114,14 @@ def run(args, world, rank, dev, metric, allreduce_sum, make_clips):
     F = C * T
     FC = min(F, max(1, getattr(args, "chunk_clips", 32)) * T)   # frames per extraction pass
     t_setup = time.perf_counter()
+    if rank == 0:  # a progress line every 30 s for the whole run (setup and warm-up print nothing else for minutes)
+        import threading
+
+        def _alive():
+            while True:
+                time.sleep(30.0)
+                print(f"[e2e] running, {time.perf_counter() - t_setup:.0f} s", file=sys.stderr, flush=True)
+        threading.Thread(target=_alive, daemon=True).start()
     # scoring model, stats and centroids from the (sharded) pre-extracted real set, as in config 2
     n_real_per_class, T_real = 8, 64
     real_idx = shard(list(range(10 * n_real_per_class)), rank, world)
