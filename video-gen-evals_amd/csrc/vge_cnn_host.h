@@ -177,6 +177,7 @@ struct ConvTuner {
   std::map<std::array<long, 10>, int> best;  // (H, W, Cin, Cout, KH, stride, act, out_f32, res, ldo) -> variant / tn
   hipEvent_t e0 = nullptr, e1 = nullptr;
   int on = -1;
+  bool lib = true;  // the library path (variant 11) for the layers it takes; the pose extractors' tuners turn it off
   ~ConvTuner() {
     if (e0) (void)hipEventDestroy(e0);
     if (e1) (void)hipEventDestroy(e1);
@@ -197,6 +198,14 @@ struct ConvCtx {
 };
 
 // encoded choice: variant * 1000 + tn
+// hipBLASLt's stream-K GEMMs rely on their workgroups being resident together; two of them on two streams at once
+// (the e2e bench runs the gate detector + TokenHMR beside YOLOX + DWPose) were seen to hang, so only one extractor
+// side uses the library: the pose extractors' 1x1 convs stay on the tuner's kernels unless VGE_POSE_GEMM_LIB=1
+inline bool pose_gemm_lib() {
+  static const bool on = getenv("VGE_POSE_GEMM_LIB") && getenv("VGE_POSE_GEMM_LIB")[0] == '1';
+  return on;
+}
+
 inline hipError_t conv_tuned_launch(ConvTuner& t, ConvLaunch& c, const std::array<long, 10>& key, hipStream_t s) {
   auto it = t.best.find(key);
   // 1x1 stride-1 convs with the epilogues the library expresses (bias, ReLU / SiLU, a bf16 residual before the ReLU)
@@ -207,7 +216,7 @@ inline hipError_t conv_tuned_launch(ConvTuner& t, ConvLaunch& c, const std::arra
     const char* e = getenv("VGE_LIB_MIN_K");
     return e ? atoi(e) : VGE_LIB_MIN_K_DEFAULT;
   }();
-  if (it == t.best.end() && c.Cin >= lib_min_k && conv_lib_epi(c) >= 0 && gemm_lib_ok(conv_lib_epi(c)))
+  if (it == t.best.end() && t.lib && c.Cin >= lib_min_k && conv_lib_epi(c) >= 0 && gemm_lib_ok(conv_lib_epi(c)))
     it = t.best.emplace(key, 11000 + 256).first;
   if (it == t.best.end()) {
     if (!t.e0 && (hipEventCreate(&t.e0) != hipSuccess || hipEventCreate(&t.e1) != hipSuccess)) return hipErrorUnknown;

@@ -266,6 +266,7 @@ int vge_dwpose_create(const vge_rtmpose_config* cfg, const vge_tensor_view* weig
   const vge_rtmpose_config c = *cfg;
   WeightMap wm(weights, n_weights);
   auto* m = new vge_dwpose();
+  m->tuner.lib = pose_gemm_lib();
   m->c = c;
   bool ok_all = true;
   for (int pass = 0; pass < 2 && ok_all; ++pass) {

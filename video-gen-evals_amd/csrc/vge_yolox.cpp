@@ -195,6 +195,7 @@ int vge_yolox_create(const vge_yolox_config* cfg, const vge_tensor_view* weights
   if (!cfg_ok(*cfg, why)) return fail(VGE_ERR_ARG, "vge_yolox_create: unsupported config: " + why);
   WeightMap wm(weights, n_weights);
   auto* m = new vge_yolox();
+  m->tuner.lib = pose_gemm_lib();
   m->c = *cfg;
   bool ok = true;
   for (int pass = 0; pass < 2 && ok; ++pass) {
