@@ -36,10 +36,10 @@ E2E_KERNEL_SOURCES = {"gemm_bf16_kernel": ["vge_vit.hip", "vge_blaslt.cpp", "vge
                       "yolox_conv": ["vge_cnn.hip", "vge_cnn_host.h", "vge_yolox.cpp", "vge_vit.hip", "vge_blaslt.cpp"],
                       "frcnn_conv": ["vge_cnn.hip", "vge_cnn_host.h", "vge_frcnn.cpp", "vge_vit.hip", "vge_gconv.hip",
                                      "vge_blaslt.cpp", "vge_frcnn_kernels.hip"]}  # (the fused stem + pool)
-YOLOX_CHUNK = 256   # frames per detector pass (tools/yolox_prof.py --chunk: 637 vs 618 TFLOP/s at 64)
+YOLOX_CHUNK = 1024  # frames per detector pass: the whole extraction pass (tools/yolox_prof.py --chunk: 246.4 / 238.7 / 234.5 ms per 1,024 frames at 256 / 512 / 1,024, profiles/ab_r06ax_chunks.json)
 # frames per Faster R-CNN workspace chunk (~0.3 GB per 800 x 800 frame): 64 was -6 % vs 32 (profiles/ab_r05m_*); 128,
 # possible since the 1x1 convs' GEMM epilogue addresses through 64-bit offsets, -1.2 % vs 64 (profiles/ab_r06b_frcnn_chunk.json)
-FRCNN_CHUNK = 128
+FRCNN_CHUNK = 256  # 197.2 -> 193.6 ms per 256 frames vs 128 (profiles/ab_r06ax_chunks.json)
 
 
 def e2e_traffic(kernel: str, frames: float):
