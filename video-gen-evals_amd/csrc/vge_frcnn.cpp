@@ -413,7 +413,6 @@ int vge_frcnn_reserve(vge_frcnn* m, int chunk, int H, int W) {
   std::vector<Buf> bufs = {
       {(void**)&m->tmp, N * H * m->nw * 3},
       {&m->in, N * m->hp * m->wp * 8 * 2},
-      {&m->stemo, N * s2 * m->c.stem_ch * 2},
       {&m->pool, N * s4 * m->c.stem_ch * 2},
       {&m->Y, N * s4 * std::max(r2, w0) * 2},
       {&m->T1, N * s4 * 2 * w0 * 2},
@@ -421,9 +420,6 @@ int vge_frcnn_reserve(vge_frcnn* m, int chunk, int H, int W) {
       {&m->SC, N * s4 * r2 * 2},
       {&m->PV[0], N * s4 * F * 2},
       {&m->PV[1], N * s4 * F * 2},
-      {&m->UP, N * s4 * F * 2},
-      {&m->RT, N * s4 * F * 2},
-      {&m->BOXF, N * P * 49 * F * 2},
       {&m->FC1, N * P * m->c.fc_dim * 2},
       {&m->FC2, N * P * m->c.fc_dim * 2},
       {(void**)&m->HEAD, N * P * m->ld_head * 4},
@@ -446,6 +442,30 @@ int vge_frcnn_reserve(vge_frcnn* m, int chunk, int H, int W) {
     if (!p) return fail(VGE_ERR_NOMEM, "vge_frcnn_reserve: hipMalloc failed");
     HIPCHK(hipMemset(p, 0, bf.bytes));
     *bf.p = p;
+  }
+  // buffers whose lifetimes do not overlap share memory (-86 MB per 800-px frame, a quarter of the workspace): the
+  // stem output (split-stem path only) lives before res2.0's conv1 writes T1; the FPN's upsampled top-down sum and
+  // the RPN conv's output after the backbone, in the shortcut / grouped-conv buffers; the ROI features after the RPN,
+  // in T1.  An alias too small for another frame size gets its own allocation.
+  struct Alias {
+    void** p;
+    size_t bytes;
+    void* over;
+    size_t over_bytes;
+  };
+  const Alias al[] = {{&m->stemo, N * s2 * m->c.stem_ch * 2, m->T1, N * s4 * 2 * w0 * 2},
+                      {&m->UP, N * s4 * F * 2, m->SC, N * s4 * r2 * 2},
+                      {&m->RT, N * s4 * F * 2, m->T2, N * s4 * w0 * 2},
+                      {&m->BOXF, N * P * 49 * F * 2, m->T1, N * s4 * 2 * w0 * 2}};
+  for (const Alias& a : al) {
+    if (a.bytes <= a.over_bytes) {
+      *a.p = a.over;
+      continue;
+    }
+    void* p = d.dmalloc(a.bytes);
+    if (!p) return fail(VGE_ERR_NOMEM, "vge_frcnn_reserve: hipMalloc failed");
+    HIPCHK(hipMemset(p, 0, a.bytes));
+    *a.p = p;
   }
   m->chunk = chunk;
   m->rH = H;
