@@ -130,7 +130,8 @@ def test_box_features_vs_oracle_on_gpu_levels(run):
 def test_roi_align_separable_matches_sample_order(run):
     """The default ROIAlign (separable per-bin cell weights, roi_align_sep_kernel) against torchvision's sample order
     (roi_align_kernel, vge_debug_set_roi_direct) on the same levels and proposals: the same sums reassociated, so
-    bins identical but for rare 1-ulp bf16 differences."""
+    bins identical but for rare 1-ulp bf16 differences.  The separable kernel's sample-loop branch (taken for bins
+    wider than its LDS tables, forced here for every ROI) is roi_align_kernel's arithmetic: identical."""
     import ctypes as C
     from vge import synth
     from vge.frcnn import FrcnnDetector
@@ -140,7 +141,7 @@ def test_roi_align_separable_matches_sample_order(run):
     got = {}
     det = FrcnnDetector(run["sd"], run["cfg"], device=DEV, chunk=NF)
     try:
-        for direct in (0, 1):
+        for direct in (0, 1, 2):  # 2: the separable kernel's own sample loop (its branch for very wide bins)
             lib.vge_debug_set_roi_direct(direct)
             taps = det.make_taps(NF, 256, 256)
             det.detect(frames, taps=taps)
@@ -150,6 +151,7 @@ def test_roi_align_separable_matches_sample_order(run):
         lib.vge_debug_set_roi_direct(0)
         det.close()
     assert torch.equal(got[0][1], got[1][1])
+    assert torch.equal(got[2][0], got[1][0]), "the separable kernel's sample loop differs from roi_align_kernel"
     for f in range(NF):
         n = int(got[0][1][f])
         a, b = got[0][0][f, :n].float(), got[1][0][f, :n].float()

@@ -620,7 +620,7 @@ __device__ __forceinline__ void roi_axis_table(float s, float bs, int n, int p, 
 
 __global__ void __launch_bounds__(224) roi_align_sep_kernel(vge::RoiLevels L, const float* __restrict__ props,
                                                             const int* __restrict__ n_prop, int P,
-                                                            bf16* __restrict__ out) {
+                                                            bf16* __restrict__ out, int maxc) {
   __shared__ float wtab[14][RA_MAXC + 4];  // + 4: a batch's columns past the table read 0
   __shared__ int c0s[14], ncs[14];
   const int f = blockIdx.x / P, r = blockIdx.x - f * P;
@@ -651,7 +651,7 @@ __global__ void __launch_bounds__(224) roi_align_sep_kernel(vge::RoiLevels L, co
   const float bw = rw / 7.f, bh = rh / 7.f;
   const int gh = (int)ceilf(rh / 7.f), gw = (int)ceilf(rw / 7.f);
   const float cnt = (float)max(gh * gw, 1);
-  if (gh + 3 > RA_MAXC || gw + 3 > RA_MAXC) {  // the sample loop (uniform per workgroup)
+  if (gh + 3 > maxc || gw + 3 > maxc) {  // the sample loop (uniform per workgroup; maxc = RA_MAXC, 0 in a test)
     for (int pw = 0; pw < 7; ++pw) {
       const int ph = g;
       float acc[8];
@@ -1197,7 +1197,8 @@ hipError_t launch_rpn_merge(const float* kept, const int* kcount, int n, int pos
   return hipGetLastError();
 }
 
-static bool g_roi_direct = false;  // vge_debug_set_roi_direct(1): the sample-order kernel (tests)
+static int g_roi_direct = 0;  // vge_debug_set_roi_direct: 1 = the sample-order kernel, 2 = the separable kernel's
+                             // sample-loop branch for every ROI (tests)
 
 hipError_t launch_roi_align(const RoiLevels& lv, const float* props, const int* n_prop, int n, int P, void* out,
                             hipStream_t s) {
@@ -1206,8 +1207,9 @@ hipError_t launch_roi_align(const RoiLevels& lv, const float* props, const int* 
     const char* e = getenv("VGE_ROI_SEP");
     return !(e && e[0] == '0');
   }();
-  if (sep && !g_roi_direct)
-    hipLaunchKernelGGL(roi_align_sep_kernel, dim3(n * P), dim3(224), 0, s, lv, props, n_prop, P, static_cast<bf16*>(out));
+  if (sep && g_roi_direct != 1)
+    hipLaunchKernelGGL(roi_align_sep_kernel, dim3(n * P), dim3(224), 0, s, lv, props, n_prop, P, static_cast<bf16*>(out),
+                       g_roi_direct == 2 ? 0 : RA_MAXC);
   else
     hipLaunchKernelGGL(roi_align_kernel, dim3(n * P), dim3(256), 0, s, lv, props, n_prop, P, static_cast<bf16*>(out));
   return hipGetLastError();
@@ -1222,7 +1224,7 @@ hipError_t launch_det_post(const DetPostArgs& a, int n, hipStream_t s) {
 
 }  // namespace vge
 
-extern "C" int vge_debug_set_roi_direct(int on) {  // tests / A/B: 1 = roi_align_kernel (torchvision's sample order)
-  vge::g_roi_direct = on != 0;
+extern "C" int vge_debug_set_roi_direct(int mode) {  // tests / A/B: 1 = roi_align_kernel (torchvision's sample
+  vge::g_roi_direct = mode;                           // order), 2 = roi_align_sep_kernel's sample loop for every ROI
   return 0;
 }
